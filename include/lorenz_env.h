@@ -1,0 +1,204 @@
+/*
+ * lorenz_env.h -- C-ABI of the MI355X-native vectorised chaotic-ODE env library
+ *                 (libgym_lorenz_amd.so).
+ *
+ * The reference (erererq/gym-lorenz) is pure Python: every env is a gym/gymnasium
+ * `Env` whose reset()/step() run scalar NumPy on 3-8 element arrays, one env per
+ * object, driven one step at a time by stable-baselines3's DummyVecEnv.  This
+ * library replaces exactly that hot path -- the env batch's reset()/step() -- with
+ * one HIP kernel launch per batched step, one env per GPU lane.  The Python package
+ * `gym_lorenz` (gym-lorenz_amd/gym_lorenz) binds it through ctypes and keeps the
+ * reference's per-env classes, ids and SB3 VecEnv surface.
+ *
+ * Entry point  ->  reference interface it replaces
+ *   lz_create / lz_config_init
+ *       -> the env constructors: dynamic.py:8-33 (lorenzEnv_transient, 3-state),
+ *          lorenz_env_transient.py:253-273 (lorenzEnv_transient, 4-state),
+ *          lorenz_env_try_pmsm.py:9-50 (PMSM_Sync_Env),
+ *          lorenz_env_try.py:19-48 (HRSyncEnv); plus gym_lorenz/__init__.py:4-23
+ *          (registration kwargs max_episode_steps -> max_episode_steps)
+ *   lz_reset
+ *       -> reset(): dynamic.py:35-47, lorenz_env_transient.py:275-297,
+ *          lorenz_env_try_pmsm.py:59-75, lorenz_env_try.py:49-78
+ *   lz_step
+ *       -> step(action): dynamic.py:61-90, lorenz_env_transient.py:314-373,
+ *          lorenz_env_try_pmsm.py:76-184, lorenz_env_try.py:80-179, batched over
+ *          the env axis with SB3 DummyVecEnv.step_wait auto-reset semantics
+ *          (terminal observation kept, post-reset observation returned)
+ *   lz_rollout
+ *       -> K consecutive step() calls fused in one launch (state kept in VGPRs)
+ *   lz_get_state / lz_set_state
+ *       -> attribute access env.state1 / state2 / state_master / state_slave /
+ *          lambda_coef ... used by code/lorenz_pmsm/test_evaluate.py:99-111
+ *
+ * Conventions
+ *   - Every function returns an lz_status (0 == LZ_OK).  Nothing throws across
+ *     the ABI; lz_last_error() returns a thread-local message for the last failure.
+ *   - All buffer pointers are DEVICE pointers on the handle's device (hipMalloc or
+ *     torch CUDA tensors), contiguous, row-major.  "T" below is float for
+ *     LZ_DTYPE_F32 handles and double for LZ_DTYPE_F64 handles.
+ *   - A handle is bound to one device and one HIP stream and is not re-entrant.
+ *     Calls are asynchronous on that stream; lz_sync() waits for it.
+ *   - Non-finite states are not errors: they reproduce the reference's IEEE
+ *     behaviour (overflow to inf/NaN is silently allowed there too).
+ */
+#ifndef LORENZ_ENV_H
+#define LORENZ_ENV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LZ_ABI_VERSION 1
+
+typedef enum lz_status {
+  LZ_OK = 0,
+  LZ_ERR_INVALID = 1,     /* bad argument / config */
+  LZ_ERR_UNSUPPORTED = 2, /* combination not supported (e.g. PMSM in fp64) */
+  LZ_ERR_HIP = 3,         /* HIP runtime error (message has hipGetErrorString) */
+  LZ_ERR_STATE = 4,       /* call order violated (step before the first reset) */
+  LZ_ERR_OOM = 5
+} lz_status;
+
+typedef enum lz_system {
+  LZ_SYS_LORENZ3 = 0, /* dynamic.py: 3-state Lorenz, Euler dt=0.01, additive action */
+  LZ_SYS_LORENZ4 = 1, /* lorenz_env_transient.py: 4-state master/slave, dt=0.001 */
+  LZ_SYS_PMSM = 2,    /* lorenz_env_try_pmsm.py: PMSM sync, fp32, Adam dual lambda */
+  LZ_SYS_HR = 3       /* lorenz_env_try.py: Hindmarsh-Rose master/slave, RK4 */
+} lz_system;
+
+typedef enum lz_dtype { LZ_DTYPE_F32 = 0, LZ_DTYPE_F64 = 1 } lz_dtype;
+
+/* State planes (SoA, one T or int32 element per env) addressable by
+ * lz_get_state / lz_set_state.  Reference attribute in brackets. */
+enum {
+  /* LZ_SYS_LORENZ3 [state1 = x,y,z] */
+  LZ_L3_X = 0, LZ_L3_Y = 1, LZ_L3_Z = 2, LZ_L3_STEP = 3,
+  /* LZ_SYS_LORENZ4 [state1 = master x1..x4, state2 = slave x1..x4] */
+  LZ_L4_M1 = 0, LZ_L4_S1 = 4, LZ_L4_STEP = 8,
+  /* LZ_SYS_PMSM [state1 (3), state2 (3), lambda_coef, m_t, v_t: float32;
+   *              adam_step, current_step: int32] */
+  LZ_PMSM_S1 = 0, LZ_PMSM_S2 = 3, LZ_PMSM_LAMBDA = 6, LZ_PMSM_M = 7, LZ_PMSM_V = 8,
+  LZ_PMSM_ADAM_STEP = 9, LZ_PMSM_STEP = 10,
+  /* LZ_SYS_HR [state_master (3), state_slave (3), sigma: T;
+   *            filtered_action (2): float32; step: int32] */
+  LZ_HR_M = 0, LZ_HR_S = 3, LZ_HR_SIGMA = 6, LZ_HR_FA = 7, LZ_HR_STEP = 9
+};
+
+/* done byte written per env by lz_step / lz_rollout */
+#define LZ_DONE_TERMINATED 1u /* the env's own termination condition */
+#define LZ_DONE_TRUNCATED 2u  /* max_episode_steps (gymnasium TimeLimit) or PMSM's own
+                                 current_step >= max_steps */
+
+/* lz_config.flags */
+#define LZ_FLAG_AUTORESET 1u   /* reset done envs inside lz_step (SB3 VecEnv semantics) */
+#define LZ_FLAG_ADD_NOISE 2u   /* PMSM / HR ctor kwarg add_noise */
+#define LZ_FLAG_EVAL_MODE 4u   /* HR ctor kwarg eval_mode (sigma = 2.0 on reset) */
+#define LZ_FLAG_ADD_FILTER 8u  /* HR ctor kwarg add_filter */
+
+#define LZ_MAX_PARAMS 16
+
+typedef struct lz_config {
+  int32_t system;            /* lz_system */
+  int32_t dtype;             /* lz_dtype; PMSM is float32 only (as the reference) */
+  int64_t num_envs;          /* envs owned by this handle (this rank's shard) */
+  int64_t global_env_offset; /* first global env id of the shard: keys the RNG, so
+                                trajectories do not depend on the GPU count */
+  uint64_t seed;             /* Philox key for on-device reset / noise draws */
+  int32_t device;            /* HIP device ordinal */
+  int32_t max_episode_steps; /* TimeLimit truncation; 0 = none */
+  uint32_t flags;            /* LZ_FLAG_* */
+  float alpha;               /* PMSM fractional-reward exponent (ctor kwarg alpha) */
+  /* System constants, filled with the reference values by lz_config_init:
+   *  LORENZ3: sigma, rho, beta, dt, action clip            (dynamic.py:56-58,73-75,88-90)
+   *  LORENZ4: a, b, c, dt, action clip, T_end              (lorenz_env_transient.py:270-273)
+   *  PMSM:    sigma, gamma, dt, f_max, lambda_lr, beta1, beta2, eps, err_threshold,
+   *           max_steps, term_threshold                    (lorenz_env_try_pmsm.py:12-50)
+   *  HR:      a, b, c, d, r, s, I_bias, x_rest, dt, scale, master_scale,
+   *           action_alpha, term_threshold                 (lorenz_env_try.py:32-40) */
+  double params[LZ_MAX_PARAMS];
+  /* LORENZ3/4 'done = (t == T)' on a float accumulator (dynamic.py:85-89): the host
+   * replays the accumulator; the step index where it fires (-1 = never, which is the
+   * case for the reference constants) is stored here by lz_create. Read-only. */
+  int32_t t_done_step;
+  int32_t reserved[7];
+} lz_config;
+
+typedef struct lz_info {
+  int32_t state_dim;   /* T elements of dynamical state per env */
+  int32_t action_dim;  /* actions per env (T elements) */
+  int32_t obs_dim;     /* observation T elements per env */
+  int32_t init_dim;    /* T elements per env of lz_reset's `init` vector */
+  int32_t n_planes;    /* SoA planes addressable by lz_get_state/lz_set_state */
+  int32_t bytes_per_env_step; /* algorithmic HBM bytes of one lz_step per env */
+  int32_t counts_steps;       /* 1 if the STEP plane is maintained by lz_step */
+  int32_t reserved;
+} lz_info;
+
+/* Fill *cfg with the reference defaults of `system` (dtype f32, 1 env, seed 0). */
+lz_status lz_config_init(lz_config* cfg, int32_t system);
+
+typedef struct lz_handle lz_handle;
+
+lz_status lz_create(const lz_config* cfg, lz_handle** out);
+lz_status lz_destroy(lz_handle* h);
+lz_status lz_get_info(const lz_handle* h, lz_info* info);
+lz_status lz_get_config(const lz_handle* h, lz_config* cfg);
+
+/* Bind the handle to a HIP stream (hipStream_t passed as void*; NULL = default). */
+lz_status lz_set_stream(lz_handle* h, void* hip_stream);
+lz_status lz_sync(lz_handle* h);
+
+/* Reset the envs selected by `mask` (uint8 [N], NULL = all).
+ * init: NULL -> draw initial states on device (Philox keyed by (seed, global env
+ *       id, call counter)), with the reference distributions;
+ *       else T [N, init_dim] initial states to inject (parity tests, per-env drop-in
+ *       classes replaying the reference's host RNG):
+ *         LORENZ3 [x,y,z]; LORENZ4 [master(4), slave(4)]; PMSM [state1(3), state2(3)];
+ *         HR [master(3), slave(3), sigma].
+ * obs_out: T [N, obs_dim] (rows of unselected envs untouched) or NULL. */
+lz_status lz_reset(lz_handle* h, const uint8_t* mask, const void* init, void* obs_out);
+
+/* One batched step of every env.
+ *   actions   T [N, action_dim]
+ *   noise     double [N, 3] injected process noise (PMSM: the N(0,3) draw of
+ *             lorenz_env_try_pmsm.py:80, used iff LZ_FLAG_ADD_NOISE; HR: the
+ *             N(0,sigma) draw of lorenz_env_try.py:136) or NULL = on-device Philox
+ *   obs_out   T [N, obs_dim]   (post-reset obs for envs auto-reset this step)
+ *   rew_out   T [N]
+ *   done_out  uint8 [N]        LZ_DONE_* bits
+ *   done_idx_out      int32 [N] or NULL: compact list of env indices done this step
+ *   terminal_obs_out  T [N, obs_dim] or NULL: their pre-reset observations
+ *   n_done_out        int32 [1] (device) or NULL: number of entries written
+ * Entries of the compact list are in unspecified order. */
+lz_status lz_step(lz_handle* h, const void* actions, const double* noise, void* obs_out,
+                  void* rew_out, uint8_t* done_out, int32_t* done_idx_out,
+                  void* terminal_obs_out, int32_t* n_done_out);
+
+/* K fused steps in ONE launch, state held in registers.  Time-major buffers:
+ *   actions T [K, N, action_dim]; obs_out T [K, N, obs_dim]; rew_out T [K, N];
+ *   done_out uint8 [K, N]; done_idx_out int64 [cap] (k * N + env) and
+ *   terminal_obs_out T [cap, obs_dim], cap entries at most (both NULL = skip);
+ *   n_done_out int32 [1] or NULL.  Noise is drawn on device. */
+lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out,
+                     void* rew_out, uint8_t* done_out, int64_t* done_idx_out,
+                     void* terminal_obs_out, int64_t cap, int32_t* n_done_out);
+
+/* Copy one SoA state plane (N elements, T or int32 / float32 as listed above)
+ * between the handle and a device buffer. */
+lz_status lz_get_state(lz_handle* h, int32_t plane, void* dst);
+lz_status lz_set_state(lz_handle* h, int32_t plane, const void* src);
+
+/* Element size in bytes of a plane (4 or 8), or 0 for an invalid plane. */
+int32_t lz_plane_elem_size(const lz_handle* h, int32_t plane);
+
+const char* lz_last_error(void);
+int32_t lz_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LORENZ_ENV_H */

@@ -1,0 +1,400 @@
+/*
+ * lz_oracle.c -- CPU restatement of the reference's env hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (gym-lorenz_amd/) links,
+ * loads or calls this file.  It is used by tests/ (the parity checker),
+ * __graft_entry__.smoke() (checker) and bench.py's cpu_baseline leg.
+ *
+ * Each function is a scalar loop over a batch of independent envs that follows
+ * the reference's Python/NumPy expression ORDER and DTYPE PROMOTION (numpy 2.2,
+ * NEP 50) line by line; file:line citations are relative to
+ * /root/reference/code/gym-lorenz/gym_lorenz/envs/.  Compiled with
+ * -ffp-contract=off (no FMA contraction, like NumPy's scalar ops).
+ *
+ * Pinning: tests/test_oracle_golden.py checks the fp64 (LORENZ3, LORENZ4, HR) and
+ * fp32 (PMSM) variants in mode ORC_REF BIT-EXACTLY against the tests/golden npz fixtures,
+ * which were produced by running the reference env classes themselves
+ * (tests/golden/make_golden.py).
+ *
+ * `mode` selects how x**k is evaluated, the only place where the reference's
+ * result depends on a libm implementation (glibc pow/powf, which NumPy's scalar
+ * power calls and which is not correctly rounded):
+ *   ORC_REF: glibc pow()/powf() exactly as NumPy          -> bit-exact vs golden
+ *   ORC_DEV: the device kernel's formulas (correctly rounded x*x, a double-double
+ *            x^3, and (float)pow((double)x, a) for PMSM's fractional power)
+ *            -> bit-exact vs the HIP kernel; differs from ORC_REF by <= 1 ulp in
+ *            the rare cases where glibc's pow is not correctly rounded.
+ * Layout: AoS batches, row i = env i.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#define ORC_REF 0
+#define ORC_DEV 1
+
+/* np.clip: NaN-propagating (maximum/minimum propagate NaN) */
+static inline double clipd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+static inline float clipf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+/* correctly rounded x*x*x via an error-free double-double product (device formula) */
+static inline double cube_dd(double x) {
+  double p = x * x;
+  double e = fma(x, x, -p);
+  double h = p * x;
+  double l = fma(p, x, -h) + e * x;
+  return h + l;
+}
+static inline float cube_ddf(float x) {
+  float p = x * x;
+  float e = fmaf(x, x, -p);
+  float h = p * x;
+  float l = fmaf(p, x, -h) + e * x;
+  return h + l;
+}
+
+/* =========================================================================
+ * LORENZ3 -- dynamic.py:5-115 lorenzEnv_transient (3-state, Euler, dt=0.01)
+ * p = {sigma(self.u)=10, rho(self.i)=28, beta(self.o)=8/3, dt=0.01, clip=500}
+ * ========================================================================= */
+#define L3_BODY(T, CLIP)                                                             \
+  /* dynamic.py:64-66 / :95-97 */                                                    \
+  static inline void l3_rhs_##T(const T* s, T* f, const T* p) {                     \
+    f[0] = p[0] * (s[1] - s[0]);                                                     \
+    f[1] = (p[1] * s[0] - s[1]) - s[0] * s[2];                                       \
+    f[2] = s[0] * s[1] - p[2] * s[2];                                                \
+  }                                                                                  \
+  /* reset obs: dynamic.py:60-75 (state0 - zeros) */                                 \
+  void orc_l3_reset_obs_##T(int64_t n, const T* st, T* obs, const double* pd) {      \
+    T p[5]; for (int j = 0; j < 5; ++j) p[j] = (T)pd[j];                             \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      T f[3]; l3_rhs_##T(st + 3 * i, f, p);                                          \
+      for (int j = 0; j < 3; ++j) { obs[6 * i + j] = st[3 * i + j] - (T)0;           \
+                                    obs[6 * i + 3 + j] = f[j] - (T)0; }              \
+    }                                                                                \
+  }                                                                                  \
+  /* step: dynamic.py:86-115 */                                                      \
+  void orc_l3_step_##T(int64_t n, T* st, const T* act, T* obs, T* rew,               \
+                       const double* pd) {                                           \
+    T p[5]; for (int j = 0; j < 5; ++j) p[j] = (T)pd[j];                             \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      T* s = st + 3 * i; T u[3], f[3];                                               \
+      for (int j = 0; j < 3; ++j) u[j] = CLIP(act[3 * i + j], -p[4], p[4]); /*:88-90*/\
+      l3_rhs_##T(s, f, p);                                          /* :95-97 */     \
+      for (int j = 0; j < 3; ++j) s[j] = (s[j] + f[j] * p[3]) + u[j]; /* :98-100 */  \
+      l3_rhs_##T(s, f, p);                                          /* :102-104 */   \
+      T* o = obs + 6 * i;                                                            \
+      for (int j = 0; j < 3; ++j) { o[j] = s[j] - (T)0; o[3 + j] = f[j] - (T)0; }    \
+      /* :109  -sum(abs(x) for x in now[0:3]) : python sum starts from int 0 */      \
+      rew[i] = -((((T)0 + (T)fabs(o[0])) + (T)fabs(o[1])) + (T)fabs(o[2]));          \
+    }                                                                                \
+  }
+L3_BODY(double, clipd)
+L3_BODY(float, clipf)
+
+/* =========================================================================
+ * LORENZ4 -- lorenz_env_transient.py:247-373 (4-state master/slave, dt=0.001)
+ * p = {a=10, b=8/3, c=28, dt=0.001, clip=2}; the action is clipped but never used
+ * ========================================================================= */
+#define L4_BODY(T)                                                                   \
+  /* :81-84 */                                                                       \
+  static inline void l4_rhs_##T(const T* s, T* f, const T* p) {                     \
+    f[0] = p[0] * (s[1] - s[0]) + s[3];                                              \
+    f[1] = (p[2] * s[0] - s[1]) - s[0] * s[2];                                       \
+    f[2] = s[0] * s[1] - p[1] * s[2];                                                \
+    f[3] = (-s[0]) * s[1] - p[1] * s[2];                                             \
+  }                                                                                  \
+  /* reset obs :275-300 : [m - s, f(m) - f(s)] ; st row = [master(4), slave(4)] */   \
+  void orc_l4_reset_obs_##T(int64_t n, const T* st, T* obs, const double* pd) {      \
+    T p[5]; for (int j = 0; j < 5; ++j) p[j] = (T)pd[j];                             \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      const T* m = st + 8 * i; const T* s = m + 4; T fm[4], fs[4];                   \
+      l4_rhs_##T(m, fm, p); l4_rhs_##T(s, fs, p);                                    \
+      for (int j = 0; j < 4; ++j) { obs[8 * i + j] = m[j] - s[j];                    \
+                                    obs[8 * i + 4 + j] = fm[j] - fs[j]; }            \
+    }                                                                                \
+  }                                                                                  \
+  /* step :314-373 ; done = (t == 5) [host] or reward < -1e6 */                      \
+  void orc_l4_step_##T(int64_t n, T* st, T* obs, T* rew, uint8_t* done,              \
+                       const double* pd) {                                           \
+    T p[5]; for (int j = 0; j < 5; ++j) p[j] = (T)pd[j];                             \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      T* m = st + 8 * i; T* s = m + 4; T f[4];                                       \
+      l4_rhs_##T(m, f, p);                                          /* :81-84 */     \
+      for (int j = 0; j < 4; ++j) m[j] = m[j] + f[j] * p[3];        /* :85-88 */     \
+      T fm[4]; l4_rhs_##T(m, fm, p);                                /* :91-94 */     \
+      l4_rhs_##T(s, f, p);                                          /* :102-105 */   \
+      for (int j = 0; j < 4; ++j) s[j] = s[j] + f[j] * p[3];        /* :106-109 */   \
+      T fs[4]; l4_rhs_##T(s, fs, p);                                /* :112-115 */   \
+      T* o = obs + 8 * i;                                                            \
+      for (int j = 0; j < 4; ++j) { o[j] = m[j] - s[j]; o[4 + j] = fm[j] - fs[j]; }  \
+      T r = -(((((T)0 + (T)fabs(o[0])) + (T)fabs(o[1])) + (T)fabs(o[2])) +           \
+              (T)fabs(o[3]));                                       /* :121 */       \
+      rew[i] = r;                                                                    \
+      done[i] = (r < (T)-1e6) ? 1 : 0;                              /* :127 */       \
+    }                                                                                \
+  }
+L4_BODY(double)
+L4_BODY(float)
+
+/* =========================================================================
+ * PMSM -- lorenz_env_try_pmsm.py:7-187 PMSM_Sync_Env (float32 throughout)
+ * p = {sigma=5.46, gamma=20, dt=0.001, f_max=50, lambda_lr=1e-3, beta1=.9,
+ *      beta2=.999, eps=1e-8, err_threshold=5, max_steps=2000, term=1000}
+ * ========================================================================= */
+/* :51-58 _get_derivatives. The action/noise adds follow NumPy promotion: python int
+ * 0 is weak (stays f32), a float64 noise promotes the sum to f64 before the final
+ * np.array(..., float32) rounding. */
+static inline void pmsm_rhs(const float* x, float a1, float a2, const double* nz, float sig,
+                            float gam, float* d) {
+  float t1 = (-x[0] + x[1] * x[2]) + a1;
+  float t2 = ((-x[1] - x[0] * x[2]) + gam * x[2]) + a2;
+  float t3 = sig * (x[1] - x[2]);
+  if (nz) {
+    d[0] = (float)((double)t1 + nz[0]);
+    d[1] = (float)((double)t2 + nz[1]);
+    d[2] = (float)((double)t3 + nz[2]);
+  } else {
+    d[0] = t1 + 0.0f; d[1] = t2 + 0.0f; d[2] = t3 + 0.0f;
+  }
+}
+
+/* reset obs :59-75 ; st row = [state1(3), state2(3)] */
+void orc_pmsm_reset_obs(int64_t n, const float* st, float* obs, const double* pd) {
+  float sig = (float)pd[0], gam = (float)pd[1];
+  for (int64_t i = 0; i < n; ++i) {
+    const float* s1 = st + 6 * i; const float* s2 = s1 + 3; float d1[3], d2[3];
+    pmsm_rhs(s1, 0.0f, 0.0f, NULL, sig, gam, d1);
+    pmsm_rhs(s2, 0.0f, 0.0f, NULL, sig, gam, d2);
+    for (int j = 0; j < 3; ++j) { obs[6 * i + j] = s1[j] - s2[j]; obs[6 * i + 3 + j] = d1[j] - d2[j]; }
+  }
+}
+
+/* f32 x**k as NumPy (glibc powf) or as the device */
+static inline float pmsm_pow(float x, float a, int mode) {
+  return mode == ORC_REF ? powf(x, a) : (float)pow((double)x, (double)a);
+}
+static inline float pmsm_sq(float x, int mode) { return mode == ORC_REF ? powf(x, 2.0f) : x * x; }
+
+/* (float)(1 - beta**k) : python float expression rounded to f32 when it meets an
+ * np.float32 (:130-131).  Both modes use libm pow; the device reads a host-built
+ * table of exactly these values. */
+static inline float pmsm_bias(double beta, int32_t k) { return (float)(1.0 - pow(beta, (double)k)); }
+
+/* step :76-184.  lam/m/v/adam_step persist across resets; cur_step is reset by the
+ * caller.  noise: double [n,3] (the N(0,3) draw, always consumed by the reference;
+ * used only when add_noise) or NULL. */
+void orc_pmsm_step(int64_t n, float* st, float* lam, float* mt, float* vt, int32_t* adam_step,
+                   int32_t* cur_step, const float* act, const double* noise, int add_noise,
+                   float alpha, int mode, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
+                   const double* pd) {
+  const float sig = (float)pd[0], gam = (float)pd[1], dt = (float)pd[2], fmax = (float)pd[3];
+  const float lr = (float)pd[4], b1 = (float)pd[5], b2 = (float)pd[6], eps = (float)pd[7];
+  const float thr = (float)pd[8], tterm = (float)pd[10];
+  const float c1 = (float)(1.0 - pd[5]), c2 = (float)(1.0 - pd[6]);
+  const int32_t max_steps = (int32_t)pd[9];
+  const float tiny = (float)1e-6;
+  for (int64_t i = 0; i < n; ++i) {
+    float* s1 = st + 6 * i; float* s2 = s1 + 3;
+    cur_step[i] += 1;                                                       /* :78 */
+    const double* nz = (add_noise && noise) ? noise + 3 * i : NULL;        /* :80,90 */
+    float a1 = clipf(act[2 * i], -1.0f, 1.0f) * fmax;                      /* :81-82 */
+    float a2 = clipf(act[2 * i + 1], -1.0f, 1.0f) * fmax;
+    float d1[3], d2[3];
+    pmsm_rhs(s1, 0.0f, 0.0f, NULL, sig, gam, d1);                          /* :88 */
+    pmsm_rhs(s2, a1, a2, nz, sig, gam, d2);                                /* :89-90 */
+    for (int j = 0; j < 3; ++j) { s1[j] = s1[j] + d1[j] * dt; s2[j] = s2[j] + d2[j] * dt; } /* :92-93 */
+    pmsm_rhs(s1, 0.0f, 0.0f, NULL, sig, gam, d1);                          /* :95 */
+    pmsm_rhs(s2, a1, a2, nz, sig, gam, d2);                                /* :96-97 */
+    float* o = obs + 6 * i;
+    for (int j = 0; j < 3; ++j) { o[j] = s1[j] - s2[j]; o[3 + j] = d1[j] - d2[j]; } /* :99-102 */
+    float e1 = fabsf(o[0]), e2 = fabsf(o[1]), e3 = fabsf(o[2]);            /* :105-107 */
+    float es = (e1 + e2) + e3;                                             /* :108 np.sum */
+    float grad = thr - es;                                                 /* :118 */
+    adam_step[i] += 1;                                                     /* :121 */
+    mt[i] = b1 * mt[i] + c1 * grad;                                        /* :124 */
+    vt[i] = b2 * vt[i] + c2 * pmsm_sq(grad, mode);                         /* :127 */
+    float mh = mt[i] / pmsm_bias(pd[5], adam_step[i]);                     /* :130 */
+    float vh = vt[i] / pmsm_bias(pd[6], adam_step[i]);                     /* :131 */
+    lam[i] = lam[i] - (lr * mh) / (sqrtf(vh) + eps);                      /* :135 */
+    lam[i] = clipf(lam[i], 0.0f, 0.5f);                                    /* :138 */
+    float fp = (pmsm_pow(fabsf(e1) + tiny, alpha, mode) +                  /* :158-160 */
+                pmsm_pow(fabsf(e2) + tiny, alpha, mode)) +
+               pmsm_pow(fabsf(e3) + tiny, alpha, mode);
+    float ap = lam[i] * (pmsm_sq(act[2 * i], mode) + pmsm_sq(act[2 * i + 1], mode)); /* :165 */
+    float r = ((-es) - fp) - ap;                                           /* :167 */
+    uint8_t te = 0;
+    if (es > tterm) { r = -1000.0f; te = 1; }                              /* :174-176 */
+    rew[i] = r;
+    term[i] = te;
+    trunc[i] = cur_step[i] >= max_steps ? 1 : 0;                           /* :179-180 */
+  }
+}
+
+/* =========================================================================
+ * HR -- lorenz_env_try.py:7-179 HRSyncEnv (RK4, dt=0.001)
+ * p = {a=1, b=3, c=1, d=5, r=0.006, s=4, I=3.2, x_rest=-1.6, dt=0.001,
+ *      scale=50, master_scale=20, action_alpha=0.95, term=70}
+ * ========================================================================= */
+#define HR_BODY(T, ABS, CUBE_DEV)                                                    \
+  static inline T hr_sq_##T(T x, int mode) {                                         \
+    return mode == ORC_REF ? (T)pow((double)x, 2.0) : x * x;                         \
+  }                                                                                  \
+  static inline T hr_cube_##T(T x, int mode) {                                       \
+    return mode == ORC_REF ? (T)pow((double)x, 3.0) : CUBE_DEV(x);                   \
+  }                                                                                  \
+  /* :7-12 hr_derivatives ; a1/a2 enter as f32 values promoted to T */               \
+  static inline void hr_rhs_##T(const T* x, T a1, T a2, const T* p, int mode, T* d) {\
+    T x2 = hr_sq_##T(x[0], mode), x3 = hr_cube_##T(x[0], mode);                      \
+    d[0] = (((x[1] - p[0] * x3) + p[1] * x2) - x[2]) + p[6];                         \
+    d[1] = ((p[2] - p[3] * x2) - x[1]) + a1;                                         \
+    d[2] = p[4] * (p[5] * (x[0] - p[7]) - x[2]) + a2;                                \
+  }                                                                                  \
+  static inline void hr_rk4_##T(T* x, T a1, T a2, const T* p, int mode, T h2, T h,   \
+                                T h6) {                                              \
+    T k1[3], k2[3], k3[3], k4[3], y[3];                                              \
+    hr_rhs_##T(x, a1, a2, p, mode, k1);                                /* :101 */    \
+    for (int j = 0; j < 3; ++j) y[j] = x[j] + h2 * k1[j];                            \
+    hr_rhs_##T(y, a1, a2, p, mode, k2);                                /* :102 */    \
+    for (int j = 0; j < 3; ++j) y[j] = x[j] + h2 * k2[j];                            \
+    hr_rhs_##T(y, a1, a2, p, mode, k3);                                /* :103 */    \
+    for (int j = 0; j < 3; ++j) y[j] = x[j] + h * k3[j];                             \
+    hr_rhs_##T(y, a1, a2, p, mode, k4);                                /* :104 */    \
+    for (int j = 0; j < 3; ++j)                                        /* :105 */    \
+      x[j] = x[j] + h6 * (((k1[j] + (T)2 * k2[j]) + (T)2 * k3[j]) + k4[j]);           \
+  }                                                                                  \
+  /* reset obs :70-78 (error clipped in reset, unlike step) ; row = [m(3), s(3)] */  \
+  void orc_hr_reset_obs_##T(int64_t n, const T* st, T* obs, const double* pd) {      \
+    const T sc = (T)pd[9], ms = (T)pd[10];                                           \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      const T* m = st + 6 * i; const T* s = m + 3;                                   \
+      for (int j = 0; j < 3; ++j) {                                                  \
+        obs[6 * i + j] = (T)clipd((double)((m[j] - s[j]) / sc), -1.0, 1.0);          \
+        obs[6 * i + 3 + j] = (T)clipd((double)(m[j] / ms), -1.0, 1.0);               \
+      }                                                                              \
+    }                                                                                \
+  }                                                                                  \
+  /* step :80-179. fa: float [n,2] filter memory. noise: T [n,3] = N(0, sigma) draws \
+   * (:136) or NULL. */                                                              \
+  void orc_hr_step_##T(int64_t n, T* st, float* fa, const float* act, const T* noise,\
+                       int add_noise, int add_filter, int mode, T* obs, T* rew,      \
+                       uint8_t* term, const double* pd) {                            \
+    T p[13]; for (int j = 0; j < 13; ++j) p[j] = (T)pd[j];                           \
+    /* dt/2, dt, dt/6.0 are python-float expressions (:102-105) */                   \
+    const T h2 = (T)(pd[8] / 2), h = (T)pd[8], h6 = (T)(pd[8] / 6.0);                \
+    const float fal = (float)pd[11], fa1 = (float)(1.0 - pd[11]);                    \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      T* m = st + 6 * i; T* s = m + 3;                                               \
+      float f0, f1;                                                                  \
+      if (add_filter) {                                                /* :85-86 */  \
+        f0 = fa1 * fa[2 * i] + fal * act[2 * i];                                     \
+        f1 = fa1 * fa[2 * i + 1] + fal * act[2 * i + 1];                             \
+        fa[2 * i] = f0; fa[2 * i + 1] = f1;                                          \
+      } else { f0 = act[2 * i]; f1 = act[2 * i + 1]; }                 /* :88 */     \
+      float a1 = clipf(f0, -1.0f, 1.0f) * 100.0f;                      /* :92-93 */  \
+      float a2 = clipf(f1, -1.0f, 1.0f) * 100.0f;                                    \
+      hr_rk4_##T(m, (T)0, (T)0, p, mode, h2, h, h6);                   /* :100-105 */\
+      hr_rk4_##T(s, (T)a1, (T)a2, p, mode, h2, h, h6);                 /* :108-113 */\
+      if (add_noise && noise)                                          /* :135-137 */\
+        for (int j = 0; j < 3; ++j) m[j] = m[j] + noise[3 * i + j] * p[8];           \
+      T e[3]; T* o = obs + 6 * i;                                                    \
+      for (int j = 0; j < 3; ++j) {                                    /* :150-156 */\
+        e[j] = m[j] - s[j];                                                          \
+        o[j] = e[j] / p[9];                                                          \
+        o[3 + j] = (T)clipd((double)(m[j] / p[10]), -1.0, 1.0);                      \
+      }                                                                              \
+      float q = act[2 * i] * act[2 * i] + act[2 * i + 1] * act[2 * i + 1];           \
+      float pen = 0.05f * q;                                                         \
+      T r = (-((ABS(o[0]) + ABS(o[1])) + ABS(o[2]))) - (T)pen;         /* :165 */    \
+      uint8_t te = 0;                                                                \
+      for (int j = 0; j < 3; ++j) if (ABS(e[j]) > p[12]) te = 1;       /* :174 */    \
+      if (te) r = (T)-2000.0;                                                        \
+      rew[i] = r; term[i] = te;                                                      \
+    }                                                                                \
+  }
+HR_BODY(double, fabs, cube_dd)
+HR_BODY(float, fabsf, cube_ddf)
+
+/* =========================================================================
+ * Philox4x32-10 + the device's draw conversions (for checking on-device resets)
+ * ========================================================================= */
+static inline void philox_round(uint32_t* c, const uint32_t* k) {
+  uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+  uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+  uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+  uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+  uint32_t n0 = hi1 ^ c[1] ^ k[0], n2 = hi0 ^ c[3] ^ k[1];
+  c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+}
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]}, k[2] = {key[0], key[1]};
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c, k);
+    k[0] += 0x9E3779B9u; k[1] += 0xBB67AE85u;
+  }
+  memcpy(out, c, sizeof(c));
+}
+
+/* word w of the Philox stream (gid, purpose, tick) -- same counter layout as
+ * csrc/lz_philox.h */
+static uint32_t draw_word(uint64_t seed, uint64_t gid, uint32_t purpose, uint64_t tick, int w) {
+  uint32_t ctr[4] = {(uint32_t)gid,
+                     (uint32_t)((gid >> 32) & 0xFFu) | ((uint32_t)(w >> 2) << 8) | (purpose << 24),
+                     (uint32_t)tick, (uint32_t)(tick >> 32)};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)}, out[4];
+  orc_philox4x32_10(ctr, key, out);
+  return out[w & 3];
+}
+static inline float u01f(uint32_t x) { return (float)(x >> 8) * 5.9604644775390625e-08f; }
+static inline double u01d(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * 1.1102230246251565e-16;
+}
+
+/* The on-device reset draws (purpose 1), per system / dtype:
+ * init rows as lz_reset's `init` layout.  f32: value j = lo + (hi-lo)*u24(word j);
+ * f64 (and PMSM, which the reference draws in f64 then casts): words (2j, 2j+1). */
+void orc_reset_draw(int32_t system, int32_t f64, int64_t n, int64_t gid0, uint64_t seed,
+                    uint64_t tick, int32_t hr_flags, void* out) {
+  const uint32_t RESET = 1;
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t g = (uint64_t)(gid0 + i);
+    int nv; double lo, hi;
+    switch (system) {
+      case 0: nv = 3; lo = -30; hi = 30; break;  /* dynamic.py:62 */
+      case 1: nv = 8; lo = 0; hi = 5; break;     /* lorenz_env_transient.py:277-278 */
+      case 2: nv = 6; lo = -30; hi = 30; break;  /* lorenz_env_try_pmsm.py:64-65 */
+      default: nv = 7; lo = -10; hi = 20; break; /* lorenz_env_try.py:55-57 (+sigma) */
+    }
+    for (int j = 0; j < nv; ++j) {
+      double l = lo, h = hi;
+      int hr_sigma = (system == 3 && j == 6);
+      if (hr_sigma) { l = 0; h = 2; }  /* :67 */
+      if (system == 2) {
+        double u = u01d(draw_word(seed, g, RESET, tick, 2 * j), draw_word(seed, g, RESET, tick, 2 * j + 1));
+        ((float*)out)[i * nv + j] = (float)(l + (h - l) * u);
+      } else if (f64) {
+        double u = u01d(draw_word(seed, g, RESET, tick, 2 * j), draw_word(seed, g, RESET, tick, 2 * j + 1));
+        double v = l + (h - l) * u;
+        if (hr_sigma) v = (hr_flags & 2) ? ((hr_flags & 4) ? 2.0 : v) : 0.0;
+        ((double*)out)[i * nv + j] = v;
+      } else {
+        float u = u01f(draw_word(seed, g, RESET, tick, j));
+        float v = (float)l + ((float)h - (float)l) * u;
+        if (hr_sigma) v = (hr_flags & 2) ? ((hr_flags & 4) ? 2.0f : v) : 0.0f;
+        ((float*)out)[i * nv + j] = v;
+      }
+    }
+  }
+}
+
+/* the reference's float accumulator done test 't == T' (dynamic.py:110-111,
+ * lorenz_env_transient.py:122,127): first step k at which it fires, or -1 */
+int32_t orc_t_done_step(double dt, double t_end, int32_t max_k) {
+  double t = 0.0;
+  for (int32_t k = 1; k <= max_k; ++k) {
+    t = t + dt;
+    if (t == t_end) return k;
+    if (t > t_end) return -1;
+  }
+  return -1;
+}
