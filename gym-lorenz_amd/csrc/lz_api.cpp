@@ -1,0 +1,420 @@
+// C-ABI of libgym_lorenz_amd.so: handle lifetime, validation, device buffers and
+// launch plumbing around the kernels in lz_kernels.hip.  See include/lorenz_env.h.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "lorenz_env.h"
+#include "lz_internal.h"
+
+using lz::KArgs;
+
+namespace {
+
+thread_local std::string g_err;
+
+lz_status fail(lz_status s, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+lz_status fail(lz_status s, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return s;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return fail(LZ_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+struct SysDesc {
+  int state_dim, action_dim, obs_dim, init_dim, n_planes;
+  int step_plane;
+};
+
+SysDesc describe(int system) {
+  switch (system) {
+    case LZ_SYS_LORENZ3: return {3, 3, 6, 3, 4, LZ_L3_STEP};
+    case LZ_SYS_LORENZ4: return {8, 3, 8, 8, 9, LZ_L4_STEP};
+    case LZ_SYS_PMSM: return {6, 2, 6, 6, 11, LZ_PMSM_STEP};
+    default: return {6, 2, 6, 7, 10, LZ_HR_STEP};
+  }
+}
+
+// element size of plane p (T planes, f32 planes, i32 planes)
+int plane_elem(int system, int f64, int p) {
+  const SysDesc d = describe(system);
+  if (p < 0 || p >= d.n_planes) return 0;
+  if (p == d.step_plane) return 4;
+  const int t = f64 ? 8 : 4;
+  switch (system) {
+    case LZ_SYS_PMSM: return 4;                   // float32 / int32 throughout
+    case LZ_SYS_HR: return p <= LZ_HR_SIGMA ? t : 4;  // filtered_action is float32
+    default: return t;
+  }
+}
+
+}  // namespace
+
+struct lz_handle {
+  lz_config cfg;
+  SysDesc desc;
+  int f64;
+  hipStream_t stream;
+  void* planes[lz::kMaxPlanes];
+  int32_t* counters;  // [2] compact-list cursors, ping-pong by call parity
+  uint64_t* ticks;    // [2] device-resident call counter (RNG counter), ping-pong
+  float* bc;          // PMSM bias-correction tables [2][bc_len]
+  int32_t bc_len;
+  int parity;         // which slot of counters/ticks the next launch reads
+  int count_steps;
+  int32_t max_steps;
+  bool was_reset;
+};
+
+extern "C" {
+
+int32_t lz_abi_version(void) { return LZ_ABI_VERSION; }
+
+const char* lz_last_error(void) { return g_err.c_str(); }
+
+lz_status lz_config_init(lz_config* cfg, int32_t system) {
+  if (!cfg) return fail(LZ_ERR_INVALID, "cfg is NULL");
+  std::memset(cfg, 0, sizeof *cfg);
+  cfg->system = system;
+  cfg->dtype = LZ_DTYPE_F32;
+  cfg->num_envs = 1;
+  cfg->t_done_step = -1;
+  double* p = cfg->params;
+  switch (system) {
+    case LZ_SYS_LORENZ3:  // dynamic.py:56-58 (u, i, o), :98-100 (0.01), :36-37 (+-500)
+      p[0] = 10; p[1] = 28; p[2] = 8.0 / 3; p[3] = 0.01; p[4] = 500; p[5] = 10;  // T_end :111
+      break;
+    case LZ_SYS_LORENZ4:  // lorenz_env_transient.py:270-273, :85-88 (0.001), :13-14, :127
+      p[0] = 10; p[1] = 8.0 / 3; p[2] = 28; p[3] = 0.001; p[4] = 2; p[5] = 5;
+      break;
+    case LZ_SYS_PMSM:  // lorenz_env_try_pmsm.py:12-14, :20-23, :39, :50, :113, :174
+      p[0] = 5.46; p[1] = 20.0; p[2] = 0.001; p[3] = 50; p[4] = 0.001; p[5] = 0.9;
+      p[6] = 0.999; p[7] = 1e-8; p[8] = 5.0; p[9] = 2000; p[10] = 1000;
+      cfg->alpha = 0.5f;  // :9
+      break;
+    case LZ_SYS_HR:  // lorenz_env_try.py:32-36, :40, :174
+      p[0] = 1.0; p[1] = 3.0; p[2] = 1.0; p[3] = 5.0; p[4] = 0.006; p[5] = 4.0; p[6] = 3.2;
+      p[7] = -1.6; p[8] = 0.001; p[9] = 50.0; p[10] = 20.0; p[11] = 0.95; p[12] = 70.0;
+      break;
+    default:
+      return fail(LZ_ERR_INVALID, "unknown system %d", system);
+  }
+  return LZ_OK;
+}
+
+lz_status lz_create(const lz_config* cfg_in, lz_handle** out) {
+  if (!cfg_in || !out) return fail(LZ_ERR_INVALID, "cfg/out is NULL");
+  *out = nullptr;
+  lz_config cfg = *cfg_in;
+  if (cfg.system < LZ_SYS_LORENZ3 || cfg.system > LZ_SYS_HR)
+    return fail(LZ_ERR_INVALID, "unknown system %d", cfg.system);
+  if (cfg.dtype != LZ_DTYPE_F32 && cfg.dtype != LZ_DTYPE_F64)
+    return fail(LZ_ERR_INVALID, "unknown dtype %d", cfg.dtype);
+  if (cfg.system == LZ_SYS_PMSM && cfg.dtype != LZ_DTYPE_F32)
+    return fail(LZ_ERR_UNSUPPORTED, "PMSM is float32 only (the reference computes it in float32)");
+  if (cfg.num_envs <= 0 || cfg.num_envs > (int64_t)INT32_MAX)
+    return fail(LZ_ERR_INVALID, "num_envs must be in [1, 2^31-1], got %lld", (long long)cfg.num_envs);
+  if (cfg.global_env_offset < 0 || cfg.global_env_offset + cfg.num_envs > (int64_t(1) << 40))
+    return fail(LZ_ERR_INVALID, "global env ids must lie in [0, 2^40)");
+  if (cfg.max_episode_steps < 0) return fail(LZ_ERR_INVALID, "max_episode_steps < 0");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (cfg.device < 0 || cfg.device >= ndev)
+    return fail(LZ_ERR_INVALID, "device %d out of range (%d devices)", cfg.device, ndev);
+  HIP_TRY(hipSetDevice(cfg.device));
+
+  lz_handle* h = new (std::nothrow) lz_handle();
+  if (!h) return fail(LZ_ERR_OOM, "host allocation failed");
+  std::memset(h->planes, 0, sizeof h->planes);
+  h->counters = nullptr;
+  h->bc = nullptr;
+  h->desc = describe(cfg.system);
+  h->f64 = cfg.dtype == LZ_DTYPE_F64;
+  h->stream = nullptr;
+  h->ticks = nullptr;
+  h->parity = 0;
+  h->was_reset = false;
+
+  // The reference's float accumulator 't += dt; done = t == T' (dynamic.py:110-111,
+  // lorenz_env_transient.py:122,127): replay it on the host in double, exactly as
+  // Python does, and record the step at which it fires (-1: never -- the case for the
+  // reference constants).
+  cfg.t_done_step = -1;
+  if (cfg.system == LZ_SYS_LORENZ3 || cfg.system == LZ_SYS_LORENZ4) {
+    const double dt = cfg.params[3], tend = cfg.params[5];
+    double t = 0.0;
+    for (int32_t k = 1; k <= 100000000; ++k) {
+      t = t + dt;
+      if (t == tend) { cfg.t_done_step = k; break; }
+      if (t > tend) break;
+    }
+  }
+  int32_t limit = cfg.max_episode_steps;
+  if (cfg.system == LZ_SYS_PMSM) {  // own truncation current_step >= max_steps (:179)
+    const int32_t own = (int32_t)cfg.params[9];
+    if (own > 0 && (limit == 0 || own < limit)) limit = own;
+  }
+  h->max_steps = limit;
+  h->count_steps = (limit > 0 || cfg.t_done_step >= 0) ? 1 : 0;
+  h->cfg = cfg;
+
+  const int64_t n = cfg.num_envs;
+  for (int p = 0; p < h->desc.n_planes; ++p) {
+    const int es = plane_elem(cfg.system, h->f64, p);
+    if (hipMalloc(&h->planes[p], (size_t)n * es) != hipSuccess) {
+      lz_destroy(h);
+      return fail(LZ_ERR_OOM, "hipMalloc of state plane %d (%lld x %d B) failed", p, (long long)n, es);
+    }
+    if (hipMemset(h->planes[p], 0, (size_t)n * es) != hipSuccess) {
+      lz_destroy(h);
+      return fail(LZ_ERR_HIP, "hipMemset of state plane %d failed", p);
+    }
+  }
+  if (hipMalloc(reinterpret_cast<void**>(&h->counters), 2 * sizeof(int32_t)) != hipSuccess ||
+      hipMemset(h->counters, 0, 2 * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&h->ticks), 2 * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(h->ticks, 0, 2 * sizeof(uint64_t)) != hipSuccess) {
+    lz_destroy(h);
+    return fail(LZ_ERR_OOM, "counter allocation failed");
+  }
+  h->bc_len = 0;
+  if (cfg.system == LZ_SYS_PMSM) {
+    // (float)(1 - beta**k) exactly as the reference's python-float expression
+    // (lorenz_env_try_pmsm.py:130-131): computed here with the same libm pow()
+    // CPython uses, tabulated until both saturate at 1.0f for good.
+    const double b1 = cfg.params[5], b2 = cfg.params[6];
+    std::vector<float> t1, t2;
+    int32_t k = 0, run = 0;
+    while (true) {
+      const float v1 = (float)(1.0 - std::pow(b1, (double)k));
+      const float v2 = (float)(1.0 - std::pow(b2, (double)k));
+      t1.push_back(v1);
+      t2.push_back(v2);
+      run = (v1 == 1.0f && v2 == 1.0f) ? run + 1 : 0;
+      ++k;
+      if (run >= 64 || k >= (1 << 22)) break;
+    }
+    h->bc_len = (int32_t)t1.size();
+    if (hipMalloc(reinterpret_cast<void**>(&h->bc), 2 * t1.size() * sizeof(float)) != hipSuccess) {
+      lz_destroy(h);
+      return fail(LZ_ERR_OOM, "bias table allocation failed");
+    }
+    if (hipMemcpy(h->bc, t1.data(), t1.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->bc + t1.size(), t2.data(), t2.size() * sizeof(float), hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      lz_destroy(h);
+      return fail(LZ_ERR_HIP, "bias table upload failed");
+    }
+  }
+  *out = h;
+  return LZ_OK;
+}
+
+lz_status lz_destroy(lz_handle* h) {
+  if (!h) return LZ_OK;
+  (void)hipSetDevice(h->cfg.device);
+  for (int p = 0; p < lz::kMaxPlanes; ++p)
+    if (h->planes[p]) (void)hipFree(h->planes[p]);
+  if (h->counters) (void)hipFree(h->counters);
+  if (h->ticks) (void)hipFree(h->ticks);
+  if (h->bc) (void)hipFree(h->bc);
+  delete h;
+  return LZ_OK;
+}
+
+lz_status lz_get_info(const lz_handle* h, lz_info* info) {
+  if (!h || !info) return fail(LZ_ERR_INVALID, "handle/info is NULL");
+  std::memset(info, 0, sizeof *info);
+  const SysDesc& d = h->desc;
+  info->state_dim = d.state_dim;
+  info->action_dim = d.action_dim;
+  info->obs_dim = d.obs_dim;
+  info->init_dim = d.init_dim;
+  info->n_planes = d.n_planes;
+  info->counts_steps = h->count_steps;
+  // algorithmic HBM bytes per env per lz_step (what roofline.achieved counts)
+  const int t = h->f64 ? 8 : 4;
+  int b = 0;
+  switch (h->cfg.system) {
+    case LZ_SYS_LORENZ3: b = 2 * 3 * t + 3 * 4 + 6 * t + t + 1; break;  // 65 B in f32
+    case LZ_SYS_LORENZ4: b = 2 * 8 * t + 8 * t + t + 1; break;         // 101 B in f32
+    case LZ_SYS_PMSM: b = 2 * (6 * 4 + 3 * 4 + 4) + 2 * 4 + 6 * 4 + 4 + 1; break;
+    case LZ_SYS_HR:
+      b = 2 * 6 * t + 2 * 4 + 6 * t + t + 1;
+      if (h->cfg.flags & LZ_FLAG_ADD_NOISE) b += t;
+      if (h->cfg.flags & LZ_FLAG_ADD_FILTER) b += 2 * 2 * 4;
+      break;
+  }
+  if (h->count_steps && h->cfg.system != LZ_SYS_PMSM) b += 8;
+  if (h->cfg.system == LZ_SYS_PMSM) b += 8;  // current_step in/out
+  info->bytes_per_env_step = b;
+  return LZ_OK;
+}
+
+lz_status lz_get_config(const lz_handle* h, lz_config* cfg) {
+  if (!h || !cfg) return fail(LZ_ERR_INVALID, "handle/cfg is NULL");
+  *cfg = h->cfg;
+  return LZ_OK;
+}
+
+lz_status lz_set_stream(lz_handle* h, void* stream) {
+  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  h->stream = static_cast<hipStream_t>(stream);
+  return LZ_OK;
+}
+
+lz_status lz_set_seed(lz_handle* h, uint64_t seed) {
+  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  h->cfg.seed = seed;
+  return LZ_OK;
+}
+
+lz_status lz_sync(lz_handle* h) {
+  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return LZ_OK;
+}
+
+static void fill_common(const lz_handle* h, KArgs& a) {
+  std::memset(&a, 0, sizeof a);
+  for (int p = 0; p < lz::kMaxPlanes; ++p) a.pl[p] = h->planes[p];
+  a.n = h->cfg.num_envs;
+  a.gid0 = h->cfg.global_env_offset;
+  a.seed = h->cfg.seed;
+  a.tick_in = h->ticks + h->parity;
+  a.tick_out = h->ticks + (1 - h->parity);
+  a.tick_adv = 1;
+  a.bc1 = h->bc;
+  a.bc2 = h->bc ? h->bc + h->bc_len : nullptr;
+  a.bc_len = h->bc_len;
+  a.max_steps = h->max_steps;
+  a.t_done_step = h->cfg.t_done_step;
+  a.count_steps = h->count_steps;
+  a.flags = h->cfg.flags;
+  a.alpha = h->cfg.alpha;
+  for (int j = 0; j < LZ_MAX_PARAMS; ++j) a.prm[j] = h->cfg.params[j];
+  a.counter = h->counters + h->parity;
+  a.counter_next = h->counters + (1 - h->parity);
+}
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+lz_status lz_reset(lz_handle* h, const uint8_t* mask, const void* init, void* obs_out) {
+  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  KArgs a;
+  fill_common(h, a);
+  a.mask = mask;
+  a.init = init;
+  a.obs = obs_out;
+  const int e = lz::launch_reset(h->cfg.system, h->f64, a, h->stream);
+  if (e != 0) return fail(LZ_ERR_HIP, "reset launch: %s", hipGetErrorString((hipError_t)e));
+  h->parity ^= 1;
+  h->was_reset = true;
+  return LZ_OK;
+}
+
+lz_status lz_step(lz_handle* h, const void* actions, const double* noise, void* obs_out,
+                  void* rew_out, uint8_t* done_out, int32_t* done_idx_out, void* terminal_obs_out,
+                  int32_t* n_done_out) {
+  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_step before the first lz_reset");
+  const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4;  // L4 ignores its action
+  if ((needs_act && !actions) || !obs_out || !rew_out || !done_out)
+    return fail(LZ_ERR_INVALID, "actions/obs_out/rew_out/done_out must be non-NULL");
+  if ((done_idx_out == nullptr) != (terminal_obs_out == nullptr))
+    return fail(LZ_ERR_INVALID, "done_idx_out and terminal_obs_out go together");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  KArgs a;
+  fill_common(h, a);
+  a.act = actions;
+  a.noise = noise;
+  a.obs = obs_out;
+  a.rew = rew_out;
+  a.done = done_out;
+  a.done_idx32 = done_idx_out;
+  a.term_obs = terminal_obs_out;
+  a.vec_ok = (!needs_act || aligned16(actions)) && aligned16(obs_out) && (a.n % 4 == 0);
+  const int e = lz::launch_step(h->cfg.system, h->f64, a, h->stream);
+  if (e != 0) return fail(LZ_ERR_HIP, "step launch: %s", hipGetErrorString((hipError_t)e));
+  if (n_done_out)
+    HIP_TRY(hipMemcpyAsync(n_done_out, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
+  h->parity ^= 1;
+  return LZ_OK;
+}
+
+lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out, void* rew_out,
+                     uint8_t* done_out, int64_t* done_idx_out, void* terminal_obs_out, int64_t cap,
+                     int32_t* n_done_out) {
+  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_rollout before the first lz_reset");
+  if (K <= 0) return fail(LZ_ERR_INVALID, "K must be >= 1");
+  const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4;
+  if ((needs_act && !actions) || !obs_out || !rew_out || !done_out)
+    return fail(LZ_ERR_INVALID, "actions/obs_out/rew_out/done_out must be non-NULL");
+  if ((done_idx_out == nullptr) != (terminal_obs_out == nullptr))
+    return fail(LZ_ERR_INVALID, "done_idx_out and terminal_obs_out go together");
+  if ((int64_t)K * h->cfg.num_envs > ((int64_t)1 << 40)) return fail(LZ_ERR_INVALID, "K*N too large");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  KArgs a;
+  fill_common(h, a);
+  a.act = actions;
+  a.obs = obs_out;
+  a.rew = rew_out;
+  a.done = done_out;
+  a.done_idx64 = done_idx_out;
+  a.term_obs = terminal_obs_out;
+  a.term_cap = cap;
+  a.K = K;
+  a.tick_adv = (uint64_t)K;
+  a.vec_ok = (!needs_act || aligned16(actions)) && aligned16(obs_out) && (a.n % 4 == 0);
+  const int e = lz::launch_rollout(h->cfg.system, h->f64, a, h->stream);
+  if (e != 0) return fail(LZ_ERR_HIP, "rollout launch: %s", hipGetErrorString((hipError_t)e));
+  if (n_done_out)
+    HIP_TRY(hipMemcpyAsync(n_done_out, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
+  h->parity ^= 1;
+  return LZ_OK;
+}
+
+int32_t lz_plane_elem_size(const lz_handle* h, int32_t plane) {
+  if (!h) return 0;
+  return plane_elem(h->cfg.system, h->f64, plane);
+}
+
+lz_status lz_get_state(lz_handle* h, int32_t plane, void* dst) {
+  if (!h || !dst) return fail(LZ_ERR_INVALID, "handle/dst is NULL");
+  const int es = plane_elem(h->cfg.system, h->f64, plane);
+  if (!es) return fail(LZ_ERR_INVALID, "invalid plane %d", plane);
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  HIP_TRY(hipMemcpyAsync(dst, h->planes[plane], (size_t)h->cfg.num_envs * es, hipMemcpyDeviceToDevice,
+                         h->stream));
+  return LZ_OK;
+}
+
+lz_status lz_set_state(lz_handle* h, int32_t plane, const void* src) {
+  if (!h || !src) return fail(LZ_ERR_INVALID, "handle/src is NULL");
+  const int es = plane_elem(h->cfg.system, h->f64, plane);
+  if (!es) return fail(LZ_ERR_INVALID, "invalid plane %d", plane);
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  HIP_TRY(hipMemcpyAsync(h->planes[plane], src, (size_t)h->cfg.num_envs * es, hipMemcpyDeviceToDevice,
+                         h->stream));
+  return LZ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// Counter-based RNG for on-device resets and process noise: Philox4x32-10
+// (Salmon, Moraes, Dror, Shaw, SC'11).  Stateless: every draw is a pure function of
+// (seed, global env id, purpose, call tick, word index), so a shard of the env axis
+// on any GPU reproduces exactly the draws of the same envs on one GPU.
+// Counter layout (mirrored by oracle/lz_oracle.c draw_word):
+//   c0 = gid[31:0]
+//   c1 = gid[39:32] | (word/4) << 8 | purpose << 24
+//   c2 = tick[31:0], c3 = tick[63:32];   key = seed
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lz {
+
+enum : uint32_t { kPurposeReset = 1, kPurposeNoise = 2 };
+
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Four consecutive words [4*blk, 4*blk+4) of the stream (gid, purpose, tick).
+__device__ __forceinline__ U4 philox_block(uint64_t seed, uint64_t gid, uint32_t purpose,
+                                           uint64_t tick, uint32_t blk) {
+  U4 c{(uint32_t)gid, (uint32_t)((gid >> 32) & 0xFFu) | (blk << 8) | (purpose << 24),
+       (uint32_t)tick, (uint32_t)(tick >> 32)};
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// [0,1) with 24 / 53 random bits -- exact conversions, identical on the CPU oracle.
+__device__ __forceinline__ float u01f(uint32_t x) {
+  return (float)(x >> 8) * 5.9604644775390625e-08f;
+}
+__device__ __forceinline__ double u01d(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * 1.1102230246251565e-16;
+}
+
+// Three standard normals (Box-Muller on two word pairs) for per-step process noise.
+__device__ __forceinline__ void normal3(uint64_t seed, uint64_t gid, uint64_t tick, float z[3]) {
+  const U4 w = philox_block(seed, gid, kPurposeNoise, tick, 0);
+  const float u1 = (float)((w.x >> 8) + 1u) * 5.9604644775390625e-08f;  // (0,1]
+  const float u2 = u01f(w.y);
+  const float u3 = (float)((w.z >> 8) + 1u) * 5.9604644775390625e-08f;
+  const float u4 = u01f(w.w);
+  const float r1 = sqrtf(-2.0f * logf(u1)), r2 = sqrtf(-2.0f * logf(u3));
+  float s1, c1, s2, c2;
+  sincospif(2.0f * u2, &s1, &c1);
+  sincospif(2.0f * u4, &s2, &c2);
+  z[0] = r1 * c1;
+  z[1] = r1 * s1;
+  z[2] = r2 * c2;
+}
+
+}  // namespace lz

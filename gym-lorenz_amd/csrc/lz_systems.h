@@ -1,0 +1,435 @@
+// Device models of the four reference env systems, one env per lane.
+//
+// Every arithmetic expression follows the reference's Python/NumPy evaluation
+// ORDER and dtype PROMOTION (numpy 2, NEP 50); the file is compiled with
+// -ffp-contract=off so no a*b+c is fused, and with HIP's default correctly rounded
+// f32 division / sqrt.  In fp64 (LORENZ3/4, HR) this is the reference's own
+// arithmetic, so LORENZ3/4 are bit-identical to dynamic.py / lorenz_env_transient.py.
+// References are file:line in /root/reference/code/gym-lorenz/gym_lorenz/envs/.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lz_internal.h"
+#include "lz_philox.h"
+
+namespace lz {
+
+// np.clip: NaN-propagating (np.maximum / np.minimum propagate NaN; fmaxf would not)
+template <typename T>
+__device__ __forceinline__ T clip(T x, T lo, T hi) {
+  return x < lo ? lo : (x > hi ? hi : x);
+}
+
+template <typename T>
+__device__ __forceinline__ T ld(const void* p, int64_t i) {
+  return static_cast<const T*>(p)[i];
+}
+template <typename T>
+__device__ __forceinline__ void st(void* p, int64_t i, T v) {
+  static_cast<T*>(p)[i] = v;
+}
+
+// Uniform initial-state draws (purpose RESET): value j of [lo, hi).
+//   T=float : word j, 24 bits         T=double : words (2j, 2j+1), 53 bits
+template <typename T>
+struct Draw;
+template <>
+struct Draw<float> {
+  __device__ static float u(uint64_t seed, uint64_t gid, uint64_t tick, int j) {
+    const U4 w = philox_block(seed, gid, kPurposeReset, tick, (uint32_t)(j >> 2));
+    const uint32_t x = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
+    return u01f(x);
+  }
+  __device__ static float uniform(uint64_t seed, uint64_t gid, uint64_t tick, int j, float lo,
+                                  float hi) {
+    return lo + (hi - lo) * u(seed, gid, tick, j);
+  }
+};
+template <>
+struct Draw<double> {
+  __device__ static double u(uint64_t seed, uint64_t gid, uint64_t tick, int j) {
+    const U4 w = philox_block(seed, gid, kPurposeReset, tick, (uint32_t)(j >> 1));
+    return (j & 1) ? u01d(w.z, w.w) : u01d(w.x, w.y);
+  }
+  __device__ static double uniform(uint64_t seed, uint64_t gid, uint64_t tick, int j, double lo,
+                                   double hi) {
+    return lo + (hi - lo) * u(seed, gid, tick, j);
+  }
+};
+
+// ===========================================================================
+// LORENZ3 -- dynamic.py:5-115, lorenzEnv_transient (3-state Lorenz, Euler)
+// params: sigma(self.u)=10, rho(self.i)=28, beta(self.o)=8/3, dt=0.01, clip=500
+// planes: x, y, z [, step]
+// ===========================================================================
+template <typename T>
+struct SysL3 {
+  static constexpr int A = 3, O = 6, NI = 3;
+  static constexpr bool kUsesAction = true, kNoise = false;
+  static constexpr int kStepPlane = LZ_L3_STEP;
+  T x, y, z;
+  T sg, rh, be, dt, cl;
+
+  __device__ void setup(const KArgs& a) {
+    sg = (T)a.prm[0]; rh = (T)a.prm[1]; be = (T)a.prm[2]; dt = (T)a.prm[3]; cl = (T)a.prm[4];
+  }
+  __device__ void load(const KArgs& a, int64_t i) {
+    x = ld<T>(a.pl[0], i); y = ld<T>(a.pl[1], i); z = ld<T>(a.pl[2], i);
+  }
+  __device__ void store(const KArgs& a, int64_t i) const {
+    st<T>(a.pl[0], i, x); st<T>(a.pl[1], i, y); st<T>(a.pl[2], i, z);
+  }
+  __device__ void store_reset(const KArgs& a, int64_t i) const { store(a, i); }
+  __device__ void store_autoreset_extra(const KArgs&, int64_t) const {}
+  // dynamic.py:64-66 / :95-97 / :102-104
+  __device__ void rhs(T& fx, T& fy, T& fz) const {
+    fx = sg * (y - x);
+    fy = (rh * x - y) - x * z;
+    fz = x * y - be * z;
+  }
+  __device__ static void draw(const KArgs& a, uint64_t gid, uint64_t tick, T* v) {
+    for (int j = 0; j < 3; ++j) v[j] = Draw<T>::uniform(a.seed, gid, tick, j, (T)-30, (T)30);  // :62
+  }
+  __device__ void init(const T* v, const KArgs&) { x = v[0]; y = v[1]; z = v[2]; }
+  // reset(): dynamic.py:60-75 -> state0 - zeros(6)
+  __device__ void reset_obs(T* o) const {
+    T fx, fy, fz;
+    rhs(fx, fy, fz);
+    o[0] = x - (T)0; o[1] = y - (T)0; o[2] = z - (T)0;
+    o[3] = fx - (T)0; o[4] = fy - (T)0; o[5] = fz - (T)0;
+  }
+  // step(): dynamic.py:86-115
+  // act: float32 (SB3 hands np.float32 actions; np.clip keeps f32, then promotes)
+  __device__ bool step(const float* act, bool, const double*, T* o, T& rew, const KArgs&) {
+    const T u1 = clip((T)act[0], -cl, cl), u2 = clip((T)act[1], -cl, cl),
+            u3 = clip((T)act[2], -cl, cl);
+    T fx, fy, fz;
+    rhs(fx, fy, fz);                 // :95-97, all from the old state
+    x = (x + fx * dt) + u1;          // :98
+    y = (y + fy * dt) + u2;          // :99
+    z = (z + fz * dt) + u3;          // :100
+    reset_obs(o);                    // :102-108 obs = [s', f(s')]
+    // :109 -sum(abs(x) for x in now[0:3]); python's sum starts from int 0
+    rew = -((((T)0 + fabs(o[0])) + fabs(o[1])) + fabs(o[2]));
+    return false;                    // :110-114 't == 10' handled by t_done_step
+  }
+};
+
+// ===========================================================================
+// LORENZ4 -- lorenz_env_transient.py:247-373 (4-state master/slave, Euler)
+// params: a=10, b=8/3, c=28, dt=0.001, clip=2; the action is never used (:316-318)
+// planes: master x1..x4, slave x1..x4 [, step]
+// ===========================================================================
+template <typename T>
+struct SysL4 {
+  static constexpr int A = 3, O = 8, NI = 8;
+  static constexpr bool kUsesAction = false, kNoise = false;
+  static constexpr int kStepPlane = LZ_L4_STEP;
+  T m[4], s[4];
+  T pa, pb, pc, dt;
+
+  __device__ void setup(const KArgs& a) {
+    pa = (T)a.prm[0]; pb = (T)a.prm[1]; pc = (T)a.prm[2]; dt = (T)a.prm[3];
+  }
+  __device__ void load(const KArgs& a, int64_t i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { m[j] = ld<T>(a.pl[j], i); s[j] = ld<T>(a.pl[4 + j], i); }
+  }
+  __device__ void store(const KArgs& a, int64_t i) const {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { st<T>(a.pl[j], i, m[j]); st<T>(a.pl[4 + j], i, s[j]); }
+  }
+  __device__ void store_reset(const KArgs& a, int64_t i) const { store(a, i); }
+  __device__ void store_autoreset_extra(const KArgs&, int64_t) const {}
+  // :81-84
+  __device__ void rhs(const T* v, T* f) const {
+    f[0] = pa * (v[1] - v[0]) + v[3];
+    f[1] = (pc * v[0] - v[1]) - v[0] * v[2];
+    f[2] = v[0] * v[1] - pb * v[2];
+    f[3] = (-v[0]) * v[1] - pb * v[2];
+  }
+  __device__ static void draw(const KArgs& a, uint64_t gid, uint64_t tick, T* v) {
+    for (int j = 0; j < 8; ++j) v[j] = Draw<T>::uniform(a.seed, gid, tick, j, (T)0, (T)5);  // :277-278
+  }
+  __device__ void init(const T* v, const KArgs&) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { m[j] = v[j]; s[j] = v[4 + j]; }
+  }
+  // :284-300 obs = [m - s, f(m) - f(s)]
+  __device__ void reset_obs(T* o) const {
+    T fm[4], fs[4];
+    rhs(m, fm);
+    rhs(s, fs);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o[j] = m[j] - s[j]; o[4 + j] = fm[j] - fs[j]; }
+  }
+  // :314-373
+  __device__ bool step(const float*, bool, const double*, T* o, T& rew, const KArgs&) {
+    T f[4];
+    rhs(m, f);                                              // :81-84
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m[j] = m[j] + f[j] * dt;    // :85-88
+    rhs(s, f);                                              // :102-105
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] = s[j] + f[j] * dt;    // :106-109
+    reset_obs(o);                                           // :91-94, :112-120
+    const T r = -(((((T)0 + fabs(o[0])) + fabs(o[1])) + fabs(o[2])) + fabs(o[3]));  // :121
+    rew = r;
+    return r < (T)-1e6;                                     // :127 (t == 5 never fires)
+  }
+};
+
+// ===========================================================================
+// PMSM -- lorenz_env_try_pmsm.py:7-187 PMSM_Sync_Env (float32 throughout)
+// params: sigma=5.46, gamma=20, dt=1e-3, f_max=50, lambda_lr=1e-3, beta1=.9,
+//         beta2=.999, eps=1e-8, err_threshold=5, max_steps=2000, term=1000
+// planes: state1(3), state2(3), lambda, m_t, v_t, adam_step(i32), step(i32)
+// ===========================================================================
+struct SysPMSM {
+  using T = float;
+  static constexpr int A = 2, O = 6, NI = 6;
+  static constexpr bool kUsesAction = true, kNoise = true;
+  static constexpr int kStepPlane = LZ_PMSM_STEP;
+  float s1[3], s2[3], lam, mt, vt;
+  int32_t adam;
+  float sg, gm, dt, fmax, lr, b1, b2, eps, thr, tterm, c1, c2, alpha;
+
+  __device__ void setup(const KArgs& a) {
+    sg = (float)a.prm[0]; gm = (float)a.prm[1]; dt = (float)a.prm[2]; fmax = (float)a.prm[3];
+    lr = (float)a.prm[4]; b1 = (float)a.prm[5]; b2 = (float)a.prm[6]; eps = (float)a.prm[7];
+    thr = (float)a.prm[8]; tterm = (float)a.prm[10];
+    c1 = (float)(1.0 - a.prm[5]); c2 = (float)(1.0 - a.prm[6]);   // (1 - beta) python floats
+    alpha = a.alpha;
+  }
+  __device__ void load(const KArgs& a, int64_t i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { s1[j] = ld<float>(a.pl[j], i); s2[j] = ld<float>(a.pl[3 + j], i); }
+    lam = ld<float>(a.pl[6], i); mt = ld<float>(a.pl[7], i); vt = ld<float>(a.pl[8], i);
+    adam = ld<int32_t>(a.pl[9], i);
+  }
+  __device__ void store(const KArgs& a, int64_t i) const {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { st<float>(a.pl[j], i, s1[j]); st<float>(a.pl[3 + j], i, s2[j]); }
+    st<float>(a.pl[6], i, lam); st<float>(a.pl[7], i, mt); st<float>(a.pl[8], i, vt);
+    st<int32_t>(a.pl[9], i, adam);
+  }
+  // reset(): Adam m/v/step and lambda are NOT reset (:59-75)
+  __device__ void store_reset(const KArgs& a, int64_t i) const {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { st<float>(a.pl[j], i, s1[j]); st<float>(a.pl[3 + j], i, s2[j]); }
+  }
+  __device__ void store_autoreset_extra(const KArgs&, int64_t) const {}
+  // :51-58 _get_derivatives; python int 0 stays f32, a float64 noise promotes the sum
+  // to f64 before np.array(..., float32) rounds it
+  __device__ void rhs(const float* x, float a1, float a2, bool use_nz, const double* nz,
+                      float* d) const {
+    const float t1 = (-x[0] + x[1] * x[2]) + a1;
+    const float t2 = ((-x[1] - x[0] * x[2]) + gm * x[2]) + a2;
+    const float t3 = sg * (x[1] - x[2]);
+    if (use_nz) {
+      d[0] = (float)((double)t1 + nz[0]);
+      d[1] = (float)((double)t2 + nz[1]);
+      d[2] = (float)((double)t3 + nz[2]);
+    } else {
+      d[0] = t1 + 0.0f; d[1] = t2 + 0.0f; d[2] = t3 + 0.0f;
+    }
+  }
+  __device__ static void draw(const KArgs& a, uint64_t gid, uint64_t tick, float* v) {
+    // :64-65 np_random.uniform(-30,30,3) in float64, then astype(float32)
+    for (int j = 0; j < 6; ++j) v[j] = (float)Draw<double>::uniform(a.seed, gid, tick, j, -30.0, 30.0);
+  }
+  __device__ void init(const float* v, const KArgs&) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { s1[j] = v[j]; s2[j] = v[3 + j]; }
+  }
+  __device__ void reset_obs(float* o) const {  // :66-74
+    float d1[3], d2[3];
+    rhs(s1, 0.0f, 0.0f, false, nullptr, d1);
+    rhs(s2, 0.0f, 0.0f, false, nullptr, d2);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { o[j] = s1[j] - s2[j]; o[3 + j] = d1[j] - d2[j]; }
+  }
+  // process noise N(0, 3) (:80), as np_random.normal(loc=0, scale=3) = 0 + 3*z
+  __device__ void noise_from_normals(const float* z, double* nz) const {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) nz[j] = 3.0 * (double)z[j];
+  }
+  __device__ static float bias(const float* tab, int32_t len, int32_t k) {
+    return k < len ? tab[k] : 1.0f;
+  }
+  // step(): :76-184
+  __device__ bool step(const float* act, bool use_nz, const double* nz, float* o, float& rew,
+                       const KArgs& a) {
+    const float a1 = clip(act[0], -1.0f, 1.0f) * fmax;     // :81-82
+    const float a2 = clip(act[1], -1.0f, 1.0f) * fmax;
+    float d1[3], d2[3];
+    rhs(s1, 0.0f, 0.0f, false, nullptr, d1);                      // :88
+    rhs(s2, a1, a2, use_nz, nz, d2);                               // :89-90
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { s1[j] = s1[j] + d1[j] * dt; s2[j] = s2[j] + d2[j] * dt; }  // :92-93
+    rhs(s1, 0.0f, 0.0f, false, nullptr, d1);                      // :95
+    rhs(s2, a1, a2, use_nz, nz, d2);                               // :96-97
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { o[j] = s1[j] - s2[j]; o[3 + j] = d1[j] - d2[j]; }  // :99-102
+    const float e1 = fabsf(o[0]), e2 = fabsf(o[1]), e3 = fabsf(o[2]);             // :105-107
+    const float es = (e1 + e2) + e3;                       // :108 np.sum (a0+a1)+a2
+    const float grad = thr - es;                           // :118
+    adam += 1;                                             // :121
+    mt = b1 * mt + c1 * grad;                              // :124
+    vt = b2 * vt + c2 * (grad * grad);                     // :127 (glibc powf(g,2) in ref)
+    const float mh = mt / bias(a.bc1, a.bc_len, adam);     // :130 (1-b1**k) -> f32
+    const float vh = vt / bias(a.bc2, a.bc_len, adam);     // :131
+    lam = lam - (lr * mh) / (sqrtf(vh) + eps);             // :135
+    lam = clip(lam, 0.0f, 0.5f);                           // :138
+    const double al = (double)alpha;                       // :158-160 (x + 1e-6)**alpha
+    const float tiny = 1e-6f;
+    const float fp = ((float)pow((double)(fabsf(e1) + tiny), al) +
+                      (float)pow((double)(fabsf(e2) + tiny), al)) +
+                     (float)pow((double)(fabsf(e3) + tiny), al);
+    const float ap = lam * (act[0] * act[0] + act[1] * act[1]);  // :165 raw action
+    float r = ((-es) - fp) - ap;                           // :167
+    bool te = false;
+    if (es > tterm) { r = -1000.0f; te = true; }           // :174-176
+    rew = r;
+    return te;
+  }
+};
+
+// ===========================================================================
+// HR -- lorenz_env_try.py:7-179 HRSyncEnv (Hindmarsh-Rose, RK4 dt=0.001)
+// params: a=1, b=3, c=1, d=5, r=0.006, s=4, I=3.2, x_rest=-1.6, dt=0.001,
+//         scale=50, master_scale=20, action_alpha=0.95, term=70
+// planes: master(3), slave(3), sigma (T), filtered_action(2) f32 [, step]
+// x1**2 / x1**3: correctly rounded here; the reference's glibc pow() is not always
+// (<= 1 ulp apart, see oracle/lz_oracle.c ORC_REF vs ORC_DEV).
+// ===========================================================================
+template <typename T>
+__device__ __forceinline__ T cube_cr(T x) {
+  const T p = x * x;
+  const T e = fma(x, x, -p);
+  const T h = p * x;
+  const T l = fma(p, x, -h) + e * x;
+  return h + l;
+}
+
+template <typename T>
+struct SysHR {
+  static constexpr int A = 2, O = 6, NI = 7;
+  static constexpr bool kUsesAction = true, kNoise = true;
+  static constexpr int kStepPlane = LZ_HR_STEP;
+  T m[3], s[3], sigma;
+  float fa0, fa1;
+  T pa, pb, pc, pd, pr, ps, pI, pxr, dt, h2, h6, sc, ms, tterm;
+  float falpha, f1m;
+
+  __device__ void setup(const KArgs& a) {
+    pa = (T)a.prm[0]; pb = (T)a.prm[1]; pc = (T)a.prm[2]; pd = (T)a.prm[3];
+    pr = (T)a.prm[4]; ps = (T)a.prm[5]; pI = (T)a.prm[6]; pxr = (T)a.prm[7];
+    dt = (T)a.prm[8]; h2 = (T)(a.prm[8] / 2); h6 = (T)(a.prm[8] / 6.0);   // :102-105
+    sc = (T)a.prm[9]; ms = (T)a.prm[10]; tterm = (T)a.prm[12];
+    falpha = (float)a.prm[11]; f1m = (float)(1.0 - a.prm[11]);            // :86
+  }
+  __device__ void load(const KArgs& a, int64_t i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { m[j] = ld<T>(a.pl[j], i); s[j] = ld<T>(a.pl[3 + j], i); }
+    if (a.flags & LZ_FLAG_ADD_NOISE) sigma = ld<T>(a.pl[6], i);
+    if (a.flags & LZ_FLAG_ADD_FILTER) { fa0 = ld<float>(a.pl[7], i); fa1 = ld<float>(a.pl[8], i); }
+  }
+  __device__ void store(const KArgs& a, int64_t i) const {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { st<T>(a.pl[j], i, m[j]); st<T>(a.pl[3 + j], i, s[j]); }
+    if (a.flags & LZ_FLAG_ADD_FILTER) { st<float>(a.pl[7], i, fa0); st<float>(a.pl[8], i, fa1); }
+  }
+  __device__ void store_reset(const KArgs& a, int64_t i) const {  // :55-69
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { st<T>(a.pl[j], i, m[j]); st<T>(a.pl[3 + j], i, s[j]); }
+    st<T>(a.pl[6], i, sigma);
+    st<float>(a.pl[7], i, 0.0f); st<float>(a.pl[8], i, 0.0f);
+  }
+  // fields init() sets that store() does not persist: the episode's sigma
+  __device__ void store_autoreset_extra(const KArgs& a, int64_t i) const {
+    st<T>(a.pl[6], i, sigma);
+  }
+  // :7-12 hr_derivatives
+  __device__ void rhs(const T* x, T a1, T a2, T* d) const {
+    const T x2 = x[0] * x[0], x3 = cube_cr(x[0]);
+    d[0] = (((x[1] - pa * x3) + pb * x2) - x[2]) + pI;
+    d[1] = ((pc - pd * x2) - x[1]) + a1;
+    d[2] = pr * (ps * (x[0] - pxr) - x[2]) + a2;
+  }
+  __device__ void rk4(T* x, T a1, T a2) const {  // :100-113
+    T k1[3], k2[3], k3[3], k4[3], y[3];
+    rhs(x, a1, a2, k1);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) y[j] = x[j] + h2 * k1[j];
+    rhs(y, a1, a2, k2);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) y[j] = x[j] + h2 * k2[j];
+    rhs(y, a1, a2, k3);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) y[j] = x[j] + dt * k3[j];
+    rhs(y, a1, a2, k4);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = x[j] + h6 * (((k1[j] + (T)2 * k2[j]) + (T)2 * k3[j]) + k4[j]);
+  }
+  __device__ static void draw(const KArgs& a, uint64_t gid, uint64_t tick, T* v) {
+    for (int j = 0; j < 6; ++j) v[j] = Draw<T>::uniform(a.seed, gid, tick, j, (T)-10, (T)20);  // :55-57
+    T sgm = (T)0;                                                                                  // :60-69
+    if (a.flags & LZ_FLAG_ADD_NOISE)
+      sgm = (a.flags & LZ_FLAG_EVAL_MODE) ? (T)2 : Draw<T>::uniform(a.seed, gid, tick, 6, (T)0, (T)2);
+    v[6] = sgm;
+  }
+  __device__ void init(const T* v, const KArgs&) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { m[j] = v[j]; s[j] = v[3 + j]; }
+    sigma = v[6];
+    fa0 = 0.0f; fa1 = 0.0f;
+  }
+  __device__ void reset_obs(T* o) const {  // :71-78 (error clipped in reset only)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      o[j] = clip((m[j] - s[j]) / sc, (T)-1, (T)1);
+      o[3 + j] = clip(m[j] / ms, (T)-1, (T)1);
+    }
+  }
+  __device__ void noise_from_normals(const float* z, double* nz) const {  // :136 N(0, sigma)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) nz[j] = (double)sigma * (double)z[j];
+  }
+  // step(): :80-179
+  __device__ bool step(const float* act, bool use_nz, const double* nz, T* o, T& rew,
+                       const KArgs& a) {
+    float f0 = act[0], f1 = act[1];
+    if (a.flags & LZ_FLAG_ADD_FILTER) {                    // :85-86
+      fa0 = f1m * fa0 + falpha * f0;
+      fa1 = f1m * fa1 + falpha * f1;
+      f0 = fa0; f1 = fa1;
+    }
+    const float a1 = clip(f0, -1.0f, 1.0f) * 100.0f;       // :92-93 np.float32 * 100.0
+    const float a2 = clip(f1, -1.0f, 1.0f) * 100.0f;
+    rk4(m, (T)0, (T)0);                                    // :100-105
+    rk4(s, (T)a1, (T)a2);                                  // :108-113
+    if (use_nz) {                                          // :135-137
+#pragma unroll
+      for (int j = 0; j < 3; ++j) m[j] = m[j] + (T)nz[j] * dt;
+    }
+    T e[3];
+    bool te = false;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {                          // :150-156
+      e[j] = m[j] - s[j];
+      o[j] = e[j] / sc;
+      o[3 + j] = clip(m[j] / ms, (T)-1, (T)1);
+      te = te || (fabs(e[j]) > tterm);                     // :174
+    }
+    const float q = act[0] * act[0] + act[1] * act[1];     // np.square + np.sum (f32)
+    const float pen = 0.05f * q;                           // 0.050 * f32 -> f32
+    T r = (-((fabs(o[0]) + fabs(o[1])) + fabs(o[2]))) - (T)pen;  // :165
+    if (te) r = (T)-2000.0;                                // :175-176
+    rew = r;
+    return te;
+  }
+};
+
+}  // namespace lz

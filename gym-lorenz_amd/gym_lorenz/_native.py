@@ -1,0 +1,108 @@
+"""ctypes binding of libgym_lorenz_amd.so (include/lorenz_env.h).
+
+The library is the only compute path: there is no CPU fallback.  If it is missing
+(not built) importing this module raises; if no HIP device is visible, lz_create
+fails with LZ_ERR_HIP / LZ_ERR_INVALID and LorenzEnvError is raised.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgym_lorenz_amd.so")
+
+LZ_OK, LZ_ERR_INVALID, LZ_ERR_UNSUPPORTED, LZ_ERR_HIP, LZ_ERR_STATE, LZ_ERR_OOM = range(6)
+LORENZ3, LORENZ4, PMSM, HR = range(4)
+F32, F64 = 0, 1
+FLAG_AUTORESET, FLAG_ADD_NOISE, FLAG_EVAL_MODE, FLAG_ADD_FILTER = 1, 2, 4, 8
+DONE_TERMINATED, DONE_TRUNCATED = 1, 2
+MAX_PARAMS = 16
+
+# state plane ids (lorenz_env.h)
+L3_X, L3_Y, L3_Z, L3_STEP = 0, 1, 2, 3
+L4_M1, L4_S1, L4_STEP = 0, 4, 8
+PMSM_S1, PMSM_S2, PMSM_LAMBDA, PMSM_M, PMSM_V, PMSM_ADAM_STEP, PMSM_STEP = 0, 3, 6, 7, 8, 9, 10
+HR_M, HR_S, HR_SIGMA, HR_FA, HR_STEP = 0, 3, 6, 7, 9
+
+
+class LorenzEnvError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__("lorenz_env status %d: %s" % (status, msg))
+        self.status = status
+
+
+class LzConfig(ctypes.Structure):
+    _fields_ = [
+        ("system", ctypes.c_int32),
+        ("dtype", ctypes.c_int32),
+        ("num_envs", ctypes.c_int64),
+        ("global_env_offset", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("device", ctypes.c_int32),
+        ("max_episode_steps", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("alpha", ctypes.c_float),
+        ("params", ctypes.c_double * MAX_PARAMS),
+        ("t_done_step", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 7),
+    ]
+
+
+class LzInfo(ctypes.Structure):
+    _fields_ = [
+        ("state_dim", ctypes.c_int32),
+        ("action_dim", ctypes.c_int32),
+        ("obs_dim", ctypes.c_int32),
+        ("init_dim", ctypes.c_int32),
+        ("n_planes", ctypes.c_int32),
+        ("bytes_per_env_step", ctypes.c_int32),
+        ("counts_steps", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+VP = ctypes.c_void_p
+_SIGS = {
+    "lz_config_init": (ctypes.c_int, [ctypes.POINTER(LzConfig), ctypes.c_int32]),
+    "lz_create": (ctypes.c_int, [ctypes.POINTER(LzConfig), ctypes.POINTER(VP)]),
+    "lz_destroy": (ctypes.c_int, [VP]),
+    "lz_get_info": (ctypes.c_int, [VP, ctypes.POINTER(LzInfo)]),
+    "lz_get_config": (ctypes.c_int, [VP, ctypes.POINTER(LzConfig)]),
+    "lz_set_stream": (ctypes.c_int, [VP, VP]),
+    "lz_set_seed": (ctypes.c_int, [VP, ctypes.c_uint64]),
+    "lz_sync": (ctypes.c_int, [VP]),
+    "lz_reset": (ctypes.c_int, [VP, VP, VP, VP]),
+    "lz_step": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+    "lz_rollout": (ctypes.c_int, [VP, ctypes.c_int32, VP, VP, VP, VP, VP, VP, ctypes.c_int64, VP]),
+    "lz_get_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
+    "lz_set_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
+    "lz_plane_elem_size": (ctypes.c_int32, [VP, ctypes.c_int32]),
+    "lz_last_error": (ctypes.c_char_p, []),
+    "lz_abi_version": (ctypes.c_int32, []),
+}
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        "gym_lorenz: native library %s is missing -- build it with "
+        "`make -C gym-lorenz_amd` (or __graft_entry__.build()); there is no CPU fallback"
+        % LIB_PATH)
+
+lib = ctypes.CDLL(LIB_PATH)
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+def check(status):
+    if status != LZ_OK:
+        raise LorenzEnvError(status, lib.lz_last_error().decode(errors="replace"))
+
+
+def config_init(system):
+    cfg = LzConfig()
+    check(lib.lz_config_init(ctypes.byref(cfg), system))
+    return cfg
+
+
+def exported_symbols():
+    return list(_SIGS)

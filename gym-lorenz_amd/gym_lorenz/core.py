@@ -1,0 +1,203 @@
+"""BatchedEnv: N independent envs of one system on one GPU, behind the C-ABI.
+
+This is the native batched engine every public surface sits on (the SB3 VecEnv
+adapter, the per-env drop-in classes, the multi-GPU shard).  Buffers are torch
+CUDA tensors used only as device memory; all env arithmetic runs in the HIP
+kernels of libgym_lorenz_amd.so.  There is no CPU path.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as nat
+
+SYSTEMS = {"lorenz3": nat.LORENZ3, "lorenz4": nat.LORENZ4, "pmsm": nat.PMSM, "hr": nat.HR}
+_TDTYPE = {nat.F32: torch.float32, nat.F64: torch.float64}
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class BatchedEnv:
+    """One handle = one shard of the env axis on one device and stream.
+
+    Arguments mirror the reference constructors (``add_noise``, ``eval_mode``,
+    ``add_filter``, ``alpha``) plus the batching knobs.  ``dtype`` is the state /
+    observation precision: "float64" reproduces the reference's fp64 arithmetic
+    (LORENZ3 / LORENZ4 bit-exactly), "float32" is the fast path.  PMSM is float32.
+    """
+
+    def __init__(self, system, num_envs, dtype="float32", device=None, seed=0,
+                 global_env_offset=0, max_episode_steps=0, autoreset=True, add_noise=False,
+                 eval_mode=False, add_filter=False, alpha=None, params=None, compact=True):
+        self.system = SYSTEMS[system] if isinstance(system, str) else int(system)
+        self.system_name = {v: k for k, v in SYSTEMS.items()}[self.system]
+        if not torch.cuda.is_available():
+            raise nat.LorenzEnvError(nat.LZ_ERR_HIP, "no HIP device visible: the env kernels "
+                                     "need an MI355X (no CPU fallback)")
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device if isinstance(device, int) else
+                                   torch.device(device).index or 0)
+        cfg = nat.config_init(self.system)
+        cfg.dtype = nat.F64 if np.dtype(dtype) == np.float64 else nat.F32
+        cfg.num_envs = int(num_envs)
+        cfg.global_env_offset = int(global_env_offset)
+        cfg.seed = int(seed) & ((1 << 64) - 1)
+        cfg.device = self.device.index
+        cfg.max_episode_steps = int(max_episode_steps or 0)
+        cfg.flags = ((nat.FLAG_AUTORESET if autoreset else 0) | (nat.FLAG_ADD_NOISE if add_noise else 0)
+                     | (nat.FLAG_EVAL_MODE if eval_mode else 0)
+                     | (nat.FLAG_ADD_FILTER if add_filter else 0))
+        if alpha is not None:
+            cfg.alpha = float(alpha)
+        if params:
+            for k, v in (params.items() if isinstance(params, dict) else enumerate(params)):
+                cfg.params[int(k)] = float(v)
+        h = ctypes.c_void_p()
+        nat.check(nat.lib.lz_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.stream = torch.cuda.current_stream(self.device)
+        nat.check(nat.lib.lz_set_stream(h, ctypes.c_void_p(self.stream.cuda_stream)))
+        info = nat.LzInfo()
+        nat.check(nat.lib.lz_get_info(h, ctypes.byref(info)))
+        self.info = info
+        got = nat.LzConfig()
+        nat.check(nat.lib.lz_get_config(h, ctypes.byref(got)))
+        self.config = got
+        self.num_envs = int(num_envs)
+        self.obs_dim, self.action_dim, self.init_dim = info.obs_dim, info.action_dim, info.init_dim
+        self.tdtype = _TDTYPE[cfg.dtype]
+        self.global_env_offset = int(global_env_offset)
+        n, o, dev = self.num_envs, self.obs_dim, self.device
+        es = torch.empty((), dtype=self.tdtype).element_size()
+        # obs | rew | done packed in one allocation: a single D2H copy brings a small
+        # batch's whole step result to the host (per-env drop-in classes)
+        self.packed = torch.empty((n * (o + 1) * es + n,), dtype=torch.uint8, device=dev)
+        self.obs = self.packed[: n * o * es].view(self.tdtype).view(n, o)
+        self.rew = self.packed[n * o * es: n * (o + 1) * es].view(self.tdtype)
+        self.done = self.packed[n * (o + 1) * es:]
+        self.compact = compact
+        if compact:
+            self.done_idx = torch.empty((n,), dtype=torch.int32, device=dev)
+            self.term_obs = torch.empty((n, o), dtype=self.tdtype, device=dev)
+            self.n_done_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
+        else:
+            self.done_idx = self.term_obs = self.n_done_dev = None
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            nat.lib.lz_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def bytes_per_env_step(self):
+        return self.info.bytes_per_env_step
+
+    def _check_dev(self, t, dtype, shape, name):
+        if t is None:
+            return None
+        if not isinstance(t, torch.Tensor):
+            t = torch.as_tensor(np.asarray(t), dtype=dtype)
+        if t.device != self.device or t.dtype != dtype or not t.is_contiguous():
+            t = t.to(device=self.device, dtype=dtype).contiguous()
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError("%s: expected shape %s, got %s" % (name, tuple(shape), tuple(t.shape)))
+        return t
+
+    # ------------------------------------------------------------------ API
+    def reset(self, mask=None, init=None, out=None):
+        """Reset selected envs (all if mask is None); init injects initial states
+        [N, init_dim] (see lz_reset).  Returns the obs tensor (rows of unselected
+        envs keep their previous values)."""
+        mask = self._check_dev(mask, torch.uint8, (self.num_envs,), "mask")
+        init = self._check_dev(init, self.tdtype, (self.num_envs, self.init_dim), "init")
+        out = self.obs if out is None else out
+        nat.check(nat.lib.lz_reset(self._h, _ptr(mask), _ptr(init), _ptr(out)))
+        return out
+
+    def step(self, actions, noise=None, want_n_done=True, out=None):
+        """One batched step.  actions: float32 [N, action_dim] (device or host).
+        Returns (obs, rew, done) device tensors -- by default internal buffers reused
+        by the next call; `out=(obs, rew, done)` writes into caller tensors (e.g. a
+        slot of an on-device rollout buffer) instead."""
+        a = self._check_dev(actions, torch.float32, (self.num_envs, self.action_dim), "actions")
+        nz = self._check_dev(noise, torch.float64, (self.num_envs, 3), "noise")
+        obs, rew, done = (self.obs, self.rew, self.done) if out is None else out
+        if out is not None:
+            n = self.num_envs
+            if (obs.shape != (n, self.obs_dim) or obs.dtype != self.tdtype or rew.shape != (n,)
+                    or rew.dtype != self.tdtype or done.shape != (n,) or done.dtype != torch.uint8
+                    or not (obs.is_contiguous() and rew.is_contiguous() and done.is_contiguous())
+                    or {obs.device, rew.device, done.device} != {self.device}):
+                raise ValueError("step(out=...): wrong shape / dtype / device / layout")
+        nat.check(nat.lib.lz_step(
+            self._h, _ptr(a), _ptr(nz), _ptr(obs), _ptr(rew), _ptr(done),
+            _ptr(self.done_idx), _ptr(self.term_obs),
+            _ptr(self.n_done_dev) if (self.compact and want_n_done) else None))
+        self._last_actions = a  # keep alive until the stream consumed it
+        return obs, rew, done
+
+    def done_list(self):
+        """(env indices, terminal observations) of envs done in the last step,
+        sorted by env index. Synchronises the stream."""
+        n = int(self.n_done_dev.item())
+        idx = self.done_idx[:n].long()
+        order = torch.argsort(idx)
+        return idx[order], self.term_obs[:n][order]
+
+    def rollout(self, actions, obs_out=None, rew_out=None, done_out=None, capture_terminal=0):
+        """K fused steps in one launch. actions: float32 [K, N, action_dim]."""
+        K = int(actions.shape[0])
+        a = self._check_dev(actions, torch.float32, (K, self.num_envs, self.action_dim), "actions")
+        n, o, dev = self.num_envs, self.obs_dim, self.device
+        obs = obs_out if obs_out is not None else torch.empty((K, n, o), dtype=self.tdtype, device=dev)
+        rew = rew_out if rew_out is not None else torch.empty((K, n), dtype=self.tdtype, device=dev)
+        done = done_out if done_out is not None else torch.empty((K, n), dtype=torch.uint8, device=dev)
+        didx = tobs = ndone = None
+        if capture_terminal:
+            didx = torch.empty((capture_terminal,), dtype=torch.int64, device=dev)
+            tobs = torch.empty((capture_terminal, o), dtype=self.tdtype, device=dev)
+            ndone = torch.zeros((1,), dtype=torch.int32, device=dev)
+        nat.check(nat.lib.lz_rollout(self._h, K, _ptr(a), _ptr(obs), _ptr(rew), _ptr(done),
+                                     _ptr(didx), _ptr(tobs), int(capture_terminal), _ptr(ndone)))
+        self._last_actions = a
+        if capture_terminal:
+            return obs, rew, done, (didx, tobs, ndone)
+        return obs, rew, done
+
+    def plane_dtype(self, plane):
+        es = nat.lib.lz_plane_elem_size(self._h, int(plane))
+        if es == 0:
+            raise ValueError("invalid state plane %d" % plane)
+        int_planes = {nat.LORENZ3: (nat.L3_STEP,), nat.LORENZ4: (nat.L4_STEP,),
+                      nat.PMSM: (nat.PMSM_ADAM_STEP, nat.PMSM_STEP), nat.HR: (nat.HR_STEP,)}
+        if plane in int_planes[self.system]:
+            return torch.int32
+        return torch.float64 if es == 8 else torch.float32
+
+    def get_state(self, plane):
+        t = torch.empty((self.num_envs,), dtype=self.plane_dtype(plane), device=self.device)
+        nat.check(nat.lib.lz_get_state(self._h, int(plane), _ptr(t)))
+        return t
+
+    def set_state(self, plane, values):
+        t = self._check_dev(values, self.plane_dtype(plane), (self.num_envs,), "plane")
+        nat.check(nat.lib.lz_set_state(self._h, int(plane), _ptr(t)))
+        self._last_plane = t
+
+    def set_seed(self, seed):
+        """Philox key for subsequent on-device resets and noise (VecEnv.seed)."""
+        nat.check(nat.lib.lz_set_seed(self._h, int(seed) & ((1 << 64) - 1)))
+
+    def sync(self):
+        nat.check(nat.lib.lz_sync(self._h))

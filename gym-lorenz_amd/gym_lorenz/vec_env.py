@@ -1,0 +1,214 @@
+"""LorenzVecEnv: a stable-baselines3 `VecEnv` whose N envs step in one HIP kernel.
+
+Replaces `DummyVecEnv([lambda: gymnasium.make(id, ...)] * N)` (the reference's
+callers, e.g. code/train.py:98-100, code/lorenz_pmsm/train.py:166) with the same
+step_wait contract (SB3 2.7.1 DummyVecEnv.step_wait):
+  obs float32 [N, obs_dim], rewards float32 [N], dones bool [N], infos list of N
+  dicts; a done env's info carries "terminal_observation" (its pre-reset obs) and
+  "TimeLimit.truncated" (= truncated and not terminated), and its returned obs row
+  is already the post-reset observation.
+VecNormalize / VecFrameStack / VecMonitor wrap it unchanged.  With
+return_tensors=True obs/rewards/dones stay on the GPU as torch tensors (no D2H).
+"""
+from collections.abc import Sequence
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .compat import HAVE_SB3, VecEnvBase
+from .core import BatchedEnv
+from .registry import spec_for
+
+# attribute name -> (first plane, count) per system, for get_attr / set_attr
+_STATE_ATTRS = {
+    nat.LORENZ3: {"state1": (nat.L3_X, 3)},
+    nat.LORENZ4: {"state1": (nat.L4_M1, 4), "state2": (nat.L4_S1, 4)},
+    nat.PMSM: {"state1": (nat.PMSM_S1, 3), "state2": (nat.PMSM_S2, 3),
+               "lambda_coef": (nat.PMSM_LAMBDA, 1), "m_t": (nat.PMSM_M, 1),
+               "v_t": (nat.PMSM_V, 1), "adam_step": (nat.PMSM_ADAM_STEP, 1),
+               "current_step": (nat.PMSM_STEP, 1)},
+    nat.HR: {"state_master": (nat.HR_M, 3), "state_slave": (nat.HR_S, 3),
+             "sigma": (nat.HR_SIGMA, 1), "filtered_action": (nat.HR_FA, 2)},
+}
+
+
+class LazyInfos(Sequence):
+    """List-like infos: a dict is materialised only when an env's entry is touched
+    (building N dicts per step dominates at 1M envs).  Mutations persist."""
+
+    def __init__(self, n, done_entries):
+        self._n = n
+        self._d = done_entries  # env index -> dict
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(self._n))]
+        if i < 0:
+            i += self._n
+        if not 0 <= i < self._n:
+            raise IndexError(i)
+        d = self._d.get(i)
+        if d is None:
+            d = self._d[i] = {}
+        return d
+
+    def done_indices(self):
+        return sorted(k for k, v in self._d.items() if "terminal_observation" in v)
+
+
+class LorenzVecEnv(VecEnvBase):
+    def __init__(self, env_id="lorenz_dynamic-v0", num_envs=1, device=None, dtype="float32",
+                 seed=0, max_episode_steps=None, return_tensors=False, lazy_infos=None,
+                 global_env_offset=0, backend=None, **env_kwargs):
+        spec = spec_for(env_id)
+        self.spec = spec
+        if max_episode_steps is None:
+            max_episode_steps = spec.max_episode_steps or 0
+        self.system = spec.system
+        obs_space, act_space = spec.spaces()
+        if backend is None:
+            backend = BatchedEnv(spec.system_name, num_envs, dtype=dtype, device=device, seed=seed,
+                                 global_env_offset=global_env_offset,
+                                 max_episode_steps=max_episode_steps, autoreset=True,
+                                 **env_kwargs)
+        self.backend = backend
+        self.return_tensors = return_tensors
+        self.lazy_infos = (num_envs > 1024) if lazy_infos is None else lazy_infos
+        self._actions = None
+        self._seed = seed
+        if HAVE_SB3:  # pragma: no cover - SB3 not installed in this image
+            super().__init__(num_envs, obs_space, act_space)
+        else:
+            self.num_envs = num_envs
+            self.observation_space = obs_space
+            self.action_space = act_space
+            self.render_mode = None
+            self.reset_infos = [{} for _ in range(num_envs)]
+        self.metadata = {"render_modes": []}
+
+    # ------------------------------------------------------------------ conversions
+    def _out(self, t, np_dtype):
+        if self.return_tensors:
+            return t
+        return t.detach().cpu().numpy().astype(np_dtype, copy=False)
+
+    # ------------------------------------------------------------------ VecEnv API
+    def reset(self):
+        obs = self.backend.reset()
+        self.reset_infos = [{} for _ in range(self.num_envs)] if not self.lazy_infos else \
+            LazyInfos(self.num_envs, {})
+        if self.return_tensors:
+            return obs.float() if obs.dtype != torch.float32 else obs.clone()
+        return obs.detach().cpu().numpy().astype(np.float32)
+
+    def step_async(self, actions):
+        self._actions = actions
+
+    def step_wait(self):
+        acts = self._actions
+        if not isinstance(acts, torch.Tensor):
+            acts = torch.from_numpy(np.asarray(acts, dtype=np.float32).reshape(
+                self.num_envs, -1))
+        obs, rew, done = self.backend.step(acts)
+        if self.return_tensors:
+            obs_o = obs.float() if obs.dtype != torch.float32 else obs.clone()
+            rew_o = rew.float() if rew.dtype != torch.float32 else rew.clone()
+            done_h = done.cpu().numpy()
+            dones = done.bool()
+        else:
+            obs_o = obs.detach().cpu().numpy().astype(np.float32)
+            rew_o = rew.detach().cpu().numpy().astype(np.float32)
+            done_h = done.cpu().numpy()
+            dones = done_h.astype(bool)
+        entries = {}
+        if done_h.any():
+            idx, tobs = self.backend.done_list()
+            idx = idx.cpu().numpy()
+            tobs = tobs.float() if self.return_tensors else tobs.cpu().numpy().astype(np.float32)
+            for j, i in enumerate(idx):
+                flag = int(done_h[i])
+                entries[int(i)] = {
+                    "terminal_observation": tobs[j],
+                    "TimeLimit.truncated": bool(flag & nat.DONE_TRUNCATED) and not bool(
+                        flag & nat.DONE_TERMINATED),
+                }
+        if self.lazy_infos:
+            infos = LazyInfos(self.num_envs, entries)
+        else:
+            infos = [entries.get(i, {}) for i in range(self.num_envs)]
+        return obs_o, rew_o, dones, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def close(self):
+        self.backend.close()
+
+    def seed(self, seed=None):
+        """SB3: seeds take effect at the next reset (on-device Philox key)."""
+        if seed is None:
+            seed = int(np.random.randint(0, 2 ** 31 - 1))
+        self._seed = seed
+        self.backend.set_seed(seed)
+        return [seed + i for i in range(self.num_envs)]
+
+    def _indices(self, indices):
+        if indices is None:
+            return list(range(self.num_envs))
+        if isinstance(indices, int):
+            return [indices]
+        return list(indices)
+
+    def get_attr(self, attr_name, indices=None):
+        idx = self._indices(indices)
+        attrs = _STATE_ATTRS[self.system]
+        if attr_name in attrs:
+            first, cnt = attrs[attr_name]
+            cols = [self.backend.get_state(first + j).cpu().numpy() for j in range(cnt)]
+            vals = np.stack(cols, axis=1)
+            return [vals[i] if cnt > 1 else vals[i, 0] for i in idx]
+        if attr_name in ("observation_space", "action_space", "render_mode", "metadata", "spec"):
+            return [getattr(self, attr_name) for _ in idx]
+        raise AttributeError("LorenzVecEnv: unknown env attribute %r" % attr_name)
+
+    def set_attr(self, attr_name, value, indices=None):
+        idx = self._indices(indices)
+        attrs = _STATE_ATTRS[self.system]
+        if attr_name not in attrs:
+            raise AttributeError("LorenzVecEnv: attribute %r is not settable" % attr_name)
+        first, cnt = attrs[attr_name]
+        v = np.asarray(value)
+        for j in range(cnt):
+            col = self.backend.get_state(first + j)
+            vj = v[..., j] if cnt > 1 else v
+            col[torch.as_tensor(idx, device=col.device)] = torch.as_tensor(
+                np.broadcast_to(vj, (len(idx),)).copy(), dtype=col.dtype, device=col.device)
+            self.backend.set_state(first + j, col)
+
+    def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
+        idx = self._indices(indices)
+        if method_name.startswith("get_current") or method_name.startswith("_get_current"):
+            k = method_name.rsplit("current", 1)[1]
+            comp = int(k) if k else 0
+            if self.system == nat.LORENZ4:
+                m = self.backend.get_state(nat.L4_M1 + comp).cpu().numpy()
+                s = self.backend.get_state(nat.L4_S1 + comp).cpu().numpy()
+                return [[m[i], s[i]] for i in idx]
+            if self.system == nat.LORENZ3:  # state2 is all-zero in dynamic.py
+                m = self.backend.get_state(nat.L3_X + comp).cpu().numpy()
+                return [[m[i], 0] for i in idx]
+        raise AttributeError("LorenzVecEnv: unsupported env_method %r" % method_name)
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        return [False for _ in self._indices(indices)]
+
+    def get_images(self):
+        return [None for _ in range(self.num_envs)]
+
+    def render(self, mode=None):
+        return None

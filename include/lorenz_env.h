@@ -41,6 +41,11 @@
  *     Calls are asynchronous on that stream; lz_sync() waits for it.
  *   - Non-finite states are not errors: they reproduce the reference's IEEE
  *     behaviour (overflow to inf/NaN is silently allowed there too).
+ *   - hipGraph capture: lz_reset / lz_step / lz_rollout enqueue kernels (and, for
+ *     n_done_out, one D2D copy) only -- no allocation, no host sync -- and keep their
+ *     RNG call counter and compact-list cursor in device memory (2-slot ping-pong
+ *     selected by a host-side call parity).  A captured sequence must therefore hold
+ *     an EVEN number of these calls so that every replay starts on the same slot.
  */
 #ifndef LORENZ_ENV_H
 #define LORENZ_ENV_H
@@ -146,6 +151,10 @@ lz_status lz_create(const lz_config* cfg, lz_handle** out);
 lz_status lz_destroy(lz_handle* h);
 lz_status lz_get_info(const lz_handle* h, lz_info* info);
 lz_status lz_get_config(const lz_handle* h, lz_config* cfg);
+
+/* Change the Philox key used by subsequent on-device resets / noise draws
+ * (SB3 VecEnv.seed()). */
+lz_status lz_set_seed(lz_handle* h, uint64_t seed);
 
 /* Bind the handle to a HIP stream (hipStream_t passed as void*; NULL = default). */
 lz_status lz_set_stream(lz_handle* h, void* hip_stream);

@@ -1,0 +1,117 @@
+"""The C-ABI library loads, exports every entry point include/lorenz_env.h declares,
+has the header's struct layout, fills the reference constants and rejects bad
+arguments with status codes (no GPU needed: no compute call is made)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "lorenz_env.h")
+
+
+@pytest.fixture(scope="module")
+def nat():
+    from gym_lorenz import _native
+
+    return _native
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\w[\w \*]*?\b(lz_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_every_declared_symbol_is_exported(nat):
+    names = declared_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(nat.lib, n), n
+    # and the python binding binds exactly the declared set
+    assert sorted(nat.exported_symbols()) == names
+    out = subprocess.run(["nm", "-D", "--defined-only", nat.LIB_PATH], capture_output=True,
+                         text=True).stdout
+    exported = set(re.findall(r" T (lz_\w+)", out))
+    assert set(names) <= exported
+
+
+def test_struct_layout_matches_header(nat, tmp_path):
+    """Compile a probe against the public header with gcc: sizes and offsets must
+    equal the ctypes mirror."""
+    c = tmp_path / "probe.c"
+    c.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "lorenz_env.h"\n'
+        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu\\n\", sizeof(lz_config),"
+        " offsetof(lz_config, params), offsetof(lz_config, t_done_step),"
+        " offsetof(lz_config, alpha), sizeof(lz_info), offsetof(lz_config, seed));return 0;}\n")
+    exe = tmp_path / "probe"
+    subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), str(c), "-o", str(exe)])
+    got = [int(v) for v in subprocess.check_output([str(exe)]).split()]
+    C = nat.LzConfig
+    want = [ctypes.sizeof(C), C.params.offset, C.t_done_step.offset, C.alpha.offset,
+            ctypes.sizeof(nat.LzInfo), C.seed.offset]
+    assert got == want
+
+
+def test_config_init_reference_constants(nat, orc):
+    for name, sysid in (("l3", nat.LORENZ3), ("l4", nat.LORENZ4), ("pmsm", nat.PMSM),
+                        ("hr", nat.HR)):
+        cfg = nat.config_init(sysid)
+        want = orc.PARAMS[name]
+        assert list(cfg.params)[: len(want)] == want, name
+        assert cfg.dtype == nat.F32 and cfg.num_envs == 1 and cfg.t_done_step == -1
+    assert nat.config_init(nat.PMSM).alpha == np.float32(0.5)
+
+
+def test_abi_version_and_errors(nat):
+    assert nat.lib.lz_abi_version() == 1
+    cfg = nat.LzConfig()
+    assert nat.lib.lz_config_init(ctypes.byref(cfg), 99) == nat.LZ_ERR_INVALID
+    assert b"unknown system" in nat.lib.lz_last_error()
+    h = ctypes.c_void_p()
+    cfg = nat.config_init(nat.PMSM)
+    cfg.dtype = nat.F64
+    assert nat.lib.lz_create(ctypes.byref(cfg), ctypes.byref(h)) == nat.LZ_ERR_UNSUPPORTED
+    cfg = nat.config_init(nat.LORENZ3)
+    cfg.num_envs = 0
+    assert nat.lib.lz_create(ctypes.byref(cfg), ctypes.byref(h)) == nat.LZ_ERR_INVALID
+    cfg = nat.config_init(nat.LORENZ3)
+    cfg.max_episode_steps = -1
+    assert nat.lib.lz_create(ctypes.byref(cfg), ctypes.byref(h)) == nat.LZ_ERR_INVALID
+    # NULL handles are rejected, never dereferenced
+    assert nat.lib.lz_step(None, None, None, None, None, None, None, None, None) == nat.LZ_ERR_INVALID
+    assert nat.lib.lz_reset(None, None, None, None) == nat.LZ_ERR_INVALID
+    assert nat.lib.lz_destroy(None) == nat.LZ_OK
+    assert nat.lib.lz_plane_elem_size(None, 0) == 0
+
+
+def test_no_gpu_fails_loudly(nat):
+    """Without a HIP device the product path raises -- it never falls back to CPU."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    cfg = nat.config_init(nat.LORENZ3)
+    h = ctypes.c_void_p()
+    st = nat.lib.lz_create(ctypes.byref(cfg), ctypes.byref(h))
+    assert st == nat.LZ_ERR_HIP and nat.lib.lz_last_error()
+    import gym_lorenz
+
+    with pytest.raises(nat.LorenzEnvError):
+        gym_lorenz.BatchedEnv("lorenz3", 16)
+    with pytest.raises(nat.LorenzEnvError):
+        gym_lorenz.make("lorenz_dynamic-v0")
+
+
+def test_product_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "gym-lorenz_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "import oracle" not in src and "liblz_oracle" not in src, f
+                assert "from oracle" not in src, f

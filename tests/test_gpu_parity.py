@@ -1,0 +1,400 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the golden fixtures of the
+reference and the CPU oracle.  Bars:
+  * LORENZ3 / LORENZ4 fp64: bit-exact vs the reference (golden), every step.
+  * all systems, both dtypes: bit-exact vs the oracle restatement of the device
+    formulas (oracle mode DEV), NaN-aware.
+  * PMSM vs reference: obs/state bit-exact; reward rel <= 1e-5 (glibc powf vs the
+    device's pow: the reward's x**alpha and the Adam g**2 are the only libm calls).
+  * HR fp64 vs reference: rel <= 1e-9 over 1000 RK4 steps (glibc pow(x,3)/(x,2) are
+    not correctly rounded; the device's are).
+  * LORENZ3 fp32 vs fp64 reference, teacher-forced per step: rel < 1e-5
+    (BASELINE.md per-step gate; |d| / max(|s|, 1)).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import bits_equal, golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gl():
+    import gym_lorenz
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return gym_lorenz
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _planes(be, first, count):
+    return np.stack([_np(be.get_state(first + j)) for j in range(count)], axis=1)
+
+
+# ----------------------------------------------------------------- LORENZ3
+@pytest.mark.parametrize("use_rollout", [False, True])
+def test_l3_f64_golden_bitexact(gl, use_rollout):
+    g = golden("l3")
+    n, T = g["x0"].shape[0], g["obs"].shape[1]
+    be = gl.BatchedEnv("lorenz3", n, dtype="float64", autoreset=False)
+    obs0 = _np(be.reset(init=torch.from_numpy(g["x0"])))
+    assert bits_equal(obs0, g["obs0"])
+    acts = torch.from_numpy(np.ascontiguousarray(g["actions"].transpose(1, 0, 2))).cuda()
+    if use_rollout:
+        obs, rew, done = be.rollout(acts)
+    else:
+        obs = torch.empty((T, n, 6), dtype=torch.float64, device="cuda")
+        rew = torch.empty((T, n), dtype=torch.float64, device="cuda")
+        done = torch.empty((T, n), dtype=torch.uint8, device="cuda")
+        for k in range(T):
+            o, r, d = be.step(acts[k])
+            obs[k].copy_(o)
+            rew[k].copy_(r)
+            done[k].copy_(d)
+    assert bits_equal(_np(obs).transpose(1, 0, 2), g["obs"])
+    assert bits_equal(_np(rew).T, g["reward"])
+    assert not _np(done).any()
+
+
+def test_l3_f32_bitexact_vs_oracle_ragged(gl, orc):
+    """Device Philox resets + 200 steps, N not a multiple of 256 nor of 4."""
+    n, T = 65536 + 37, 200
+    be = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=1234, autoreset=False)
+    obs0 = _np(be.reset())
+    init = orc.reset_draw("l3", np.float32, n, 0, 1234, 0)
+    assert bits_equal(_planes(be, 0, 3), init)
+    assert bits_equal(obs0, orc.l3_reset_obs(init))
+    rng = np.random.default_rng(5)
+    st = init.copy()
+    for k in range(T):
+        a = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+        if k == 3:
+            a[:100] *= 900.0  # clip path
+        o, r, _ = be.step(torch.from_numpy(a))
+        with np.errstate(all="ignore"):
+            oo, rr = orc.l3_step(st, a.astype(np.float32))
+        if k % 40 == 0 or k == T - 1:
+            assert bits_equal(_np(o), oo), k
+            assert bits_equal(_np(r), rr), k
+    assert bits_equal(_planes(be, 0, 3), st)
+
+
+def test_l3_f32_teacher_forced_vs_reference(gl):
+    """Every (env, step) pair of the fp64 golden as its own env: start from the
+    reference state rounded to f32, one f32 step, compare with the reference's
+    next state.  Gate: relative error |d|/max(|s|,1) < 1e-5."""
+    g = golden("l3")
+    s_prev = np.concatenate([g["x0"][:, None, :], g["obs"][:, :-1, :3]], axis=1)  # [n,T,3]
+    s_next = g["obs"][:, :, :3]
+    acts = g["actions"]
+    fin = np.isfinite(s_prev).all(-1) & np.isfinite(s_next).all(-1) & (np.abs(s_next) < 1e6).all(-1)
+    sp, sn, a = s_prev[fin], s_next[fin], acts[fin]
+    be = gl.BatchedEnv("lorenz3", sp.shape[0], dtype="float32", autoreset=False)
+    be.reset(init=torch.from_numpy(sp.astype(np.float32)))
+    o, r, _ = be.step(torch.from_numpy(a.astype(np.float32)))
+    got = _np(o)[:, :3].astype(np.float64)
+    rel = np.abs(got - sn) / np.maximum(np.abs(sn), 1.0)
+    assert rel.max() < 1e-5, rel.max()
+
+
+# ----------------------------------------------------------------- LORENZ4
+def test_l4_f64_golden_bitexact(gl):
+    g = golden("l4")
+    n, T = g["init"].shape[0], g["obs"].shape[1]
+    be = gl.BatchedEnv("lorenz4", n, dtype="float64", autoreset=False)
+    assert bits_equal(_np(be.reset(init=torch.from_numpy(g["init"]))), g["obs0"])
+    acts = torch.from_numpy(np.ascontiguousarray(g["actions"].transpose(1, 0, 2))).cuda()
+    obs, rew, done = be.rollout(acts)
+    assert bits_equal(_np(obs).transpose(1, 0, 2), g["obs"])
+    assert bits_equal(_np(rew).T, g["reward"])
+    assert np.array_equal(_np(done).T.astype(bool), g["done"])
+
+
+def test_l4_f32_vs_oracle(gl, orc):
+    n, T = 3000, 100
+    be = gl.BatchedEnv("lorenz4", n, dtype="float32", seed=9, autoreset=False)
+    be.reset()
+    st = orc.reset_draw("l4", np.float32, n, 0, 9, 0)
+    assert bits_equal(np.concatenate([_planes(be, 0, 4), _planes(be, 4, 4)], 1), st)
+    st = st.copy()
+    for k in range(T):
+        o, r, d = be.step(torch.zeros((n, 3)))
+        with np.errstate(all="ignore"):
+            oo, rr, dd = orc.l4_step(st)
+    assert bits_equal(_np(o), oo) and bits_equal(_np(r), rr)
+
+
+# ----------------------------------------------------------------- PMSM
+def _pmsm_case(gl, g, i):
+    T = g["obs"].shape[1]
+    be = gl.BatchedEnv("pmsm", 1, alpha=float(g["alpha"][i]), add_noise=bool(g["add_noise"][i]),
+                       autoreset=False)
+    be.reset(init=torch.from_numpy(g["init"][i, 0].reshape(1, 6)))
+    noise = torch.from_numpy(g["noise"][i]).cuda()
+    acts = torch.from_numpy(g["actions"][i]).cuda()
+    obs = torch.empty((T, 6), device="cuda")
+    rew = torch.empty((T,), device="cuda")
+    flags = torch.empty((T,), dtype=torch.uint8, device="cuda")
+    lam = torch.empty((T,), device="cuda")
+    for k in range(T):
+        if k == int(g["reset_at"]):
+            be.reset(init=torch.from_numpy(g["init"][i, 1].reshape(1, 6)))
+        o, r, d = be.step(acts[k:k + 1], noise[k:k + 1] if g["add_noise"][i] else None)
+        obs[k].copy_(o[0])
+        rew[k].copy_(r[0])
+        flags[k].copy_(d[0])
+        lam[k].copy_(be.get_state(6)[0])
+    return _np(obs), _np(rew), _np(flags), _np(lam)
+
+
+@pytest.mark.parametrize("i", range(9))
+def test_pmsm_vs_reference_and_oracle(gl, orc, i):
+    g = golden("pmsm")
+    obs, rew, flags, lam = _pmsm_case(gl, g, i)
+    # reference: state path bit-exact, reward within the powf tolerance
+    assert bits_equal(obs, g["obs"][i])
+    assert np.array_equal((flags & 1).astype(bool), g["terminated"][i])
+    assert np.array_equal((flags & 2).astype(bool), g["truncated"][i])
+    fin = np.isfinite(g["reward"][i])
+    np.testing.assert_allclose(rew[fin], g["reward"][i][fin], rtol=1e-5, atol=0)
+    # oracle DEV: everything bit-exact
+    from test_oracle_golden import _run_pmsm
+
+    ref = _run_pmsm(orc, g, i, orc.DEV)
+    assert bits_equal(rew, ref["rew"])
+    assert bits_equal(lam, ref["lam"])
+
+
+# ----------------------------------------------------------------- HR
+@pytest.mark.parametrize("i", range(8))
+def test_hr_f64_vs_reference_and_oracle(gl, orc, i):
+    g = golden("hr")
+    T = g["obs"].shape[1]
+    be = gl.BatchedEnv("hr", 1, dtype="float64", autoreset=False,
+                       add_noise=bool(g["add_noise"][i]), add_filter=bool(g["add_filter"][i]),
+                       eval_mode=bool(g["eval_mode"][i]))
+    o0 = _np(be.reset(init=torch.from_numpy(g["init"][i].reshape(1, 7))))
+    assert bits_equal(o0[0].astype(np.float32), g["obs0"][i])
+    noise = torch.from_numpy(g["noise"][i]).cuda()
+    acts = torch.from_numpy(g["actions"][i]).cuda()
+    obs = torch.empty((T, 6), dtype=torch.float64, device="cuda")
+    rew = torch.empty((T,), dtype=torch.float64, device="cuda")
+    fl = torch.empty((T,), dtype=torch.uint8, device="cuda")
+    for k in range(T):
+        o, r, d = be.step(acts[k:k + 1], noise[k:k + 1] if g["add_noise"][i] else None)
+        obs[k].copy_(o[0])
+        rew[k].copy_(r[0])
+        fl[k].copy_(d[0])
+    obs, rew, fl = _np(obs), _np(rew), _np(fl)
+    from test_oracle_golden import _run_hr
+
+    oo, rr, tt = _run_hr(orc, g, i, orc.DEV)
+    assert bits_equal(obs, oo) and bits_equal(rew, rr)
+    assert np.array_equal((fl & 1).astype(bool), tt)
+    np.testing.assert_allclose(obs.astype(np.float32), g["obs"][i], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(rew, g["reward"][i], rtol=1e-9, atol=1e-12)
+    assert np.array_equal((fl & 1).astype(bool), g["terminated"][i])
+
+
+# ----------------------------------------------------------------- RNG / resets
+@pytest.mark.parametrize("system,dtype,kw", [
+    ("lorenz3", "float64", {}), ("lorenz4", "float64", {}), ("lorenz4", "float32", {}),
+    ("pmsm", "float32", {}), ("hr", "float64", {"add_noise": True}),
+    ("hr", "float32", {"add_noise": True, "eval_mode": True}), ("hr", "float32", {})])
+def test_device_reset_draws_match_oracle(gl, orc, system, dtype, kw):
+    n = 5000
+    be = gl.BatchedEnv(system, n, dtype=dtype, seed=77, global_env_offset=123, autoreset=False, **kw)
+    be.reset()
+    want = orc.reset_draw({"lorenz3": "l3", "lorenz4": "l4", "pmsm": "pmsm", "hr": "hr"}[system],
+                          np.dtype(dtype), n, 123, 77, 0, add_noise=kw.get("add_noise", False),
+                          eval_mode=kw.get("eval_mode", False))
+    cnt = want.shape[1]
+    got = _planes(be, 0, cnt)
+    if system == "hr" and not kw.get("add_noise"):
+        want[:, 6] = 0
+    assert bits_equal(got.astype(want.dtype), want)
+
+
+def test_autoreset_compaction_truncation(gl, orc):
+    """TimeLimit truncation at step 7: every env done, compact list complete,
+    terminal obs = the oracle's pre-reset obs, returned obs = fresh reset obs."""
+    n, L = 3000, 7
+    be = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=3, max_episode_steps=L)
+    be.reset()
+    st = orc.reset_draw("l3", np.float32, n, 0, 3, 0)
+    a = np.random.default_rng(1).uniform(-1, 1, (n, 3)).astype(np.float32)
+    for k in range(L):
+        o, r, d = be.step(torch.from_numpy(a))
+        oo, _ = orc.l3_step(st, a)
+        if k < L - 1:
+            assert not _np(d).any()
+    assert (_np(d) == 2).all()
+    idx, tobs = be.done_list()
+    assert np.array_equal(_np(idx), np.arange(n))
+    assert bits_equal(_np(tobs), oo)
+    fresh = orc.reset_draw("l3", np.float32, n, 0, 3, L)  # auto-reset draws at tick L
+    assert bits_equal(_np(o), orc.l3_reset_obs(fresh))
+    assert bits_equal(_planes(be, 0, 3), fresh)
+    assert (_np(be.get_state(3)) == 0).all()
+    o, r, d = be.step(torch.from_numpy(a))
+    assert not _np(d).any()
+
+
+def test_autoreset_termination_pmsm(gl, orc):
+    """PMSM error_sum > 1000 termination with auto-reset; Adam state persists."""
+    n = 512
+    be = gl.BatchedEnv("pmsm", n, seed=5)
+    init = orc.reset_draw("pmsm", np.float32, n, 0, 5, 0)
+    init[::2, 3:] += np.array([600, -600, 600], np.float32)  # push every other slave away
+    be.reset(init=torch.from_numpy(init))
+    S = orc.PmsmState(n)
+    S.st[:] = init
+    with np.errstate(all="ignore"):
+        oo, rr, te, tr = orc.pmsm_step(S, np.zeros((n, 2), np.float32), None, False, 0.5, orc.DEV)
+    o, r, d = be.step(torch.zeros((n, 2)))
+    dd = _np(d)
+    assert te[::2].mean() > 0.9 and not te[1::2].any()
+    assert np.array_equal((dd & 1).astype(bool), te) and not (dd & 2).any()
+    assert bits_equal(_np(r), rr)
+    idx, tobs = be.done_list()
+    assert np.array_equal(_np(idx), np.nonzero(te)[0])
+    assert bits_equal(_np(tobs), oo[te])
+    fresh = orc.reset_draw("pmsm", np.float32, n, 0, 5, 1)
+    assert bits_equal(_np(o)[te], orc.pmsm_reset_obs(fresh)[te])
+    assert bits_equal(_np(o)[~te], oo[~te])
+    assert (_np(be.get_state(9)) == 1).all()  # adam_step kept counting through the reset
+    assert bits_equal(_np(be.get_state(6)), S.lam)
+
+
+def test_shard_invariance(gl):
+    """Two shards [0,n/2) and [n/2,n) reproduce one handle of n envs bit for bit."""
+    n, T = 8192, 20
+    full = gl.BatchedEnv("hr", n, dtype="float32", seed=11, add_noise=True, max_episode_steps=9)
+    parts = [gl.BatchedEnv("hr", n // 2, dtype="float32", seed=11, add_noise=True,
+                           global_env_offset=r * n // 2, max_episode_steps=9) for r in range(2)]
+    of = _np(full.reset())
+    op = np.concatenate([_np(p.reset()) for p in parts])
+    assert bits_equal(of, op)
+    a = np.random.default_rng(2).uniform(-1, 1, (T, n, 2)).astype(np.float32)
+    for k in range(T):
+        of, rf, df = [_np(x) for x in full.step(torch.from_numpy(a[k]))]
+        outs = [[_np(x) for x in p.step(torch.from_numpy(a[k][r * n // 2:(r + 1) * n // 2]))]
+                for r, p in enumerate(parts)]
+        assert bits_equal(of, np.concatenate([x[0] for x in outs]))
+        assert bits_equal(rf, np.concatenate([x[1] for x in outs]))
+        assert np.array_equal(df, np.concatenate([x[2] for x in outs]))
+
+
+@pytest.mark.parametrize("system,dtype", [("lorenz3", "float32"), ("pmsm", "float32"),
+                                          ("hr", "float64"), ("lorenz4", "float32")])
+def test_rollout_equals_steps(gl, system, dtype):
+    n, K = 1000, 33
+    kw = {"add_noise": True} if system in ("pmsm", "hr") else {}
+    a_be = gl.BatchedEnv(system, n, dtype=dtype, seed=4, max_episode_steps=10, **kw)
+    b_be = gl.BatchedEnv(system, n, dtype=dtype, seed=4, max_episode_steps=10, **kw)
+    a_be.reset()
+    b_be.reset()
+    A = torch.from_numpy(np.random.default_rng(3).uniform(-1.5, 1.5, (K, n, a_be.action_dim))
+                         .astype(np.float32)).cuda()
+    obs, rew, done, (didx, tobs, nd) = a_be.rollout(A, capture_terminal=K * n)
+    for k in range(K):
+        o, r, d = b_be.step(A[k])
+        assert bits_equal(_np(obs[k]), _np(o)), k
+        assert bits_equal(_np(rew[k]), _np(r)), k
+        assert np.array_equal(_np(done[k]), _np(d)), k
+    nd = int(nd.item())
+    assert nd == int((_np(done) != 0).sum())
+
+
+def test_l3_1m_envs_vs_oracle(gl, orc):
+    """BASELINE size: 1,048,576 envs, 30 fp32 steps, bit-exact on the whole batch."""
+    n, T = 1 << 20, 30
+    be = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=0, autoreset=False)
+    be.reset()
+    st = orc.reset_draw("l3", np.float32, n, 0, 0, 0)
+    A = np.random.default_rng(0).uniform(-1, 1, (T, n, 3)).astype(np.float32)
+    At = torch.from_numpy(A).cuda()
+    with np.errstate(all="ignore"):
+        for k in range(T):
+            o, r, _ = be.step(At[k])
+            oo, rr = orc.l3_step(st, A[k])
+    assert bits_equal(_np(o), oo) and bits_equal(_np(r), rr)
+
+
+# ----------------------------------------------------------------- drop-in classes
+def test_dropin_dynamic_reproduces_reference(gl):
+    """gym_lorenz.envs.LorenzDynamicEnv with the reference's np.random seeding gives
+    the reference's exact obs0 and trajectory (fp64)."""
+    g = golden("l3")
+    for i in (0, 5, 11):
+        np.random.seed(int(g["seeds"][i]))
+        env = gl.LorenzDynamicEnv()
+        o = env.reset()
+        assert o.dtype == np.float64 and bits_equal(o, g["obs0"][i])
+        for k in range(200):
+            o, r, d, info = env.step(g["actions"][i, k])
+            assert bits_equal(o, g["obs"][i, k]) and bits_equal(r, g["reward"][i, k])
+            assert d is False and info == {}
+        env.close()
+
+
+def test_dropin_pmsm_reproduces_reference(gl):
+    g = golden("pmsm")
+    for i in (0, 2):
+        env = gl.make("lorenz_pmsm-v0", alpha=float(g["alpha"][i]), add_noise=bool(g["add_noise"][i]))
+        o, info = env.reset(seed=int(g["seeds"][i]))
+        assert o.dtype == np.float32 and bits_equal(o, g["obs0"][i, 0])
+        for k in range(300):
+            o, r, te, tr, _ = env.step(g["actions"][i, k])
+            assert bits_equal(o, g["obs"][i, k]), k
+            assert abs(r - g["reward"][i, k]) <= 1e-5 * abs(g["reward"][i, k])
+        env.close()
+
+
+def test_dropin_hr_close_to_reference(gl):
+    g = golden("hr")
+    for i in (0, 4):
+        np.random.seed(10 + i)
+        env = gl.HRSyncEnv(add_noise=bool(g["add_noise"][i]), eval_mode=bool(g["eval_mode"][i]),
+                           add_filter=bool(g["add_filter"][i]))
+        o, _ = env.reset(seed=10 + i)
+        assert bits_equal(o, g["obs0"][i])
+        for k in range(300):
+            o, r, te, tr, _ = env.step(g["actions"][i, k])
+        np.testing.assert_allclose(o, g["obs"][i, 299], rtol=1e-6, atol=1e-7)
+        env.close()
+
+
+def test_dropin_l4_reproduces_reference(gl):
+    g = golden("l4")
+    np.random.seed(100)
+    env = gl.make("lorenz_transient-v0")
+    o = env.reset()
+    assert bits_equal(o, g["obs0"][0])
+    for k in range(100):
+        o, r, d, info = env.step(g["actions"][0, k])
+    assert bits_equal(o, g["obs"][0, 99])
+    m, s = env.unwrapped.get_current()
+    assert np.isfinite(m) and np.isfinite(s)
+    env.close()
+
+
+# ----------------------------------------------------------------- VecEnv
+def test_vecenv_sb3_contract(gl):
+    n = 4096
+    venv = gl.make_vec("lorenz_pmsm-v0", n, seed=1)
+    obs = venv.reset()
+    assert obs.shape == (n, 6) and obs.dtype == np.float32
+    a = np.zeros((n, 2), np.float32)
+    for k in range(2000):
+        obs, rew, dones, infos = venv.step(a)
+    assert obs.shape == (n, 6) and rew.dtype == np.float32 and dones.dtype == bool
+    assert dones.all()  # PMSM truncates at 2000 steps
+    i0 = infos[0]
+    assert i0["TimeLimit.truncated"] is True and i0["terminal_observation"].shape == (6,)
+    assert len(venv.get_attr("lambda_coef")) == n
+    venv.close()
