@@ -45,6 +45,7 @@ struct KArgs {
   uint32_t flags;            // LZ_FLAG_*
   int32_t vec_ok;            // act/obs base pointers 16-B aligned
   int32_t K;                 // rollout length
+  int32_t variant;           // step-kernel tuning variant (lz_config.reserved[0])
   float alpha;               // PMSM
   double prm[LZ_MAX_PARAMS];
 };

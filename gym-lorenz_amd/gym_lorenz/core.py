@@ -31,7 +31,8 @@ class BatchedEnv:
 
     def __init__(self, system, num_envs, dtype="float32", device=None, seed=0,
                  global_env_offset=0, max_episode_steps=0, autoreset=True, add_noise=False,
-                 eval_mode=False, add_filter=False, alpha=None, params=None, compact=True):
+                 eval_mode=False, add_filter=False, alpha=None, params=None, compact=True,
+                 variant=0):
         self.system = SYSTEMS[system] if isinstance(system, str) else int(system)
         self.system_name = {v: k for k, v in SYSTEMS.items()}[self.system]
         if not torch.cuda.is_available():
@@ -53,6 +54,7 @@ class BatchedEnv:
                      | (nat.FLAG_ADD_FILTER if add_filter else 0))
         if alpha is not None:
             cfg.alpha = float(alpha)
+        cfg.reserved[0] = int(variant)  # step-kernel tuning variant (A/B experiments)
         if params:
             for k, v in (params.items() if isinstance(params, dict) else enumerate(params)):
                 cfg.params[int(k)] = float(v)

@@ -1,0 +1,78 @@
+"""Interleaved A/B of lz_step kernel variants (one process, hipGraph-replayed steps,
+HIP-event timing on the launch stream).  Usage: python tools/ab_step.py [envs...]"""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gym-lorenz_amd"))
+import gym_lorenz as gl  # noqa: E402
+from gym_lorenz import _native as nat  # noqa: E402
+
+
+def make(variant, n, system="lorenz3", R=16):
+    env = gl.BatchedEnv(system, n, dtype="float32", autoreset=True, variant=variant)
+    env.reset()
+    dev = env.device
+    acts = torch.rand((R, n, env.action_dim), device=dev) * 2 - 1
+    obs = torch.empty((R, n, env.obs_dim), device=dev)
+    rew = torch.empty((R, n), device=dev)
+    done = torch.empty((R, n), dtype=torch.uint8, device=dev)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    slots = [(P(acts[r]), P(obs[r]), P(rew[r]), P(done[r])) for r in range(R)]
+    stream = torch.cuda.Stream()
+    nat.check(nat.lib.lz_set_stream(env._h, ctypes.c_void_p(stream.cuda_stream)))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(stream):
+        for k in range(4):
+            nat.check(nat.lib.lz_step(env._h, *slots[k % R][:1], None, *slots[k % R][1:],
+                                      P(env.done_idx), P(env.term_obs), None))
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=stream):
+            for k in range(32):
+                a, o, r_, d = slots[k % R]
+                nat.check(nat.lib.lz_step(env._h, a, None, o, r_, d, P(env.done_idx),
+                                          P(env.term_obs), None))
+    keep = (env, acts, obs, rew, done)
+    return g, stream, keep
+
+
+def timeit(g, stream, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        g.replay()
+        e0.record(stream)
+        for _ in range(reps):
+            g.replay()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (reps * 32)  # us per step
+
+
+def main():
+    envs = [int(x) for x in sys.argv[1:]] or [131072, 1048576, 4194304]
+    variants = [0, 1, 2, 3]
+    system = os.environ.get("AB_SYSTEM", "lorenz3")
+    res = {}
+    for n in envs:
+        runs = {v: make(v, n, system) for v in variants}
+        reps = max(4, int(2e5 / n * 4))
+        samples = {v: [] for v in variants}
+        for _ in range(7):
+            for v in variants:
+                samples[v].append(timeit(runs[v][0], runs[v][1], reps))
+        bps = runs[0][2][0].bytes_per_env_step
+        for v in variants:
+            s = sorted(samples[v])
+            med = s[len(s) // 2]
+            res["%s n=%d v=%d" % (system, n, v)] = {"us_med": med, "us_min": s[0],
+                                                    "GBps": bps * n / med / 1e3}
+        del runs
+        torch.cuda.empty_cache()
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

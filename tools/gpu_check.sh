@@ -27,6 +27,16 @@ for step in "$@"; do
     prof)
       export TMPDIR=/tmp
       run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2000 --warmup 200 --no-cpu-baseline --no-drift ;;
+    ab) run ab_step 600 python tools/ab_step.py 131072 1048576 4194304 ;;
+    ab_pmsm) AB_SYSTEM=pmsm run ab_pmsm 600 python tools/ab_step.py 262144 1048576 ;;
+    counters) run counters 120 rocprofv3 -L ;;
+    pmc)
+      export TMPDIR=/tmp
+      run pmc_f_calib 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o calib --output-format csv -- ./tools/pmc_calib
+      run pmc_w_calib 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o calib --output-format csv -- ./tools/pmc_calib
+      run pmc_f_step 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o step --output-format csv -- python bench.py --steps 256 --warmup 64 --no-cpu-baseline --no-drift --launch eager
+      run pmc_w_step 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o step --output-format csv -- python bench.py --steps 256 --warmup 64 --no-cpu-baseline --no-drift --launch eager
+      run pmc_summary 60 python tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write 1048576 gpurun_out/pmc_summary.json ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
