@@ -29,7 +29,6 @@ sys.path.insert(0, os.path.join(ROOT, "gym-lorenz_amd"))
 
 METRIC = "env-steps/sec at 1M parallel Lorenz envs, 1/2/4/8 MI355X; fp32 drift vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-KERNEL = "_ZN2lz6k_stepINS_5SysL3IfEEfLi0EEEvNS_5KArgsE"
 
 
 def parse():
@@ -46,6 +45,13 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-drift", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--system", choices=["lorenz3", "lorenz4", "pmsm", "hr"], default="lorenz3",
+                   help="lorenz3 = the BASELINE headline (dynamic.py env); pmsm = cfg4")
+    p.add_argument("--mode", choices=["step", "rollout"], default="step",
+                   help="rollout = cfg5's fused K-step on-device rollout")
+    p.add_argument("--K", type=int, default=2048, help="rollout length (--mode rollout)")
+    p.add_argument("--max-episode-steps", type=int, default=0,
+                   help="TimeLimit truncation (auto-reset inside the kernel); 0 = none")
     return p.parse_args()
 
 
@@ -121,6 +127,22 @@ def fp32_drift(gl, torch, device):
             "sample": "%d envs x %d steps, actions U(-1,1)^3" % (n, T)}
 
 
+SYSTEM_INFO = {  # system -> (reference env, mangled k_step / k_rollout names, action range)
+    "lorenz3": ("dynamic.py 3-state Lorenz env", "SysL3IfEEf", 1.0),
+    "lorenz4": ("lorenz_env_transient.py 4-state master/slave env", "SysL4IfEEf", 2.0),
+    "pmsm": ("lorenz_env_try_pmsm.py PMSM sync env (add_noise=True, alpha=0.5)", "SysPMSMEf", 1.2),
+    "hr": ("lorenz_env_try.py Hindmarsh-Rose RK4 env", "SysHRIfEEf", 1.2),
+}
+
+
+def kernel_name(system, mode, n):
+    tag = SYSTEM_INFO[system][1]
+    pre = "_ZN2lz6k_stepINS_%s%sLi0EEEvNS_5KArgsE"
+    if mode == "rollout":  # one-wave workgroups below 2 x 256-lane groups per CU
+        pre = "_ZN2lz9k_rolloutINS_%%s%%sLi%dEEEvNS_5KArgsE" % (64 if n < 2 * 256 * 256 else 256)
+    return pre % ("7" if system == "pmsm" else "5", tag)
+
+
 def main():
     args = parse()
     import torch
@@ -129,14 +151,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus %d needs torch.distributed.run with %d processes"
-                             % (args.gpus, args.gpus))
+    if world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus %d needs torch.distributed.run with %d processes"
+                         % (args.gpus, args.gpus))
+    # LZ_BENCH_BACKEND=gloo + ranks sharing a GPU: rehearsal of the multi-rank path on a
+    # 1-GPU box (the driver's 8-GPU runs use the default: RCCL, one GPU per rank)
+    backend = os.environ.get("LZ_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     import gym_lorenz as gl
     from gym_lorenz import _native as nat
@@ -149,55 +177,69 @@ def main():
         n = args.envs
         total = n * world
         start = rank * n
-    env = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=0, global_env_offset=start,
-                        autoreset=True, device=local)
-    R = args.ring
+    kw = {"add_noise": True, "alpha": 0.5} if args.system == "pmsm" else {}
+    env = gl.BatchedEnv(args.system, n, dtype="float32", seed=0, global_env_offset=start,
+                        autoreset=True, device=local, max_episode_steps=args.max_episode_steps,
+                        **kw)
+    A, O = env.action_dim, env.obs_dim
+    arange = SYSTEM_INFO[args.system][2]
+    rollout = args.mode == "rollout"
+    R = args.ring if not rollout else 1
+    T = args.K if rollout else 1
     g = torch.Generator(device=device).manual_seed(1000 + rank)
-    acts = torch.rand((R, n, 3), generator=g, device=device) * 2 - 1
-    obs = torch.empty((R, n, 6), device=device)
-    rew = torch.empty((R, n), device=device)
-    done = torch.empty((R, n), dtype=torch.uint8, device=device)
+    acts = (torch.rand((R, T, n, A), generator=g, device=device) * 2 - 1) * arange
+    obs = torch.empty((R, T, n, O), device=device)
+    rew = torch.empty((R, T, n), device=device)
+    done = torch.empty((R, T, n), dtype=torch.uint8, device=device)
     env.reset()
 
     h = env._h
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     slots = [(P(acts[r]), P(obs[r]), P(rew[r]), P(done[r])) for r in range(R)]
     didx, tobs = P(env.done_idx), P(env.term_obs)
-    lz_step = nat.lib.lz_step
+    lz_step, lz_rollout = nat.lib.lz_step, nat.lib.lz_rollout
 
     def one(k):
         a, o, r_, d = slots[k % R]
-        st = lz_step(h, a, None, o, r_, d, didx, tobs, None)
+        if rollout:
+            st = lz_rollout(h, T, a, o, r_, d, None, None, 0, None)
+        else:
+            st = lz_step(h, a, None, o, r_, d, didx, tobs, None)
         if st:
             nat.check(st)
 
     stream = torch.cuda.Stream(device)
     graph = None
     L = max(2, args.graph_len - args.graph_len % 2)  # even: keeps the ping-pong parity
-    if L % R and R % L:
+    if R > 1 and L % R and R % L:
         L = R
+    launches = args.steps if not rollout else max(2, args.steps // T)
+    warm = args.warmup if not rollout else 2
+    if rollout:
+        L = 2
     with torch.cuda.stream(stream):
         nat.check(nat.lib.lz_set_stream(h, ctypes.c_void_p(stream.cuda_stream)))
-        for k in range(max(args.warmup, 2)):
+        for k in range(max(warm, 2)):
             one(k)
-        if args.launch == "graph":
+        if args.launch == "graph" and not rollout:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=stream):
                 for k in range(L):
                     one(k)
         torch.cuda.synchronize(device)
 
-        def run(nsteps):
+        def run(nlaunch):
             if graph is None:
-                for k in range(nsteps):
+                for k in range(nlaunch):
                     one(k)
-                return nsteps
-            reps = max(1, nsteps // L)
+                return nlaunch
+            reps = max(1, nlaunch // L)
             for _ in range(reps):
                 graph.replay()
             return reps * L
 
-        run(max(args.warmup, L))  # warm the graph path too
+        if not rollout:
+            run(max(warm, L))  # warm the graph path too
         torch.cuda.synchronize(device)
         if world > 1:
             dist.barrier()
@@ -206,12 +248,13 @@ def main():
         ev1 = torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
-        K = run(args.steps)
+        nl = run(launches)
         ev1.record(stream)
         torch.cuda.synchronize(device)
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
+    K = nl * T  # env steps per env in the timed region
     elapsed = t1 - t0
     ev_ms = ev0.elapsed_time(ev1)
     if world > 1:
@@ -219,47 +262,60 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, ev_ms = float(t[0]), float(t[1])
 
-    bytes_step = env.bytes_per_env_step  # 65 B/env-step (12 state in, 12 out, 12 act, 24 obs, 4 rew, 1 done)
-    launch_s = ev_ms / 1e3 / K
-    achieved = bytes_step * n / launch_s / 1e9
+    info = env.info
+    if rollout:  # state planes once per launch, per-step I/O every step
+        bytes_step = info.bytes_per_env_step - info.state_io_bytes + info.state_io_bytes / T
+    else:
+        bytes_step = info.bytes_per_env_step  # LORENZ3 f32: 65 B (24 state + 12 act + 29 out)
+    launch_s = ev_ms / 1e3 / nl
+    achieved = bytes_step * n * T / launch_s / 1e9
+    ref_env = SYSTEM_INFO[args.system][0]
+    if rollout:
+        workload = ("%s: %d-step fused on-device rollout (lz_rollout, fp32, state in VGPRs), "
+                    "%d envs total, %d per GPU, time-major [K,N,.] rollout buffers"
+                    % (ref_env, T, total, n))
+    else:
+        workload = ("%s step (lz_step, fp32), %d envs total, %d per GPU, actions/obs/reward/"
+                    "done in a %d-slot on-device rollout ring" % (ref_env, total, n, R))
     out = {
         "metric": METRIC,
         "value": total * K / elapsed,
         "unit": "env-steps/s",
         "n_gpus": world,
         "steps": K,
-        "warmup": args.warmup,
+        "warmup": warm,
         "ms_per_step": elapsed * 1e3 / K,
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: x0 ~ U(-30,30)^3 on-device Philox keyed by global env id; "
-                "actions ~ U(-1,1)^3 f32 pre-generated on device",
+        "data": "synthetic: initial states from on-device Philox keyed by global env id "
+                "(reference distributions); actions ~ U(-%g,%g) f32 pre-generated on device"
+                % (arange, arange),
         "config": {
-            "workload": "dynamic.py 3-state Lorenz env step (lz_step, LORENZ3 fp32), "
-                        "%d envs total, %d per GPU, actions/obs/reward/done in a %d-slot "
-                        "on-device rollout ring" % (total, n, R),
-            "system": "lorenz3", "envs_total": total, "envs_per_gpu": n,
+            "workload": workload, "system": args.system, "envs_total": total,
+            "envs_per_gpu": n, "mode": args.mode,
             "parallelism": "env shard x%d (contiguous global ids, no collective on step)" % world,
-            "launch": "hipGraph of %d lz_step launches" % L if graph is not None else "eager",
+            "launch": ("hipGraph of %d lz_step launches" % L) if graph is not None else
+                      ("%d-step lz_rollout launches" % T if rollout else "eager"),
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": KERNEL, "avg_launch_us": launch_s * 1e6,
+            "kernel": kernel_name(args.system, args.mode, n), "avg_launch_us": launch_s * 1e6,
             "bytes_per_env_step": bytes_step,
-            "note": "achieved = algorithmic bytes per launch (bytes_per_env_step x envs_per_gpu) "
-                    "/ HIP-event average launch time on the launch stream",
+            "note": "achieved = algorithmic bytes per launch (bytes_per_env_step x envs_per_gpu"
+                    " x steps per launch) / HIP-event average launch time on the launch stream",
         },
     }
-    traffic = load_traffic(n)
+    traffic = load_traffic(out["roofline"]["kernel"], n)
     if traffic is not None:
         out["roofline"]["traffic"] = traffic["bytes_per_launch"]
         out["roofline"]["traffic_source"] = traffic["source"]
-    if rank == 0 and world == 1 and not args.no_drift:
+    headline = args.system == "lorenz3" and not rollout
+    if rank == 0 and world == 1 and headline and not args.no_drift:
         out["fp32_drift"] = fp32_drift(gl, torch, device)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and headline and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     env.close()
     if world > 1:
@@ -269,7 +325,7 @@ def main():
         print(json.dumps(out), flush=True)
 
 
-def load_traffic(n):
+def load_traffic(kernel, n):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload
     (profiles/<round>/*pmc_summary.json, written by tools/pmc_summary.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950-calibrated), if one matches
@@ -282,7 +338,7 @@ def load_traffic(n):
             d = json.load(open(f))
         except Exception:  # noqa: BLE001
             continue
-        if d.get("kernel") == KERNEL and d.get("envs_per_gpu") == n:
+        if d.get("kernel") == kernel and d.get("envs_per_gpu") == n:
             return {"bytes_per_launch": d["hbm_bytes_per_launch"],
                     "source": os.path.relpath(f, ROOT)}
     return None

@@ -247,21 +247,25 @@ lz_status lz_get_info(const lz_handle* h, lz_info* info) {
   info->init_dim = d.init_dim;
   info->n_planes = d.n_planes;
   info->counts_steps = h->count_steps;
-  // algorithmic HBM bytes per env per lz_step (what roofline.achieved counts)
+  // algorithmic HBM bytes per env per lz_step (what roofline.achieved counts):
+  // sio = state planes read + written, io = actions + obs + reward + done
   const int t = h->f64 ? 8 : 4;
-  int b = 0;
+  int sio = 0, io = 0;
   switch (h->cfg.system) {
-    case LZ_SYS_LORENZ3: b = 2 * 3 * t + 3 * 4 + 6 * t + t + 1; break;  // 65 B in f32
-    case LZ_SYS_LORENZ4: b = 2 * 8 * t + 8 * t + t + 1; break;         // 101 B in f32
-    case LZ_SYS_PMSM: b = 2 * (6 * 4 + 3 * 4 + 4) + 2 * 4 + 6 * 4 + 4 + 1; break;
+    case LZ_SYS_LORENZ3: sio = 2 * 3 * t; io = 3 * 4 + 6 * t + t + 1; break;  // 24 + 41 (f32)
+    case LZ_SYS_LORENZ4: sio = 2 * 8 * t; io = 8 * t + t + 1; break;          // 64 + 37, no act
+    case LZ_SYS_PMSM:  // s1,s2 + lambda,m,v + adam_step + current_step
+      sio = 2 * (6 * 4 + 3 * 4 + 4 + 4); io = 2 * 4 + 6 * 4 + 4 + 1; break;   // 88 + 37
     case LZ_SYS_HR:
-      b = 2 * 6 * t + 2 * 4 + 6 * t + t + 1;
-      if (h->cfg.flags & LZ_FLAG_ADD_NOISE) b += t;
-      if (h->cfg.flags & LZ_FLAG_ADD_FILTER) b += 2 * 2 * 4;
+      sio = 2 * 6 * t;
+      if (h->cfg.flags & LZ_FLAG_ADD_NOISE) sio += t;        // sigma read
+      if (h->cfg.flags & LZ_FLAG_ADD_FILTER) sio += 2 * 2 * 4;  // filtered_action
+      io = 2 * 4 + 6 * t + t + 1;
       break;
   }
-  if (h->count_steps && h->cfg.system != LZ_SYS_PMSM) b += 8;
-  if (h->cfg.system == LZ_SYS_PMSM) b += 8;  // current_step in/out
+  if (h->count_steps && h->cfg.system != LZ_SYS_PMSM) sio += 8;
+  const int b = sio + io;
+  info->state_io_bytes = sio;
   info->bytes_per_env_step = b;
   return LZ_OK;
 }
@@ -351,7 +355,9 @@ lz_status lz_step(lz_handle* h, const void* actions, const double* noise, void* 
   a.done = done_out;
   a.done_idx32 = done_idx_out;
   a.term_obs = terminal_obs_out;
-  a.vec_ok = (!needs_act || aligned16(actions)) && aligned16(obs_out) && (a.n % 4 == 0);
+  // full 256-env blocks start at 256*A*4 / 256*O*sizeof(T) byte offsets: only the
+  // base pointers need 16-B alignment (ragged tail blocks take the scalar path)
+  a.vec_ok = (!needs_act || aligned16(actions)) && aligned16(obs_out);
   const int e = lz::launch_step(h->cfg.system, h->f64, a, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "step launch: %s", hipGetErrorString((hipError_t)e));
   if (n_done_out)

@@ -14,6 +14,8 @@
 // See lz_systems.h for the per-system arithmetic and its reference citations.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "lz_internal.h"
 #include "lz_systems.h"
 
@@ -38,33 +40,46 @@ __device__ __forceinline__ void gstore(V* p, V v) {
 
 // ------------------------------------------------------------------ LDS staging
 // Copy the block's [nb, W] slice of a row-major T tensor into LDS (row = env).
-template <bool NT, typename T, int W>
+template <bool NT, typename T, int W, int B = kBlock>
 __device__ __forceinline__ void stage_in(T* __restrict__ lds, const T* __restrict__ g, int nb,
                                          int tid, bool vec) {
-  constexpr int kElems = kBlock * W;
-  if (vec && nb == kBlock) {
+  constexpr int kElems = B * W;
+  if (vec && nb == B) {
     constexpr int kVec = kElems * (int)sizeof(T) / 16;
     const f4v* __restrict__ gv = reinterpret_cast<const f4v*>(g);
     f4v* lv = reinterpret_cast<f4v*>(lds);
 #pragma unroll
-    for (int v = tid; v < kVec; v += kBlock) lv[v] = gload<NT>(gv + v);
+    for (int v = tid; v < kVec; v += B) lv[v] = gload<NT>(gv + v);
   } else {
-    for (int e = tid; e < nb * W; e += kBlock) lds[e] = gload<NT>(g + e);
+    for (int e = tid; e < nb * W; e += B) lds[e] = gload<NT>(g + e);
   }
 }
 
-template <bool NT, typename T, int W>
+template <bool NT, typename T, int W, int B = kBlock>
 __device__ __forceinline__ void stage_out(T* __restrict__ g, const T* __restrict__ lds, int nb,
                                           int tid, bool vec) {
-  constexpr int kElems = kBlock * W;
-  if (vec && nb == kBlock) {
+  constexpr int kElems = B * W;
+  if (vec && nb == B) {
     constexpr int kVec = kElems * (int)sizeof(T) / 16;
     f4v* __restrict__ gv = reinterpret_cast<f4v*>(g);
     const f4v* lv = reinterpret_cast<const f4v*>(lds);
 #pragma unroll
-    for (int v = tid; v < kVec; v += kBlock) gstore<NT>(gv + v, lv[v]);
+    for (int v = tid; v < kVec; v += B) gstore<NT>(gv + v, lv[v]);
   } else {
-    for (int e = tid; e < nb * W; e += kBlock) gstore<NT>(g + e, lds[e]);
+    for (int e = tid; e < nb * W; e += B) gstore<NT>(g + e, lds[e]);
+  }
+}
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also drains vmcnt, i.e.
+// waits until every global STORE of the wave has been acknowledged; the staging here
+// only needs this wave's LDS ops complete (lgkmcnt(0)) before the s_barrier, so the
+// obs / reward / state stores stay in flight across it.
+template <bool kFull>
+__device__ __forceinline__ void wg_barrier() {
+  if constexpr (kFull) {
+    __syncthreads();
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 }
 
@@ -82,10 +97,10 @@ __device__ __forceinline__ int32_t wave_compact(bool flag, int32_t* counter) {
   return flag ? base + (int32_t)__popcll(lt) : -1;
 }
 
-template <class Sys, typename T>
+template <class Sys, typename T, bool kInjectable>
 __device__ __forceinline__ void make_noise(const Sys& sys, const KArgs& a, int64_t i, uint64_t tick,
                                            double* nz) {
-  if (a.noise) {
+  if (kInjectable && a.noise) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) nz[j] = a.noise[3 * i + j];
   } else {
@@ -137,7 +152,7 @@ __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KAr
     bool use_nz = false;
     if constexpr (Sys::kNoise) {
       if (a.flags & LZ_FLAG_ADD_NOISE) {
-        make_noise<Sys, T>(sys, a, i, tick, nz);
+        make_noise<Sys, T, !kRollout>(sys, a, i, tick, nz);
         use_nz = true;
       }
     }
@@ -181,12 +196,14 @@ __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KAr
 // ------------------------------------------------------------------ step
 // V (tuning variant, lz_config.reserved[0], default 0): bit 0 = plain (temporal)
 // act/obs/rew/done accesses instead of non-temporal, bit 1 = lanes access their own
-// act/obs rows directly instead of LDS staging.  Measured at 1M envs (profiles/r01):
-// non-temporal I/O is 13% faster than plain, LDS staging 7-11% faster than direct.
+// act/obs rows directly instead of LDS staging, bit 2 = __syncthreads() instead of the
+// LDS-only barrier.  Measured at 1M envs (profiles/r01): non-temporal I/O is 13%
+// faster than plain, LDS staging 7-11% faster than direct.
 template <class Sys, typename T, int V>
 __global__ __launch_bounds__(kBlock) void k_step(KArgs a) {
   constexpr bool NT = (V & 1) == 0;
   constexpr bool kLds = (V & 2) == 0;
+  constexpr bool kFullBar = (V & 4) != 0;
   __shared__ __attribute__((aligned(16))) float s_act[kLds ? kBlock * Sys::A : 4];
   __shared__ __attribute__((aligned(16))) T s_obs[kLds ? kBlock * Sys::O : 2];
   const int tid = (int)threadIdx.x;
@@ -212,7 +229,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KArgs a) {
     const float* ga = static_cast<const float*>(a.act);
     if constexpr (kLds) {
       stage_in<NT, float, Sys::A>(s_act, ga + base * Sys::A, nb, tid, vec);
-      __syncthreads();
+      wg_barrier<kFullBar>();
       if (live) {
 #pragma unroll
         for (int j = 0; j < Sys::A; ++j) act[j] = s_act[tid * Sys::A + j];
@@ -242,47 +259,152 @@ __global__ __launch_bounds__(kBlock) void k_step(KArgs a) {
     gstore<NT>(a.done + i, dflag);
   }
   if constexpr (kLds) {
-    __syncthreads();
+    wg_barrier<kFullBar>();
     stage_out<NT, T, Sys::O>(static_cast<T*>(a.obs) + base * Sys::O, s_obs, nb, tid, vec);
   }
 }
 
 // ------------------------------------------------------------------ fused rollout
-template <class Sys, typename T>
-__global__ __launch_bounds__(kBlock) void k_rollout(KArgs a) {
-  __shared__ __attribute__((aligned(16))) float s_act[kBlock * Sys::A];
-  __shared__ __attribute__((aligned(16))) T s_obs[kBlock * Sys::O];
-  const int tid = (int)threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kBlock;
-  const int64_t i = base + tid;
-  const int nb = (int)((a.n - base) < kBlock ? (a.n - base) : kBlock);
-  const bool live = tid < nb;
-  const bool vec = a.vec_ok != 0;
-  const uint64_t tick = *a.tick_in;
-  if (blockIdx.x == 0 && tid == 0) {
-    *a.counter_next = 0;
-    *a.tick_out = tick + a.tick_adv;
-  }
+// K steps in one launch, state in VGPRs.  B = envs per workgroup: 256, or 64 (one
+// wave) when N is too small to give every CU several 256-lane workgroups (cfg5:
+// 32,768 envs per GPU -> 512 one-wave groups).
+//
+// Full workgroups take a branch-free path: every lane moves exactly its row's bytes
+// of the act / obs slices in fixed-size chunks (chunk c = j*B + lane: each wave
+// instruction stays contiguous), and the next step's actions are prefetched into
+// registers.  With no exec-masked stores the compiler can count the vector-memory
+// ops issued after the prefetch and wait for the prefetch alone (vmcnt(N)) instead
+// of for every outstanding store (vmcnt(0)) -- a store-ack round trip per step.
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <int RB>
+struct Chunk {  // widest power-of-two chunk (<= 16 B) that tiles a RB-byte row
+  using t = typename std::conditional<RB % 16 == 0, f4v,
+                                      typename std::conditional<RB % 8 == 0, f2v, float>::type>::type;
+  static constexpr int N = RB / (int)sizeof(t);
+};
 
-  Sys sys;
-  sys.setup(a);
-  int32_t steps = 0;
-  bool any_reset = false;
-  if (live) {
-    sys.load(a, i);
-    if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
+// Action prefetch by LDS-DMA (global_load_lds_dword, non-temporal), issued from inline
+// asm: the data lands in LDS without a VGPR destination and hipcc does not see the
+// DMA at all -- so it neither drains vmcnt(0) before later LDS reads (its LDS-DMA
+// alias rule) nor before reusing the address VGPRs, both of which it does for the
+// builtin.  The loop waits explicitly with vmcnt(N), N = the vector-memory
+// instructions it knows were issued after the DMA; older stores stay in flight.
+// Destination = M0 (wave-uniform LDS byte offset) + lane * 4.
+typedef __attribute__((address_space(3))) void* las_t;
+__device__ __forceinline__ uint32_t lds_off(const float* p) {
+  return (uint32_t)(uintptr_t)(las_t)(const_cast<float*>(p));
+}
+__device__ __forceinline__ void dma4_nt(const float* g, const float* lds_wave_base) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_wave_base));
+  uint32_t saved;  // M0 is a reserved register hipcc may hold a value in: save/restore
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dword %1, off nt\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(saved)
+               : "v"(g), "s"(m0)
+               : "memory");
+}
+// LDS reads of the DMA'd slot, also from asm (with their own lgkmcnt wait), so that
+// no compiler-visible LDS access depends on the hidden DMA.
+template <int A>
+__device__ __forceinline__ void lds_read_act(float* act, const float* p0, int stride) {
+  if constexpr (A == 3) {
+    asm volatile("ds_read_b32 %0, %3\n\tds_read_b32 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(act[0]), "=&v"(act[1]), "=&v"(act[2])
+                 : "v"(lds_off(p0)), "v"(lds_off(p0 + stride)), "v"(lds_off(p0 + 2 * stride))
+                 : "memory");
+  } else {
+    static_assert(A == 2, "action dim");
+    asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(act[0]), "=&v"(act[1])
+                 : "v"(lds_off(p0)), "v"(lds_off(p0 + stride))
+                 : "memory");
+  }
+}
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 63, "vmcnt immediate (6 bits on gfx9)");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Prefetch distance of the fused rollout's action DMA (steps in flight).
+constexpr int kDmaDist = 3;
+constexpr int kDmaSlots = kDmaDist + 1;
+
+template <class Sys, typename T, int B, bool FULL>
+__device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any_reset,
+                                             const KArgs& a, int64_t base, int tid, int nb,
+                                             uint64_t tick, float* s_act, T* s_obs) {
+  using CO = Chunk<Sys::O * (int)sizeof(T)>;
+  using co_t = typename CO::t;
+  const int64_t i = base + tid;
+  const bool live = FULL || tid < nb;
+  const float* gact = static_cast<const float*>(a.act);
+  const int wave = tid >> 6;
+  // One-wave workgroups (small N, latency-bound): no LDS obs staging and no barriers --
+  // each lane writes its own obs row (the L2 merges the partial lines of the row's
+  // stores before they leave for HBM) and reads its actions from a [A][64] LDS slot.
+  constexpr bool kDirect = FULL && B == 64;
+  // Lower bound on the vector-memory instructions every full-path step issues after
+  // its DMA, whatever the branch: the reward store, the done store and the obs stores
+  // -- CO::N chunk stores B*chunk bytes apart (never merged), or a lane's contiguous
+  // row, which hipcc may merge into ceil(row/16) stores.  A LOWER bound is safe.
+  constexpr int kRowB = Sys::O * (int)sizeof(T);
+  constexpr int kSt = 2 + (kDirect ? (kRowB + 15) / 16 : CO::N);
+  constexpr int kA = Sys::A;  // DMA instructions per step
+  // vmcnt at the top of step k: vm ops issued after step k's DMA -- for k < D the
+  // prologue's later DMAs and k earlier steps' (DMA + stores); then one step's stores
+  // plus D-1 steps' (DMA + stores).  All lower bounds (see kSt).
+  constexpr int D = kDmaDist;
+  auto wait_for_step = [&](int k) __attribute__((always_inline)) {
+    constexpr int W0 = (D - 1) * kA, W1 = (D - 2) * kA + (kA + kSt);
+    constexpr int W2 = (D - 3) * kA + 2 * (kA + kSt), WN = kSt + (D - 1) * (kA + kSt);
+    if (k == 0) wait_vmcnt<W0>();
+    else if (D > 1 && k == 1) wait_vmcnt<(D > 1 ? W1 : 0)>();
+    else if (D > 2 && k == 2) wait_vmcnt<(D > 2 ? W2 : 0)>();
+    else wait_vmcnt<WN>();
+  };
+  static_assert(D >= 1 && D <= 3, "wait ladder covers distances 1..3");
+  // DMA step kk's action slice into LDS slot `slot` (B*A floats):
+  // direct: component-major [A][B]; staged: a verbatim copy of the row-major slice.
+  auto issue = [&](int kk, int slot) __attribute__((always_inline)) {
+    const int64_t koff = (int64_t)kk * a.n;
+    float* dst = s_act + slot * (B * Sys::A);
+#pragma unroll
+    for (int j = 0; j < Sys::A; ++j) {
+      const float* src = kDirect ? gact + (koff + base + tid) * Sys::A + j
+                                 : gact + (koff + base) * Sys::A + j * B + tid;
+      dma4_nt(src, dst + j * B + wave * 64);
+    }
+  };
+  // settle every compiler-visible load of the prologue (state planes) here, so that
+  // hipcc's wait bookkeeping enters the loop with nothing pending and emits no drain
+  // inside it (vmcnt(0) alone: 0x0F70 = expcnt 7, lgkmcnt 15, vmcnt 0)
+  if constexpr (FULL) __builtin_amdgcn_s_waitcnt(0x0F70);
+  if constexpr (FULL && Sys::kUsesAction) {
+#pragma unroll
+    for (int d = 0; d < kDmaDist; ++d) issue(d < a.K ? d : a.K - 1, d);
   }
   for (int k = 0; k < a.K; ++k) {
     const int64_t off = (int64_t)k * a.n;
-    if constexpr (Sys::kUsesAction)
-      stage_in<true, float, Sys::A>(s_act, static_cast<const float*>(a.act) + (off + base) * Sys::A, nb,
-                                   tid, vec);
-    __syncthreads();
     float act[Sys::A];
     if constexpr (Sys::kUsesAction) {
-      if (live) {
+      if constexpr (FULL) {
+        wait_for_step(k);  // step k's DMA has >= N younger vm ops
+        if constexpr (!kDirect) wg_barrier<false>();  // every wave's DMA has landed
+        const float* slot = s_act + (k % kDmaSlots) * (B * Sys::A);
+        if constexpr (kDirect) lds_read_act<Sys::A>(act, slot + tid, B);
+        else lds_read_act<Sys::A>(act, slot + tid * Sys::A, 1);
+        // prefetch step k+D into the slot step k-1 used (every reader is past this
+        // point); near the end re-read step K-1: no branch, same op count
+        const int kk = k + kDmaDist < a.K ? k + kDmaDist : a.K - 1;
+        issue(kk, (k + kDmaDist) % kDmaSlots);
+      } else {
+        stage_in<true, float, Sys::A, B>(s_act, gact + (off + base) * Sys::A, nb, tid, false);
+        wg_barrier<false>();
+        if (live) {
 #pragma unroll
-        for (int j = 0; j < Sys::A; ++j) act[j] = s_act[tid * Sys::A + j];
+          for (int j = 0; j < Sys::A; ++j) act[j] = s_act[tid * Sys::A + j];
+        }
       }
     }
     T o[Sys::O];
@@ -291,15 +413,59 @@ __global__ __launch_bounds__(kBlock) void k_rollout(KArgs a) {
     const uint8_t dflag = step_body<Sys, T, true>(sys, steps, a, i, live, act, tick + (uint64_t)k,
                                                   k, o, rew, did_reset);
     any_reset = any_reset || did_reset;
+    T* gobs = static_cast<T*>(a.obs) + (off + base) * Sys::O;
+    if constexpr (kDirect) {
+      gstore<true>(static_cast<T*>(a.rew) + off + i, rew);
+      gstore<true>(a.done + off + i, dflag);
+      const co_t* src = reinterpret_cast<const co_t*>(o);
+#pragma unroll
+      for (int j = 0; j < CO::N; ++j) gstore<false>(reinterpret_cast<co_t*>(gobs) + tid * CO::N + j, src[j]);
+      continue;
+    }
     if (live) {
 #pragma unroll
       for (int j = 0; j < Sys::O; ++j) s_obs[tid * Sys::O + j] = o[j];
       gstore<true>(static_cast<T*>(a.rew) + off + i, rew);
       gstore<true>(a.done + off + i, dflag);
     }
-    __syncthreads();
-    stage_out<true, T, Sys::O>(static_cast<T*>(a.obs) + (off + base) * Sys::O, s_obs, nb, tid, vec);
+    wg_barrier<false>();
+    if constexpr (FULL) {
+#pragma unroll
+      for (int j = 0; j < CO::N; ++j)
+        gstore<true>(reinterpret_cast<co_t*>(gobs) + j * B + tid,
+                     reinterpret_cast<const co_t*>(s_obs)[j * B + tid]);
+    } else {
+      stage_out<true, T, Sys::O, B>(gobs, s_obs, nb, tid, false);
+    }
   }
+}
+
+template <class Sys, typename T, int B>
+__global__ __launch_bounds__(B) void k_rollout(KArgs a) {
+  __shared__ __attribute__((aligned(16))) float s_act[kDmaSlots * B * Sys::A];  // DMA ring
+  __shared__ __attribute__((aligned(16))) T s_obs[B * Sys::O];
+  const int tid = (int)threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * B;
+  const int64_t i = base + tid;
+  const int nb = (int)((a.n - base) < B ? (a.n - base) : B);
+  const bool live = tid < nb;
+  const uint64_t tick = *a.tick_in;
+  if (blockIdx.x == 0 && tid == 0) {
+    *a.counter_next = 0;
+    *a.tick_out = tick + a.tick_adv;
+  }
+  Sys sys;
+  sys.setup(a);
+  int32_t steps = 0;
+  bool any_reset = false;
+  if (live) {
+    sys.load(a, i);
+    if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
+  }
+  if (nb == B && a.vec_ok)
+    rollout_loop<Sys, T, B, true>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
+  else
+    rollout_loop<Sys, T, B, false>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
   if (live) {
     sys.store(a, i);
     if (any_reset) sys.store_autoreset_extra(a, i);
@@ -316,14 +482,20 @@ static int launch_all(int which, const KArgs& a, hipStream_t s) {
   if (which == 0)
     hipLaunchKernelGGL((k_reset<Sys, T>), grid, block, 0, s, a);
   else if (which == 1) {
-    switch (a.variant & 3) {
+    switch (a.variant & 7) {
       case 1: hipLaunchKernelGGL((k_step<Sys, T, 1>), grid, block, 0, s, a); break;
       case 2: hipLaunchKernelGGL((k_step<Sys, T, 2>), grid, block, 0, s, a); break;
       case 3: hipLaunchKernelGGL((k_step<Sys, T, 3>), grid, block, 0, s, a); break;
+      case 4: hipLaunchKernelGGL((k_step<Sys, T, 4>), grid, block, 0, s, a); break;
+      case 5: hipLaunchKernelGGL((k_step<Sys, T, 5>), grid, block, 0, s, a); break;
       default: hipLaunchKernelGGL((k_step<Sys, T, 0>), grid, block, 0, s, a); break;
     }
-  } else
-    hipLaunchKernelGGL((k_rollout<Sys, T>), grid, block, 0, s, a);
+  } else if (a.n < 2 * 256 * kBlock) {  // < 2 full workgroups per CU: one-wave groups
+    hipLaunchKernelGGL((k_rollout<Sys, T, 64>), dim3((unsigned)((a.n + 63) / 64)), dim3(64), 0, s,
+                       a);
+  } else {
+    hipLaunchKernelGGL((k_rollout<Sys, T, kBlock>), grid, block, 0, s, a);
+  }
   return (int)hipGetLastError();
 }
 

@@ -255,6 +255,14 @@ struct SysPMSM {
 #pragma unroll
     for (int j = 0; j < 3; ++j) nz[j] = 3.0 * (double)z[j];
   }
+  // f32 x**alpha: (float)pow((double)x, alpha) -- correctly rounded except in rare
+  // cases, reproducible by the CPU oracle; alpha = 0.5 (the reference default and
+  // cfg4) is exactly sqrtf (double-rounding of a square root through double is
+  // innocuous), which keeps the fp64 pow off the hot path.
+  __device__ float fpow(float x) const {
+    if (alpha == 0.5f) return sqrtf(x);
+    return (float)pow((double)x, (double)alpha);
+  }
   __device__ static float bias(const float* tab, int32_t len, int32_t k) {
     return k < len ? tab[k] : 1.0f;
   }
@@ -282,11 +290,8 @@ struct SysPMSM {
     const float vh = vt / bias(a.bc2, a.bc_len, adam);     // :131
     lam = lam - (lr * mh) / (sqrtf(vh) + eps);             // :135
     lam = clip(lam, 0.0f, 0.5f);                           // :138
-    const double al = (double)alpha;                       // :158-160 (x + 1e-6)**alpha
-    const float tiny = 1e-6f;
-    const float fp = ((float)pow((double)(fabsf(e1) + tiny), al) +
-                      (float)pow((double)(fabsf(e2) + tiny), al)) +
-                     (float)pow((double)(fabsf(e3) + tiny), al);
+    const float tiny = 1e-6f;                              // :158-160 (x + 1e-6)**alpha
+    const float fp = (fpow(fabsf(e1) + tiny) + fpow(fabsf(e2) + tiny)) + fpow(fabsf(e3) + tiny);
     const float ap = lam * (act[0] * act[0] + act[1] * act[1]);  // :165 raw action
     float r = ((-es) - fp) - ap;                           // :167
     bool te = false;

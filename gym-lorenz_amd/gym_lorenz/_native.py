@@ -56,7 +56,7 @@ class LzInfo(ctypes.Structure):
         ("n_planes", ctypes.c_int32),
         ("bytes_per_env_step", ctypes.c_int32),
         ("counts_steps", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("state_io_bytes", ctypes.c_int32),
     ]
 
 

@@ -139,7 +139,8 @@ typedef struct lz_info {
   int32_t n_planes;    /* SoA planes addressable by lz_get_state/lz_set_state */
   int32_t bytes_per_env_step; /* algorithmic HBM bytes of one lz_step per env */
   int32_t counts_steps;       /* 1 if the STEP plane is maintained by lz_step */
-  int32_t reserved;
+  int32_t state_io_bytes;     /* of bytes_per_env_step: state planes read + written
+                                 (paid once per launch by lz_rollout, not per step) */
 } lz_info;
 
 /* Fill *cfg with the reference defaults of `system` (dtype f32, 1 env, seed 0). */

@@ -172,7 +172,9 @@ void orc_pmsm_reset_obs(int64_t n, const float* st, float* obs, const double* pd
 
 /* f32 x**k as NumPy (glibc powf) or as the device */
 static inline float pmsm_pow(float x, float a, int mode) {
-  return mode == ORC_REF ? powf(x, a) : (float)pow((double)x, (double)a);
+  if (mode == ORC_REF) return powf(x, a);
+  if (a == 0.5f) return sqrtf(x); /* device: exact (rounding sqrt via double is innocuous) */
+  return (float)pow((double)x, (double)a);
 }
 static inline float pmsm_sq(float x, int mode) { return mode == ORC_REF ? powf(x, 2.0f) : x * x; }
 

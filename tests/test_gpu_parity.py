@@ -289,10 +289,12 @@ def test_shard_invariance(gl):
         assert np.array_equal(df, np.concatenate([x[2] for x in outs]))
 
 
-@pytest.mark.parametrize("system,dtype", [("lorenz3", "float32"), ("pmsm", "float32"),
-                                          ("hr", "float64"), ("lorenz4", "float32")])
-def test_rollout_equals_steps(gl, system, dtype):
-    n, K = 1000, 33
+@pytest.mark.parametrize("system,dtype,n", [("lorenz3", "float32", 1000), ("pmsm", "float32", 1000),
+                                            ("hr", "float64", 1000), ("lorenz4", "float32", 1000),
+                                            ("lorenz3", "float32", 140000)])
+def test_rollout_equals_steps(gl, system, dtype, n):
+    """Fused rollout (one-wave workgroups below 131,072 envs, 256-lane above) == K steps."""
+    K = 33
     kw = {"add_noise": True} if system in ("pmsm", "hr") else {}
     a_be = gl.BatchedEnv(system, n, dtype=dtype, seed=4, max_episode_steps=10, **kw)
     b_be = gl.BatchedEnv(system, n, dtype=dtype, seed=4, max_episode_steps=10, **kw)
@@ -398,3 +400,48 @@ def test_vecenv_sb3_contract(gl):
     assert i0["TimeLimit.truncated"] is True and i0["terminal_observation"].shape == (6,)
     assert len(venv.get_attr("lambda_coef")) == n
     venv.close()
+
+
+@pytest.mark.parametrize("add_filter", [False, True])
+def test_hr_f32_vs_oracle(gl, orc, add_filter):
+    """HR in fp32 (the VecEnv default): device RK4 == the oracle's fp32 DEV restatement,
+    injected noise, filter on/off, 300 steps, 2048 envs."""
+    n, T = 2048, 300
+    be = gl.BatchedEnv("hr", n, dtype="float32", seed=21, add_noise=True, add_filter=add_filter,
+                       autoreset=False)
+    be.reset()
+    init = orc.reset_draw("hr", np.float32, n, 0, 21, 0, add_noise=True)
+    assert bits_equal(_planes(be, 0, 7), init)
+    st = np.ascontiguousarray(init[:, :6])
+    fa = np.zeros((n, 2), np.float32)
+    rng = np.random.default_rng(8)
+    with np.errstate(all="ignore"):
+        for k in range(T):
+            a = rng.uniform(-1.2, 1.2, (n, 2)).astype(np.float32)
+            nz = rng.normal(0, 1, (n, 3)) * init[:, 6:7]
+            o, r, d = be.step(torch.from_numpy(a), torch.from_numpy(nz))
+            oo, rr, tt = orc.hr_step(st, fa, a, nz.astype(np.float32), True, add_filter, orc.DEV)
+    assert bits_equal(_np(o), oo) and bits_equal(_np(r), rr)
+    assert np.array_equal((_np(d) & 1).astype(bool), tt)
+
+
+def test_device_noise_statistics(gl, orc):
+    """On-device Philox/Box-Muller process noise: PMSM N(0,3) enters the slave's Euler
+    update (lorenz_env_try_pmsm.py:80-93), so (state2_device - state2_noiseless)/dt
+    recovers the noise up to f32 rounding (~0.03 abs); its moments must be N(0, 3),
+    independent across components."""
+    n = 1 << 18
+    be = gl.BatchedEnv("pmsm", n, seed=3, add_noise=True, autoreset=False)
+    be.reset()
+    S = orc.PmsmState(n)
+    S.st[:] = orc.reset_draw("pmsm", np.float32, n, 0, 3, 0)
+    a = np.zeros((n, 2), np.float32)
+    be.step(torch.from_numpy(a))
+    orc.pmsm_step(S, a, None, False, 0.5, orc.DEV)
+    s2 = _planes(be, 3, 3).astype(np.float64)
+    nz = (s2 - S.st[:, 3:].astype(np.float64)) / 1e-3
+    assert abs(nz.mean()) < 0.03 and abs(nz.std() - 3.0) < 0.03
+    c = np.corrcoef(nz.T)
+    assert np.abs(c - np.eye(3)).max() < 0.01
+    # the master is noiseless (lorenz_env_try_pmsm.py:88)
+    assert bits_equal(_planes(be, 0, 3), S.st[:, :3])

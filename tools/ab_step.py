@@ -53,7 +53,7 @@ def timeit(g, stream, reps):
 
 def main():
     envs = [int(x) for x in sys.argv[1:]] or [131072, 1048576, 4194304]
-    variants = [0, 1, 2, 3]
+    variants = [int(v) for v in os.environ.get("AB_VARIANTS", "0,1,2,3").split(",")]
     system = os.environ.get("AB_SYSTEM", "lorenz3")
     res = {}
     for n in envs:
@@ -63,7 +63,7 @@ def main():
         for _ in range(7):
             for v in variants:
                 samples[v].append(timeit(runs[v][0], runs[v][1], reps))
-        bps = runs[0][2][0].bytes_per_env_step
+        bps = runs[variants[0]][2][0].bytes_per_env_step
         for v in variants:
             s = sorted(samples[v])
             med = s[len(s) // 2]

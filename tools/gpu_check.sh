@@ -28,8 +28,24 @@ for step in "$@"; do
       export TMPDIR=/tmp
       run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2000 --warmup 200 --no-cpu-baseline --no-drift ;;
     ab) run ab_step 600 python tools/ab_step.py 131072 1048576 4194304 ;;
+    ab_bar) AB_VARIANTS=0,4 run ab_bar 600 python tools/ab_step.py 65536 131072 1048576 4194304 ;;
     ab_pmsm) AB_SYSTEM=pmsm run ab_pmsm 600 python tools/ab_step.py 262144 1048576 ;;
     counters) run counters 120 rocprofv3 -L ;;
+    configs)
+      run cfg2_l3_65k 200 python bench.py --envs 65536 --no-cpu-baseline --no-drift
+      run cfg3_l3_1M_strong8_shard 200 python bench.py --envs 131072 --no-cpu-baseline --no-drift
+      run cfg4_pmsm_262k 300 python bench.py --system pmsm --envs 262144 --steps 4000
+      run cfg5_rollout_32k 300 python bench.py --mode rollout --K 2048 --envs 32768 --steps 16384
+      run cfg5_rollout_262k 300 python bench.py --mode rollout --K 2048 --envs 262144 --steps 8192
+      run l4_1M 200 python bench.py --system lorenz4 --envs 1048576
+      run hr_1M 200 python bench.py --system hr --envs 1048576
+      run l3_4M 200 python bench.py --envs 4194304 --steps 2000 --no-cpu-baseline --no-drift ;;
+    configs2)
+      run cfg4_pmsm_262k 300 python bench.py --system pmsm --envs 262144 --steps 4000
+      run cfg5_rollout_32k 300 python bench.py --mode rollout --K 2048 --envs 32768 --steps 16384
+      run cfg5_rollout_262k 300 python bench.py --mode rollout --K 2048 --envs 262144 --steps 8192 ;;
+    split) run ab_split 600 python tools/ab_split.py 131072 1048576 ;;
+    dist2) LZ_BENCH_BACKEND=gloo run dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 500 --warmup 64 --envs 262144 ;;
     pmc)
       export TMPDIR=/tmp
       run pmc_f_calib 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o calib --output-format csv -- ./tools/pmc_calib
