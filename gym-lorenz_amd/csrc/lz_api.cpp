@@ -65,6 +65,13 @@ int plane_elem(int system, int f64, int p) {
 
 }  // namespace
 
+namespace lz {
+lz_status set_error(lz_status s, const char* msg) {
+  g_err = msg;
+  return s;
+}
+}  // namespace lz
+
 struct lz_handle {
   lz_config cfg;
   SysDesc desc;

@@ -50,6 +50,9 @@ struct KArgs {
   double prm[LZ_MAX_PARAMS];
 };
 
+// record the thread-local message lz_last_error() returns; returns s
+lz_status set_error(lz_status s, const char* msg);
+
 // host-side launchers (lz_kernels.hip)
 int launch_reset(int system, int f64, const KArgs& a, void* stream);
 int launch_step(int system, int f64, const KArgs& a, void* stream);

@@ -76,6 +76,18 @@ _SIGS = {
     "lz_get_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
     "lz_set_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
     "lz_plane_elem_size": (ctypes.c_int32, [VP, ctypes.c_int32]),
+    "lz_rms_create": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_double,
+                                     ctypes.POINTER(VP)]),
+    "lz_rms_destroy": (ctypes.c_int, [VP]),
+    "lz_rms_set_stream": (ctypes.c_int, [VP, VP]),
+    "lz_rms_state": (ctypes.c_int, [VP, ctypes.POINTER(VP), ctypes.POINTER(VP),
+                                    ctypes.POINTER(VP)]),
+    "lz_rms_moments": (ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int64, VP]),
+    "lz_rms_update": (ctypes.c_int, [VP, VP]),
+    "lz_rms_normalize": (ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int64, VP, ctypes.c_int32,
+                                        ctypes.c_double, ctypes.c_double]),
+    "lz_returns_update": (ctypes.c_int, [VP, VP, ctypes.c_int32, VP, ctypes.c_int64, ctypes.c_double,
+                                         ctypes.c_int32, ctypes.c_int32, VP]),
     "lz_last_error": (ctypes.c_char_p, []),
     "lz_abi_version": (ctypes.c_int32, []),
 }

@@ -204,6 +204,36 @@ lz_status lz_set_state(lz_handle* h, int32_t plane, const void* src);
 /* Element size in bytes of a plane (4 or 8), or 0 for an invalid plane. */
 int32_t lz_plane_elem_size(const lz_handle* h, int32_t plane);
 
+/* ------------------------------------------------------------------------------
+ * On-device VecNormalize statistics (stable-baselines3 2.7.1 RunningMeanStd /
+ * VecNormalize, common/running_mean_std.py and common/vec_env/vec_normalize.py, as
+ * wrapped around the reference envs by code/lorenz_pmsm/train.py:118,170).  Float64
+ * statistics on the device; batch moments are plain sums (count, sum, sum of squares)
+ * so a multi-GPU caller all-reduces them before lz_rms_update.
+ * ------------------------------------------------------------------------------ */
+typedef struct lz_rms lz_rms;
+
+/* RunningMeanStd(epsilon=count_init, shape=(dim,)): mean 0, var 1, count count_init. */
+lz_status lz_rms_create(int32_t dim, int32_t device, double count_init, lz_rms** out);
+lz_status lz_rms_destroy(lz_rms* r);
+lz_status lz_rms_set_stream(lz_rms* r, void* hip_stream);
+/* Device pointers to the statistics: mean[dim], var[dim], count[1] (double). */
+lz_status lz_rms_state(lz_rms* r, double** mean, double** var, double** count);
+/* moments_out (device double [1 + 2*dim]) = (n, column sums, column sums of squares)
+ * of x [n, dim] (dtype LZ_DTYPE_F32 / F64); deterministic reduction order. */
+lz_status lz_rms_moments(lz_rms* r, const void* x, int32_t dtype, int64_t n, double* moments_out);
+/* RunningMeanStd.update_from_moments with those moments (possibly all-reduced). */
+lz_status lz_rms_update(lz_rms* r, const double* moments);
+/* y (float32 [n, dim]) = clip((x - mean if center else x) / sqrt(var + eps), -clip, clip)
+ * (VecNormalize.normalize_obs with center=1, normalize_reward with center=0). */
+lz_status lz_rms_normalize(lz_rms* r, const void* x, int32_t dtype, int64_t n, float* y,
+                           int32_t center, double eps, double clip);
+/* VecNormalize discounted returns (double [n]): phase 0: returns = returns*gamma + rew;
+ * phase 1: returns[done != 0] = 0. */
+lz_status lz_returns_update(double* returns, const void* rew, int32_t dtype, const uint8_t* done,
+                            int64_t n, double gamma, int32_t phase, int32_t device,
+                            void* hip_stream);
+
 const char* lz_last_error(void);
 int32_t lz_abi_version(void);
 

@@ -445,3 +445,47 @@ def test_device_noise_statistics(gl, orc):
     assert np.abs(c - np.eye(3)).max() < 0.01
     # the master is noiseless (lorenz_env_try_pmsm.py:88)
     assert bits_equal(_planes(be, 0, 3), S.st[:, :3])
+
+
+# ----------------------------------------------------------------- VecNormalize (f1)
+@pytest.mark.parametrize("norm_reward", [False, True])
+def test_device_vecnormalize_matches_sb3_restatement(gl, norm_reward):
+    """LorenzVecNormalize (device statistics) vs the NumPy restatement of SB3 2.7.1
+    VecNormalize (oracle/sb3_vecnorm.py) fed the raw outputs of an identical env, as
+    code/lorenz_pmsm/train.py:170 configures it (norm_obs, clip_obs=10)."""
+    from gym_lorenz.vec_normalize import LorenzVecNormalize
+    from oracle.sb3_vecnorm import VecNormalizeRef
+
+    n, T = 4096, 120
+    raw = gl.make_vec("lorenz_pmsm-v0", n, seed=5, max_episode_steps=37)
+    dev = LorenzVecNormalize(gl.make_vec("lorenz_pmsm-v0", n, seed=5, max_episode_steps=37),
+                             norm_obs=True, norm_reward=norm_reward, clip_obs=10.0)
+    ref = VecNormalizeRef(n, 6, norm_obs=True, norm_reward=norm_reward, clip_obs=10.0)
+    o_raw = raw.reset()
+    o_ref = ref.reset(o_raw)
+    o_dev = dev.reset()
+    np.testing.assert_allclose(o_dev, o_ref, rtol=1e-5, atol=1e-5)
+    rng = np.random.default_rng(0)
+    saw_done = False
+    for k in range(T):
+        a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        o_raw, r_raw, d_raw, i_raw = raw.step(a)
+        term = {i: i_raw[i]["terminal_observation"] for i in range(n) if d_raw[i]}
+        o_ref, r_ref, d_ref, tn_ref = ref.step(o_raw, r_raw, d_raw, term)
+        o_dev, r_dev, d_dev, i_dev = dev.step(a)
+        assert np.array_equal(d_dev, d_raw)
+        np.testing.assert_allclose(o_dev, o_ref, rtol=2e-5, atol=2e-5)
+        np.testing.assert_allclose(r_dev, r_ref, rtol=2e-5, atol=2e-5)
+        for i, t in tn_ref.items():
+            saw_done = True
+            np.testing.assert_allclose(i_dev[i]["terminal_observation"], t, rtol=2e-5, atol=2e-5)
+            assert i_dev[i]["TimeLimit.truncated"] == i_raw[i]["TimeLimit.truncated"]
+    assert saw_done
+    np.testing.assert_allclose(dev.obs_rms.mean, ref.obs_rms.mean, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(dev.obs_rms.var, ref.obs_rms.var, rtol=1e-6)
+    assert dev.obs_rms.count == pytest.approx(ref.obs_rms.count)
+    np.testing.assert_allclose(dev.ret_rms.var, ref.ret_rms.var, rtol=1e-6)
+    dev.save("/tmp/_vn.npz")
+    dev2 = LorenzVecNormalize(gl.make_vec("lorenz_pmsm-v0", 16, seed=1))
+    dev2.load("/tmp/_vn.npz")
+    np.testing.assert_array_equal(dev2.obs_rms.mean, dev.obs_rms.mean)
