@@ -107,3 +107,73 @@ class FakeBackend:
 
     def close(self):
         pass
+
+
+class FakeSingleCore:
+    """Test double of gym_lorenz.envs._single.SingleEnvCore (one env) driven by the
+    oracle in mode REF (glibc pow: the reference's own arithmetic), so the drop-in
+    classes' host logic -- RNG draw order, attribute bookkeeping, API shapes -- can be
+    checked against the golden fixtures without a GPU."""
+
+    PLANES = {0: 3, 1: 8, 2: 6, 3: 6}
+
+    def __init__(self, system, dtype, device=None, alpha=0.5, add_noise=False, eval_mode=False,
+                 add_filter=False):
+        self.system = system
+        self.dt = np.float32 if (system == 2 or np.dtype(dtype) == np.float32) else np.float64
+        self.alpha, self.add_noise, self.add_filter = alpha, add_noise, add_filter
+        self.S = oracle.PmsmState(1) if system == 2 else None
+        self.st = np.zeros((1, self.PLANES[system]), self.dt)
+        self.fa = np.zeros((1, 2), np.float32)
+
+    def reset(self, init):
+        init = np.asarray(init, self.dt).reshape(1, -1)
+        if self.system == 0:
+            self.st[:] = init
+            return oracle.l3_reset_obs(self.st)[0]
+        if self.system == 1:
+            self.st[:] = init
+            return oracle.l4_reset_obs(self.st)[0]
+        if self.system == 2:
+            self.S.st[:] = init
+            self.S.cur_step[:] = 0
+            return oracle.pmsm_reset_obs(self.S.st)[0]
+        self.st[:] = init[:, :6]
+        self.fa[:] = 0
+        return oracle.hr_reset_obs(self.st)[0]
+
+    def step(self, action, noise=None):
+        a = np.asarray(action, np.float32).reshape(1, -1)
+        with np.errstate(all="ignore"):
+            if self.system == 0:
+                o, r = oracle.l3_step(self.st, a.astype(self.dt))
+                return o[0], r[0], 0
+            if self.system == 1:
+                o, r, d = oracle.l4_step(self.st)
+                return o[0], r[0], int(d[0])
+            if self.system == 2:
+                nz = None if noise is None else np.asarray(noise, np.float64).reshape(1, 3)
+                o, r, te, tr = oracle.pmsm_step(self.S, a, nz, noise is not None, self.alpha,
+                                                oracle.REF)
+                return o[0], r[0], int(te[0]) | (2 * int(tr[0]))
+            nz = None if noise is None else np.asarray(noise, self.dt).reshape(1, 3)
+            o, r, te = oracle.hr_step(self.st, self.fa, a, nz, noise is not None, self.add_filter,
+                                      oracle.REF)
+            return o[0], r[0], int(te[0])
+
+    def plane(self, p):
+        if self.system == 2:
+            cols = {6: self.S.lam, 7: self.S.m, 8: self.S.v, 9: self.S.adam_step}
+            return cols[p][0] if p in cols else self.S.st[0, p]
+        return self.st[0, p]
+
+    def planes(self, first, count):
+        return np.array([self.plane(first + j) for j in range(count)])
+
+    def set_planes(self, first, values, dtype=None):
+        v = np.asarray(values).reshape(-1)
+        tgt = self.S.st if self.system == 2 else self.st
+        tgt[0, first:first + len(v)] = v
+
+    def close(self):
+        pass
