@@ -199,17 +199,23 @@ __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KAr
 // act/obs rows directly instead of LDS staging, bit 2 = __syncthreads() instead of the
 // LDS-only barrier.  Measured at 1M envs (profiles/r01): non-temporal I/O is 13%
 // faster than plain, LDS staging 7-11% faster than direct.
+template <int V>
+constexpr int step_block() {  // bits 3-4 of V: workgroup size
+  return ((V >> 3) & 3) == 1 ? 512 : ((V >> 3) & 3) == 2 ? 128 : ((V >> 3) & 3) == 3 ? 1024 : 256;
+}
+
 template <class Sys, typename T, int V>
-__global__ __launch_bounds__(kBlock) void k_step(KArgs a) {
+__global__ __launch_bounds__(step_block<V>()) void k_step(KArgs a) {
+  constexpr int SB = step_block<V>();
   constexpr bool NT = (V & 1) == 0;
   constexpr bool kLds = (V & 2) == 0;
   constexpr bool kFullBar = (V & 4) != 0;
-  __shared__ __attribute__((aligned(16))) float s_act[kLds ? kBlock * Sys::A : 4];
-  __shared__ __attribute__((aligned(16))) T s_obs[kLds ? kBlock * Sys::O : 2];
+  __shared__ __attribute__((aligned(16))) float s_act[kLds ? SB * Sys::A : 4];
+  __shared__ __attribute__((aligned(16))) T s_obs[kLds ? SB * Sys::O : 2];
   const int tid = (int)threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kBlock;
+  const int64_t base = (int64_t)blockIdx.x * SB;
   const int64_t i = base + tid;
-  const int nb = (int)((a.n - base) < kBlock ? (a.n - base) : kBlock);
+  const int nb = (int)((a.n - base) < SB ? (a.n - base) : SB);
   const bool live = tid < nb;
   const bool vec = a.vec_ok != 0;
   const uint64_t tick = *a.tick_in;
@@ -228,7 +234,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KArgs a) {
   if constexpr (Sys::kUsesAction) {
     const float* ga = static_cast<const float*>(a.act);
     if constexpr (kLds) {
-      stage_in<NT, float, Sys::A>(s_act, ga + base * Sys::A, nb, tid, vec);
+      stage_in<NT, float, Sys::A, SB>(s_act, ga + base * Sys::A, nb, tid, vec);
       wg_barrier<kFullBar>();
       if (live) {
 #pragma unroll
@@ -260,7 +266,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KArgs a) {
   }
   if constexpr (kLds) {
     wg_barrier<kFullBar>();
-    stage_out<NT, T, Sys::O>(static_cast<T*>(a.obs) + base * Sys::O, s_obs, nb, tid, vec);
+    stage_out<NT, T, Sys::O, SB>(static_cast<T*>(a.obs) + base * Sys::O, s_obs, nb, tid, vec);
   }
 }
 
@@ -482,12 +488,16 @@ static int launch_all(int which, const KArgs& a, hipStream_t s) {
   if (which == 0)
     hipLaunchKernelGGL((k_reset<Sys, T>), grid, block, 0, s, a);
   else if (which == 1) {
-    switch (a.variant & 7) {
-      case 1: hipLaunchKernelGGL((k_step<Sys, T, 1>), grid, block, 0, s, a); break;
-      case 2: hipLaunchKernelGGL((k_step<Sys, T, 2>), grid, block, 0, s, a); break;
-      case 3: hipLaunchKernelGGL((k_step<Sys, T, 3>), grid, block, 0, s, a); break;
-      case 4: hipLaunchKernelGGL((k_step<Sys, T, 4>), grid, block, 0, s, a); break;
-      case 5: hipLaunchKernelGGL((k_step<Sys, T, 5>), grid, block, 0, s, a); break;
+    switch (a.variant & 31) {
+#define LZ_STEP_V(VV)                                                                   \
+  case VV:                                                                              \
+    hipLaunchKernelGGL((k_step<Sys, T, VV>),                                            \
+                       dim3((unsigned)((a.n + step_block<VV>() - 1) / step_block<VV>())), \
+                       dim3(step_block<VV>()), 0, s, a);                                \
+    break;
+      LZ_STEP_V(1) LZ_STEP_V(2) LZ_STEP_V(3) LZ_STEP_V(4) LZ_STEP_V(5)
+      LZ_STEP_V(8) LZ_STEP_V(16) LZ_STEP_V(24)
+#undef LZ_STEP_V
       default: hipLaunchKernelGGL((k_step<Sys, T, 0>), grid, block, 0, s, a); break;
     }
   } else if (a.n < 2 * 256 * kBlock) {  // < 2 full workgroups per CU: one-wave groups

@@ -28,6 +28,7 @@ for step in "$@"; do
       export TMPDIR=/tmp
       run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2000 --warmup 200 --no-cpu-baseline --no-drift ;;
     ab) run ab_step 600 python tools/ab_step.py 131072 1048576 4194304 ;;
+    ab_blk) AB_VARIANTS=0,8,16,24 run ab_blk 600 python tools/ab_step.py 131072 1048576 4194304 ;;
     ab_bar) AB_VARIANTS=0,4 run ab_bar 600 python tools/ab_step.py 65536 131072 1048576 4194304 ;;
     ab_pmsm) AB_SYSTEM=pmsm run ab_pmsm 600 python tools/ab_step.py 262144 1048576 ;;
     counters) run counters 120 rocprofv3 -L ;;
