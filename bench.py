@@ -29,6 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "gym-lorenz_amd"))
 
 METRIC = "env-steps/sec at 1M parallel Lorenz envs, 1/2/4/8 MI355X; fp32 drift vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 
 
 def parse():
@@ -47,8 +48,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--system", choices=["lorenz3", "lorenz4", "pmsm", "hr"], default="lorenz3",
                    help="lorenz3 = the BASELINE headline (dynamic.py env); pmsm = cfg4")
-    p.add_argument("--mode", choices=["step", "rollout"], default="step",
-                   help="rollout = cfg5's fused K-step on-device rollout")
+    p.add_argument("--mode", choices=["step", "rollout", "policy"], default="step",
+                   help="rollout = cfg5's fused K-step on-device rollout; policy = the fused "
+                        "SB3 actor-critic rollout (lz_rollout_policy + VecNormalize + GAE)")
     p.add_argument("--K", type=int, default=2048, help="rollout length (--mode rollout)")
     p.add_argument("--max-episode-steps", type=int, default=0,
                    help="TimeLimit truncation (auto-reset inside the kernel); 0 = none")
@@ -143,6 +145,108 @@ def kernel_name(system, mode, n):
     return pre % ("7" if system == "pmsm" else "5", tag)
 
 
+def policy_flops(O, A, H=128):
+    """Useful FLOP per env-step of the SB3 MlpPolicy forward (pi and vf nets)."""
+    return 2 * (O * H + H * H + H * A) + 2 * (O * H + H * H + H)
+
+
+def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
+    """--mode policy: the reference's PMSM learner loop (code/lorenz_pmsm/train.py:155-178:
+    A2C MlpPolicy pi/vf [128,128] Tanh, VecNormalize(norm_obs, clip_obs=10), n_steps=16)
+    collected on the GPU: per rollout one lz_rollout_policy launch (K steps of policy
+    forward + sample + env step + bootstrap), the obs_rms update from its moments, and
+    lz_gae.  One "step" = one env step of every env (policy forward included)."""
+    import torch.distributed as dist
+
+    from gym_lorenz.policy import ActorCriticMlp, FusedRolloutCollector
+    from gym_lorenz.vec_normalize import DeviceRunningMeanStd
+
+    K = args.K
+    O, A = env.obs_dim, env.action_dim
+    net = ActorCriticMlp(O, A, seed=0)  # SB3 init (orthogonal, log_std 0): random weights
+    rms = DeviceRunningMeanStd(O, device)
+    col = FusedRolloutCollector(env, net.state_dict(), gamma=0.99, gae_lambda=0.95, obs_rms=rms,
+                                clip_obs=10.0, training=True, bootstrap=True)
+    stream = torch.cuda.Stream(device)
+    with torch.cuda.stream(stream):
+        nat.check(nat.lib.lz_set_stream(env._h, ctypes.c_void_p(stream.cuda_stream)))
+        nat.check(nat.lib.lz_rms_set_stream(rms._h, ctypes.c_void_p(stream.cuda_stream)))
+        col.reset()
+        launches = max(2, args.steps // K)
+        warm = 2
+
+        def one():
+            b = col.collect(K)
+            col.compute_returns_and_advantage(b)
+
+        for _ in range(warm):
+            one()
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(launches):
+            one()
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        # the dominant kernel alone (k_rollout_policy), HIP events on its stream
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * launches)]
+        for j in range(launches):
+            evs[2 * j].record(stream)
+            col.collect(K)
+            evs[2 * j + 1].record(stream)
+        torch.cuda.synchronize(device)
+    elapsed = t1 - t0
+    steps = launches * K
+    # collect() = lz_rollout_policy + moments-final + rms update (tiny): per-launch time
+    launch_s = sum(evs[2 * j].elapsed_time(evs[2 * j + 1]) for j in range(launches)) / launches / 1e3
+    if world > 1:
+        t = torch.tensor([elapsed, launch_s], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, launch_s = float(t[0]), float(t[1])
+    fl = policy_flops(O, A)
+    achieved = fl * n * K / launch_s / 1e12
+    mangled = {"pmsm": "7SysPMSME", "lorenz3": "5SysL3IfEE", "lorenz4": "5SysL4IfEE",
+               "hr": "5SysHRIfEE"}[args.system]
+    return {
+        "metric": METRIC,
+        "value": total * steps / elapsed,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warm * K,
+        "ms_per_step": elapsed * 1e3 / steps,
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "bf16 MFMA (fp32 accumulate), f32 env",
+        "data": "synthetic: on-device Philox initial states and Gaussian action samples; "
+                "SB3-initialised (orthogonal) random policy weights",
+        "config": {
+            "workload": "%s with the SB3 A2C/PPO MlpPolicy (pi/vf [128,128] Tanh) in the loop: "
+                        "%d-step fused rollout (lz_rollout_policy: policy forward + DiagGaussian "
+                        "sample + clip + env step + truncation bootstrap + VecNormalize obs), "
+                        "obs_rms update, GAE (lz_gae); %d envs total, %d per GPU"
+                        % (SYSTEM_INFO[args.system][0], K, total, n),
+            "system": args.system, "envs_total": total, "envs_per_gpu": n, "mode": "policy",
+            "K": K, "parallelism": "env shard x%d (no collective on step; obs_rms moments "
+                                   "all-reduced once per rollout when N>1)" % world,
+        },
+        "roofline": {
+            "bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS, "traffic": None,
+            "kernel": "_ZN2lz16k_rollout_policyINS_%sLi8EEEvNS_5KArgsENS_5PArgsE" % mangled,
+            "avg_launch_us": launch_s * 1e6, "flop_per_env_step": fl,
+            "note": "achieved = useful MLP FLOP (pi + vf, %d per env-step) x envs x K / HIP-event "
+                    "time of one collect() (policy kernel + a 1-block moments reduction + the "
+                    "obs_rms update)" % fl,
+        },
+    }
+
+
 def main():
     args = parse()
     import torch
@@ -181,6 +285,15 @@ def main():
     env = gl.BatchedEnv(args.system, n, dtype="float32", seed=0, global_env_offset=start,
                         autoreset=True, device=local, max_episode_steps=args.max_episode_steps,
                         **kw)
+    if args.mode == "policy":
+        out = bench_policy(args, gl, nat, torch, env, device, world, rank, total, n)
+        env.close()
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        return
     A, O = env.action_dim, env.obs_dim
     arange = SYSTEM_INFO[args.system][2]
     rollout = args.mode == "rollout"

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <new>
 #include <string>
@@ -86,6 +87,9 @@ struct lz_handle {
   int count_steps;
   int32_t max_steps;
   bool was_reset;
+  int num_cus;         // compute units of the device (policy rollout grid)
+  double* pol_part;    // policy rollout obs-moment partials (lazily allocated)
+  int64_t pol_part_n;  // doubles allocated
 };
 
 extern "C" {
@@ -156,6 +160,13 @@ lz_status lz_create(const lz_config* cfg_in, lz_handle** out) {
   h->ticks = nullptr;
   h->parity = 0;
   h->was_reset = false;
+  h->pol_part = nullptr;
+  h->pol_part_n = 0;
+  h->num_cus = 0;
+  if (hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, cfg.device) !=
+          hipSuccess ||
+      h->num_cus <= 0)
+    h->num_cus = 256;
 
   // The reference's float accumulator 't += dt; done = t == T' (dynamic.py:110-111,
   // lorenz_env_transient.py:122,127): replay it on the host in double, exactly as
@@ -240,6 +251,7 @@ lz_status lz_destroy(lz_handle* h) {
   if (h->counters) (void)hipFree(h->counters);
   if (h->ticks) (void)hipFree(h->ticks);
   if (h->bc) (void)hipFree(h->bc);
+  if (h->pol_part) (void)hipFree(h->pol_part);
   delete h;
   return LZ_OK;
 }
@@ -402,6 +414,73 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
   if (e != 0) return fail(LZ_ERR_HIP, "rollout launch: %s", hipGetErrorString((hipError_t)e));
   if (n_done_out)
     HIP_TRY(hipMemcpyAsync(n_done_out, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
+  h->parity ^= 1;
+  return LZ_OK;
+}
+
+lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r) {
+  if (!h || !r) return fail(LZ_ERR_INVALID, "handle/args is NULL");
+  if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_rollout_policy before the first lz_reset");
+  if (h->f64) return fail(LZ_ERR_UNSUPPORTED, "the policy rollout runs float32 handles only");
+  if (r->K <= 0) return fail(LZ_ERR_INVALID, "K must be >= 1");
+  if (!r->blob || !r->obs_in || !r->obs_last || !r->obs_buf || !r->act_buf || !r->logp_buf ||
+      !r->val_buf || !r->rew_buf || !r->done_buf || !r->last_values)
+    return fail(LZ_ERR_INVALID, "blob / obs / rollout buffers must be non-NULL");
+  if ((r->done_idx == nullptr) != (r->terminal_obs == nullptr))
+    return fail(LZ_ERR_INVALID, "done_idx and terminal_obs go together");
+  if ((int64_t)r->K * h->cfg.num_envs > ((int64_t)1 << 40)) return fail(LZ_ERR_INVALID, "K*N too large");
+  if (!(r->act_low <= r->act_high)) return fail(LZ_ERR_INVALID, "act_low > act_high");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  const int64_t n = h->cfg.num_envs;
+  const int W = lz::kPolWaves;
+  const int64_t ntiles = (n + 31) / 32;
+  const int grid = (int)std::min<int64_t>(h->num_cus, (ntiles + W - 1) / W);
+  const int O = h->desc.obs_dim;
+  const int64_t need = (int64_t)grid * W * 2 * O;
+  if (r->obs_moments && h->pol_part_n < need) {
+    if (h->pol_part) HIP_TRY(hipFree(h->pol_part));
+    h->pol_part = nullptr;
+    h->pol_part_n = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&h->pol_part), (size_t)need * sizeof(double)) != hipSuccess)
+      return fail(LZ_ERR_OOM, "policy moment scratch allocation failed");
+    h->pol_part_n = need;
+  }
+  KArgs a;
+  fill_common(h, a);
+  a.obs = r->obs_buf;
+  a.rew = r->rew_buf;
+  a.done = r->done_buf;
+  a.done_idx64 = r->done_idx;
+  a.term_obs = r->terminal_obs;
+  a.term_cap = r->cap;
+  a.K = r->K;
+  a.tick_adv = (uint64_t)r->K;
+  lz::PArgs p;
+  std::memset(&p, 0, sizeof p);
+  p.blob = static_cast<const uint8_t*>(r->blob);
+  p.obs_in = r->obs_in;
+  p.obs_last = r->obs_last;
+  p.norm = r->obs_norm;
+  p.eps = r->norm_eps;
+  p.clip = r->clip_obs;
+  p.gamma = (float)r->gamma;
+  p.act_lo = r->act_low;
+  p.act_hi = r->act_high;
+  p.pflags = r->flags;
+  p.act = r->act_buf;
+  p.logp = r->logp_buf;
+  p.val = r->val_buf;
+  p.last_val = r->last_values;
+  p.partials = r->obs_moments ? h->pol_part : nullptr;
+  int e = lz::launch_rollout_policy(h->cfg.system, a, p, grid, h->stream);
+  if (e != 0) return fail(LZ_ERR_HIP, "policy rollout launch: %s", hipGetErrorString((hipError_t)e));
+  if (r->obs_moments) {
+    e = lz::launch_policy_moments_final(h->pol_part, grid * W, 2 * O, (double)r->K * (double)n,
+                                        r->obs_moments, h->stream);
+    if (e != 0) return fail(LZ_ERR_HIP, "moments launch: %s", hipGetErrorString((hipError_t)e));
+  }
+  if (r->n_done)
+    HIP_TRY(hipMemcpyAsync(r->n_done, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
   h->parity ^= 1;
   return LZ_OK;
 }

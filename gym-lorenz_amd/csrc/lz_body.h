@@ -1,0 +1,118 @@
+// Device building blocks shared by the env kernels (lz_kernels.hip) and the
+// policy rollout (lz_policy.hip): global access helpers, wave compaction of done
+// envs, process noise and the one-step body (env step + done bits + compact list +
+// auto-reset).  Internal, not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "lz_internal.h"
+#include "lz_systems.h"
+
+namespace lz {
+
+// ------------------------------------------------------------------ global access
+// NT = non-temporal (streaming) hint for buffers touched once per step (actions in,
+// obs / reward / done out); the state planes are re-read next step and keep the
+// default policy.
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+template <bool NT, typename V>
+__device__ __forceinline__ V gload(const V* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, typename V>
+__device__ __forceinline__ void gstore(V* p, V v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// 64-lane ballot compaction: returns this lane's slot in the compact list (or -1).
+// Must be reached by every lane of the wave.
+__device__ __forceinline__ int32_t wave_compact(bool flag, int32_t* counter) {
+  const unsigned long long m = __ballot(flag);
+  if (m == 0ull) return -1;
+  const int lane = (int)(threadIdx.x & 63u);
+  const int leader = __ffsll((long long)m) - 1;
+  int32_t base = 0;
+  if (lane == leader) base = atomicAdd(counter, (int32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  const unsigned long long lt = (lane == 0) ? 0ull : (m & (~0ull >> (64 - lane)));
+  return flag ? base + (int32_t)__popcll(lt) : -1;
+}
+
+template <class Sys, typename T, bool kInjectable>
+__device__ __forceinline__ void make_noise(const Sys& sys, const KArgs& a, int64_t i, uint64_t tick,
+                                           double* nz) {
+  if (kInjectable && a.noise) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) nz[j] = a.noise[3 * i + j];
+  } else {
+    float z[3];
+    normal3(a.seed, (uint64_t)(a.gid0 + i), tick, z);
+    sys.noise_from_normals(z, nz);
+  }
+}
+
+// ------------------------------------------------------------------ one step body
+// Shared by k_step (K = 1, state in HBM), k_rollout and k_rollout_policy (state in
+// VGPRs across K).  Returns the done byte; o[] holds the observation to emit
+// (post-reset if reset); with kKeepTerm, o_term[] receives the pre-reset observation.
+template <class Sys, typename T, bool kRollout, bool kKeepTerm = false>
+__device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KArgs& a, int64_t i,
+                                             bool live, const float* act, uint64_t tick, int k,
+                                             T* o, T& rew, bool& did_reset,
+                                             T* o_term = nullptr) {
+  uint8_t dflag = 0;
+  did_reset = false;
+  if (live) {
+    double nz[3] = {0.0, 0.0, 0.0};
+    bool use_nz = false;
+    if constexpr (Sys::kNoise) {
+      if (a.flags & LZ_FLAG_ADD_NOISE) {
+        make_noise<Sys, T, !kRollout>(sys, a, i, tick, nz);
+        use_nz = true;
+      }
+    }
+    bool term = sys.step(act, use_nz, nz, o, rew, a);
+    bool trunc = false;
+    if (a.count_steps) {
+      steps += 1;
+      if (steps == a.t_done_step) term = true;            // reference 't == T'
+      if (a.max_steps > 0 && steps >= a.max_steps) trunc = true;
+    }
+    dflag = (uint8_t)((term ? LZ_DONE_TERMINATED : 0u) | (trunc ? LZ_DONE_TRUNCATED : 0u));
+  }
+  // compact list of done envs: ballot + one atomic per wave (all lanes reach this)
+  if (a.term_obs) {
+    const int32_t pos = wave_compact(dflag != 0, a.counter);
+    if (pos >= 0) {
+      if constexpr (kRollout) {
+        if (pos < a.term_cap) {
+          a.done_idx64[pos] = (int64_t)k * a.n + i;
+#pragma unroll
+          for (int j = 0; j < Sys::O; ++j) static_cast<T*>(a.term_obs)[(int64_t)pos * Sys::O + j] = o[j];
+        }
+      } else {
+        a.done_idx32[pos] = (int32_t)i;
+#pragma unroll
+        for (int j = 0; j < Sys::O; ++j) static_cast<T*>(a.term_obs)[(int64_t)pos * Sys::O + j] = o[j];
+      }
+    }
+  }
+  if constexpr (kKeepTerm) {
+#pragma unroll
+    for (int j = 0; j < Sys::O; ++j) o_term[j] = o[j];
+  }
+  if (live && dflag && (a.flags & LZ_FLAG_AUTORESET)) {  // SB3 DummyVecEnv auto-reset
+    T v[Sys::NI];
+    Sys::draw(a, (uint64_t)(a.gid0 + i), tick, v);
+    sys.init(v, a);
+    sys.reset_obs(o);
+    steps = 0;
+    did_reset = true;
+  }
+  return dflag;
+}
+
+}  // namespace lz

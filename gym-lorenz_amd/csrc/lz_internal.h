@@ -50,6 +50,43 @@ struct KArgs {
   double prm[LZ_MAX_PARAMS];
 };
 
+// Policy-in-the-loop rollout (lz_policy.hip): SB3 ActorCriticPolicy (MlpPolicy,
+// net_arch pi=[128,128] vf=[128,128], Tanh, DiagGaussian) packed as bf16 MFMA
+// fragments.  Blob layout (bytes) -- produced by lz_policy_pack, read by the kernel:
+//   net 0 = policy (mlp_extractor.policy_net + action_net) at 0,
+//   net 1 = value (mlp_extractor.value_net + value_net) at kPolNet,
+//   log_std float[4] at kPolLogStd.
+// Per net: W1 A-fragments [4 out tiles][64 lanes] bf16x8, W2 [4][8 k-steps][64] bf16x8,
+// W3 [8 k-steps][64] bf16x8, biases as accumulator initialisers b1/b2 [4][2 halves][16]
+// f32 and b3 [2][16] f32 (see lz_policy.hip for the fragment index maps).
+constexpr int kPolHidden = 128;
+constexpr int kPolW1 = 0;
+constexpr int kPolW2 = kPolW1 + 4 * 64 * 16;
+constexpr int kPolW3 = kPolW2 + 4 * 8 * 64 * 16;
+constexpr int kPolB1 = kPolW3 + 8 * 64 * 16;
+constexpr int kPolB2 = kPolB1 + 4 * 2 * 16 * 4;
+constexpr int kPolB3 = kPolB2 + 4 * 2 * 16 * 4;
+constexpr int kPolNet = kPolB3 + 2 * 16 * 4;       // 46208 B
+constexpr int kPolLogStd = 2 * kPolNet;
+constexpr int kPolBlobBytes = kPolLogStd + 64;     // 92480 B (resident in LDS)
+constexpr int kPolMaxObs = 8, kPolMaxAct = 4;
+
+struct PArgs {
+  const uint8_t* blob;     // device copy of the packed policy
+  const float* obs_in;     // [N, O] raw observation at rollout start
+  float* obs_last;         // [N, O] raw observation after K steps
+  const double* norm;      // VecNormalize obs_rms: mean[O], var[O] (nullable)
+  double eps, clip;
+  float gamma;             // truncation bootstrap discount
+  float act_lo, act_hi;    // action-space clip before env.step
+  uint32_t pflags;         // LZ_POLICY_*
+  float* act;              // [K, N, A] sampled (unclipped) actions
+  float* logp;             // [K, N]
+  float* val;              // [K, N]
+  float* last_val;         // [N]
+  double* partials;        // [grid * waves][2 * O] obs moment partials (nullable)
+};
+
 // record the thread-local message lz_last_error() returns; returns s
 lz_status set_error(lz_status s, const char* msg);
 
@@ -57,5 +94,10 @@ lz_status set_error(lz_status s, const char* msg);
 int launch_reset(int system, int f64, const KArgs& a, void* stream);
 int launch_step(int system, int f64, const KArgs& a, void* stream);
 int launch_rollout(int system, int f64, const KArgs& a, void* stream);
+// grid = workgroups of kPolWaves waves; returns a hipError_t
+constexpr int kPolWaves = 8;
+int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, int grid, void* stream);
+int launch_policy_moments_final(const double* partials, int nparts, int width, double count,
+                                double* out, void* stream);
 
 }  // namespace lz

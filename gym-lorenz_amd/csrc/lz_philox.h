@@ -12,7 +12,7 @@
 
 namespace lz {
 
-enum : uint32_t { kPurposeReset = 1, kPurposeNoise = 2 };
+enum : uint32_t { kPurposeReset = 1, kPurposeNoise = 2, kPurposePolicy = 3 };
 
 struct U4 {
   uint32_t x, y, z, w;
@@ -60,6 +60,21 @@ __device__ __forceinline__ void normal3(uint64_t seed, uint64_t gid, uint64_t ti
   z[0] = r1 * c1;
   z[1] = r1 * s1;
   z[2] = r2 * c2;
+}
+
+// Four standard normals for the policy's Gaussian action sample (purpose 3).
+__device__ __forceinline__ void normal4(uint64_t seed, uint64_t gid, uint64_t tick, float z[4]) {
+  const U4 w = philox_block(seed, gid, kPurposePolicy, tick, 0);
+  const float u1 = (float)((w.x >> 8) + 1u) * 5.9604644775390625e-08f;
+  const float u3 = (float)((w.z >> 8) + 1u) * 5.9604644775390625e-08f;
+  const float r1 = sqrtf(-2.0f * logf(u1)), r2 = sqrtf(-2.0f * logf(u3));
+  float s1, c1, s2, c2;
+  sincospif(2.0f * u01f(w.y), &s1, &c1);
+  sincospif(2.0f * u01f(w.w), &s2, &c2);
+  z[0] = r1 * c1;
+  z[1] = r1 * s1;
+  z[2] = r2 * c2;
+  z[3] = r2 * s2;
 }
 
 }  // namespace lz

@@ -1,0 +1,466 @@
+// Policy in the loop: the SB3 actor-critic forward fused with the env
+// step in a K-step rollout, plus RolloutBuffer.compute_returns_and_advantage.
+//
+// What the reference's learners run per env step (stable-baselines3 2.7.1, absent
+// from the image; call sites code/lorenz_pmsm/train.py:155-178, code/lorenz_filter/
+// train.py:117-127, code/gym_try.py:106-116):
+//   OnPolicyAlgorithm.collect_rollouts:
+//     actions, values, log_probs = policy(obs)       ActorCriticPolicy.forward
+//     clipped = np.clip(actions, low, high); env.step(clipped)
+//     truncated & terminal_observation: rewards += gamma * V(terminal_obs)
+//     rollout_buffer.add(last_obs, actions, rewards, last_episode_starts, values, log_probs)
+//   ActorCriticPolicy (MlpPolicy, net_arch pi=[128,128] vf=[128,128], Tanh):
+//     latent_pi = tanh(W2 tanh(W1 obs + b1) + b2)   (mlp_extractor.policy_net)
+//     mean = action_net(latent_pi); DiagGaussian(mean, exp(log_std)): a = mean + std*z
+//     log_prob = sum_j Normal(mean_j, std_j).log_prob(a_j); value = value_net(latent_vf)
+//
+// MI355X mapping.  One wave owns a tile of 32 envs for all K steps.  Each 128-wide
+// layer is a chain of v_mfma_f32_32x32x16_bf16 with the WEIGHTS as the A operand
+// (32 output units x 16 inputs) and the ACTIVATIONS as the B operand (16 inputs x 32
+// envs): the f32 accumulator of layer l (output units in the 16 registers, env on the
+// lane) is, after tanh and a pairwise bf16 conversion, exactly the B fragment of layer
+// l+1 -- no LDS round trip, no lane shuffles.  The k order inside such a fragment is
+// permuted (register j of lane half h of k-step s holds unit 16s + 8(j>>2) + 4h + (j&3)
+// of its 32-unit tile), so the packer stores W2/W3 columns in that order.  Biases are
+// the accumulator initialisers.  All weights (92.5 KB as bf16 fragments) stay in LDS
+// for the whole launch; a workgroup is 8 waves on one CU.
+//   Per env-step: pi 6->128->128->A and vf 6->128->128->1 = 69 kFLOP useful (padded
+//   MFMA work 90 kFLOP: K=16 for the 6 inputs, M=32 for the heads); 512 tanh.
+// Lane halves: lanes l and l+32 hold the two k-halves of the same env column.  The env
+// step, the sample and every store run in the h = 0 half (the head's rows 0..3 land
+// there); the h = 1 half only contributes its MFMA operands (zero obs inputs).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "lz_body.h"
+#include "lz_internal.h"
+#include "lz_philox.h"
+#include "lz_systems.h"
+
+namespace lz {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// tanh(x) = 1 - 2 / (exp(2x) + 1): v_exp_f32 + v_rcp_f32; |error| <= 2e-7 over all x
+// (+-inf limits exact), far below the bf16 rounding every activation takes next.
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // 2 / ln 2
+  return fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+template <int S>
+__device__ __forceinline__ bf16x8 act8(const f32x16& c) {  // registers 8S..8S+7
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {  // one v_cvt_pk_bf16_f32 per pair (RNE)
+    const f32x2 t = {tanh_fast(c[8 * S + j]), tanh_fast(c[8 * S + j + 1])};
+    const bf16x2 b = __builtin_convertvector(t, bf16x2);
+    r[j] = b[0];
+    r[j + 1] = b[1];
+  }
+  return r;
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// One net (3 linear layers) on this wave's 32-env tile.  x = the layer-1 B fragment
+// (lane half 0: obs[0..7], half 1: zeros).  Returns the head accumulator: lane (env
+// l & 31, half h) register g = head row (g & 3) + 8 (g >> 2) + 4 h.
+__device__ __forceinline__ f32x16 mlp_tile(const uint8_t* net, bf16x8 x, int lane) {
+  // The weight fragments are loop-invariant LDS loads: without this barrier LLVM hoists
+  // all 44 of them (176 VGPRs per net) out of the step loop and spills.  Re-reading
+  // them from LDS every step costs ~0.7 KB/lane of LDS bandwidth, far from the limit.
+  asm volatile("" ::: "memory");
+  const int h = lane >> 5;
+  const bf16x8* w1 = reinterpret_cast<const bf16x8*>(net + kPolW1) + lane;
+  const bf16x8* w2 = reinterpret_cast<const bf16x8*>(net + kPolW2) + lane;
+  const bf16x8* w3 = reinterpret_cast<const bf16x8*>(net + kPolW3) + lane;
+  const f32x16* b1 = reinterpret_cast<const f32x16*>(net + kPolB1) + h;
+  const f32x16* b2 = reinterpret_cast<const f32x16*>(net + kPolB2) + h;
+  const f32x16* b3 = reinterpret_cast<const f32x16*>(net + kPolB3) + h;
+  bf16x8 h1[8];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f32x16 c = mfma(w1[t * 64], x, b1[2 * t]);
+    h1[2 * t] = act8<0>(c);
+    h1[2 * t + 1] = act8<1>(c);
+  }
+  // layer 2 tile by tile, each tile's two activation fragments consumed by the head
+  // at once (k-steps 2t, 2t+1): only 2 of layer 2's 8 fragments are ever live
+  f32x16 head = *b3;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    // the tile's 8 W2 fragments are issued together (32 VGPRs) so the MFMA chain
+    // does not pay one LDS round trip per MFMA; the barriers keep the loads of
+    // different tiles from piling up
+    asm volatile("" ::: "memory");
+    bf16x8 wf[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) wf[kk] = w2[(t * 8 + kk) * 64];
+    f32x16 c = b2[2 * t];
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) c = mfma(wf[kk], h1[kk], c);
+    head = mfma(w3[(2 * t) * 64], act8<0>(c), head);
+    head = mfma(w3[(2 * t + 1) * 64], act8<1>(c), head);
+  }
+  return head;
+}
+
+// VecNormalize.normalize_obs (float64, then float32 for the policy: obs_as_tensor)
+template <int O>
+__device__ __forceinline__ void normalize(const float* o, float* x, bool on, const double* mu,
+                                          const double* sd, double clip) {  // mu, sd: LDS
+#pragma unroll
+  for (int j = 0; j < O; ++j) {
+    if (!on) {
+      x[j] = o[j];
+      continue;
+    }
+    double v = ((double)o[j] - mu[j]) / sd[j];
+    v = v < -clip ? -clip : (v > clip ? clip : v);  // np.clip (NaN-propagating)
+    x[j] = (float)v;
+  }
+}
+
+template <int O>
+__device__ __forceinline__ bf16x8 obs_frag(const float* x, bool use) {
+  bf16x8 b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = (__bf16)((use && j < O) ? x[j < O ? j : 0] : 0.0f);
+  return b;
+}
+
+template <class Sys, int W>
+__global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
+  constexpr int O = Sys::O, A = Sys::A;
+  static_assert(O <= kPolMaxObs && A <= kPolMaxAct, "policy tile shape");
+  __shared__ __attribute__((aligned(64))) uint8_t s_blob[kPolBlobBytes];
+  __shared__ double s_norm[2 * kPolMaxObs];
+  __shared__ double s_mom[W * 32 * 2 * O];
+  const int tid = (int)threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, r = lane & 31;
+  {
+    const f4v* src = reinterpret_cast<const f4v*>(p.blob);
+    f4v* dst = reinterpret_cast<f4v*>(s_blob);
+    for (int v = tid; v < kPolBlobBytes / 16; v += W * 64) dst[v] = src[v];
+  }
+  if (tid < O) {  // VecNormalize: mean and sqrt(var + eps) per obs dim
+    s_norm[tid] = p.norm ? p.norm[tid] : 0.0;
+    s_norm[kPolMaxObs + tid] = p.norm ? sqrt(p.norm[O + tid] + p.eps) : 1.0;
+  }
+  const uint64_t tick = *a.tick_in;
+  if (blockIdx.x == 0 && tid == 0) {
+    *a.counter_next = 0;
+    *a.tick_out = tick + a.tick_adv;
+  }
+  __syncthreads();
+  const uint8_t* pi_net = s_blob;
+  const uint8_t* vf_net = s_blob + kPolNet;
+  // torch.distributions.Normal constants, computed by the packer: scale = exp(log_std),
+  // 2 * scale**2, log(scale) (LDS, wave-uniform broadcast reads)
+  const float* g_scale = reinterpret_cast<const float*>(s_blob + kPolLogStd) + 4;
+  const float* g_var2 = g_scale + 4;
+  const float* g_lscale = g_scale + 8;
+  const bool norm = p.norm != nullptr;
+  const double* mu = s_norm;
+  const double* sd = s_norm + kPolMaxObs;
+  const bool det = (p.pflags & LZ_POLICY_DETERMINISTIC) != 0;
+  const bool boot = (p.pflags & LZ_POLICY_BOOTSTRAP) != 0;
+  const float gamma = p.gamma;
+  // per-lane float64 obs-moment accumulators of the h = 0 lanes, in LDS
+  double* mom = s_mom + (wave * 32 + r) * (2 * O);
+  if (h == 0) {
+#pragma unroll
+    for (int j = 0; j < 2 * O; ++j) mom[j] = 0.0;
+  }
+
+  Sys sys;
+  sys.setup(a);
+  float* obs_buf = static_cast<float*>(a.obs);
+  float* rew_buf = static_cast<float*>(a.rew);
+  const int64_t ntiles = (a.n + 31) >> 5;
+  for (int64_t tile = (int64_t)blockIdx.x * W + wave; tile < ntiles; tile += (int64_t)gridDim.x * W) {
+    const int64_t i = tile * 32 + r;
+    const bool in = i < a.n;
+    const bool live = in && h == 0;
+    int32_t steps = 0;
+    bool any_reset = false;
+    float o[O];
+#pragma unroll
+    for (int j = 0; j < O; ++j) o[j] = 0.0f;
+    if (live) {
+      sys.load(a, i);
+      if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
+#pragma unroll
+      for (int j = 0; j < O; ++j) o[j] = p.obs_in[i * O + j];
+    }
+    for (int k = 0; k < a.K; ++k) {
+      const int64_t off = (int64_t)k * a.n + i;
+      float x[O];
+      normalize<O>(o, x, norm, mu, sd, p.clip);
+      const bf16x8 xb = obs_frag<O>(x, live);
+      const f32x16 pi = mlp_tile(pi_net, xb, lane);
+      const f32x16 vf = mlp_tile(vf_net, xb, lane);
+      float act_c[A];
+      if (live) {
+        float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (!det) normal4(a.seed, (uint64_t)(a.gid0 + i), tick + (uint64_t)k, z);
+        float lp = 0.0f;
+#pragma unroll
+        for (int j = 0; j < A; ++j) {
+          const float mean = pi[j];
+          const float aj = det ? mean : mean + z[j] * g_scale[j];  // Normal.rsample
+          const float d = aj - mean;
+          const float lpj = (-(d * d)) / g_var2[j] - g_lscale[j] - 0.91893853320467274f;
+          lp = j == 0 ? lpj : lp + lpj;
+          act_c[j] = clip(aj, p.act_lo, p.act_hi);
+          p.act[off * A + j] = aj;
+        }
+#pragma unroll
+        for (int j = 0; j < O; ++j) obs_buf[off * O + j] = x[j];
+        p.logp[off] = lp;
+        p.val[off] = vf[0];
+      }
+      float on[O], ot[O];
+      float rew = 0.0f;
+      bool did_reset;
+      const uint8_t df = step_body<Sys, float, true, true>(sys, steps, a, i, live, act_c,
+                                                           tick + (uint64_t)k, k, on, rew,
+                                                           did_reset, ot);
+      any_reset = any_reset || did_reset;
+      if (boot) {  // SB3: truncated (not terminated) -> rewards += gamma * V(terminal obs)
+        const bool bt = live && (df & LZ_DONE_TRUNCATED) && !(df & LZ_DONE_TERMINATED);
+        if (__ballot(bt) != 0ull) {  // wave-uniform branch
+          float xt[O];
+          normalize<O>(ot, xt, norm, mu, sd, p.clip);
+          const f32x16 vt = mlp_tile(vf_net, obs_frag<O>(xt, bt), lane);
+          if (bt) rew = rew + gamma * vt[0];
+        }
+      }
+      if (live) {
+        rew_buf[off] = rew;
+        a.done[off] = df;
+        if (p.partials) {
+#pragma unroll
+          for (int j = 0; j < O; ++j) {
+            const double v = (double)on[j];
+            mom[j] += v;
+            mom[O + j] += v * v;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < O; ++j) o[j] = on[j];
+    }
+    float x[O];
+    normalize<O>(o, x, norm, mu, sd, p.clip);
+    const f32x16 vl = mlp_tile(vf_net, obs_frag<O>(x, live), lane);
+    if (live) {
+      p.last_val[i] = vl[0];
+#pragma unroll
+      for (int j = 0; j < O; ++j) p.obs_last[i * O + j] = o[j];
+      sys.store(a, i);
+      if (any_reset) sys.store_autoreset_extra(a, i);
+      if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
+    }
+  }
+  if (p.partials) {  // fixed-order butterfly over the 32 h = 0 lanes: deterministic
+    double* dst = p.partials + ((int64_t)blockIdx.x * W + wave) * (2 * O);
+#pragma unroll
+    for (int j = 0; j < 2 * O; ++j) {
+      double v = h == 0 ? mom[j] : 0.0;
+#pragma unroll
+      for (int m = 16; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+      if (lane == 0) dst[j] = v;
+    }
+  }
+}
+
+// obs moments: out = (count, column sums, column sums of squares) from the per-wave
+// partials, summed in a fixed order.
+__global__ __launch_bounds__(256) void k_pol_moments_final(const double* part, int nparts, int width,
+                                                          double count, double* out) {
+  __shared__ double s[256];
+  for (int c = 0; c < width; ++c) {
+    double v = 0.0;
+    for (int q = (int)threadIdx.x; q < nparts; q += 256) v += part[(int64_t)q * width + c];
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int m = 128; m >= 1; m >>= 1) {
+      if ((int)threadIdx.x < m) s[threadIdx.x] += s[threadIdx.x + m];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) out[1 + c] = s[0];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = count;
+}
+
+// RolloutBuffer.compute_returns_and_advantage (SB3 2.7.1 common/buffers.py), float32:
+//   delta = rewards[t] + gamma * next_values * next_non_terminal - values[t]
+//   last_gae_lam = delta + gamma * gae_lambda * next_non_terminal * last_gae_lam
+//   returns = advantages + values
+// with next_non_terminal = 1 - episode_starts[t+1] = 1 - done[t].
+__global__ __launch_bounds__(256) void k_gae(int64_t n, int K, const float* rew, const float* val,
+                                            const uint8_t* done, const float* last_val, float gamma,
+                                            float gl, float* adv, float* ret) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float last = 0.0f;
+  for (int k = K - 1; k >= 0; --k) {
+    const int64_t off = (int64_t)k * n + i;
+    const float nnt = 1.0f - (done[off] ? 1.0f : 0.0f);
+    const float nv = k == K - 1 ? last_val[i] : val[off + n];
+    const float v = val[off];
+    const float delta = (rew[off] + (gamma * nv) * nnt) - v;
+    last = delta + (gl * nnt) * last;
+    adv[off] = last;
+    ret[off] = last + v;
+  }
+}
+
+template <class Sys>
+static int launch_pol(const KArgs& a, const PArgs& p, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((k_rollout_policy<Sys, kPolWaves>), dim3((unsigned)grid), dim3(kPolWaves * 64),
+                     0, s, a, p);
+  return (int)hipGetLastError();
+}
+
+int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, int grid, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (system) {
+    case LZ_SYS_LORENZ3: return launch_pol<SysL3<float>>(a, p, grid, s);
+    case LZ_SYS_LORENZ4: return launch_pol<SysL4<float>>(a, p, grid, s);
+    case LZ_SYS_PMSM: return launch_pol<SysPMSM>(a, p, grid, s);
+    case LZ_SYS_HR: return launch_pol<SysHR<float>>(a, p, grid, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+int launch_policy_moments_final(const double* partials, int nparts, int width, double count,
+                                double* out, void* stream) {
+  hipLaunchKernelGGL(k_pol_moments_final, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     partials, nparts, width, count, out);
+  return (int)hipGetLastError();
+}
+
+}  // namespace lz
+
+// ------------------------------------------------------------------ host-side C-ABI
+namespace {
+
+uint16_t bf16_rne(float f) {  // round to nearest even (= v_cvt_pk_bf16_f32, torch)
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) return (uint16_t)((u >> 16) | 0x40u);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// unit of a 128-wide input feeding k-step kk, element j, lane half h (see file header)
+inline int unit_of(int kk, int h, int j) {
+  return 32 * (kk >> 1) + 16 * (kk & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
+}
+// output row held by accumulator register g of lane half h within a 32-row tile
+inline int row_of(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
+
+void pack_net(uint8_t* net, int O, int rows3, const float* w1, const float* b1, const float* w2,
+              const float* b2, const float* w3, const float* b3) {
+  using lz::kPolHidden;
+  uint16_t* f1 = reinterpret_cast<uint16_t*>(net + lz::kPolW1);
+  uint16_t* f2 = reinterpret_cast<uint16_t*>(net + lz::kPolW2);
+  uint16_t* f3 = reinterpret_cast<uint16_t*>(net + lz::kPolW3);
+  float* c1 = reinterpret_cast<float*>(net + lz::kPolB1);
+  float* c2 = reinterpret_cast<float*>(net + lz::kPolB2);
+  float* c3 = reinterpret_cast<float*>(net + lz::kPolB3);
+  for (int lane = 0; lane < 64; ++lane) {
+    const int r = lane & 31, h = lane >> 5;
+    for (int j = 0; j < 8; ++j) {
+      for (int t = 0; t < 4; ++t) {  // layer 1: A[row r][k = 8h + j], natural k order
+        const int k = 8 * h + j;
+        f1[(t * 64 + lane) * 8 + j] = bf16_rne(k < O ? w1[(32 * t + r) * O + k] : 0.0f);
+      }
+      for (int t = 0; t < 4; ++t)
+        for (int kk = 0; kk < 8; ++kk)
+          f2[((t * 8 + kk) * 64 + lane) * 8 + j] =
+              bf16_rne(w2[(32 * t + r) * kPolHidden + unit_of(kk, h, j)]);
+      for (int kk = 0; kk < 8; ++kk)
+        f3[(kk * 64 + lane) * 8 + j] =
+            bf16_rne(r < rows3 ? w3[r * kPolHidden + unit_of(kk, h, j)] : 0.0f);
+    }
+  }
+  for (int h = 0; h < 2; ++h)
+    for (int g = 0; g < 16; ++g) {
+      for (int t = 0; t < 4; ++t) {
+        c1[(2 * t + h) * 16 + g] = b1[32 * t + row_of(g, h)];
+        c2[(2 * t + h) * 16 + g] = b2[32 * t + row_of(g, h)];
+      }
+      c3[h * 16 + g] = row_of(g, h) < rows3 ? b3[row_of(g, h)] : 0.0f;
+    }
+}
+
+lz_status pfail(lz_status s, const char* msg) {
+  return lz::set_error(s, msg);
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t lz_policy_blob_bytes(void) { return lz::kPolBlobBytes; }
+
+lz_status lz_policy_pack(const lz_mlp_policy* p, void* host_blob, int64_t cap) {
+  if (!p || !host_blob) return pfail(LZ_ERR_INVALID, "policy/blob is NULL");
+  if (cap < lz::kPolBlobBytes) return pfail(LZ_ERR_INVALID, "blob capacity too small");
+  if (p->obs_dim < 1 || p->obs_dim > lz::kPolMaxObs || p->act_dim < 1 || p->act_dim > lz::kPolMaxAct)
+    return pfail(LZ_ERR_UNSUPPORTED, "policy supports obs_dim 1..8 and act_dim 1..4");
+  const float* req[] = {p->pi_w1, p->pi_b1, p->pi_w2, p->pi_b2, p->vf_w1, p->vf_b1, p->vf_w2,
+                        p->vf_b2, p->act_w, p->act_b, p->val_w, p->val_b, p->log_std};
+  for (const float* q : req)
+    if (!q) return pfail(LZ_ERR_INVALID, "a policy weight pointer is NULL");
+  uint8_t* b = static_cast<uint8_t*>(host_blob);
+  std::memset(b, 0, lz::kPolBlobBytes);
+  pack_net(b, p->obs_dim, p->act_dim, p->pi_w1, p->pi_b1, p->pi_w2, p->pi_b2, p->act_w, p->act_b);
+  pack_net(b + lz::kPolNet, p->obs_dim, 1, p->vf_w1, p->vf_b1, p->vf_w2, p->vf_b2, p->val_w,
+           p->val_b);
+  // [log_std(4)][scale(4)][2 scale^2 (4)][log scale (4)]: torch Normal's
+  // scale = exp(log_std), var = scale**2 (the kernel divides by 2 * var), log(scale)
+  float* ls = reinterpret_cast<float*>(b + lz::kPolLogStd);
+  for (int j = 0; j < p->act_dim; ++j) {
+    const float sc = std::exp(p->log_std[j]);
+    ls[j] = p->log_std[j];
+    ls[4 + j] = sc;
+    ls[8 + j] = 2.0f * (sc * sc);
+    ls[12 + j] = std::log(sc);
+  }
+  return LZ_OK;
+}
+
+lz_status lz_gae(int64_t n, int32_t K, const float* rew, const float* values, const uint8_t* done,
+                 const float* last_values, double gamma, double gae_lambda, float* advantages,
+                 float* returns, int32_t device, void* stream) {
+  if (!rew || !values || !done || !last_values || !advantages || !returns)
+    return pfail(LZ_ERR_INVALID, "NULL buffer");
+  if (n < 0 || K < 1) return pfail(LZ_ERR_INVALID, "n >= 0 and K >= 1 required");
+  if (n == 0) return LZ_OK;
+  if (hipSetDevice(device) != hipSuccess) return pfail(LZ_ERR_HIP, "hipSetDevice failed");
+  // NumPy: python-float gamma * float32 array -> float32(gamma); gamma * gae_lambda is a
+  // python-float product rounded once to float32
+  hipLaunchKernelGGL(lz::k_gae, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), n, K, rew, values, done, last_values,
+                     (float)gamma, (float)(gamma * gae_lambda), advantages, returns);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pfail(LZ_ERR_HIP, hipGetErrorString(e));
+  return LZ_OK;
+}
+
+}  // extern "C"

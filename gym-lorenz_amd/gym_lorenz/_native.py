@@ -60,6 +60,45 @@ class LzInfo(ctypes.Structure):
     ]
 
 
+POLICY_DETERMINISTIC, POLICY_BOOTSTRAP = 1, 2
+POLICY_HIDDEN = 128
+
+
+class LzMlpPolicy(ctypes.Structure):
+    _fields_ = [("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32)] + [
+        (name, ctypes.c_void_p) for name in (
+            "pi_w1", "pi_b1", "pi_w2", "pi_b2", "vf_w1", "vf_b1", "vf_w2", "vf_b2",
+            "act_w", "act_b", "val_w", "val_b", "log_std")]
+
+
+class LzPolicyRolloutArgs(ctypes.Structure):
+    _fields_ = [
+        ("K", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("blob", ctypes.c_void_p),
+        ("obs_in", ctypes.c_void_p),
+        ("obs_last", ctypes.c_void_p),
+        ("obs_norm", ctypes.c_void_p),
+        ("norm_eps", ctypes.c_double),
+        ("clip_obs", ctypes.c_double),
+        ("gamma", ctypes.c_double),
+        ("act_low", ctypes.c_float),
+        ("act_high", ctypes.c_float),
+        ("obs_buf", ctypes.c_void_p),
+        ("act_buf", ctypes.c_void_p),
+        ("logp_buf", ctypes.c_void_p),
+        ("val_buf", ctypes.c_void_p),
+        ("rew_buf", ctypes.c_void_p),
+        ("done_buf", ctypes.c_void_p),
+        ("last_values", ctypes.c_void_p),
+        ("obs_moments", ctypes.c_void_p),
+        ("done_idx", ctypes.c_void_p),
+        ("terminal_obs", ctypes.c_void_p),
+        ("cap", ctypes.c_int64),
+        ("n_done", ctypes.c_void_p),
+    ]
+
+
 VP = ctypes.c_void_p
 _SIGS = {
     "lz_config_init": (ctypes.c_int, [ctypes.POINTER(LzConfig), ctypes.c_int32]),
@@ -88,6 +127,11 @@ _SIGS = {
                                         ctypes.c_double, ctypes.c_double]),
     "lz_returns_update": (ctypes.c_int, [VP, VP, ctypes.c_int32, VP, ctypes.c_int64, ctypes.c_double,
                                          ctypes.c_int32, ctypes.c_int32, VP]),
+    "lz_policy_blob_bytes": (ctypes.c_int64, []),
+    "lz_policy_pack": (ctypes.c_int, [ctypes.POINTER(LzMlpPolicy), VP, ctypes.c_int64]),
+    "lz_rollout_policy": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
+    "lz_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, ctypes.c_double,
+                              ctypes.c_double, VP, VP, ctypes.c_int32, VP]),
     "lz_last_error": (ctypes.c_char_p, []),
     "lz_abi_version": (ctypes.c_int32, []),
 }

@@ -1,0 +1,267 @@
+"""Policy in the loop: SB3 on-policy rollout collection fused on the GPU.
+
+The reference trains its envs with stable-baselines3 A2C / PPO ``"MlpPolicy"``
+actor-critics, ``net_arch=dict(pi=[128, 128], vf=[128, 128])`` with Tanh
+(code/lorenz_pmsm/train.py:155-178: A2C, n_steps=16, VecNormalize(norm_obs=True,
+norm_reward=False, clip_obs=10); code/lorenz_filter/train.py:117-127 and
+code/gym_try.py:106-116: PPO, n_steps=2048, gae_lambda=0.95; code/gym_run.py:79).
+SB3 then runs ``OnPolicyAlgorithm.collect_rollouts``: per step one policy forward on
+the host, one ``DummyVecEnv.step`` over the envs one at a time, a RolloutBuffer add,
+and finally ``RolloutBuffer.compute_returns_and_advantage``.
+
+``FusedRolloutCollector.collect(K)`` does all K steps in ONE kernel launch
+(``lz_rollout_policy``): the two 6->128->128 MLPs on bf16 MFMA with fp32
+accumulation, the Gaussian sample (Philox), the action-space clip, the env step with
+auto-reset, SB3's truncation bootstrap, and VecNormalize's observation normalisation
+(statistics frozen for the K steps and updated once from the K steps' moments).
+``compute_returns_and_advantage`` is ``lz_gae``.  The buffers come back as
+time-major device tensors in SB3's RolloutBuffer layout ([K, N, ...]).
+
+``ActorCriticMlp`` is a plain-torch restatement of SB3's ActorCriticPolicy for this
+net_arch (same state_dict keys, same orthogonal init) -- the weight source when SB3 is
+absent and the fp32 reference in the tests.  An SB3 policy's ``state_dict()`` can be
+passed to ``set_params`` directly.
+"""
+import ctypes
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from . import _native as nat
+from .registry import SPECS
+
+HIDDEN = nat.POLICY_HIDDEN
+
+KEYS = ("mlp_extractor.policy_net.0.weight", "mlp_extractor.policy_net.0.bias",
+        "mlp_extractor.policy_net.2.weight", "mlp_extractor.policy_net.2.bias",
+        "mlp_extractor.value_net.0.weight", "mlp_extractor.value_net.0.bias",
+        "mlp_extractor.value_net.2.weight", "mlp_extractor.value_net.2.bias",
+        "action_net.weight", "action_net.bias", "value_net.weight", "value_net.bias", "log_std")
+_FIELDS = ("pi_w1", "pi_b1", "pi_w2", "pi_b2", "vf_w1", "vf_b1", "vf_w2", "vf_b2",
+           "act_w", "act_b", "val_w", "val_b", "log_std")
+
+
+def action_bounds(system_name):
+    for spec in SPECS.values():
+        if spec.system_name == system_name:
+            return float(spec.act[0]), float(spec.act[1])
+    raise KeyError(system_name)
+
+
+class _MlpExtractor(nn.Module):
+    def __init__(self, obs_dim, hidden=HIDDEN):
+        super().__init__()
+        self.policy_net = nn.Sequential(nn.Linear(obs_dim, hidden), nn.Tanh(),
+                                        nn.Linear(hidden, hidden), nn.Tanh())
+        self.value_net = nn.Sequential(nn.Linear(obs_dim, hidden), nn.Tanh(),
+                                       nn.Linear(hidden, hidden), nn.Tanh())
+
+
+class ActorCriticMlp(nn.Module):
+    """SB3 ActorCriticPolicy (MlpPolicy, net_arch pi=[128,128] vf=[128,128], Tanh,
+    DiagGaussian, log_std_init=0, ortho_init=True) in plain torch, fp32."""
+
+    def __init__(self, obs_dim, act_dim, hidden=HIDDEN, log_std_init=0.0, seed=None):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed) if seed is not None else None
+        self.mlp_extractor = _MlpExtractor(obs_dim, hidden)
+        self.action_net = nn.Linear(hidden, act_dim)
+        self.value_net = nn.Linear(hidden, 1)
+        self.log_std = nn.Parameter(torch.ones(act_dim) * log_std_init)
+        # SB3 ActorCriticPolicy._build: orthogonal init, gains sqrt(2) / 0.01 / 1, zero bias
+        with torch.no_grad():
+            for mod, gain in ((self.mlp_extractor, math.sqrt(2)), (self.action_net, 0.01),
+                              (self.value_net, 1.0)):
+                for m in mod.modules():
+                    if isinstance(m, nn.Linear):
+                        nn.init.orthogonal_(m.weight, gain=gain, generator=g)
+                        m.bias.zero_()
+
+    def forward(self, obs):
+        """(mean actions, values) in fp32."""
+        mean = self.action_net(self.mlp_extractor.policy_net(obs))
+        value = self.value_net(self.mlp_extractor.value_net(obs)).flatten()
+        return mean, value
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+def reference_forward_bf16(state_dict, obs):
+    """The fused kernel's arithmetic restated in torch: bf16 operands (weights and each
+    layer's input activations rounded to bf16, round-to-nearest-even), fp32 bias and
+    accumulation.  Differs from the kernel only in fp32 summation order and the tanh
+    implementation (|err| <= 2e-7).  Returns (mean, value)."""
+    sd = {k: torch.as_tensor(np.asarray(_np(v)), dtype=torch.float32) for k, v in state_dict.items()}
+    x = _bf(torch.as_tensor(obs, dtype=torch.float32))
+
+    def net(prefix, w3, b3):
+        h = _bf(torch.tanh(x @ _bf(sd[prefix + ".0.weight"]).T + sd[prefix + ".0.bias"]))
+        h = _bf(torch.tanh(h @ _bf(sd[prefix + ".2.weight"]).T + sd[prefix + ".2.bias"]))
+        return h @ _bf(sd[w3]).T + sd[b3]
+
+    mean = net("mlp_extractor.policy_net", "action_net.weight", "action_net.bias")
+    value = net("mlp_extractor.value_net", "value_net.weight", "value_net.bias").flatten()
+    return mean, value
+
+
+def _np(v):
+    if isinstance(v, torch.Tensor):
+        return v.detach().to("cpu", torch.float32).numpy()
+    return np.asarray(v, np.float32)
+
+
+def pack_policy(state_dict, obs_dim, act_dim):
+    """lz_policy_pack: SB3 state_dict -> uint8 numpy blob (host; needs no GPU)."""
+    arrs = []
+    for key in KEYS:
+        if key not in state_dict:
+            raise KeyError("policy state_dict lacks %r (expected SB3 MlpPolicy with "
+                           "net_arch pi=[128,128] vf=[128,128])" % key)
+        arrs.append(np.ascontiguousarray(_np(state_dict[key]), dtype=np.float32))
+    shapes = [(HIDDEN, obs_dim), (HIDDEN,), (HIDDEN, HIDDEN), (HIDDEN,)] * 2 + [
+        (act_dim, HIDDEN), (act_dim,), (1, HIDDEN), (1,), (act_dim,)]
+    for key, a, shp in zip(KEYS, arrs, shapes):
+        if a.shape != shp:
+            raise ValueError("%s has shape %s, expected %s" % (key, a.shape, shp))
+    p = nat.LzMlpPolicy()
+    p.obs_dim, p.act_dim = int(obs_dim), int(act_dim)
+    for f, a in zip(_FIELDS, arrs):
+        setattr(p, f, a.ctypes.data)
+    blob = np.zeros(int(nat.lib.lz_policy_blob_bytes()), np.uint8)
+    nat.check(nat.lib.lz_policy_pack(ctypes.byref(p), blob.ctypes.data, blob.size))
+    return blob
+
+
+@dataclass
+class RolloutBatch:
+    """SB3 RolloutBuffer contents, time-major device tensors."""
+    observations: torch.Tensor   # [K, N, O] what the policy saw (normalised)
+    actions: torch.Tensor        # [K, N, A] unclipped samples
+    log_probs: torch.Tensor      # [K, N]
+    values: torch.Tensor         # [K, N]
+    rewards: torch.Tensor        # [K, N] (+ gamma * V(terminal obs) on truncation)
+    dones: torch.Tensor          # [K, N] uint8 LZ_DONE_* bits of each step
+    episode_starts: torch.Tensor  # [K, N] float32 (SB3 _last_episode_starts per step)
+    last_values: torch.Tensor    # [N] V(normalised last obs)
+    last_obs: torch.Tensor       # [N, O] raw
+    obs_moments: torch.Tensor = None  # [1 + 2 O] float64 or None
+    done_idx: torch.Tensor = None     # compact list k*N + env
+    terminal_obs: torch.Tensor = None
+    n_done: torch.Tensor = None
+    advantages: torch.Tensor = None
+    returns: torch.Tensor = None
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+class FusedRolloutCollector:
+    """OnPolicyAlgorithm.collect_rollouts over a BatchedEnv, one launch per rollout.
+
+    backend:       gym_lorenz.core.BatchedEnv (float32, autoreset)
+    state_dict:    SB3 ActorCriticPolicy / ActorCriticMlp state_dict
+    obs_rms:       gym_lorenz.vec_normalize.DeviceRunningMeanStd or None
+    training:      update obs_rms after each rollout (VecNormalize.training)
+    """
+
+    def __init__(self, backend, state_dict=None, gamma=0.99, gae_lambda=0.95, obs_rms=None,
+                 clip_obs=10.0, norm_eps=1e-8, training=True, bootstrap=True,
+                 deterministic=False, capture_terminal=0, group=None):
+        if backend.tdtype != torch.float32:
+            raise ValueError("the fused policy rollout runs float32 env handles")
+        self.env = backend
+        self.device = backend.device
+        self.n, self.O, self.A = backend.num_envs, backend.obs_dim, backend.action_dim
+        self.gamma, self.gae_lambda = float(gamma), float(gae_lambda)
+        self.obs_rms, self.clip_obs, self.norm_eps = obs_rms, float(clip_obs), float(norm_eps)
+        self.training, self.bootstrap, self.deterministic = training, bootstrap, deterministic
+        self.capture_terminal = int(capture_terminal)
+        self.group = group
+        self.act_low, self.act_high = action_bounds(backend.system_name)
+        self.blob = None
+        self.last_obs = None
+        self.last_episode_starts = torch.ones((self.n,), dtype=torch.float32, device=self.device)
+        if state_dict is not None:
+            self.set_params(state_dict)
+
+    def set_params(self, state_dict):
+        """Pack and upload the actor-critic weights (call after every optimizer step)."""
+        blob = pack_policy(state_dict, self.O, self.A)
+        self.blob = torch.from_numpy(blob).to(self.device)
+
+    def reset(self):
+        """VecEnv.reset(): fresh episodes; the next rollout starts from their obs."""
+        obs = self.env.reset()
+        self.last_obs = obs.clone()
+        self.last_episode_starts.fill_(1.0)
+        if self.obs_rms is not None and self.training:
+            self.obs_rms.update(self.last_obs, self.group)
+        return self.last_obs
+
+    def collect(self, K):
+        if self.blob is None:
+            raise RuntimeError("set_params() first")
+        if self.last_obs is None:
+            self.reset()
+        n, O, A, dev = self.n, self.O, self.A, self.device
+        f32 = torch.float32
+        obs_buf = torch.empty((K, n, O), dtype=f32, device=dev)
+        act_buf = torch.empty((K, n, A), dtype=f32, device=dev)
+        logp = torch.empty((K, n), dtype=f32, device=dev)
+        val = torch.empty((K, n), dtype=f32, device=dev)
+        rew = torch.empty((K, n), dtype=f32, device=dev)
+        done = torch.empty((K, n), dtype=torch.uint8, device=dev)
+        last_val = torch.empty((n,), dtype=f32, device=dev)
+        obs_last = torch.empty((n, O), dtype=f32, device=dev)
+        want_mom = self.obs_rms is not None and self.training
+        mom = torch.empty((1 + 2 * O,), dtype=torch.float64, device=dev) if want_mom else None
+        didx = tobs = ndone = None
+        if self.capture_terminal:
+            didx = torch.empty((self.capture_terminal,), dtype=torch.int64, device=dev)
+            tobs = torch.empty((self.capture_terminal, O), dtype=f32, device=dev)
+            ndone = torch.zeros((1,), dtype=torch.int32, device=dev)
+        r = nat.LzPolicyRolloutArgs()
+        r.K = int(K)
+        r.flags = ((nat.POLICY_DETERMINISTIC if self.deterministic else 0)
+                   | (nat.POLICY_BOOTSTRAP if self.bootstrap else 0))
+        r.blob, r.obs_in, r.obs_last = _p(self.blob), _p(self.last_obs), _p(obs_last)
+        r.obs_norm = _p(self.obs_rms.state) if self.obs_rms is not None else None
+        r.norm_eps, r.clip_obs, r.gamma = self.norm_eps, self.clip_obs, self.gamma
+        r.act_low, r.act_high = self.act_low, self.act_high
+        r.obs_buf, r.act_buf, r.logp_buf, r.val_buf = _p(obs_buf), _p(act_buf), _p(logp), _p(val)
+        r.rew_buf, r.done_buf, r.last_values = _p(rew), _p(done), _p(last_val)
+        r.obs_moments = _p(mom)
+        r.done_idx, r.terminal_obs, r.cap, r.n_done = _p(didx), _p(tobs), self.capture_terminal, _p(ndone)
+        nat.check(nat.lib.lz_rollout_policy(self.env._h, ctypes.byref(r)))
+        starts = torch.empty((K, n), dtype=f32, device=dev)
+        starts[0] = self.last_episode_starts
+        if K > 1:
+            starts[1:] = (done[:-1] != 0).to(f32)
+        self.last_episode_starts = (done[-1] != 0).to(f32)
+        self._keep = (self.blob, self.last_obs)  # alive until the stream consumed them
+        self.last_obs = obs_last
+        if want_mom:
+            if self.group is not None:
+                dist.all_reduce(mom, group=self.group)
+            nat.check(nat.lib.lz_rms_update(self.obs_rms._h, ctypes.c_void_p(mom.data_ptr())))
+        return RolloutBatch(obs_buf, act_buf, logp, val, rew, done, starts, last_val, obs_last,
+                            mom, didx, tobs, ndone)
+
+    def compute_returns_and_advantage(self, batch):
+        """RolloutBuffer.compute_returns_and_advantage(last_values, dones) on device."""
+        K, n = batch.rewards.shape
+        adv = torch.empty_like(batch.rewards)
+        ret = torch.empty_like(batch.rewards)
+        nat.check(nat.lib.lz_gae(n, K, _p(batch.rewards), _p(batch.values), _p(batch.dones),
+                                 _p(batch.last_values), self.gamma, self.gae_lambda, _p(adv), _p(ret),
+                                 self.device.index,
+                                 ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+        batch.advantages, batch.returns = adv, ret
+        return adv, ret

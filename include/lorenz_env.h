@@ -196,6 +196,93 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
                      void* rew_out, uint8_t* done_out, int64_t* done_idx_out,
                      void* terminal_obs_out, int64_t cap, int32_t* n_done_out);
 
+/* ------------------------------------------------------------------------------
+ * Policy in the loop.  The reference's learners drive these envs with
+ * stable-baselines3 A2C / PPO "MlpPolicy" actor-critics -- net_arch
+ * dict(pi=[128, 128], vf=[128, 128]), activation Tanh, DiagGaussian actions
+ * (code/lorenz_pmsm/train.py:155-178 A2C n_steps=16; code/lorenz_filter/train.py:
+ * 117-127 and code/gym_try.py:106-116 PPO n_steps=2048, gae_lambda=0.95;
+ * code/gym_run.py:79) -- stepping the env through DummyVecEnv one env at a time
+ * (SB3 2.7.1 OnPolicyAlgorithm.collect_rollouts + RolloutBuffer).  lz_rollout_policy
+ * fuses that whole collection loop into one launch: per step, the policy forward
+ * (bf16 MFMA, fp32 accumulate), the Gaussian sample, the action-space clip, the env
+ * step with auto-reset, and SB3's truncation bootstrap.  lz_gae is
+ * RolloutBuffer.compute_returns_and_advantage.
+ * ------------------------------------------------------------------------------ */
+#define LZ_POLICY_HIDDEN 128
+#define LZ_POLICY_DETERMINISTIC 1u /* action = mean (SB3 predict(deterministic=True)) */
+#define LZ_POLICY_BOOTSTRAP 2u     /* reward += gamma * V(terminal obs) when truncated */
+
+/* Float32 weights in torch nn.Linear layout ([out, in], row-major), host memory.
+ * Names are the SB3 ActorCriticPolicy state_dict keys. */
+typedef struct lz_mlp_policy {
+  int32_t obs_dim;     /* 1..8 */
+  int32_t act_dim;     /* 1..4 */
+  const float* pi_w1;  /* mlp_extractor.policy_net.0.weight [128, obs_dim] */
+  const float* pi_b1;  /* mlp_extractor.policy_net.0.bias   [128] */
+  const float* pi_w2;  /* mlp_extractor.policy_net.2.weight [128, 128] */
+  const float* pi_b2;  /* mlp_extractor.policy_net.2.bias   [128] */
+  const float* vf_w1;  /* mlp_extractor.value_net.0.weight  [128, obs_dim] */
+  const float* vf_b1;
+  const float* vf_w2;  /* mlp_extractor.value_net.2.weight  [128, 128] */
+  const float* vf_b2;
+  const float* act_w;  /* action_net.weight [act_dim, 128] */
+  const float* act_b;  /* action_net.bias   [act_dim] */
+  const float* val_w;  /* value_net.weight  [1, 128] */
+  const float* val_b;  /* value_net.bias    [1] */
+  const float* log_std; /* log_std [act_dim] */
+} lz_mlp_policy;
+
+/* Size of the packed policy blob (bf16 MFMA fragments + f32 biases). */
+int64_t lz_policy_blob_bytes(void);
+/* Pack *p into host_blob (host memory, cap >= lz_policy_blob_bytes()).  The caller
+ * copies the blob to the device (e.g. torch.uint8 CUDA tensor) for lz_rollout_policy.
+ * Host-only: needs no GPU. */
+lz_status lz_policy_pack(const lz_mlp_policy* p, void* host_blob, int64_t cap);
+
+typedef struct lz_policy_rollout_args {
+  int32_t K;                /* steps (SB3 n_steps) */
+  uint32_t flags;           /* LZ_POLICY_* */
+  const void* blob;         /* device copy of the packed policy */
+  const float* obs_in;      /* [N, O] raw obs the rollout starts from (SB3 _last_obs
+                               before normalisation) */
+  float* obs_last;          /* [N, O] raw obs after the K steps (may alias obs_in) */
+  const double* obs_norm;   /* VecNormalize obs_rms [mean(O), var(O)] (double, device) or
+                               NULL: the policy sees clip((o - mean)/sqrt(var + eps),
+                               +-clip_obs), frozen for the K steps */
+  double norm_eps, clip_obs;
+  double gamma;             /* LZ_POLICY_BOOTSTRAP discount */
+  float act_low, act_high;  /* action space Box bounds (np.clip before env.step) */
+  float* obs_buf;           /* [K, N, O] observations the policy saw (normalised) */
+  float* act_buf;           /* [K, N, A] sampled actions (unclipped, as SB3 stores) */
+  float* logp_buf;          /* [K, N] log pi(a|s) */
+  float* val_buf;           /* [K, N] V(s) */
+  float* rew_buf;           /* [K, N] rewards (+ bootstrap) */
+  uint8_t* done_buf;        /* [K, N] LZ_DONE_* bits of each step */
+  float* last_values;       /* [N] V(normalised obs_last) */
+  double* obs_moments;      /* device double [1 + 2*O]: (K*N, sums, sums of squares) of
+                               the raw step outputs -- what VecNormalize's K per-step
+                               obs_rms updates would see -- or NULL */
+  int64_t* done_idx;        /* compact list k*N + env (cap entries) or NULL */
+  float* terminal_obs;      /* [cap, O] raw pre-reset observations or NULL */
+  int64_t cap;
+  int32_t* n_done;          /* int32 [1] device or NULL */
+} lz_policy_rollout_args;
+
+/* K policy+env steps in one launch (float32 handles; env state and policy activations
+ * in registers, weights in LDS).  The Gaussian sample is Philox keyed by (seed,
+ * global env id, call counter + k), purpose 3.  The first call on a handle allocates
+ * a small scratch buffer for obs_moments (do not capture that first call). */
+lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r);
+
+/* SB3 RolloutBuffer.compute_returns_and_advantage over time-major [K, N] float32
+ * buffers (float32 arithmetic in NumPy's order): advantages and returns out.
+ * done = the done bytes of each step (episode_starts shifted by one). */
+lz_status lz_gae(int64_t n, int32_t K, const float* rew, const float* values,
+                 const uint8_t* done, const float* last_values, double gamma,
+                 double gae_lambda, float* advantages, float* returns, int32_t device,
+                 void* hip_stream);
+
 /* Copy one SoA state plane (N elements, T or int32 / float32 as listed above)
  * between the handle and a device buffer. */
 lz_status lz_get_state(lz_handle* h, int32_t plane, void* dst);

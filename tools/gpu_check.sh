@@ -45,6 +45,14 @@ for step in "$@"; do
       run cfg4_pmsm_262k 300 python bench.py --system pmsm --envs 262144 --steps 4000
       run cfg5_rollout_32k 300 python bench.py --mode rollout --K 2048 --envs 32768 --steps 16384
       run cfg5_rollout_262k 300 python bench.py --mode rollout --K 2048 --envs 262144 --steps 8192 ;;
+    policy_tests) run gpu_policy_tests 600 python -m pytest tests/test_gpu_policy.py -q -m gpu -p no:cacheprovider -s ;;
+    policy_bench)
+      run policy_pmsm_262k_K16 300 python bench.py --mode policy --system pmsm --envs 262144 --K 16 --steps 4096
+      run policy_pmsm_32k_K2048 300 python bench.py --mode policy --system pmsm --envs 32768 --K 2048 --steps 8192
+      run policy_l3_1M_K16 300 python bench.py --mode policy --system lorenz3 --envs 1048576 --K 16 --steps 1024 ;;
+    policy_prof)
+      export TMPDIR=/tmp
+      run policy_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/policy_prof -o run --output-format csv -- python bench.py --mode policy --system pmsm --envs 262144 --K 16 --steps 2048 ;;
     split) run ab_split 600 python tools/ab_split.py 131072 1048576 ;;
     dist2) LZ_BENCH_BACKEND=gloo run dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 500 --warmup 64 --envs 262144 ;;
     pmc)
