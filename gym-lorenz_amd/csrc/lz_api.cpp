@@ -433,8 +433,7 @@ lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r) {
   HIP_TRY(hipSetDevice(h->cfg.device));
   const int64_t n = h->cfg.num_envs;
   const int W = lz::kPolWaves;
-  const int64_t ntiles = (n + 31) / 32;
-  const int grid = (int)std::min<int64_t>(h->num_cus, (ntiles + W - 1) / W);
+  const int grid = lz::policy_grid(n, h->num_cus);
   const int O = h->desc.obs_dim;
   const int64_t need = (int64_t)grid * W * 2 * O;
   if (r->obs_moments && h->pol_part_n < need) {

@@ -96,6 +96,14 @@ int launch_step(int system, int f64, const KArgs& a, void* stream);
 int launch_rollout(int system, int f64, const KArgs& a, void* stream);
 // grid = workgroups of kPolWaves waves; returns a hipError_t
 constexpr int kPolWaves = 8;
+// envs per wave of the policy rollout: 64 (two 32-env MFMA column tiles, every lane
+// steps an env) once there are enough envs for 8 such waves per CU, else 32
+inline int policy_envs_per_wave(int64_t n) { return n >= 131072 ? 64 : 32; }
+inline int policy_grid(int64_t n, int num_cus) {
+  const int64_t e = policy_envs_per_wave(n);
+  const int64_t groups = ((n + e - 1) / e + kPolWaves - 1) / kPolWaves;
+  return (int)(groups < num_cus ? groups : num_cus);
+}
 int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, int grid, void* stream);
 int launch_policy_moments_final(const double* partials, int nparts, int width, double count,
                                 double* out, void* stream);

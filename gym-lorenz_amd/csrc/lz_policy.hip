@@ -139,15 +139,49 @@ __device__ __forceinline__ bf16x8 obs_frag(const float* x, bool use) {
   return b;
 }
 
-template <class Sys, int W>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// One net's forward for the wave's E envs (E = 32: lane r and r + 32 both stand for env
+// r; E = 64: lane l owns env l and the wave runs two 32-env MFMA column tiles, the
+// upper half's observations moved to the lower lanes for tile B and its results moved
+// back).  Each lane gets its own env's head rows 0..N-1 in out[] (E = 32: h = 0 lanes).
+template <int E, int O, int N>
+__device__ __forceinline__ void net_fwd(const uint8_t* net, const float* x, bool use, int lane,
+                                        float* out) {
+  const int h = lane >> 5;
+  const bf16x8 own = obs_frag<O>(x, use);
+  const bf16x8 zero = obs_frag<O>(x, false);
+  if constexpr (E == 32) {
+    const f32x16 c = mlp_tile(net, h == 0 ? own : zero, lane);
+#pragma unroll
+    for (int j = 0; j < N; ++j) out[j] = c[j];
+  } else {
+    const u32x4 ou = __builtin_bit_cast(u32x4, own);
+    u32x4 sw;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sw[q] = (uint32_t)__shfl_xor((int)ou[q], 32, 64);
+    const f32x16 ca = mlp_tile(net, h == 0 ? own : zero, lane);
+    const f32x16 cb = mlp_tile(net, h == 0 ? __builtin_bit_cast(bf16x8, sw) : zero, lane);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const float b = __shfl_xor(cb[j], 32, 64);
+      out[j] = h == 0 ? ca[j] : b;
+    }
+  }
+}
+
+template <class Sys, int W, int E>
 __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   constexpr int O = Sys::O, A = Sys::A;
   static_assert(O <= kPolMaxObs && A <= kPolMaxAct, "policy tile shape");
+  static_assert(E == 32 || E == 64, "envs per wave");
   __shared__ __attribute__((aligned(64))) uint8_t s_blob[kPolBlobBytes];
   __shared__ double s_norm[2 * kPolMaxObs];
-  __shared__ double s_mom[W * 32 * 2 * O];
+  __shared__ double s_mom[W * E * 2 * O];
   const int tid = (int)threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, r = lane & 31;
+  const int lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int slot = E == 64 ? lane : (lane & 31);  // this lane's env within the tile
+  const bool owner = E == 64 || h == 0;           // lanes that step an env
   {
     const f4v* src = reinterpret_cast<const f4v*>(p.blob);
     f4v* dst = reinterpret_cast<f4v*>(s_blob);
@@ -176,9 +210,9 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   const bool det = (p.pflags & LZ_POLICY_DETERMINISTIC) != 0;
   const bool boot = (p.pflags & LZ_POLICY_BOOTSTRAP) != 0;
   const float gamma = p.gamma;
-  // per-lane float64 obs-moment accumulators of the h = 0 lanes, in LDS
-  double* mom = s_mom + (wave * 32 + r) * (2 * O);
-  if (h == 0) {
+  // per-lane float64 obs-moment accumulators of the env-owning lanes, in LDS
+  double* mom = s_mom + (wave * E + slot) * (2 * O);
+  if (owner) {
 #pragma unroll
     for (int j = 0; j < 2 * O; ++j) mom[j] = 0.0;
   }
@@ -187,11 +221,10 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   sys.setup(a);
   float* obs_buf = static_cast<float*>(a.obs);
   float* rew_buf = static_cast<float*>(a.rew);
-  const int64_t ntiles = (a.n + 31) >> 5;
+  const int64_t ntiles = (a.n + E - 1) / E;
   for (int64_t tile = (int64_t)blockIdx.x * W + wave; tile < ntiles; tile += (int64_t)gridDim.x * W) {
-    const int64_t i = tile * 32 + r;
-    const bool in = i < a.n;
-    const bool live = in && h == 0;
+    const int64_t i = tile * E + slot;
+    const bool live = owner && i < a.n;
     int32_t steps = 0;
     bool any_reset = false;
     float o[O];
@@ -207,9 +240,13 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       const int64_t off = (int64_t)k * a.n + i;
       float x[O];
       normalize<O>(o, x, norm, mu, sd, p.clip);
-      const bf16x8 xb = obs_frag<O>(x, live);
-      const f32x16 pi = mlp_tile(pi_net, xb, lane);
-      const f32x16 vf = mlp_tile(vf_net, xb, lane);
+      if (live) {  // the observation the policy sees (SB3 rollout_buffer.add(_last_obs))
+#pragma unroll
+        for (int j = 0; j < O; ++j) obs_buf[off * O + j] = x[j];
+      }
+      float mean[A], val[1];
+      net_fwd<E, O, A>(pi_net, x, live, lane, mean);
+      net_fwd<E, O, 1>(vf_net, x, live, lane, val);
       float act_c[A];
       if (live) {
         float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -217,18 +254,15 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
         float lp = 0.0f;
 #pragma unroll
         for (int j = 0; j < A; ++j) {
-          const float mean = pi[j];
-          const float aj = det ? mean : mean + z[j] * g_scale[j];  // Normal.rsample
-          const float d = aj - mean;
+          const float aj = det ? mean[j] : mean[j] + z[j] * g_scale[j];  // Normal.rsample
+          const float d = aj - mean[j];
           const float lpj = (-(d * d)) / g_var2[j] - g_lscale[j] - 0.91893853320467274f;
           lp = j == 0 ? lpj : lp + lpj;
           act_c[j] = clip(aj, p.act_lo, p.act_hi);
           p.act[off * A + j] = aj;
         }
-#pragma unroll
-        for (int j = 0; j < O; ++j) obs_buf[off * O + j] = x[j];
         p.logp[off] = lp;
-        p.val[off] = vf[0];
+        p.val[off] = val[0];
       }
       float on[O], ot[O];
       float rew = 0.0f;
@@ -240,9 +274,9 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       if (boot) {  // SB3: truncated (not terminated) -> rewards += gamma * V(terminal obs)
         const bool bt = live && (df & LZ_DONE_TRUNCATED) && !(df & LZ_DONE_TERMINATED);
         if (__ballot(bt) != 0ull) {  // wave-uniform branch
-          float xt[O];
+          float xt[O], vt[1];
           normalize<O>(ot, xt, norm, mu, sd, p.clip);
-          const f32x16 vt = mlp_tile(vf_net, obs_frag<O>(xt, bt), lane);
+          net_fwd<E, O, 1>(vf_net, xt, bt, lane, vt);
           if (bt) rew = rew + gamma * vt[0];
         }
       }
@@ -261,9 +295,9 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
 #pragma unroll
       for (int j = 0; j < O; ++j) o[j] = on[j];
     }
-    float x[O];
+    float x[O], vl[1];
     normalize<O>(o, x, norm, mu, sd, p.clip);
-    const f32x16 vl = mlp_tile(vf_net, obs_frag<O>(x, live), lane);
+    net_fwd<E, O, 1>(vf_net, x, live, lane, vl);
     if (live) {
       p.last_val[i] = vl[0];
 #pragma unroll
@@ -273,13 +307,13 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
     }
   }
-  if (p.partials) {  // fixed-order butterfly over the 32 h = 0 lanes: deterministic
+  if (p.partials) {  // fixed-order butterfly over the wave: deterministic for a given grid
     double* dst = p.partials + ((int64_t)blockIdx.x * W + wave) * (2 * O);
 #pragma unroll
     for (int j = 0; j < 2 * O; ++j) {
-      double v = h == 0 ? mom[j] : 0.0;
+      double v = owner ? mom[j] : 0.0;
 #pragma unroll
-      for (int m = 16; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
       if (lane == 0) dst[j] = v;
     }
   }
@@ -330,8 +364,14 @@ __global__ __launch_bounds__(256) void k_gae(int64_t n, int K, const float* rew,
 
 template <class Sys>
 static int launch_pol(const KArgs& a, const PArgs& p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((k_rollout_policy<Sys, kPolWaves>), dim3((unsigned)grid), dim3(kPolWaves * 64),
-                     0, s, a, p);
+  // lz_config.reserved[0] bit 5 forces 32-env waves (A/B experiments); the kernel's
+  // grid-stride tile loop is correct for any grid
+  if (policy_envs_per_wave(a.n) == 64 && !(a.variant & 32))
+    hipLaunchKernelGGL((k_rollout_policy<Sys, kPolWaves, 64>), dim3((unsigned)grid),
+                       dim3(kPolWaves * 64), 0, s, a, p);
+  else
+    hipLaunchKernelGGL((k_rollout_policy<Sys, kPolWaves, 32>), dim3((unsigned)grid),
+                       dim3(kPolWaves * 64), 0, s, a, p);
   return (int)hipGetLastError();
 }
 
