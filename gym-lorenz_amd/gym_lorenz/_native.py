@@ -132,6 +132,8 @@ _SIGS = {
     "lz_rollout_policy": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
     "lz_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, ctypes.c_double,
                               ctypes.c_double, VP, VP, ctypes.c_int32, VP]),
+    "lz_frame_stack": (ctypes.c_int, [VP, VP, VP, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_int32, ctypes.c_int32, VP]),
     "lz_last_error": (ctypes.c_char_p, []),
     "lz_abi_version": (ctypes.c_int32, []),
 }

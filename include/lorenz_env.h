@@ -321,6 +321,21 @@ lz_status lz_returns_update(double* returns, const void* rew, int32_t dtype, con
                             int64_t n, double gamma, int32_t phase, int32_t device,
                             void* hip_stream);
 
+/* ------------------------------------------------------------------------------
+ * VecFrameStack(venv, n_stack) on the device (SB3 2.7.1 common/vec_env/
+ * stacked_observations.py StackedObservations, 1-D Box, channels-last), as the
+ * reference stacks 4 HR observations (code/lorenz_filter/train.py:113-115).
+ * stacked float32 [n, n_stack * obs_dim] (in place), obs float32 [n, obs_dim]:
+ *   reset != 0: stacked = 0, last obs_dim columns = obs          (reset())
+ *   reset == 0: shift left by obs_dim, rows with done[i] != 0 zeroed, then the last
+ *               obs_dim columns = obs                           (update())
+ * The stacked terminal observation of a done env is
+ * concat(stacked_before[i, obs_dim:], terminal_obs[i]) -- build it before this call.
+ * ------------------------------------------------------------------------------ */
+lz_status lz_frame_stack(float* stacked, const float* obs, const uint8_t* done, int64_t n,
+                         int32_t n_stack, int32_t obs_dim, int32_t reset, int32_t device,
+                         void* hip_stream);
+
 const char* lz_last_error(void);
 int32_t lz_abi_version(void);
 

@@ -174,3 +174,15 @@ def test_policy_structs_match_header(tmp_path):
             R.act_low.offset, R.cap.offset, R.n_done.offset]
     assert got == want
     assert nat.lib.lz_policy_blob_bytes() == 92480
+
+
+def test_sb3_framestack_restatement_hand_case():
+    from oracle.sb3_framestack import StackedObservations
+
+    so = StackedObservations(2, 3, 2)
+    st = so.reset(np.array([[1, 2], [3, 4]], np.float32))
+    assert st.tolist() == [[0, 0, 0, 0, 1, 2], [0, 0, 0, 0, 3, 4]]
+    infos = [{}, {"terminal_observation": np.array([9, 9], np.float32)}]
+    st, infos = so.update(np.array([[5, 6], [7, 8]], np.float32), np.array([False, True]), infos)
+    assert st.tolist() == [[0, 0, 1, 2, 5, 6], [0, 0, 0, 0, 7, 8]]
+    assert infos[1]["terminal_observation"].tolist() == [0, 0, 3, 4, 9, 9]
