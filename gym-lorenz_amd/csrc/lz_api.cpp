@@ -47,6 +47,10 @@ SysDesc describe(int system) {
     case LZ_SYS_LORENZ3: return {3, 3, 6, 3, 4, LZ_L3_STEP};
     case LZ_SYS_LORENZ4: return {8, 3, 8, 8, 9, LZ_L4_STEP};
     case LZ_SYS_PMSM: return {6, 2, 6, 6, 11, LZ_PMSM_STEP};
+    case LZ_SYS_T1: return {3, 2, 6, 3, 4, LZ_T1_STEP};
+    case LZ_SYS_T2: return {8, 3, 8, 8, 9, LZ_T2_STEP};
+    case LZ_SYS_TP: return {6, 2, 6, 6, 7, LZ_TP_STEP};
+    case LZ_SYS_SC: return {3, 2, 6, 3, 4, LZ_SC_STEP};
     default: return {6, 2, 6, 7, 10, LZ_HR_STEP};
   }
 }
@@ -122,6 +126,23 @@ lz_status lz_config_init(lz_config* cfg, int32_t system) {
       p[0] = 1.0; p[1] = 3.0; p[2] = 1.0; p[3] = 5.0; p[4] = 0.006; p[5] = 4.0; p[6] = 3.2;
       p[7] = -1.6; p[8] = 0.001; p[9] = 50.0; p[10] = 20.0; p[11] = 0.95; p[12] = 70.0;
       break;
+    case LZ_SYS_T1:  // lorenz_env_transient1.py:21-22 (clip), :38-39 (a, b), :84 (0.01), :100
+      p[0] = 5.46; p[1] = 20; p[3] = 0.01; p[4] = 10; p[5] = 10;
+      break;
+    case LZ_SYS_T2:  // lorenz_env_transient2.py:118-119, :133-137, :193 (0.001), :211 (100),
+                     // :192 (0.01), :235
+      p[0] = 30; p[1] = 1; p[2] = 36; p[3] = 0.001; p[4] = 2; p[5] = 5; p[6] = 0.5;
+      p[7] = 0.003; p[8] = 100; p[9] = 0.01;
+      break;
+    case LZ_SYS_TP:  // lorenz_env_transient_pmsm.py:22-23, :40-41, :91 (20), :97, :129, :86
+      p[0] = 5.46; p[1] = 20; p[2] = 20; p[3] = 0.01; p[4] = 2; p[5] = 5; p[6] = 3;
+      cfg->flags = LZ_FLAG_ADD_NOISE;
+      break;
+    case LZ_SYS_SC:  // lorenz_singlecontrol.py:100-101, :117-118, :121, :147, :154, :169
+      p[0] = 5.46; p[1] = 20; p[3] = 0.01; p[4] = 100; p[5] = 1000; p[6] = 3;
+      p[7] = 25; p[8] = 1; p[9] = -1;
+      cfg->flags = LZ_FLAG_ADD_NOISE;
+      break;
     default:
       return fail(LZ_ERR_INVALID, "unknown system %d", system);
   }
@@ -132,7 +153,7 @@ lz_status lz_create(const lz_config* cfg_in, lz_handle** out) {
   if (!cfg_in || !out) return fail(LZ_ERR_INVALID, "cfg/out is NULL");
   *out = nullptr;
   lz_config cfg = *cfg_in;
-  if (cfg.system < LZ_SYS_LORENZ3 || cfg.system > LZ_SYS_HR)
+  if (cfg.system < LZ_SYS_LORENZ3 || cfg.system > LZ_SYS_SC)
     return fail(LZ_ERR_INVALID, "unknown system %d", cfg.system);
   if (cfg.dtype != LZ_DTYPE_F32 && cfg.dtype != LZ_DTYPE_F64)
     return fail(LZ_ERR_INVALID, "unknown dtype %d", cfg.dtype);
@@ -173,7 +194,7 @@ lz_status lz_create(const lz_config* cfg_in, lz_handle** out) {
   // Python does, and record the step at which it fires (-1: never -- the case for the
   // reference constants).
   cfg.t_done_step = -1;
-  if (cfg.system == LZ_SYS_LORENZ3 || cfg.system == LZ_SYS_LORENZ4) {
+  if (cfg.system != LZ_SYS_PMSM && cfg.system != LZ_SYS_HR) {  // dt = p[3], T = p[5]
     const double dt = cfg.params[3], tend = cfg.params[5];
     double t = 0.0;
     for (int32_t k = 1; k <= 100000000; ++k) {
@@ -281,6 +302,10 @@ lz_status lz_get_info(const lz_handle* h, lz_info* info) {
       if (h->cfg.flags & LZ_FLAG_ADD_FILTER) sio += 2 * 2 * 4;  // filtered_action
       io = 2 * 4 + 6 * t + t + 1;
       break;
+    case LZ_SYS_T1: sio = 2 * 3 * t; io = 2 * 4 + 6 * t + t + 1; break;
+    case LZ_SYS_T2: sio = 2 * 8 * t; io = 3 * 4 + 8 * t + t + 1; break;
+    case LZ_SYS_TP: sio = 2 * 6 * t; io = 2 * 4 + 6 * t + t + 1; break;
+    case LZ_SYS_SC: sio = 2 * 3 * t; io = 6 * t + t + 1; break;  // no action
   }
   if (h->count_steps && h->cfg.system != LZ_SYS_PMSM) sio += 8;
   const int b = sio + io;
@@ -359,7 +384,8 @@ lz_status lz_step(lz_handle* h, const void* actions, const double* noise, void* 
                   int32_t* n_done_out) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_step before the first lz_reset");
-  const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4;  // L4 ignores its action
+  // LORENZ4 ignores its action, SC takes none
+  const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4 && h->cfg.system != LZ_SYS_SC;
   if ((needs_act && !actions) || !obs_out || !rew_out || !done_out)
     return fail(LZ_ERR_INVALID, "actions/obs_out/rew_out/done_out must be non-NULL");
   if ((done_idx_out == nullptr) != (terminal_obs_out == nullptr))
@@ -391,7 +417,7 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_rollout before the first lz_reset");
   if (K <= 0) return fail(LZ_ERR_INVALID, "K must be >= 1");
-  const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4;
+  const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4 && h->cfg.system != LZ_SYS_SC;
   if ((needs_act && !actions) || !obs_out || !rew_out || !done_out)
     return fail(LZ_ERR_INVALID, "actions/obs_out/rew_out/done_out must be non-NULL");
   if ((done_idx_out == nullptr) != (terminal_obs_out == nullptr))

@@ -384,12 +384,16 @@ __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
 // ------------------------------------------------------------------ launchers
 static inline int64_t grid_for(int64_t n) { return (n + kBlock - 1) / kBlock; }
 
-template <class Sys, typename T>
+// kVariants: instantiate the step-kernel tuning variants (A/B tools use LORENZ3 and
+// PMSM; the other systems always run the default variant)
+template <class Sys, typename T, bool kVariants = false>
 static int launch_all(int which, const KArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)grid_for(a.n)), block(kBlock);
   if (which == 0)
     hipLaunchKernelGGL((k_reset<Sys, T>), grid, block, 0, s, a);
-  else if (which == 1) {
+  else if (which == 1 && !kVariants) {
+    hipLaunchKernelGGL((k_step<Sys, T, 0>), grid, block, 0, s, a);
+  } else if (which == 1) {
     switch (a.variant & 31) {
 #define LZ_STEP_V(VV)                                                                   \
   case VV:                                                                              \
@@ -416,15 +420,27 @@ static int dispatch(int which, int system, int f64, const KArgs& a, void* stream
   switch (system) {
     case LZ_SYS_LORENZ3:
       return f64 ? launch_all<SysL3<double>, double>(which, a, s)
-                 : launch_all<SysL3<float>, float>(which, a, s);
+                 : launch_all<SysL3<float>, float, true>(which, a, s);
     case LZ_SYS_LORENZ4:
       return f64 ? launch_all<SysL4<double>, double>(which, a, s)
                  : launch_all<SysL4<float>, float>(which, a, s);
     case LZ_SYS_PMSM:
-      return launch_all<SysPMSM, float>(which, a, s);
+      return launch_all<SysPMSM, float, true>(which, a, s);
     case LZ_SYS_HR:
       return f64 ? launch_all<SysHR<double>, double>(which, a, s)
                  : launch_all<SysHR<float>, float>(which, a, s);
+    case LZ_SYS_T1:
+      return f64 ? launch_all<SysT1<double>, double>(which, a, s)
+                 : launch_all<SysT1<float>, float>(which, a, s);
+    case LZ_SYS_T2:
+      return f64 ? launch_all<SysT2<double>, double>(which, a, s)
+                 : launch_all<SysT2<float>, float>(which, a, s);
+    case LZ_SYS_TP:
+      return f64 ? launch_all<SysTP<double>, double>(which, a, s)
+                 : launch_all<SysTP<float>, float>(which, a, s);
+    case LZ_SYS_SC:
+      return f64 ? launch_all<SysSC<double>, double>(which, a, s)
+                 : launch_all<SysSC<float>, float>(which, a, s);
   }
   return (int)hipErrorInvalidValue;
 }

@@ -382,6 +382,10 @@ int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, int grid, 
     case LZ_SYS_LORENZ4: return launch_pol<SysL4<float>>(a, p, grid, s);
     case LZ_SYS_PMSM: return launch_pol<SysPMSM>(a, p, grid, s);
     case LZ_SYS_HR: return launch_pol<SysHR<float>>(a, p, grid, s);
+    case LZ_SYS_T1: return launch_pol<SysT1<float>>(a, p, grid, s);
+    case LZ_SYS_T2: return launch_pol<SysT2<float>>(a, p, grid, s);
+    case LZ_SYS_TP: return launch_pol<SysTP<float>>(a, p, grid, s);
+    case LZ_SYS_SC: return launch_pol<SysSC<float>>(a, p, grid, s);
   }
   return (int)hipErrorInvalidValue;
 }

@@ -437,4 +437,268 @@ struct SysHR {
   }
 };
 
+// ===========================================================================
+// Legacy, unregistered variants, fp64 in the reference.  Shared RHS
+// of the PMSM-form 3-state system (a = 5.46, b = 20):
+//   f = [(-x) + y*z, ((-y) - x*z) + b*z, a*(y - z)]   (python evaluation order)
+// ===========================================================================
+template <typename T>
+__device__ __forceinline__ void pmsm3_rhs(T x, T y, T z, T pa, T pb, T* f) {
+  f[0] = (-x) + y * z;
+  f[1] = ((-y) - x * z) + pb * z;
+  f[2] = pa * (y - z);
+}
+
+// T1 -- lorenz_env_transient1.py:18-104: one controlled system, additive actions
+// (clip +-10, np.float32) on x and y, Euler dt=0.01; the N(0,1) draw of :77 is unused.
+// params: a=5.46, b=20, -, dt=0.01, clip=10, T_end=10.  planes: x, y, z [, step]
+template <typename T>
+struct SysT1 {
+  static constexpr int A = 2, O = 6, NI = 3;
+  static constexpr bool kUsesAction = true, kNoise = false;
+  static constexpr int kStepPlane = LZ_T1_STEP;
+  T v[3];
+  T pa, pb, dt;
+  float cl;
+
+  __device__ void setup(const KArgs& a) {
+    pa = (T)a.prm[0]; pb = (T)a.prm[1]; dt = (T)a.prm[3]; cl = (float)a.prm[4];
+  }
+  __device__ void load(const KArgs& a, int64_t i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) v[j] = ld<T>(a.pl[j], i);
+  }
+  __device__ void store(const KArgs& a, int64_t i) const {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) st<T>(a.pl[j], i, v[j]);
+  }
+  __device__ void store_reset(const KArgs& a, int64_t i) const { store(a, i); }
+  __device__ void store_autoreset_extra(const KArgs&, int64_t) const {}
+  __device__ static void draw(const KArgs& a, uint64_t gid, uint64_t tick, T* w) {
+    for (int j = 0; j < 3; ++j) w[j] = Draw<T>::uniform(a.seed, gid, tick, j, (T)-30, (T)30);  // :43
+  }
+  __device__ void init(const T* w, const KArgs&) { v[0] = w[0]; v[1] = w[1]; v[2] = w[2]; }
+  __device__ void reset_obs(T* o) const {  // :44-57 [s, f(s)] - zeros(6)
+    T f[3];
+    pmsm3_rhs(v[0], v[1], v[2], pa, pb, f);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { o[j] = v[j] - (T)0; o[3 + j] = f[j] - (T)0; }
+  }
+  __device__ void noise_from_normals(const float*, double* nz) const { nz[0] = nz[1] = nz[2] = 0.0; }
+  __device__ bool step(const float* act, bool, const double*, T* o, T& rew, const KArgs&) {
+    const float u1 = clip(act[0], -cl, cl), u2 = clip(act[1], -cl, cl);  // :71-72
+    T f[3];
+    pmsm3_rhs(v[0], v[1], v[2], pa, pb, f);                              // :78-80
+    v[0] = (v[0] + f[0] * dt) + (T)u1;                                   // :84
+    v[1] = (v[1] + f[1] * dt) + (T)u2;                                   // :85
+    v[2] = v[2] + f[2] * dt;                                             // :86
+    reset_obs(o);                                                        // :88-97
+    rew = -((((T)0 + fabs(o[0])) + fabs(o[1])) + fabs(o[2]));            // :98
+    return false;                                                        // :100 never fires
+  }
+};
+
+// T2 -- lorenz_env_transient2.py:115-240: 4-state master/slave, actions (clip +-2,
+// np.float32, * 100 in float32) on slave x1, x2, x4, Euler dt=0.001; the N(0,0.5)
+// draw of :209 is unused; reward -S - S**(1/3).
+// params: a=30, b=1, c=36, dt=0.001, clip=2, T_end=5, d=0.5, h=0.003, gain=100, 0.01
+// planes: master x1..x4, slave x1..x4 [, step]
+template <typename T>
+struct SysT2 {
+  static constexpr int A = 3, O = 8, NI = 8;
+  static constexpr bool kUsesAction = true, kNoise = false;
+  static constexpr int kStepPlane = LZ_T2_STEP;
+  T m[4], s[4];
+  T pa, pb, pc, dt, pd, ph, dmp;
+  float cl, gain;
+
+  __device__ void setup(const KArgs& a) {
+    pa = (T)a.prm[0]; pb = (T)a.prm[1]; pc = (T)a.prm[2]; dt = (T)a.prm[3];
+    cl = (float)a.prm[4]; pd = (T)a.prm[6]; ph = (T)a.prm[7]; gain = (float)a.prm[8];
+    dmp = (T)a.prm[9];
+  }
+  __device__ void load(const KArgs& a, int64_t i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { m[j] = ld<T>(a.pl[j], i); s[j] = ld<T>(a.pl[4 + j], i); }
+  }
+  __device__ void store(const KArgs& a, int64_t i) const {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { st<T>(a.pl[j], i, m[j]); st<T>(a.pl[4 + j], i, s[j]); }
+  }
+  __device__ void store_reset(const KArgs& a, int64_t i) const { store(a, i); }
+  __device__ void store_autoreset_extra(const KArgs&, int64_t) const {}
+  // :145-148 / :189-192
+  __device__ void rhs(const T* x, T* f) const {
+    const T q = ((T)2 * x[3]) * x[3];
+    f[0] = pa * (q * (x[1] - x[0]) + pd * x[0]);
+    f[1] = pb * (q * (x[0] - x[1]) - x[2]);
+    f[2] = pc * (x[1] - ph * x[2]);
+    f[3] = (x[1] - x[0]) - dmp * x[3];
+  }
+  __device__ static void draw(const KArgs& a, uint64_t gid, uint64_t tick, T* w) {
+    for (int j = 0; j < 8; ++j) w[j] = Draw<T>::uniform(a.seed, gid, tick, j, (T)0, (T)5);  // :141-142
+  }
+  __device__ void init(const T* w, const KArgs&) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { m[j] = w[j]; s[j] = w[4 + j]; }
+  }
+  __device__ void reset_obs(T* o) const {  // :143-166 [m, f(m)] - [s, f(s)]
+    T fm[4], fs[4];
+    rhs(m, fm);
+    rhs(s, fs);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o[j] = m[j] - s[j]; o[4 + j] = fm[j] - fs[j]; }
+  }
+  __device__ void noise_from_normals(const float*, double* nz) const { nz[0] = nz[1] = nz[2] = 0.0; }
+  __device__ bool step(const float* act, bool, const double*, T* o, T& rew, const KArgs&) {
+    const float g1 = clip(act[0], -cl, cl) * gain;   // :182-184, :210-213 u*100 in f32
+    const float g2 = clip(act[1], -cl, cl) * gain;
+    const float g3 = clip(act[2], -cl, cl) * gain;
+    T f[4];
+    rhs(m, f);                                       // :189-192
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m[j] = m[j] + f[j] * dt;   // :193-196
+    rhs(s, f);                                       // :210-213
+    f[0] = f[0] + (T)g1;
+    f[1] = f[1] + (T)g2;
+    f[3] = f[3] + (T)g3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] = s[j] + f[j] * dt;   // :214-217
+    reset_obs(o);                                    // :198-227
+    const T S = ((((T)0 + fabs(o[0])) + fabs(o[1])) + fabs(o[2])) + fabs(o[3]);
+    const T r = (-S) - (T)pow((double)S, 1.0 / 3.0);  // :229
+    rew = r;
+    return r < (T)-1e6;                              // :235 (t == 5 never fires)
+  }
+};
+
+// TP -- lorenz_env_transient_pmsm.py:17-133: PMSM-form master/slave, actions (clip
+// +-2, * 20 in float32) and process noise N(0,3) (:86) on the slave, Euler dt=0.01,
+// reward -S - S**(1/10).  The reference always adds the noise (LZ_FLAG_ADD_NOISE is
+// this system's default).
+// params: a=5.46, b=20, gain=20, dt=0.01, clip=2, T_end=5, noise std=3
+// planes: master(3), slave(3) [, step]
+template <typename T>
+struct SysTP {
+  static constexpr int A = 2, O = 6, NI = 6;
+  static constexpr bool kUsesAction = true, kNoise = true;
+  static constexpr int kStepPlane = LZ_TP_STEP;
+  T m[3], s[3];
+  T pa, pb, dt;
+  float cl, gain;
+  double nstd;
+
+  __device__ void setup(const KArgs& a) {
+    pa = (T)a.prm[0]; pb = (T)a.prm[1]; gain = (float)a.prm[2]; dt = (T)a.prm[3];
+    cl = (float)a.prm[4]; nstd = a.prm[6];
+  }
+  __device__ void load(const KArgs& a, int64_t i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { m[j] = ld<T>(a.pl[j], i); s[j] = ld<T>(a.pl[3 + j], i); }
+  }
+  __device__ void store(const KArgs& a, int64_t i) const {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { st<T>(a.pl[j], i, m[j]); st<T>(a.pl[3 + j], i, s[j]); }
+  }
+  __device__ void store_reset(const KArgs& a, int64_t i) const { store(a, i); }
+  __device__ void store_autoreset_extra(const KArgs&, int64_t) const {}
+  __device__ static void draw(const KArgs& a, uint64_t gid, uint64_t tick, T* w) {
+    for (int j = 0; j < 6; ++j) w[j] = Draw<T>::uniform(a.seed, gid, tick, j, (T)-10, (T)10);  // :45-46
+  }
+  __device__ void init(const T* w, const KArgs&) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { m[j] = w[j]; s[j] = w[3 + j]; }
+  }
+  __device__ void reset_obs(T* o) const {  // :47-65
+    T fm[3], fs[3];
+    pmsm3_rhs(m[0], m[1], m[2], pa, pb, fm);
+    pmsm3_rhs(s[0], s[1], s[2], pa, pb, fs);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { o[j] = m[j] - s[j]; o[3 + j] = fm[j] - fs[j]; }
+  }
+  __device__ void noise_from_normals(const float* z, double* nz) const {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) nz[j] = nstd * (double)z[j];
+  }
+  __device__ bool step(const float* act, bool use_nz, const double* nz, T* o, T& rew,
+                       const KArgs&) {
+    const float g1 = clip(act[0], -cl, cl) * gain;   // :78-79, :91-92 u*20 in f32
+    const float g2 = clip(act[1], -cl, cl) * gain;
+    T f[3];
+    pmsm3_rhs(m[0], m[1], m[2], pa, pb, f);          // :87-89
+#pragma unroll
+    for (int j = 0; j < 3; ++j) m[j] = m[j] + f[j] * dt;   // :97-99
+    pmsm3_rhs(s[0], s[1], s[2], pa, pb, f);          // :91-93
+    f[0] = f[0] + (T)g1;
+    f[1] = f[1] + (T)g2;
+    if (use_nz) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) f[j] = f[j] + (T)nz[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) s[j] = s[j] + f[j] * dt;   // :101-103
+    reset_obs(o);                                    // :104-121
+    const T S = (((T)0 + fabs(o[0])) + fabs(o[1])) + fabs(o[2]);
+    const T r = (-S) - (T)pow((double)S, 0.1);       // :122
+    rew = r;
+    return r < (T)-1e6;                              // :129 (t == 5 never fires)
+  }
+};
+
+// SC -- lorenz_singlecontrol.py:97-172: a fixed-start ([25, 1, -1], :121) PMSM-form
+// system driven only by process noise N(0,3) on its derivatives (:147-153), no action
+// (step() takes none), Euler dt=0.01.  Noise is always on in the reference.
+// params: a=5.46, b=20, -, dt=0.01, clip=100, T_end=1000, noise std=3, x0, y0, z0
+// planes: x, y, z [, step]
+template <typename T>
+struct SysSC {
+  static constexpr int A = 2, O = 6, NI = 3;
+  static constexpr bool kUsesAction = false, kNoise = true;
+  static constexpr int kStepPlane = LZ_SC_STEP;
+  T v[3];
+  T pa, pb, dt;
+  double nstd;
+
+  __device__ void setup(const KArgs& a) {
+    pa = (T)a.prm[0]; pb = (T)a.prm[1]; dt = (T)a.prm[3]; nstd = a.prm[6];
+  }
+  __device__ void load(const KArgs& a, int64_t i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) v[j] = ld<T>(a.pl[j], i);
+  }
+  __device__ void store(const KArgs& a, int64_t i) const {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) st<T>(a.pl[j], i, v[j]);
+  }
+  __device__ void store_reset(const KArgs& a, int64_t i) const { store(a, i); }
+  __device__ void store_autoreset_extra(const KArgs&, int64_t) const {}
+  __device__ static void draw(const KArgs& a, uint64_t, uint64_t, T* w) {
+    w[0] = (T)a.prm[7]; w[1] = (T)a.prm[8]; w[2] = (T)a.prm[9];   // :121 fixed start
+  }
+  __device__ void init(const T* w, const KArgs&) { v[0] = w[0]; v[1] = w[1]; v[2] = w[2]; }
+  __device__ void reset_obs(T* o) const {  // :122-131
+    T f[3];
+    pmsm3_rhs(v[0], v[1], v[2], pa, pb, f);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { o[j] = v[j] - (T)0; o[3 + j] = f[j] - (T)0; }
+  }
+  __device__ void noise_from_normals(const float* z, double* nz) const {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) nz[j] = nstd * (double)z[j];
+  }
+  __device__ bool step(const float*, bool use_nz, const double* nz, T* o, T& rew, const KArgs&) {
+    T f[3];
+    pmsm3_rhs(v[0], v[1], v[2], pa, pb, f);          // :150-152
+    if (use_nz) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) f[j] = f[j] + (T)nz[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) v[j] = v[j] + f[j] * dt;   // :154-156
+    reset_obs(o);                                    // :158-164
+    rew = -((((T)0 + fabs(o[0])) + fabs(o[1])) + fabs(o[2]));   // :165
+    return false;                                    // :169 't == 1000' never fires
+  }
+};
+
 }  // namespace lz

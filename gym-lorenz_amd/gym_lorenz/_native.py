@@ -12,6 +12,7 @@ LIB_PATH = os.path.join(_HERE, "libgym_lorenz_amd.so")
 
 LZ_OK, LZ_ERR_INVALID, LZ_ERR_UNSUPPORTED, LZ_ERR_HIP, LZ_ERR_STATE, LZ_ERR_OOM = range(6)
 LORENZ3, LORENZ4, PMSM, HR = range(4)
+T1, T2, TP, SC = range(4, 8)  # legacy, unregistered variants
 F32, F64 = 0, 1
 FLAG_AUTORESET, FLAG_ADD_NOISE, FLAG_EVAL_MODE, FLAG_ADD_FILTER = 1, 2, 4, 8
 DONE_TERMINATED, DONE_TRUNCATED = 1, 2
@@ -22,6 +23,10 @@ L3_X, L3_Y, L3_Z, L3_STEP = 0, 1, 2, 3
 L4_M1, L4_S1, L4_STEP = 0, 4, 8
 PMSM_S1, PMSM_S2, PMSM_LAMBDA, PMSM_M, PMSM_V, PMSM_ADAM_STEP, PMSM_STEP = 0, 3, 6, 7, 8, 9, 10
 HR_M, HR_S, HR_SIGMA, HR_FA, HR_STEP = 0, 3, 6, 7, 9
+T1_X, T1_STEP = 0, 3
+T2_M1, T2_S1, T2_STEP = 0, 4, 8
+TP_M, TP_S, TP_STEP = 0, 3, 6
+SC_X, SC_STEP = 0, 3
 
 
 class LorenzEnvError(RuntimeError):

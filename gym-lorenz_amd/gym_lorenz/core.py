@@ -12,7 +12,10 @@ import torch
 
 from . import _native as nat
 
-SYSTEMS = {"lorenz3": nat.LORENZ3, "lorenz4": nat.LORENZ4, "pmsm": nat.PMSM, "hr": nat.HR}
+SYSTEMS = {"lorenz3": nat.LORENZ3, "lorenz4": nat.LORENZ4, "pmsm": nat.PMSM, "hr": nat.HR,
+           # legacy, unregistered variants of the reference
+           "transient1": nat.T1, "transient2": nat.T2, "transient_pmsm": nat.TP,
+           "singlecontrol": nat.SC}
 _TDTYPE = {nat.F32: torch.float32, nat.F64: torch.float64}
 
 
@@ -24,13 +27,14 @@ class BatchedEnv:
     """One handle = one shard of the env axis on one device and stream.
 
     Arguments mirror the reference constructors (``add_noise``, ``eval_mode``,
-    ``add_filter``, ``alpha``) plus the batching knobs.  ``dtype`` is the state /
+    ``add_filter``, ``alpha``) plus the batching knobs; ``add_noise=None`` keeps the
+    system's default (off, except the legacy TP / SC whose noise is unconditional).  ``dtype`` is the state /
     observation precision: "float64" reproduces the reference's fp64 arithmetic
     (LORENZ3 / LORENZ4 bit-exactly), "float32" is the fast path.  PMSM is float32.
     """
 
     def __init__(self, system, num_envs, dtype="float32", device=None, seed=0,
-                 global_env_offset=0, max_episode_steps=0, autoreset=True, add_noise=False,
+                 global_env_offset=0, max_episode_steps=0, autoreset=True, add_noise=None,
                  eval_mode=False, add_filter=False, alpha=None, params=None, compact=True,
                  variant=0):
         self.system = SYSTEMS[system] if isinstance(system, str) else int(system)
@@ -49,6 +53,8 @@ class BatchedEnv:
         cfg.seed = int(seed) & ((1 << 64) - 1)
         cfg.device = self.device.index
         cfg.max_episode_steps = int(max_episode_steps or 0)
+        if add_noise is None:  # the system's default (TP / SC: always noisy, as the reference)
+            add_noise = bool(cfg.flags & nat.FLAG_ADD_NOISE)
         cfg.flags = ((nat.FLAG_AUTORESET if autoreset else 0) | (nat.FLAG_ADD_NOISE if add_noise else 0)
                      | (nat.FLAG_EVAL_MODE if eval_mode else 0)
                      | (nat.FLAG_ADD_FILTER if add_filter else 0))
@@ -182,7 +188,9 @@ class BatchedEnv:
         if es == 0:
             raise ValueError("invalid state plane %d" % plane)
         int_planes = {nat.LORENZ3: (nat.L3_STEP,), nat.LORENZ4: (nat.L4_STEP,),
-                      nat.PMSM: (nat.PMSM_ADAM_STEP, nat.PMSM_STEP), nat.HR: (nat.HR_STEP,)}
+                      nat.PMSM: (nat.PMSM_ADAM_STEP, nat.PMSM_STEP), nat.HR: (nat.HR_STEP,),
+                      nat.T1: (nat.T1_STEP,), nat.T2: (nat.T2_STEP,), nat.TP: (nat.TP_STEP,),
+                      nat.SC: (nat.SC_STEP,)}
         if plane in int_planes[self.system]:
             return torch.int32
         return torch.float64 if es == 8 else torch.float32

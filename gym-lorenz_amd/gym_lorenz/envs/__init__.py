@@ -8,7 +8,10 @@ two different classes with that name.
 from .dynamic import lorenzEnv_transient as LorenzDynamicEnv
 from .lorenz_env_transient import lorenzEnv_transient
 from .lorenz_env_try import HRSyncEnv, hr_derivatives
+from .legacy import (LorenzSingleControlEnv, LorenzTransient1Env, LorenzTransient2Env,
+                     LorenzTransientPmsmEnv)
 from .lorenz_env_try_pmsm import PMSM_Sync_Env
 
 __all__ = ["HRSyncEnv", "PMSM_Sync_Env", "lorenzEnv_transient", "LorenzDynamicEnv",
-           "hr_derivatives"]
+           "hr_derivatives", "LorenzTransient1Env", "LorenzTransient2Env",
+           "LorenzTransientPmsmEnv", "LorenzSingleControlEnv"]

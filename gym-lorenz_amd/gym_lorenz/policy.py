@@ -32,7 +32,7 @@ import torch.distributed as dist
 from torch import nn
 
 from . import _native as nat
-from .registry import SPECS
+from .registry import LEGACY_SPECS, SPECS
 
 HIDDEN = nat.POLICY_HIDDEN
 
@@ -46,7 +46,7 @@ _FIELDS = ("pi_w1", "pi_b1", "pi_w2", "pi_b2", "vf_w1", "vf_b1", "vf_w2", "vf_b2
 
 
 def action_bounds(system_name):
-    for spec in SPECS.values():
+    for spec in list(SPECS.values()) + list(LEGACY_SPECS.values()):
         if spec.system_name == system_name:
             return float(spec.act[0]), float(spec.act[1])
     raise KeyError(system_name)

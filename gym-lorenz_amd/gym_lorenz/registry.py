@@ -53,9 +53,26 @@ SPECS = {
 }
 
 
+# The reference's unregistered env modules (no gym id there; addressed here by system
+# name, e.g. make_vec("transient_pmsm", N)): lorenz_env_transient1.py,
+# lorenz_env_transient2.py, lorenz_env_transient_pmsm.py, lorenz_singlecontrol.py
+LEGACY_SPECS = {
+    "transient1": EnvSpec("transient1", "gym_lorenz.envs.legacy:LorenzTransient1Env", nat.T1,
+                          "transient1", None, 6, (-10.0, 10.0, 2)),
+    "transient2": EnvSpec("transient2", "gym_lorenz.envs.legacy:LorenzTransient2Env", nat.T2,
+                          "transient2", None, 8, (-2.0, 2.0, 3)),
+    "transient_pmsm": EnvSpec("transient_pmsm", "gym_lorenz.envs.legacy:LorenzTransientPmsmEnv",
+                              nat.TP, "transient_pmsm", None, 6, (-2.0, 2.0, 2)),
+    "singlecontrol": EnvSpec("singlecontrol", "gym_lorenz.envs.legacy:LorenzSingleControlEnv",
+                             nat.SC, "singlecontrol", None, 6, (-100.0, 100.0, 2)),
+}
+
+
 def spec_for(env_id):
     if env_id in SPECS:
         return SPECS[env_id]
+    if env_id in LEGACY_SPECS:
+        return LEGACY_SPECS[env_id]
     for s in SPECS.values():  # also accept a system name
         if s.system_name == env_id:
             return s

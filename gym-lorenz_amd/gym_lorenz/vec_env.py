@@ -30,6 +30,10 @@ _STATE_ATTRS = {
                "current_step": (nat.PMSM_STEP, 1)},
     nat.HR: {"state_master": (nat.HR_M, 3), "state_slave": (nat.HR_S, 3),
              "sigma": (nat.HR_SIGMA, 1), "filtered_action": (nat.HR_FA, 2)},
+    nat.T1: {"state1": (nat.T1_X, 3)},
+    nat.T2: {"state1": (nat.T2_M1, 4), "state2": (nat.T2_S1, 4)},
+    nat.TP: {"state1": (nat.TP_M, 3), "state2": (nat.TP_S, 3)},
+    nat.SC: {"state1": (nat.SC_X, 3)},
 }
 
 
@@ -195,13 +199,18 @@ class LorenzVecEnv(VecEnvBase):
         if method_name.startswith("get_current") or method_name.startswith("_get_current"):
             k = method_name.rsplit("current", 1)[1]
             comp = int(k) if k else 0
-            if self.system == nat.LORENZ4:
-                m = self.backend.get_state(nat.L4_M1 + comp).cpu().numpy()
-                s = self.backend.get_state(nat.L4_S1 + comp).cpu().numpy()
+            # (master first plane, slave first plane or None: the reference's state2
+            # is an all-zero array for the single-system variants)
+            pairs = {nat.LORENZ4: (nat.L4_M1, nat.L4_S1), nat.LORENZ3: (nat.L3_X, None),
+                     nat.T1: (nat.T1_X, None), nat.T2: (nat.T2_M1, nat.T2_S1),
+                     nat.TP: (nat.TP_M, nat.TP_S), nat.SC: (nat.SC_X, None)}
+            if self.system in pairs:
+                mf, sf = pairs[self.system]
+                m = self.backend.get_state(mf + comp).cpu().numpy()
+                if sf is None:
+                    return [[m[i], 0] for i in idx]
+                s = self.backend.get_state(sf + comp).cpu().numpy()
                 return [[m[i], s[i]] for i in idx]
-            if self.system == nat.LORENZ3:  # state2 is all-zero in dynamic.py
-                m = self.backend.get_state(nat.L3_X + comp).cpu().numpy()
-                return [[m[i], 0] for i in idx]
         raise AttributeError("LorenzVecEnv: unsupported env_method %r" % method_name)
 
     def env_is_wrapped(self, wrapper_class, indices=None):

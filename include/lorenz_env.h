@@ -27,6 +27,9 @@
  *          (terminal observation kept, post-reset observation returned)
  *   lz_rollout
  *       -> K consecutive step() calls fused in one launch (state kept in VGPRs)
+ *   (legacy, unregistered: lorenz_env_transient1.py:18-104,
+ *    lorenz_env_transient2.py:115-240, lorenz_env_transient_pmsm.py:17-133,
+ *    lorenz_singlecontrol.py:97-172 -- LZ_SYS_T1 / T2 / TP / SC)
  *   lz_get_state / lz_set_state
  *       -> attribute access env.state1 / state2 / state_master / state_slave /
  *          lambda_coef ... used by code/lorenz_pmsm/test_evaluate.py:99-111
@@ -71,7 +74,12 @@ typedef enum lz_system {
   LZ_SYS_LORENZ3 = 0, /* dynamic.py: 3-state Lorenz, Euler dt=0.01, additive action */
   LZ_SYS_LORENZ4 = 1, /* lorenz_env_transient.py: 4-state master/slave, dt=0.001 */
   LZ_SYS_PMSM = 2,    /* lorenz_env_try_pmsm.py: PMSM sync, fp32, Adam dual lambda */
-  LZ_SYS_HR = 3       /* lorenz_env_try.py: Hindmarsh-Rose master/slave, RK4 */
+  LZ_SYS_HR = 3,      /* lorenz_env_try.py: Hindmarsh-Rose master/slave, RK4 */
+  /* legacy, unregistered variants (fp64 in the reference) */
+  LZ_SYS_T1 = 4,      /* lorenz_env_transient1.py: one PMSM-form system, additive actions */
+  LZ_SYS_T2 = 5,      /* lorenz_env_transient2.py: 4-state master/slave, dt=0.001 */
+  LZ_SYS_TP = 6,      /* lorenz_env_transient_pmsm.py: PMSM-form master/slave + noise */
+  LZ_SYS_SC = 7       /* lorenz_singlecontrol.py: fixed start, noise only, no action */
 } lz_system;
 
 typedef enum lz_dtype { LZ_DTYPE_F32 = 0, LZ_DTYPE_F64 = 1 } lz_dtype;
@@ -89,7 +97,13 @@ enum {
   LZ_PMSM_ADAM_STEP = 9, LZ_PMSM_STEP = 10,
   /* LZ_SYS_HR [state_master (3), state_slave (3), sigma: T;
    *            filtered_action (2): float32; step: int32] */
-  LZ_HR_M = 0, LZ_HR_S = 3, LZ_HR_SIGMA = 6, LZ_HR_FA = 7, LZ_HR_STEP = 9
+  LZ_HR_M = 0, LZ_HR_S = 3, LZ_HR_SIGMA = 6, LZ_HR_FA = 7, LZ_HR_STEP = 9,
+  /* legacy: LZ_SYS_T1 [state1 = x,y,z]; LZ_SYS_T2 [state1 (4), state2 (4)];
+   * LZ_SYS_TP [state1 (3), state2 (3)]; LZ_SYS_SC [state1 = x,y,z]  (all T) */
+  LZ_T1_X = 0, LZ_T1_STEP = 3,
+  LZ_T2_M1 = 0, LZ_T2_S1 = 4, LZ_T2_STEP = 8,
+  LZ_TP_M = 0, LZ_TP_S = 3, LZ_TP_STEP = 6,
+  LZ_SC_X = 0, LZ_SC_STEP = 3
 };
 
 /* done byte written per env by lz_step / lz_rollout */
@@ -122,7 +136,15 @@ typedef struct lz_config {
    *  PMSM:    sigma, gamma, dt, f_max, lambda_lr, beta1, beta2, eps, err_threshold,
    *           max_steps, term_threshold                    (lorenz_env_try_pmsm.py:12-50)
    *  HR:      a, b, c, d, r, s, I_bias, x_rest, dt, scale, master_scale,
-   *           action_alpha, term_threshold                 (lorenz_env_try.py:32-40) */
+   *           action_alpha, term_threshold                 (lorenz_env_try.py:32-40)
+   *  T1:      a, b, -, dt, action clip, T_end              (lorenz_env_transient1.py:21-39)
+   *  T2:      a, b, c, dt, action clip, T_end, d, h, action gain, x4 damping
+   *                                                        (lorenz_env_transient2.py:118-137)
+   *  TP:      a, b, action gain, dt, action clip, T_end, noise std
+   *                                                        (lorenz_env_transient_pmsm.py:22-41)
+   *  SC:      a, b, -, dt, action clip, T_end, noise std, x0, y0, z0
+   *                                                        (lorenz_singlecontrol.py:100-121)
+   * lz_config_init sets LZ_FLAG_ADD_NOISE for TP and SC (their noise is unconditional). */
   double params[LZ_MAX_PARAMS];
   /* LORENZ3/4 'done = (t == T)' on a float accumulator (dynamic.py:85-89): the host
    * replays the accumulator; the step index where it fires (-1 = never, which is the

@@ -365,7 +365,18 @@ void orc_reset_draw(int32_t system, int32_t f64, int64_t n, int64_t gid0, uint64
       case 0: nv = 3; lo = -30; hi = 30; break;  /* dynamic.py:62 */
       case 1: nv = 8; lo = 0; hi = 5; break;     /* lorenz_env_transient.py:277-278 */
       case 2: nv = 6; lo = -30; hi = 30; break;  /* lorenz_env_try_pmsm.py:64-65 */
-      default: nv = 7; lo = -10; hi = 20; break; /* lorenz_env_try.py:55-57 (+sigma) */
+      case 3: nv = 7; lo = -10; hi = 20; break;  /* lorenz_env_try.py:55-57 (+sigma) */
+      case 4: nv = 3; lo = -30; hi = 30; break;  /* lorenz_env_transient1.py:43 */
+      case 5: nv = 8; lo = 0; hi = 5; break;     /* lorenz_env_transient2.py:141-142 */
+      case 6: nv = 6; lo = -10; hi = 10; break;  /* lorenz_env_transient_pmsm.py:45-46 */
+      default: {                                 /* lorenz_singlecontrol.py:121 fixed */
+        const double x0[3] = {25.0, 1.0, -1.0};
+        for (int j = 0; j < 3; ++j) {
+          if (f64) ((double*)out)[i * 3 + j] = x0[j];
+          else ((float*)out)[i * 3 + j] = (float)x0[j];
+        }
+        continue;
+      }
     }
     for (int j = 0; j < nv; ++j) {
       double l = lo, h = hi;
@@ -400,3 +411,130 @@ int32_t orc_t_done_step(double dt, double t_end, int32_t max_k) {
   }
   return -1;
 }
+
+/* =========================================================================
+ * Legacy, unregistered variants (fp64 in the reference).  PMSM-form RHS
+ * f = [(-x) + y*z, ((-y) - x*z) + b*z, a*(y - z)]   (python evaluation order)
+ * ========================================================================= */
+#define LEGACY_BODY(T)                                                               \
+  static inline void p3_rhs_##T(const T* v, T a, T b, T* f) {                       \
+    f[0] = (-v[0]) + v[1] * v[2];                                                    \
+    f[1] = ((-v[1]) - v[0] * v[2]) + b * v[2];                                       \
+    f[2] = a * (v[1] - v[2]);                                                        \
+  }                                                                                  \
+  /* T1 -- lorenz_env_transient1.py:41-104; p = {a, b, -, dt, clip, T_end} */        \
+  void orc_t1_reset_obs_##T(int64_t n, const T* st, T* obs, const double* pd) {      \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      T f[3]; p3_rhs_##T(st + 3 * i, (T)pd[0], (T)pd[1], f);        /* :44-52 */     \
+      for (int j = 0; j < 3; ++j) { obs[6 * i + j] = st[3 * i + j] - (T)0;           \
+                                    obs[6 * i + 3 + j] = f[j] - (T)0; }              \
+    }                                                                                \
+  }                                                                                  \
+  void orc_t1_step_##T(int64_t n, T* st, const float* act, T* obs, T* rew,           \
+                       const double* pd) {                                           \
+    const T a = (T)pd[0], b = (T)pd[1], dt = (T)pd[3]; const float cl = (float)pd[4];\
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      T* v = st + 3 * i; T f[3];                                                     \
+      float u1 = clipf(act[2 * i], -cl, cl), u2 = clipf(act[2 * i + 1], -cl, cl); /* :71-72 */ \
+      p3_rhs_##T(v, a, b, f);                                       /* :78-80 */     \
+      v[0] = (v[0] + f[0] * dt) + (T)u1;                            /* :84 */        \
+      v[1] = (v[1] + f[1] * dt) + (T)u2;                            /* :85 */        \
+      v[2] = v[2] + f[2] * dt;                                      /* :86 */        \
+      p3_rhs_##T(v, a, b, f);                                       /* :88-91 */     \
+      T* o = obs + 6 * i;                                                            \
+      for (int j = 0; j < 3; ++j) { o[j] = v[j] - (T)0; o[3 + j] = f[j] - (T)0; }    \
+      rew[i] = -((((T)0 + (T)fabs(o[0])) + (T)fabs(o[1])) + (T)fabs(o[2])); /* :98 */\
+    }                                                                                \
+  }                                                                                  \
+  /* T2 -- lorenz_env_transient2.py:139-240;                                        \
+   * p = {a, b, c, dt, clip, T_end, d, h, gain, damping}; st row [m(4), s(4)] */     \
+  static inline void t2_rhs_##T(const T* x, const double* pd, T* f) {                \
+    const T q = ((T)2 * x[3]) * x[3];                                                \
+    f[0] = (T)pd[0] * (q * (x[1] - x[0]) + (T)pd[6] * x[0]);                         \
+    f[1] = (T)pd[1] * (q * (x[0] - x[1]) - x[2]);                                    \
+    f[2] = (T)pd[2] * (x[1] - (T)pd[7] * x[2]);                                      \
+    f[3] = (x[1] - x[0]) - (T)pd[9] * x[3];                                          \
+  }                                                                                  \
+  void orc_t2_reset_obs_##T(int64_t n, const T* st, T* obs, const double* pd) {      \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      const T* m = st + 8 * i; const T* s = m + 4; T fm[4], fs[4];                   \
+      t2_rhs_##T(m, pd, fm); t2_rhs_##T(s, pd, fs);                 /* :143-160 */   \
+      for (int j = 0; j < 4; ++j) { obs[8 * i + j] = m[j] - s[j];                    \
+                                    obs[8 * i + 4 + j] = fm[j] - fs[j]; }            \
+    }                                                                                \
+  }                                                                                  \
+  void orc_t2_step_##T(int64_t n, T* st, const float* act, T* obs, T* rew,           \
+                       uint8_t* done, const double* pd) {                            \
+    const T dt = (T)pd[3]; const float cl = (float)pd[4], g = (float)pd[8];         \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      T* m = st + 8 * i; T* s = m + 4; T f[4];                                       \
+      float g1 = clipf(act[3 * i], -cl, cl) * g;                    /* :182-184 */   \
+      float g2 = clipf(act[3 * i + 1], -cl, cl) * g;                /* u*100: f32 */ \
+      float g3 = clipf(act[3 * i + 2], -cl, cl) * g;                                 \
+      t2_rhs_##T(m, pd, f);                                         /* :189-192 */   \
+      for (int j = 0; j < 4; ++j) m[j] = m[j] + f[j] * dt;          /* :193-196 */   \
+      t2_rhs_##T(s, pd, f);                                         /* :210-213 */   \
+      f[0] = f[0] + (T)g1; f[1] = f[1] + (T)g2; f[3] = f[3] + (T)g3;                 \
+      for (int j = 0; j < 4; ++j) s[j] = s[j] + f[j] * dt;          /* :214-217 */   \
+      T fm[4], fs[4]; t2_rhs_##T(m, pd, fm); t2_rhs_##T(s, pd, fs);  /* :198-224 */  \
+      T* o = obs + 8 * i;                                                            \
+      for (int j = 0; j < 4; ++j) { o[j] = m[j] - s[j]; o[4 + j] = fm[j] - fs[j]; }  \
+      T S = (((((T)0 + (T)fabs(o[0])) + (T)fabs(o[1])) + (T)fabs(o[2])) +            \
+             (T)fabs(o[3]));                                                         \
+      /* :229 -S - S**(1/3): glibc pow as NumPy; the GPU's OCML pow may differ by */ \
+      /* an ulp, so the device reward is checked within a relative tolerance */       \
+      T r = (-S) - (T)pow((double)S, 1.0 / 3.0);                                     \
+      rew[i] = r;                                                                    \
+      done[i] = r < (T)-1e6 ? 1 : 0;                                /* :235 */       \
+    }                                                                                \
+  }                                                                                  \
+  /* TP -- lorenz_env_transient_pmsm.py:43-133; p = {a, b, gain, dt, clip, T_end,   \
+   * noise std}; st row [m(3), s(3)]; noise double [n,3] (the N(0,3) draw) or NULL */\
+  void orc_tp_reset_obs_##T(int64_t n, const T* st, T* obs, const double* pd) {      \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      const T* m = st + 6 * i; const T* s = m + 3; T fm[3], fs[3];                   \
+      p3_rhs_##T(m, (T)pd[0], (T)pd[1], fm); p3_rhs_##T(s, (T)pd[0], (T)pd[1], fs);  \
+      for (int j = 0; j < 3; ++j) { obs[6 * i + j] = m[j] - s[j];    /* :47-65 */    \
+                                    obs[6 * i + 3 + j] = fm[j] - fs[j]; }            \
+    }                                                                                \
+  }                                                                                  \
+  void orc_tp_step_##T(int64_t n, T* st, const float* act, const double* noise,      \
+                       T* obs, T* rew, uint8_t* done, const double* pd) {            \
+    const T a = (T)pd[0], b = (T)pd[1], dt = (T)pd[3];                               \
+    const float g = (float)pd[2], cl = (float)pd[4];                                 \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      T* m = st + 6 * i; T* s = m + 3; T f[3];                                       \
+      float g1 = clipf(act[2 * i], -cl, cl) * g;                    /* :78-79 */     \
+      float g2 = clipf(act[2 * i + 1], -cl, cl) * g;                /* u*20: f32 */  \
+      p3_rhs_##T(m, a, b, f);                                       /* :87-89 */     \
+      for (int j = 0; j < 3; ++j) m[j] = m[j] + f[j] * dt;          /* :97-99 */     \
+      p3_rhs_##T(s, a, b, f);                                       /* :91-93 */     \
+      f[0] = f[0] + (T)g1; f[1] = f[1] + (T)g2;                                      \
+      if (noise) for (int j = 0; j < 3; ++j) f[j] = f[j] + (T)noise[3 * i + j];      \
+      for (int j = 0; j < 3; ++j) s[j] = s[j] + f[j] * dt;          /* :101-103 */   \
+      T fm[3], fs[3]; p3_rhs_##T(m, a, b, fm); p3_rhs_##T(s, a, b, fs); /* :108-120 */\
+      T* o = obs + 6 * i;                                                            \
+      for (int j = 0; j < 3; ++j) { o[j] = m[j] - s[j]; o[3 + j] = fm[j] - fs[j]; }  \
+      T S = (((T)0 + (T)fabs(o[0])) + (T)fabs(o[1])) + (T)fabs(o[2]);                \
+      T r = (-S) - (T)pow((double)S, 0.1);                          /* :122 */     \
+      rew[i] = r;                                                                    \
+      done[i] = r < (T)-1e6 ? 1 : 0;                                /* :129 */       \
+    }                                                                                \
+  }                                                                                  \
+  /* SC -- lorenz_singlecontrol.py:120-172; p = {a, b, -, dt, clip, T_end, std, x0..}*/\
+  void orc_sc_step_##T(int64_t n, T* st, const double* noise, T* obs, T* rew,        \
+                       const double* pd) {                                           \
+    const T a = (T)pd[0], b = (T)pd[1], dt = (T)pd[3];                               \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      T* v = st + 3 * i; T f[3];                                                     \
+      p3_rhs_##T(v, a, b, f);                                       /* :150-152 */   \
+      if (noise) for (int j = 0; j < 3; ++j) f[j] = f[j] + (T)noise[3 * i + j];      \
+      for (int j = 0; j < 3; ++j) v[j] = v[j] + f[j] * dt;          /* :154-156 */   \
+      p3_rhs_##T(v, a, b, f);                                       /* :158-161 */   \
+      T* o = obs + 6 * i;                                                            \
+      for (int j = 0; j < 3; ++j) { o[j] = v[j] - (T)0; o[3 + j] = f[j] - (T)0; }    \
+      rew[i] = -((((T)0 + (T)fabs(o[0])) + (T)fabs(o[1])) + (T)fabs(o[2])); /* :165 */\
+    }                                                                                \
+  }
+LEGACY_BODY(double)
+LEGACY_BODY(float)

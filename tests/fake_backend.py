@@ -115,7 +115,8 @@ class FakeSingleCore:
     classes' host logic -- RNG draw order, attribute bookkeeping, API shapes -- can be
     checked against the golden fixtures without a GPU."""
 
-    PLANES = {0: 3, 1: 8, 2: 6, 3: 6}
+    PLANES = {0: 3, 1: 8, 2: 6, 3: 6, 4: 3, 5: 8, 6: 6, 7: 3}
+    LEGACY = {4: "t1", 5: "t2", 6: "tp", 7: "sc"}
 
     def __init__(self, system, dtype, device=None, alpha=0.5, add_noise=False, eval_mode=False,
                  add_filter=False):
@@ -128,6 +129,9 @@ class FakeSingleCore:
 
     def reset(self, init):
         init = np.asarray(init, self.dt).reshape(1, -1)
+        if self.system in self.LEGACY:
+            self.st[:] = init
+            return oracle.legacy_reset_obs(self.LEGACY[self.system], self.st)[0]
         if self.system == 0:
             self.st[:] = init
             return oracle.l3_reset_obs(self.st)[0]
@@ -145,6 +149,11 @@ class FakeSingleCore:
     def step(self, action, noise=None):
         a = np.asarray(action, np.float32).reshape(1, -1)
         with np.errstate(all="ignore"):
+            if self.system in self.LEGACY:
+                key = self.LEGACY[self.system]
+                nz = None if noise is None else np.asarray(noise, np.float64).reshape(1, 3)
+                o, r, d = oracle.legacy_step(key, self.st, None if key == "sc" else a, nz)
+                return o[0], r[0], int(d[0])
             if self.system == 0:
                 o, r = oracle.l3_step(self.st, a.astype(self.dt))
                 return o[0], r[0], 0

@@ -13,6 +13,9 @@ Fixtures (all arrays are what the reference itself returned / held):
   l4.npz    lorenz_env_transient.py:247 lorenzEnv_transient (4-state, fp64)
   pmsm.npz  lorenz_env_try_pmsm.py:7 PMSM_Sync_Env (fp32, Adam dual)
   hr.npz    lorenz_env_try.py:13 HRSyncEnv        (RK4 dt=0.001, fp64)
+  legacy.npz  the unregistered variants (fp64): lorenz_env_transient1.py:18 (t1_*),
+            lorenz_env_transient2.py:115 (t2_*), lorenz_env_transient_pmsm.py:17
+            (tp_*), lorenz_singlecontrol.py:97 (sc_*)
 """
 import importlib.util
 import os
@@ -53,6 +56,11 @@ class _GymnasiumEnv:  # gymnasium.Env.reset(seed) seeding semantics
 
 
 def _install_stubs():
+    # the legacy env modules import plotting / ODE helpers they never call
+    for name in ("matplotlib", "matplotlib.pyplot", "mpl_toolkits", "mpl_toolkits.mplot3d"):
+        m = types.ModuleType(name)
+        m.Axes3D = object
+        sys.modules.setdefault(name, m)
     spaces = types.ModuleType("spaces")
     spaces.Box = _Box
     for name, env in (("gym", _OldEnv), ("gymnasium", _GymnasiumEnv)):
@@ -270,8 +278,76 @@ def gen_hr(mod, n_steps=1000):
     print("hr", n, "envs; terminations", term.sum())
 
 
+# --------------------------------------------------------------------------- legacy
+def gen_legacy(n_steps=600):
+    """The four unregistered variants, each env seeded through np.random.seed(s) (they
+    draw from the global MT19937 stream); per-step noise recovered by replaying it."""
+    import contextlib
+    import io
+
+    out = {}
+    specs = {  # key: (file, module, n envs, action dim, action range, seeds)
+        "t1": ("lorenz_env_transient1.py", "ref_t1", 8, 2, 1.0, 300),
+        "t2": ("lorenz_env_transient2.py", "ref_t2", 8, 3, 2.5, 310),
+        "tp": ("lorenz_env_transient_pmsm.py", "ref_tp", 8, 2, 2.5, 320),
+        "sc": ("lorenz_singlecontrol.py", "ref_sc", 4, 0, 0.0, 330),
+    }
+    for key, (fname, modname, n, adim, arange, seed0) in specs.items():
+        mod = _load(fname, modname)
+        arng = np.random.default_rng(seed0)
+        acts = arng.uniform(-arange, arange, (n, n_steps, max(adim, 1))).astype(np.float32)
+        if key == "t1":  # exercise the +-10 clip on the first steps
+            acts[1, :3] = np.float32(25.0)
+            acts[2, :3] = np.float32(-25.0)
+        if key == "t2":  # the slave diverges under +-2 * 100 forcing: keep 6 envs gentle
+            acts[:6] *= np.float32(0.02)
+            acts[6, :2] = np.float32(3.0)  # clip
+        O = 8 if key == "t2" else 6
+        NI = {"t1": 3, "t2": 8, "tp": 6, "sc": 3}[key]
+        init = np.zeros((n, NI))
+        obs0 = np.zeros((n, O))
+        obs = np.zeros((n, n_steps, O))
+        rew = np.zeros((n, n_steps))
+        done = np.zeros((n, n_steps), bool)
+        noise = np.zeros((n, n_steps, 3))
+        for i in range(n):
+            s = seed0 + i
+            np.random.seed(s)
+            e = mod.lorenzEnv_transient()
+            with contextlib.redirect_stdout(io.StringIO()):
+                o = e.reset()
+            obs0[i] = o
+            if key in ("t1", "sc"):
+                init[i] = np.asarray(e.state1, np.float64)
+            elif key == "t2":
+                init[i, :4], init[i, 4:] = e.state1, np.asarray(e.state2[:4])
+            else:
+                init[i, :3], init[i, 3:] = e.state1, np.asarray(e.state2[:3])
+            if key in ("tp", "sc"):  # the per-step N(0,3) draws, replayed
+                st = np.random.get_state()
+                np.random.seed(s)
+                if key == "tp":
+                    np.random.uniform(-10, 10, 3)
+                    np.random.uniform(-10, 10, 3)
+                for k in range(n_steps):
+                    noise[i, k] = np.random.normal(0, 3, 3)
+                np.random.set_state(st)
+            with np.errstate(all="ignore"), contextlib.redirect_stdout(io.StringIO()):
+                for k in range(n_steps):
+                    o, r, d, _ = e.step() if key == "sc" else e.step(acts[i, k])
+                    obs[i, k], rew[i, k], done[i, k] = o, r, d
+        out.update({key + "_init": init, key + "_obs0": obs0, key + "_actions": acts,
+                    key + "_noise": noise, key + "_obs": obs, key + "_reward": rew,
+                    key + "_done": done})
+        print(key, n, "envs; done", done.sum(), "nonfinite", int((~np.isfinite(obs)).sum()))
+    np.savez_compressed(os.path.join(OUT, "legacy.npz"), **out)
+
+
 if __name__ == "__main__":
     _install_stubs()
+    if sys.argv[1:] == ["legacy"]:
+        gen_legacy()
+        sys.exit(0)
     gen_l3(_load("dynamic.py", "ref_dynamic"))
     gen_l4(_load("lorenz_env_transient.py", "ref_l4"))
     gen_pmsm(_load("lorenz_env_try_pmsm.py", "ref_pmsm"))

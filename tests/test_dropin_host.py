@@ -100,3 +100,34 @@ def test_pmsm_get_derivatives_helper_promotes_like_reference():
     d = env._get_derivatives(st, [0.5, -0.5], [0.1, 0.2, 0.3])
     assert d.dtype == np.float32
     assert d[0] == np.float32(-st[0] + st[1] * st[2] + np.float32(0.5) + 0.1)
+
+
+@pytest.mark.parametrize("key,cls", [("t1", "LorenzTransient1Env"), ("t2", "LorenzTransient2Env"),
+                                     ("tp", "LorenzTransientPmsmEnv"),
+                                     ("sc", "LorenzSingleControlEnv")])
+def test_legacy_classes_reproduce_reference(monkeypatch, key, cls):
+    """The unregistered variants: np.random.seed(s) + reset() + step() reproduce the
+    reference's golden trajectories (the host consumes the global RNG as the reference
+    does -- incl. the unused per-step normal draws of t1 / t2 -- and injects tp / sc's
+    process noise)."""
+    from gym_lorenz.envs import legacy
+
+    monkeypatch.setattr(legacy, "SingleEnvCore", FakeSingleCore)
+    g = golden("legacy")
+    seed0 = {"t1": 300, "t2": 310, "tp": 320, "sc": 330}[key]
+    for i in (0, 1):
+        np.random.seed(seed0 + i)
+        env = getattr(legacy, cls)()
+        o = env.reset()
+        assert bits_equal(o, g[key + "_obs0"][i])
+        for k in range(200):
+            if key == "sc":
+                o, r, d, info = env.step()
+            else:
+                o, r, d, info = env.step(g[key + "_actions"][i, k])
+            assert bits_equal(o, g[key + "_obs"][i, k]), k
+            assert bits_equal(r, g[key + "_reward"][i, k]), k
+            assert d == bool(g[key + "_done"][i, k]) and info == {}
+        assert env.observation_space.shape == (8 if key == "t2" else 6,)
+        m, s = env._get_current()
+        assert np.isfinite(m)

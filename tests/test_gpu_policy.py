@@ -72,6 +72,9 @@ def _clip_actions(pol, system, act):
     ("lorenz3", 2051, 12, dict(max_episode_steps=5)),
     ("hr", 640, 10, dict(add_noise=True, add_filter=True)),
     ("lorenz4", 333, 9, dict(max_episode_steps=4)),
+    ("transient2", 640, 8, dict(max_episode_steps=5)),
+    ("transient_pmsm", 500, 8, dict(max_episode_steps=3)),
+    ("singlecontrol", 300, 6, dict(max_episode_steps=4)),
 ])
 def test_policy_rollout_env_part_bitexact(gl, pol, system, n, K, kw):
     envp, envr = _twins(gl, system, n, seed=11, **kw)

@@ -158,3 +158,35 @@ def test_reset_draw_ranges(orc):
     # keyed by global id: a shard reproduces the slice of the full draw
     full = orc.reset_draw("l3", np.float32, 100, 0, 11, 5)
     assert np.array_equal(orc.reset_draw("l3", np.float32, 50, 50, 11, 5), full[50:])
+
+
+# ----------------------------------------------------------------- legacy variants
+def _legacy_init(g, key):
+    return np.ascontiguousarray(g[key + "_init"], np.float64)
+
+
+@pytest.mark.parametrize("key", ["t1", "t2", "tp", "sc"])
+def test_legacy_golden_bitexact(orc, key):
+    """The unregistered variants (lorenz_env_transient1/2.py, lorenz_env_transient_pmsm.py,
+    lorenz_singlecontrol.py), fp64: reset observation and every step bit-exact against
+    the reference's own outputs (tests/golden/legacy.npz), noise injected for TP / SC."""
+    g = golden("legacy")
+    st = _legacy_init(g, key)
+    assert bits_equal(orc.legacy_reset_obs(key, st), g[key + "_obs0"])
+    acts = g[key + "_actions"]
+    with np.errstate(all="ignore"):
+        for k in range(g[key + "_obs"].shape[1]):
+            a = None if key == "sc" else acts[:, k]
+            nz = g[key + "_noise"][:, k] if key in ("tp", "sc") else None
+            o, r, d = orc.legacy_step(key, st, a, nz)
+            assert bits_equal(o, g[key + "_obs"][:, k]), k
+            assert bits_equal(r, g[key + "_reward"][:, k]), k
+            assert np.array_equal(d, g[key + "_done"][:, k]), k
+
+
+def test_legacy_done_accumulators_never_fire(orc):
+    """'t == T' on the reference's float accumulators (t1 :99-100, t2 :230-235,
+    tp :124-129, sc :166-169) never holds exactly: t_done_step = -1."""
+    for key in ("t1", "t2", "tp", "sc"):
+        p = orc.PARAMS[key]
+        assert orc.t_done_step(p[3], p[5]) == -1, key
