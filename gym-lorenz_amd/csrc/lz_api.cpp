@@ -458,8 +458,8 @@ lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r) {
   if (!(r->act_low <= r->act_high)) return fail(LZ_ERR_INVALID, "act_low > act_high");
   HIP_TRY(hipSetDevice(h->cfg.device));
   const int64_t n = h->cfg.num_envs;
-  const int W = lz::kPolWaves;
-  const int grid = lz::policy_grid(n, h->num_cus);
+  const lz::PolShape sh = lz::policy_shape(n, h->cfg.reserved[0], h->num_cus);
+  const int W = sh.waves, grid = sh.grid;
   const int O = h->desc.obs_dim;
   const int64_t need = (int64_t)grid * W * 2 * O;
   if (r->obs_moments && h->pol_part_n < need) {
@@ -497,7 +497,7 @@ lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r) {
   p.val = r->val_buf;
   p.last_val = r->last_values;
   p.partials = r->obs_moments ? h->pol_part : nullptr;
-  int e = lz::launch_rollout_policy(h->cfg.system, a, p, grid, h->stream);
+  int e = lz::launch_rollout_policy(h->cfg.system, a, p, sh, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "policy rollout launch: %s", hipGetErrorString((hipError_t)e));
   if (r->obs_moments) {
     e = lz::launch_policy_moments_final(h->pol_part, grid * W, 2 * O, (double)r->K * (double)n,

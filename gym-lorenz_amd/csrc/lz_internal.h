@@ -94,17 +94,35 @@ lz_status set_error(lz_status s, const char* msg);
 int launch_reset(int system, int f64, const KArgs& a, void* stream);
 int launch_step(int system, int f64, const KArgs& a, void* stream);
 int launch_rollout(int system, int f64, const KArgs& a, void* stream);
-// grid = workgroups of kPolWaves waves; returns a hipError_t
-constexpr int kPolWaves = 8;
-// envs per wave of the policy rollout: 64 (two 32-env MFMA column tiles, every lane
-// steps an env) once there are enough envs for 8 such waves per CU, else 32
-inline int policy_envs_per_wave(int64_t n) { return n >= 131072 ? 64 : 32; }
-inline int policy_grid(int64_t n, int num_cus) {
-  const int64_t e = policy_envs_per_wave(n);
-  const int64_t groups = ((n + e - 1) / e + kPolWaves - 1) / kPolWaves;
-  return (int)(groups < num_cus ? groups : num_cus);
+// Launch shape of the policy rollout (one workgroup per CU: the weights fill LDS).
+//   >= 131,072 envs: 64 envs per wave (two 32-env MFMA column tiles, every lane steps
+//                    an env), 8 waves per workgroup (2 per SIMD);
+//   fewer, but enough for 2 waves per SIMD of 32 envs: 32 envs per wave, 8 waves;
+//   fewer still (e.g. cfg5's 32,768 envs per GPU): 32 envs per wave, 4 waves (one per
+//                    SIMD) running the policy and value nets interleaved in one
+//                    instruction stream for ILP, with the 512 registers one wave per
+//                    SIMD allows.
+// Measured (profiles/r01/policy/ab_shapes.json): 32,768 envs +56% for the interleaved
+// shape over 8 serial waves; 65,536 envs 8 serial waves +21% over it; 262,144 envs
+// 64-env waves +30% over it.  lz_config.reserved[0] bit 5 / bit 6 force the
+// (32, 8, serial) / interleaved shape (A/B experiments).  The kernel's grid-stride
+// tile loop is correct for any grid.
+struct PolShape {
+  int envs_per_wave, waves, pair, grid;
+};
+inline PolShape policy_shape(int64_t n, int variant, int num_cus) {
+  PolShape s;
+  const int64_t waves32 = (n + 31) / 32;
+  if (variant & 32) s = {32, 8, 0, 0};
+  else if ((variant & 64) || waves32 < 8 * (int64_t)num_cus) s = {32, 4, 1, 0};
+  else if (n < 131072) s = {32, 8, 0, 0};
+  else s = {64, 8, 0, 0};
+  const int64_t groups = ((n + s.envs_per_wave - 1) / s.envs_per_wave + s.waves - 1) / s.waves;
+  s.grid = (int)(groups < num_cus ? groups : num_cus);
+  return s;
 }
-int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, int grid, void* stream);
+int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, const PolShape& sh,
+                          void* stream);
 int launch_policy_moments_final(const double* partials, int nparts, int width, double count,
                                 double* out, void* stream);
 

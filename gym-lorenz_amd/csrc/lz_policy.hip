@@ -115,6 +115,58 @@ __device__ __forceinline__ f32x16 mlp_tile(const uint8_t* net, bf16x8 x, int lan
   return head;
 }
 
+// Both nets on the same 32-env tile in one instruction stream (layer by layer, tile by
+// tile): two independent MFMA / tanh chains the scheduler can interleave, for the
+// one-wave-per-SIMD small-batch shape where no other wave hides the latencies.
+__device__ __forceinline__ void mlp_pair(const uint8_t* na, const uint8_t* nb, bf16x8 x, int lane,
+                                         f32x16& head_a, f32x16& head_b) {
+  asm volatile("" ::: "memory");
+  const int h = lane >> 5;
+  const bf16x8* w1a = reinterpret_cast<const bf16x8*>(na + kPolW1) + lane;
+  const bf16x8* w1b = reinterpret_cast<const bf16x8*>(nb + kPolW1) + lane;
+  const bf16x8* w2a = reinterpret_cast<const bf16x8*>(na + kPolW2) + lane;
+  const bf16x8* w2b = reinterpret_cast<const bf16x8*>(nb + kPolW2) + lane;
+  const bf16x8* w3a = reinterpret_cast<const bf16x8*>(na + kPolW3) + lane;
+  const bf16x8* w3b = reinterpret_cast<const bf16x8*>(nb + kPolW3) + lane;
+  const f32x16* b1a = reinterpret_cast<const f32x16*>(na + kPolB1) + h;
+  const f32x16* b1b = reinterpret_cast<const f32x16*>(nb + kPolB1) + h;
+  const f32x16* b2a = reinterpret_cast<const f32x16*>(na + kPolB2) + h;
+  const f32x16* b2b = reinterpret_cast<const f32x16*>(nb + kPolB2) + h;
+  bf16x8 h1a[8], h1b[8];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f32x16 ca = mfma(w1a[t * 64], x, b1a[2 * t]);
+    const f32x16 cb = mfma(w1b[t * 64], x, b1b[2 * t]);
+    h1a[2 * t] = act8<0>(ca);
+    h1b[2 * t] = act8<0>(cb);
+    h1a[2 * t + 1] = act8<1>(ca);
+    h1b[2 * t + 1] = act8<1>(cb);
+  }
+  head_a = *(reinterpret_cast<const f32x16*>(na + kPolB3) + h);
+  head_b = *(reinterpret_cast<const f32x16*>(nb + kPolB3) + h);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    asm volatile("" ::: "memory");
+    bf16x8 wfa[8], wfb[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      wfa[kk] = w2a[(t * 8 + kk) * 64];
+      wfb[kk] = w2b[(t * 8 + kk) * 64];
+    }
+    f32x16 ca = b2a[2 * t], cb = b2b[2 * t];
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      ca = mfma(wfa[kk], h1a[kk], ca);
+      cb = mfma(wfb[kk], h1b[kk], cb);
+    }
+    head_a = mfma(w3a[(2 * t) * 64], act8<0>(ca), head_a);
+    head_b = mfma(w3b[(2 * t) * 64], act8<0>(cb), head_b);
+    head_a = mfma(w3a[(2 * t + 1) * 64], act8<1>(ca), head_a);
+    head_b = mfma(w3b[(2 * t + 1) * 64], act8<1>(cb), head_b);
+  }
+}
+
 // VecNormalize.normalize_obs (float64, then float32 for the policy: obs_as_tensor)
 template <int O>
 __device__ __forceinline__ void normalize(const float* o, float* x, bool on, const double* mu,
@@ -170,8 +222,9 @@ __device__ __forceinline__ void net_fwd(const uint8_t* net, const float* x, bool
   }
 }
 
-template <class Sys, int W, int E>
+template <class Sys, int W, int E, bool kPair>
 __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
+  static_assert(!kPair || E == 32, "the interleaved pair runs 32-env tiles");
   constexpr int O = Sys::O, A = Sys::A;
   static_assert(O <= kPolMaxObs && A <= kPolMaxAct, "policy tile shape");
   static_assert(E == 32 || E == 64, "envs per wave");
@@ -245,8 +298,16 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
         for (int j = 0; j < O; ++j) obs_buf[off * O + j] = x[j];
       }
       float mean[A], val[1];
-      net_fwd<E, O, A>(pi_net, x, live, lane, mean);
-      net_fwd<E, O, 1>(vf_net, x, live, lane, val);
+      if constexpr (kPair) {
+        f32x16 hp, hv;
+        mlp_pair(pi_net, vf_net, obs_frag<O>(x, live), lane, hp, hv);
+#pragma unroll
+        for (int j = 0; j < A; ++j) mean[j] = hp[j];
+        val[0] = hv[0];
+      } else {
+        net_fwd<E, O, A>(pi_net, x, live, lane, mean);
+        net_fwd<E, O, 1>(vf_net, x, live, lane, val);
+      }
       float act_c[A];
       if (live) {
         float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -363,19 +424,19 @@ __global__ __launch_bounds__(256) void k_gae(int64_t n, int K, const float* rew,
 }
 
 template <class Sys>
-static int launch_pol(const KArgs& a, const PArgs& p, int grid, hipStream_t s) {
-  // lz_config.reserved[0] bit 5 forces 32-env waves (A/B experiments); the kernel's
-  // grid-stride tile loop is correct for any grid
-  if (policy_envs_per_wave(a.n) == 64 && !(a.variant & 32))
-    hipLaunchKernelGGL((k_rollout_policy<Sys, kPolWaves, 64>), dim3((unsigned)grid),
-                       dim3(kPolWaves * 64), 0, s, a, p);
+static int launch_pol(const KArgs& a, const PArgs& p, const PolShape& sh, hipStream_t s) {
+  const dim3 grid((unsigned)sh.grid);
+  if (sh.envs_per_wave == 64)
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 64, false>), grid, dim3(8 * 64), 0, s, a, p);
+  else if (sh.pair)
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, true>), grid, dim3(4 * 64), 0, s, a, p);
   else
-    hipLaunchKernelGGL((k_rollout_policy<Sys, kPolWaves, 32>), dim3((unsigned)grid),
-                       dim3(kPolWaves * 64), 0, s, a, p);
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 32, false>), grid, dim3(8 * 64), 0, s, a, p);
   return (int)hipGetLastError();
 }
 
-int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, int grid, void* stream) {
+int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, const PolShape& grid,
+                          void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (system) {
     case LZ_SYS_LORENZ3: return launch_pol<SysL3<float>>(a, p, grid, s);

@@ -300,3 +300,28 @@ def test_policy_rollout_large_batch(gl, pol):
     boot = ((b.dones & 2) != 0) & ((b.dones & 1) == 0)
     assert torch.equal(b.rewards[~boot], rew_r[~boot])
     assert torch.isfinite(b.values).all() and torch.isfinite(b.log_probs).all()
+
+
+@pytest.mark.parametrize("n", [70000, 262144])
+def test_policy_launch_shapes_agree_bitwise(gl, pol, n):
+    """The three launch shapes (64-env waves / 32-env waves x 8 / 32-env waves x 4 with
+    interleaved nets, lz_internal.h policy_shape) run the same per-env arithmetic: every
+    output is bit-identical across them (only the moments' summation order differs)."""
+    from gym_lorenz.vec_normalize import DeviceRunningMeanStd
+
+    K = 5
+    outs = []
+    for var in (0, 32, 64):
+        env = gl.BatchedEnv("pmsm", n, seed=77, add_noise=True, max_episode_steps=3, variant=var)
+        _, sd = _random_policy(pol, 6, 2, seed=12, scale=0.2)
+        rms = DeviceRunningMeanStd(6, env.device)
+        rms.set_state(np.zeros(6), np.full(6, 40.0), 10.0)
+        col = pol.FusedRolloutCollector(env, sd, obs_rms=rms, training=True)
+        col.last_obs = env.reset().clone()
+        b = col.collect(K)
+        outs.append(b)
+    for b in outs[1:]:
+        for f in ("observations", "actions", "log_probs", "values", "rewards", "dones",
+                  "last_values", "last_obs"):
+            assert torch.equal(getattr(b, f), getattr(outs[0], f)), f
+        np.testing.assert_allclose(_np(b.obs_moments), _np(outs[0].obs_moments), rtol=1e-12)

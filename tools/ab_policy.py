@@ -1,5 +1,7 @@
-"""A/B of the fused policy rollout's wave layouts (interleaved, one process):
-E=64 (two 32-env MFMA column tiles per wave) vs E=32 (lz_config.reserved[0] bit 5)."""
+"""A/B of the fused policy rollout's launch shapes (interleaved, one process):
+variant 0 = the default shape for n (E=64 / 8 waves above 131,072 envs, else E=32 /
+4 waves with interleaved nets), 32 = E=32 / 8 waves serial nets, 64 = the small
+shape forced (lz_config.reserved[0] bits, lz_internal.h policy_shape)."""
 import json
 import os
 import sys
@@ -27,23 +29,24 @@ def timed(col, K, reps):
 
 def main():
     system = sys.argv[1] if len(sys.argv) > 1 else "pmsm"
-    K = 16
+    K = int(os.environ.get("AB_K", "16"))
+    variants = [int(v) for v in os.environ.get("AB_VARIANTS", "0,32").split(",")]
     out = {}
     for n in (int(v) for v in (sys.argv[2:] or ["262144", "1048576"])):
         cols = {}
-        for var in (0, 32):
+        for var in variants:
             env = gl.BatchedEnv(system, n, seed=0, variant=var, add_noise=(system == "pmsm"))
             net = ActorCriticMlp(env.obs_dim, env.action_dim, seed=0)
             c = FusedRolloutCollector(env, net.state_dict())
             c.reset()
             cols[var] = c
-        res = {0: [], 32: []}
+        res = {v: [] for v in variants}
         for _ in range(5):
-            for var in (0, 32):
-                res[var].append(timed(cols[var], K, 10))
-        for var in (0, 32):
+            for var in variants:
+                res[var].append(timed(cols[var], K, max(2, 160 // K)))
+        for var in variants:
             us = sorted(res[var])[len(res[var]) // 2]
-            out["%s n=%d E=%d" % (system, n, 64 if var == 0 and n >= 131072 else 32)] = {
+            out["%s n=%d K=%d variant=%d" % (system, n, K, var)] = {
                 "us_per_collect": us, "env_steps_per_s": n * K / us * 1e6}
     print(json.dumps(out, indent=1))
 
