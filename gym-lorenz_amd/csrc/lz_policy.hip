@@ -44,10 +44,13 @@ namespace lz {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// tanh(x) = 1 - 2 / (exp(2x) + 1): v_exp_f32 + v_rcp_f32; |error| <= 2e-7 over all x
-// (+-inf limits exact), far below the bf16 rounding every activation takes next.
-__device__ __forceinline__ float tanh_fast(float x) {
-  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // 2 / ln 2
+// tanh(x) = 1 - 2 / (exp(2x) + 1) = 1 - 2 / (2^(s x) + 1), s = 2 / ln 2: v_exp_f32 +
+// v_rcp_f32; |error| <= 2e-7 over all x (+-inf limits exact), far below the bf16
+// rounding every activation takes next.  The packer folds s into the tanh layers'
+// weights and biases (bf16(s W), s b), so the accumulator already holds s x and the
+// multiply is gone (one VALU op of five per activation).
+__device__ __forceinline__ float tanh_scaled(float sx) {
+  const float e = __builtin_amdgcn_exp2f(sx);
   return fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
 }
 
@@ -59,7 +62,7 @@ __device__ __forceinline__ bf16x8 act8(const f32x16& c) {  // registers 8S..8S+7
   bf16x8 r;
 #pragma unroll
   for (int j = 0; j < 8; j += 2) {  // one v_cvt_pk_bf16_f32 per pair (RNE)
-    const f32x2 t = {tanh_fast(c[8 * S + j]), tanh_fast(c[8 * S + j + 1])};
+    const f32x2 t = {tanh_scaled(c[8 * S + j]), tanh_scaled(c[8 * S + j + 1])};
     const bf16x2 b = __builtin_convertvector(t, bf16x2);
     r[j] = b[0];
     r[j + 1] = b[1];
@@ -471,6 +474,10 @@ uint16_t bf16_rne(float f) {  // round to nearest even (= v_cvt_pk_bf16_f32, tor
   return (uint16_t)(u >> 16);
 }
 
+// 2 / ln 2 as float: the tanh layers' weights and biases are packed pre-scaled by it
+// (bf16(s * W) in float32 arithmetic, s * b), see tanh_scaled
+constexpr float kTanhScale = 2.8853900817779268f;
+
 // unit of a 128-wide input feeding k-step kk, element j, lane half h (see file header)
 inline int unit_of(int kk, int h, int j) {
   return 32 * (kk >> 1) + 16 * (kk & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
@@ -492,12 +499,13 @@ void pack_net(uint8_t* net, int O, int rows3, const float* w1, const float* b1, 
     for (int j = 0; j < 8; ++j) {
       for (int t = 0; t < 4; ++t) {  // layer 1: A[row r][k = 8h + j], natural k order
         const int k = 8 * h + j;
-        f1[(t * 64 + lane) * 8 + j] = bf16_rne(k < O ? w1[(32 * t + r) * O + k] : 0.0f);
+        f1[(t * 64 + lane) * 8 + j] =
+            bf16_rne(k < O ? kTanhScale * w1[(32 * t + r) * O + k] : 0.0f);
       }
       for (int t = 0; t < 4; ++t)
         for (int kk = 0; kk < 8; ++kk)
           f2[((t * 8 + kk) * 64 + lane) * 8 + j] =
-              bf16_rne(w2[(32 * t + r) * kPolHidden + unit_of(kk, h, j)]);
+              bf16_rne(kTanhScale * w2[(32 * t + r) * kPolHidden + unit_of(kk, h, j)]);
       for (int kk = 0; kk < 8; ++kk)
         f3[(kk * 64 + lane) * 8 + j] =
             bf16_rne(r < rows3 ? w3[r * kPolHidden + unit_of(kk, h, j)] : 0.0f);
@@ -506,8 +514,8 @@ void pack_net(uint8_t* net, int O, int rows3, const float* w1, const float* b1, 
   for (int h = 0; h < 2; ++h)
     for (int g = 0; g < 16; ++g) {
       for (int t = 0; t < 4; ++t) {
-        c1[(2 * t + h) * 16 + g] = b1[32 * t + row_of(g, h)];
-        c2[(2 * t + h) * 16 + g] = b2[32 * t + row_of(g, h)];
+        c1[(2 * t + h) * 16 + g] = kTanhScale * b1[32 * t + row_of(g, h)];
+        c2[(2 * t + h) * 16 + g] = kTanhScale * b2[32 * t + row_of(g, h)];
       }
       c3[h * 16 + g] = row_of(g, h) < rows3 ? b3[row_of(g, h)] : 0.0f;
     }

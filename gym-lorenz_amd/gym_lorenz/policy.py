@@ -92,17 +92,26 @@ def _bf(t):
     return t.to(torch.bfloat16).to(torch.float32)
 
 
+# 2 / ln 2 in float32: lz_policy_pack stores the two tanh layers as bf16(s * W) and
+# s * b so that the kernel's tanh needs no multiply (lz_policy.hip tanh_scaled)
+TANH_SCALE = np.float32(2.8853900817779268)
+
+
 def reference_forward_bf16(state_dict, obs):
-    """The fused kernel's arithmetic restated in torch: bf16 operands (weights and each
+    """The fused kernel's arithmetic restated in torch: bf16 operands (the tanh layers'
+    weights as bf16(s W) with s = 2/ln 2 folded in, the head's as bf16(W), and each
     layer's input activations rounded to bf16, round-to-nearest-even), fp32 bias and
-    accumulation.  Differs from the kernel only in fp32 summation order and the tanh
-    implementation (|err| <= 2e-7).  Returns (mean, value)."""
+    accumulation, tanh(acc / s).  Differs from the kernel only in fp32 summation order
+    and the tanh implementation (|err| <= 2e-7).  Returns (mean, value)."""
     sd = {k: torch.as_tensor(np.asarray(_np(v)), dtype=torch.float32) for k, v in state_dict.items()}
     x = _bf(torch.as_tensor(obs, dtype=torch.float32))
+    s = torch.tensor(TANH_SCALE)
 
     def net(prefix, w3, b3):
-        h = _bf(torch.tanh(x @ _bf(sd[prefix + ".0.weight"]).T + sd[prefix + ".0.bias"]))
-        h = _bf(torch.tanh(h @ _bf(sd[prefix + ".2.weight"]).T + sd[prefix + ".2.bias"]))
+        h = x
+        for layer in (".0", ".2"):
+            acc = h @ _bf(s * sd[prefix + layer + ".weight"]).T + s * sd[prefix + layer + ".bias"]
+            h = _bf(torch.tanh(acc / s))
         return h @ _bf(sd[w3]).T + sd[b3]
 
     mean = net("mlp_extractor.policy_net", "action_net.weight", "action_net.bias")

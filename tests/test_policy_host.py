@@ -56,8 +56,10 @@ def _mfma(a, b, c):
 
 
 def _act(c):
-    """tanh, then registers 8s..8s+7 -> bf16 B fragment of k-step s."""
-    t = _bf16(np.tanh(c.astype(np.float64)).astype(np.float32))
+    """tanh of the pre-scaled accumulator (the packer folds s = 2/ln 2 into the tanh
+    layers), then registers 8s..8s+7 -> bf16 B fragment of k-step s."""
+    t = _bf16(np.tanh(c.astype(np.float64) / np.float64(np.float32(2.8853900817779268)))
+              .astype(np.float32))
     return [t[:, 0:8], t[:, 8:16]]
 
 
