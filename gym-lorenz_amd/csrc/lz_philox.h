@@ -62,6 +62,18 @@ __device__ __forceinline__ void normal3(uint64_t seed, uint64_t gid, uint64_t ti
   z[2] = r2 * c2;
 }
 
+// Two standard normals for the policy's Gaussian action sample (purpose 3): the first
+// Box-Muller pair of normal4 (identical values), for action dims <= 2.
+__device__ __forceinline__ void normal2(uint64_t seed, uint64_t gid, uint64_t tick, float z[4]) {
+  const U4 w = philox_block(seed, gid, kPurposePolicy, tick, 0);
+  const float u1 = (float)((w.x >> 8) + 1u) * 5.9604644775390625e-08f;
+  const float r1 = sqrtf(-2.0f * logf(u1));
+  float s1, c1;
+  sincospif(2.0f * u01f(w.y), &s1, &c1);
+  z[0] = r1 * c1;
+  z[1] = r1 * s1;
+}
+
 // Four standard normals for the policy's Gaussian action sample (purpose 3).
 __device__ __forceinline__ void normal4(uint64_t seed, uint64_t gid, uint64_t tick, float z[4]) {
   const U4 w = philox_block(seed, gid, kPurposePolicy, tick, 0);

@@ -314,7 +314,10 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       float act_c[A];
       if (live) {
         float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (!det) normal4(a.seed, (uint64_t)(a.gid0 + i), tick + (uint64_t)k, z);
+        if (!det) {
+          if constexpr (A <= 2) normal2(a.seed, (uint64_t)(a.gid0 + i), tick + (uint64_t)k, z);
+          else normal4(a.seed, (uint64_t)(a.gid0 + i), tick + (uint64_t)k, z);
+        }
         float lp = 0.0f;
 #pragma unroll
         for (int j = 0; j < A; ++j) {
