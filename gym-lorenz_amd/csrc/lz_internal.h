@@ -105,7 +105,8 @@ int launch_rollout(int system, int f64, const KArgs& a, void* stream);
 // Measured (profiles/r01/policy/ab_shapes.json): 32,768 envs +56% for the interleaved
 // shape over 8 serial waves; 65,536 envs 8 serial waves +21% over it; 262,144 envs
 // 64-env waves +30% over it.  lz_config.reserved[0] bit 5 / bit 6 force the
-// (32, 8, serial) / interleaved shape (A/B experiments).  The kernel's grid-stride
+// (32, 8, serial) / interleaved shape, bit 7 selects the interleaved nets without the
+// pipelined weight loads (A/B experiments).  The kernel's grid-stride
 // tile loop is correct for any grid.
 struct PolShape {
   int envs_per_wave, waves, pair, grid;
@@ -114,7 +115,7 @@ inline PolShape policy_shape(int64_t n, int variant, int num_cus) {
   PolShape s;
   const int64_t waves32 = (n + 31) / 32;
   if (variant & 32) s = {32, 8, 0, 0};
-  else if ((variant & 64) || waves32 < 8 * (int64_t)num_cus) s = {32, 4, 1, 0};
+  else if ((variant & 64) || waves32 < 8 * (int64_t)num_cus) s = {32, 4, (variant & 128) ? 1 : 2, 0};
   else if (n < 131072) s = {32, 8, 0, 0};
   else s = {64, 8, 0, 0};
   const int64_t groups = ((n + s.envs_per_wave - 1) / s.envs_per_wave + s.waves - 1) / s.waves;

@@ -170,6 +170,73 @@ __device__ __forceinline__ void mlp_pair(const uint8_t* na, const uint8_t* nb, b
   }
 }
 
+// mlp_pair with the layer-2 weight fragments software-pipelined: tile t+1's 16
+// fragments are issued before tile t's MFMAs (LDS returns in order, so tile t waits
+// with 16 newer loads still in flight), and the head fragments up front.  Register
+// hungry (two tiles of fragments for both nets): for the one-wave-per-SIMD shape.
+__device__ __forceinline__ void mlp_pair_pipe(const uint8_t* na, const uint8_t* nb, bf16x8 x,
+                                              int lane, f32x16& head_a, f32x16& head_b) {
+  asm volatile("" ::: "memory");
+  const int h = lane >> 5;
+  const bf16x8* w1a = reinterpret_cast<const bf16x8*>(na + kPolW1) + lane;
+  const bf16x8* w1b = reinterpret_cast<const bf16x8*>(nb + kPolW1) + lane;
+  const bf16x8* w2a = reinterpret_cast<const bf16x8*>(na + kPolW2) + lane;
+  const bf16x8* w2b = reinterpret_cast<const bf16x8*>(nb + kPolW2) + lane;
+  const bf16x8* w3a = reinterpret_cast<const bf16x8*>(na + kPolW3) + lane;
+  const bf16x8* w3b = reinterpret_cast<const bf16x8*>(nb + kPolW3) + lane;
+  const f32x16* b1a = reinterpret_cast<const f32x16*>(na + kPolB1) + h;
+  const f32x16* b1b = reinterpret_cast<const f32x16*>(nb + kPolB1) + h;
+  const f32x16* b2a = reinterpret_cast<const f32x16*>(na + kPolB2) + h;
+  const f32x16* b2b = reinterpret_cast<const f32x16*>(nb + kPolB2) + h;
+  bf16x8 l1a[4], l1b[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) { l1a[t] = w1a[t * 64]; l1b[t] = w1b[t * 64]; }
+  bf16x8 cur_a[8], cur_b[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) { cur_a[kk] = w2a[kk * 64]; cur_b[kk] = w2b[kk * 64]; }
+  asm volatile("" ::: "memory");
+  bf16x8 h1a[8], h1b[8];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f32x16 ca = mfma(l1a[t], x, b1a[2 * t]);
+    const f32x16 cb = mfma(l1b[t], x, b1b[2 * t]);
+    h1a[2 * t] = act8<0>(ca);
+    h1b[2 * t] = act8<0>(cb);
+    h1a[2 * t + 1] = act8<1>(ca);
+    h1b[2 * t + 1] = act8<1>(cb);
+  }
+  head_a = *(reinterpret_cast<const f32x16*>(na + kPolB3) + h);
+  head_b = *(reinterpret_cast<const f32x16*>(nb + kPolB3) + h);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    bf16x8 nxt_a[8], nxt_b[8], h3a[2], h3b[2];
+    if (t < 3) {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        nxt_a[kk] = w2a[((t + 1) * 8 + kk) * 64];
+        nxt_b[kk] = w2b[((t + 1) * 8 + kk) * 64];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) { h3a[q] = w3a[(2 * t + q) * 64]; h3b[q] = w3b[(2 * t + q) * 64]; }
+    f32x16 ca = b2a[2 * t], cb = b2b[2 * t];
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      ca = mfma(cur_a[kk], h1a[kk], ca);
+      cb = mfma(cur_b[kk], h1b[kk], cb);
+    }
+    head_a = mfma(h3a[0], act8<0>(ca), head_a);
+    head_b = mfma(h3b[0], act8<0>(cb), head_b);
+    head_a = mfma(h3a[1], act8<1>(ca), head_a);
+    head_b = mfma(h3b[1], act8<1>(cb), head_b);
+    if (t < 3) {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) { cur_a[kk] = nxt_a[kk]; cur_b[kk] = nxt_b[kk]; }
+    }
+  }
+}
+
 // VecNormalize.normalize_obs (float64, then float32 for the policy: obs_as_tensor)
 template <int O>
 __device__ __forceinline__ void normalize(const float* o, float* x, bool on, const double* mu,
@@ -225,7 +292,9 @@ __device__ __forceinline__ void net_fwd(const uint8_t* net, const float* x, bool
   }
 }
 
-template <class Sys, int W, int E, bool kPair>
+// kPair: 0 = the nets one after the other, 1 = interleaved (mlp_pair),
+// 2 = interleaved + pipelined weight loads (mlp_pair_pipe)
+template <class Sys, int W, int E, int kPair>
 __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   static_assert(!kPair || E == 32, "the interleaved pair runs 32-env tiles");
   constexpr int O = Sys::O, A = Sys::A;
@@ -292,6 +361,10 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
 #pragma unroll
       for (int j = 0; j < O; ++j) o[j] = p.obs_in[i * O + j];
     }
+    // settle the tile's loads (state planes, obs_in) here: otherwise
+    // hipcc places their first-use waits inside the step loop, where a vmcnt(0) also
+    // drains every store of the previous step -- a store round trip per step
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt untouched
     for (int k = 0; k < a.K; ++k) {
       const int64_t off = (int64_t)k * a.n + i;
       float x[O];
@@ -303,7 +376,8 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       float mean[A], val[1];
       if constexpr (kPair) {
         f32x16 hp, hv;
-        mlp_pair(pi_net, vf_net, obs_frag<O>(x, live), lane, hp, hv);
+        if constexpr (kPair == 2) mlp_pair_pipe(pi_net, vf_net, obs_frag<O>(x, live), lane, hp, hv);
+        else mlp_pair(pi_net, vf_net, obs_frag<O>(x, live), lane, hp, hv);
 #pragma unroll
         for (int j = 0; j < A; ++j) mean[j] = hp[j];
         val[0] = hv[0];
@@ -433,11 +507,13 @@ template <class Sys>
 static int launch_pol(const KArgs& a, const PArgs& p, const PolShape& sh, hipStream_t s) {
   const dim3 grid((unsigned)sh.grid);
   if (sh.envs_per_wave == 64)
-    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 64, false>), grid, dim3(8 * 64), 0, s, a, p);
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 64, 0>), grid, dim3(8 * 64), 0, s, a, p);
+  else if (sh.pair == 2)
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, 2>), grid, dim3(4 * 64), 0, s, a, p);
   else if (sh.pair)
-    hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, true>), grid, dim3(4 * 64), 0, s, a, p);
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, 1>), grid, dim3(4 * 64), 0, s, a, p);
   else
-    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 32, false>), grid, dim3(8 * 64), 0, s, a, p);
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 32, 0>), grid, dim3(8 * 64), 0, s, a, p);
   return (int)hipGetLastError();
 }
 

@@ -266,6 +266,30 @@ struct SysPMSM {
   __device__ static float bias(const float* tab, int32_t len, int32_t k) {
     return k < len ? tab[k] : 1.0f;
   }
+  // The two table values for this env's Adam step, by SCALAR loads issued from asm
+  // (waited on with lgkmcnt): a vector load would be waited on with vmcnt, which in the
+  // fused rollouts also drains every store still in flight from the previous step.  A
+  // waterfall over the distinct steps in the wave -- normally one: all envs of a batch
+  // step their (never reset) Adam counters together.  The loads are asm so that hipcc
+  // cannot rewrite the uniform index back into the lane's own (a vector load).
+  __device__ static float sload(const float* p) {
+    float v;
+    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    return v;
+  }
+  __device__ void bias_pair(const KArgs& a, float& bm, float& bv) const {
+    for (;;) {
+      const int32_t k0 = __builtin_amdgcn_readfirstlane(adam);
+      const bool in = k0 < a.bc_len;
+      const float m = in ? sload(a.bc1 + k0) : 1.0f;
+      const float v = in ? sload(a.bc2 + k0) : 1.0f;
+      if (adam == k0) {
+        bm = m;
+        bv = v;
+        break;
+      }
+    }
+  }
   // step(): :76-184
   __device__ bool step(const float* act, bool use_nz, const double* nz, float* o, float& rew,
                        const KArgs& a) {
@@ -286,8 +310,10 @@ struct SysPMSM {
     adam += 1;                                             // :121
     mt = b1 * mt + c1 * grad;                              // :124
     vt = b2 * vt + c2 * (grad * grad);                     // :127 (glibc powf(g,2) in ref)
-    const float mh = mt / bias(a.bc1, a.bc_len, adam);     // :130 (1-b1**k) -> f32
-    const float vh = vt / bias(a.bc2, a.bc_len, adam);     // :131
+    float bcm, bcv;
+    bias_pair(a, bcm, bcv);
+    const float mh = mt / bcm;                             // :130 (1-b1**k) -> f32
+    const float vh = vt / bcv;                             // :131
     lam = lam - (lr * mh) / (sqrtf(vh) + eps);             // :135
     lam = clip(lam, 0.0f, 0.5f);                           // :138
     const float tiny = 1e-6f;                              // :158-160 (x + 1e-6)**alpha
