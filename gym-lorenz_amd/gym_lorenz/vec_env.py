@@ -93,8 +93,31 @@ class LorenzVecEnv(VecEnvBase):
             self.render_mode = None
             self.reset_infos = [{} for _ in range(num_envs)]
         self.metadata = {"render_modes": []}
+        self._pin_act = self._pin_out = self._dev_act = None
+        if not return_tensors and isinstance(backend, BatchedEnv):
+            # host-buffer path: pinned staging, one copy each way
+            self._pin_act = torch.empty((num_envs, backend.action_dim), dtype=torch.float32,
+                                        pin_memory=True)
+            self._pin_out = torch.empty(backend.packed.shape, dtype=torch.uint8, pin_memory=True)
+            self._dev_act = torch.empty((num_envs, backend.action_dim), dtype=torch.float32,
+                                        device=backend.device)
 
     # ------------------------------------------------------------------ conversions
+    def _host_results(self):
+        """obs float32 [N, O], rewards float32 [N], done bytes [N] as NumPy arrays: one
+        pinned D2H copy of the packed obs|rew|done buffer, then one host copy each
+        (SB3's DummyVecEnv also hands out copies)."""
+        be = self.backend
+        self._pin_out.copy_(be.packed, non_blocking=True)
+        torch.cuda.current_stream(be.device).synchronize()
+        raw = self._pin_out.numpy()
+        n, o = self.num_envs, be.obs_dim
+        dt = np.float64 if be.tdtype == torch.float64 else np.float32
+        es = np.dtype(dt).itemsize
+        obs = raw[: n * o * es].view(dt).reshape(n, o).astype(np.float32)
+        rew = raw[n * o * es: n * (o + 1) * es].view(dt).astype(np.float32)
+        done = raw[n * (o + 1) * es:].copy()
+        return obs, rew, done
     def _out(self, t, np_dtype):
         if self.return_tensors:
             return t
@@ -107,6 +130,8 @@ class LorenzVecEnv(VecEnvBase):
             LazyInfos(self.num_envs, {})
         if self.return_tensors:
             return obs.float() if obs.dtype != torch.float32 else obs.clone()
+        if self._pin_out is not None:
+            return self._host_results()[0]
         return obs.detach().cpu().numpy().astype(np.float32)
 
     def step_async(self, actions):
@@ -114,7 +139,12 @@ class LorenzVecEnv(VecEnvBase):
 
     def step_wait(self):
         acts = self._actions
-        if not isinstance(acts, torch.Tensor):
+        if not isinstance(acts, torch.Tensor) and self._pin_act is not None:
+            np.copyto(self._pin_act.numpy(),
+                      np.asarray(acts, dtype=np.float32).reshape(self.num_envs, -1))
+            self._dev_act.copy_(self._pin_act, non_blocking=True)
+            acts = self._dev_act
+        elif not isinstance(acts, torch.Tensor):
             acts = torch.from_numpy(np.asarray(acts, dtype=np.float32).reshape(
                 self.num_envs, -1))
         obs, rew, done = self.backend.step(acts)
@@ -123,7 +153,10 @@ class LorenzVecEnv(VecEnvBase):
             rew_o = rew.float() if rew.dtype != torch.float32 else rew.clone()
             done_h = done.cpu().numpy()
             dones = done.bool()
-        else:
+        elif self._pin_out is not None:
+            obs_o, rew_o, done_h = self._host_results()
+            dones = done_h.astype(bool)
+        else:  # a test double of the backend
             obs_o = obs.detach().cpu().numpy().astype(np.float32)
             rew_o = rew.detach().cpu().numpy().astype(np.float32)
             done_h = done.cpu().numpy()
