@@ -202,8 +202,7 @@ typedef __attribute__((address_space(3))) void* las_t;
 __device__ __forceinline__ uint32_t lds_off(const float* p) {
   return (uint32_t)(uintptr_t)(las_t)(const_cast<float*>(p));
 }
-__device__ __forceinline__ void dma4_nt(const float* g, const float* lds_wave_base) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_wave_base));
+__device__ __forceinline__ void dma4_nt(const float* g, uint32_t m0) {
   uint32_t saved;  // M0 is a reserved register hipcc may hold a value in: save/restore
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dword %1, off nt\n\t"
                "s_mov_b32 m0, %0"
@@ -274,15 +273,21 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   static_assert(D >= 1 && D <= 3, "wait ladder covers distances 1..3");
   // DMA step kk's action slice into LDS slot `slot` (B*A floats):
   // direct: component-major [A][B]; staged: a verbatim copy of the row-major slice.
-  auto issue = [&](int kk, int slot) __attribute__((always_inline)) {
-    const int64_t koff = (int64_t)kk * a.n;
-    float* dst = s_act + slot * (B * Sys::A);
+  // src = this lane's first source float of step kk (component j is j, resp. j*B, on).
+  // M0 = LDS byte address of this wave's 64 destination floats: computed once,
+  // wave-uniform, then constant offsets per slot / component (no per-DMA address-space
+  // cast or readfirstlane)
+  const uint32_t m0_wave = __builtin_amdgcn_readfirstlane(lds_off(s_act) + (uint32_t)wave * 256u);
+  auto issue = [&](const float* src, int slot) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < Sys::A; ++j) {
-      const float* src = kDirect ? gact + (koff + base + tid) * Sys::A + j
-                                 : gact + (koff + base) * Sys::A + j * B + tid;
-      dma4_nt(src, dst + j * B + wave * 64);
-    }
+    for (int j = 0; j < Sys::A; ++j)
+      dma4_nt(src + (kDirect ? j : j * B), m0_wave + (uint32_t)((slot * Sys::A + j) * B) * 4u);
+  };
+  // this lane's DMA source pointer for step kk, and the per-step advance
+  const int64_t lane0 = kDirect ? (base + tid) * Sys::A : base * Sys::A + tid;
+  const int64_t dstride = a.n * Sys::A;
+  auto dma_src = [&](int kk) __attribute__((always_inline)) {
+    return gact + ((int64_t)kk * dstride + lane0);
   };
   // settle every compiler-visible load of the prologue (state planes) here, so that
   // hipcc's wait bookkeeping enters the loop with nothing pending and emits no drain
@@ -290,22 +295,28 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   if constexpr (FULL) __builtin_amdgcn_s_waitcnt(0x0F70);
   if constexpr (FULL && Sys::kUsesAction) {
 #pragma unroll
-    for (int d = 0; d < kDmaDist; ++d) issue(d < a.K ? d : a.K - 1, d);
+    for (int d = 0; d < kDmaDist; ++d) issue(dma_src(d < a.K ? d : a.K - 1), d);
   }
-  for (int k = 0; k < a.K; ++k) {
+  // running source of the DMA issued at step k (step min(k + D, K - 1)): advanced by
+  // one step per step until it reaches the last (no per-step 64-bit multiply)
+  const float* dsrc = dma_src(kDmaDist < a.K ? kDmaDist : a.K - 1);
+  // kLadder: one of the first D steps (its wait count depends on k); later steps all
+  // wait with the steady-state count -- peeled so the hot loop carries no ladder
+  auto run_step = [&](int k, auto ladder) __attribute__((always_inline)) {
     const int64_t off = (int64_t)k * a.n;
     float act[Sys::A];
     if constexpr (Sys::kUsesAction) {
       if constexpr (FULL) {
-        wait_for_step(k);  // step k's DMA has >= N younger vm ops
+        if constexpr (decltype(ladder)::value) wait_for_step(k);
+        else wait_vmcnt<kSt + (D - 1) * (kA + kSt)>();  // step k's DMA has >= N younger ops
         if constexpr (!kDirect) wg_barrier<false>();  // every wave's DMA has landed
         const float* slot = s_act + (k % kDmaSlots) * (B * Sys::A);
         if constexpr (kDirect) lds_read_act<Sys::A>(act, slot + tid, B);
         else lds_read_act<Sys::A>(act, slot + tid * Sys::A, 1);
         // prefetch step k+D into the slot step k-1 used (every reader is past this
         // point); near the end re-read step K-1: no branch, same op count
-        const int kk = k + kDmaDist < a.K ? k + kDmaDist : a.K - 1;
-        issue(kk, (k + kDmaDist) % kDmaSlots);
+        issue(dsrc, (k + kDmaDist) % kDmaSlots);
+        if (k + kDmaDist + 1 < a.K) dsrc += dstride;
       } else {
         stage_in<true, float, Sys::A, B>(s_act, gact + (off + base) * Sys::A, nb, tid, false);
         wg_barrier<false>();
@@ -328,7 +339,7 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
       const co_t* src = reinterpret_cast<const co_t*>(o);
 #pragma unroll
       for (int j = 0; j < CO::N; ++j) gstore<false>(reinterpret_cast<co_t*>(gobs) + tid * CO::N + j, src[j]);
-      continue;
+      return;
     }
     if (live) {
 #pragma unroll
@@ -345,7 +356,13 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
     } else {
       stage_out<true, T, Sys::O, B>(gobs, s_obs, nb, tid, false);
     }
+  };
+  int k = 0;
+  if constexpr (FULL && Sys::kUsesAction) {
+    const int kp = kDmaDist < a.K ? kDmaDist : a.K;
+    for (; k < kp; ++k) run_step(k, std::true_type{});
   }
+  for (; k < a.K; ++k) run_step(k, std::false_type{});
 }
 
 template <class Sys, typename T, int B>
