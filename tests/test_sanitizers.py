@@ -1,0 +1,60 @@
+"""Host code under AddressSanitizer + UndefinedBehaviorSanitizer, no GPU:
+
+  * the CPU oracle (oracle/lz_oracle.c): every function on exact-size heap buffers;
+  * the library's host-side C-ABI (lz_api.cpp, the policy packer, argument checks and
+    error paths of lz_rms / lz_gae / lz_frame_stack), built with
+    `hipcc -Xarch_host -fsanitize=...` (device code unsanitized, never launched here).
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+CSRC = os.path.join(ROOT, "gym-lorenz_amd", "csrc")
+INC = os.path.join(ROOT, "include")
+HIPCC = "/opt/rocm/bin/hipcc"
+SAN_ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", UBSAN_OPTIONS="print_stacktrace=1")
+
+
+def test_oracle_under_asan_ubsan(tmp_path):
+    gcc = shutil.which("gcc")
+    exe = tmp_path / "osan"
+    subprocess.check_call([gcc, "-O1", "-g", "-fsanitize=address,undefined",
+                           "-fno-sanitize-recover=all", "-ffp-contract=off", "-I", INC,
+                           os.path.join(ROOT, "oracle", "lz_oracle.c"),
+                           os.path.join(ROOT, "tests", "c_abi", "oracle_sanitize.c"), "-lm",
+                           "-o", str(exe)])
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=SAN_ENV)
+    assert out.returncode == 0, out.stderr[-4000:]
+    assert "clean" in out.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_host_abi_under_asan_ubsan(tmp_path):
+    common = [HIPCC, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
+              "-fPIC", "-I", INC, "-I", CSRC]
+    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+           "-Xarch_host", "-fno-sanitize-recover=all"]
+    kern = os.path.join(ROOT, "gym-lorenz_amd", "build", "lz_kernels.o")
+    if not os.path.exists(kern):  # kernels + launchers: built unsanitized (device code)
+        kern = str(tmp_path / "k.o")
+        subprocess.check_call(common + ["-O3", "-c", os.path.join(CSRC, "lz_kernels.hip"),
+                                        "-o", kern])
+    objs = [kern]
+    for f in ("lz_rms.hip", "lz_policy.hip", "lz_wrappers.hip", "lz_api.cpp"):
+        o = str(tmp_path / (f + ".o"))
+        lang = ["-x", "hip"] if f.endswith(".cpp") else []
+        subprocess.check_call(common + san + lang + ["-c", os.path.join(CSRC, f), "-o", o])
+        objs.append(o)
+    drv = str(tmp_path / "drv.o")
+    subprocess.check_call(["gcc", "-g", "-fsanitize=address,undefined", "-I", INC, "-c",
+                           os.path.join(ROOT, "tests", "c_abi", "host_sanitize.c"), "-o", drv])
+    exe = str(tmp_path / "hsan")
+    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-fsanitize=address,undefined",
+                           "-fno-gpu-sanitize"] + objs + [drv, "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=SAN_ENV)
+    assert out.returncode == 0, out.stderr[-4000:]
+    assert "clean" in out.stdout
