@@ -133,11 +133,12 @@ class BatchedEnv:
         nat.check(nat.lib.lz_reset(self._h, _ptr(mask), _ptr(init), _ptr(out)))
         return out
 
-    def step(self, actions, noise=None, want_n_done=True, out=None):
+    def step(self, actions, noise=None, want_n_done=True, out=None, compact_out=None):
         """One batched step.  actions: float32 [N, action_dim] (device or host).
         Returns (obs, rew, done) device tensors -- by default internal buffers reused
         by the next call; `out=(obs, rew, done)` writes into caller tensors (e.g. a
-        slot of an on-device rollout buffer) instead."""
+        slot of an on-device rollout buffer) instead, and `compact_out=(done_idx int32
+        [N], terminal_obs [N, O], n_done int32 [1])` the compact done list."""
         a = self._check_dev(actions, torch.float32, (self.num_envs, self.action_dim), "actions")
         nz = self._check_dev(noise, torch.float64, (self.num_envs, 3), "noise")
         obs, rew, done = (self.obs, self.rew, self.done) if out is None else out
@@ -148,10 +149,14 @@ class BatchedEnv:
                     or not (obs.is_contiguous() and rew.is_contiguous() and done.is_contiguous())
                     or {obs.device, rew.device, done.device} != {self.device}):
                 raise ValueError("step(out=...): wrong shape / dtype / device / layout")
+        if compact_out is not None:
+            didx, tobs, ndone = compact_out
+        else:
+            didx, tobs = self.done_idx, self.term_obs
+            ndone = self.n_done_dev if (self.compact and want_n_done) else None
         nat.check(nat.lib.lz_step(
             self._h, _ptr(a), _ptr(nz), _ptr(obs), _ptr(rew), _ptr(done),
-            _ptr(self.done_idx), _ptr(self.term_obs),
-            _ptr(self.n_done_dev) if (self.compact and want_n_done) else None))
+            _ptr(didx), _ptr(tobs), _ptr(ndone)))
         self._last_actions = a  # keep alive until the stream consumed it
         return obs, rew, done
 

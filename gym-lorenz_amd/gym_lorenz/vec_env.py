@@ -64,6 +64,45 @@ class LazyInfos(Sequence):
         return sorted(k for k, v in self._d.items() if "terminal_observation" in v)
 
 
+class DeviceLazyInfos(Sequence):
+    """The infos of a `return_tensors=True` step, sync-free until touched: the step's
+    done bytes and compact done list stay in device tensors of their own, and the
+    first access synchronises once and materialises the done envs' dicts
+    ("terminal_observation" as a device tensor row, "TimeLimit.truncated")."""
+
+    def __init__(self, n, done, done_idx, term_obs, n_done):
+        self._n = n
+        self._dev = (done, done_idx, term_obs, n_done)
+        self._li = None
+
+    def _mat(self):
+        if self._li is None:
+            done, didx, tobs, nd = self._dev
+            m = int(nd.item())
+            idx = didx[:m].cpu().numpy()
+            flags = done.cpu().numpy()
+            t = tobs[:m].float()
+            entries = {}
+            for j, i in enumerate(idx):
+                f = int(flags[i])
+                entries[int(i)] = {
+                    "terminal_observation": t[j],
+                    "TimeLimit.truncated": bool(f & nat.DONE_TRUNCATED) and not bool(
+                        f & nat.DONE_TERMINATED)}
+            self._li = LazyInfos(self._n, entries)
+            self._dev = None
+        return self._li
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        return self._mat()[i]
+
+    def done_indices(self):
+        return self._mat().done_indices()
+
+
 class LorenzVecEnv(VecEnvBase):
     def __init__(self, env_id="lorenz_dynamic-v0", num_envs=1, device=None, dtype="float32",
                  seed=0, max_episode_steps=None, return_tensors=False, lazy_infos=None,
@@ -147,6 +186,20 @@ class LorenzVecEnv(VecEnvBase):
         elif not isinstance(acts, torch.Tensor):
             acts = torch.from_numpy(np.asarray(acts, dtype=np.float32).reshape(
                 self.num_envs, -1))
+        if self.return_tensors and isinstance(self.backend, BatchedEnv):
+            # sync-free: fresh output tensors per step (the caching allocator recycles
+            # them) and the compact done list kept for DeviceLazyInfos
+            be, n, o = self.backend, self.num_envs, self.backend.obs_dim
+            dev, td = be.device, be.tdtype
+            out = (torch.empty((n, o), dtype=td, device=dev), torch.empty((n,), dtype=td, device=dev),
+                   torch.empty((n,), dtype=torch.uint8, device=dev))
+            comp = (torch.empty((n,), dtype=torch.int32, device=dev),
+                    torch.empty((n, o), dtype=td, device=dev),
+                    torch.empty((1,), dtype=torch.int32, device=dev))
+            obs, rew, done = be.step(acts, out=out, compact_out=comp)
+            obs_o = obs.float() if obs.dtype != torch.float32 else obs
+            rew_o = rew.float() if rew.dtype != torch.float32 else rew
+            return obs_o, rew_o, done.bool(), DeviceLazyInfos(n, done, *comp)
         obs, rew, done = self.backend.step(acts)
         if self.return_tensors:
             obs_o = obs.float() if obs.dtype != torch.float32 else obs.clone()

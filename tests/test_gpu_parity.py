@@ -489,3 +489,28 @@ def test_device_vecnormalize_matches_sb3_restatement(gl, norm_reward):
     dev2 = LorenzVecNormalize(gl.make_vec("lorenz_pmsm-v0", 16, seed=1))
     dev2.load("/tmp/_vn.npz")
     np.testing.assert_array_equal(dev2.obs_rms.mean, dev.obs_rms.mean)
+
+
+def test_vecenv_return_tensors_matches_numpy(gl):
+    """The sync-free device-tensor VecEnv path (DeviceLazyInfos) returns what the NumPy
+    path returns: obs / rewards / dones and, for done envs, terminal_observation and
+    TimeLimit.truncated."""
+    n = 3000
+    va = gl.make_vec("lorenz_pmsm-v0", n, return_tensors=True, max_episode_steps=4, seed=5)
+    vb = gl.make_vec("lorenz_pmsm-v0", n, max_episode_steps=4, seed=5)
+    assert np.array_equal(_np(va.reset()), vb.reset())
+    rng = np.random.default_rng(0)
+    seen = 0
+    for k in range(9):
+        a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        oa, ra, da, ia = va.step(torch.from_numpy(a).cuda())
+        ob, rb, db, ib = vb.step(a)
+        assert np.array_equal(_np(oa), ob) and np.array_equal(_np(ra), rb)
+        assert np.array_equal(_np(da), db)
+        for i in np.nonzero(db)[0]:
+            assert np.array_equal(_np(ia[int(i)]["terminal_observation"]),
+                                  ib[int(i)]["terminal_observation"])
+            assert ia[int(i)]["TimeLimit.truncated"] == ib[int(i)]["TimeLimit.truncated"]
+            seen += 1
+        assert len(ia) == n and ia[0] is not None
+    assert seen > 0
