@@ -138,11 +138,17 @@ SYSTEM_INFO = {  # system -> (reference env, mangled k_step / k_rollout names, a
 
 
 def kernel_name(system, mode, n):
+    """Mangled name of the dominant kernel (lz_kernels.hip launch_all / launch_rollout_d)."""
     tag = SYSTEM_INFO[system][1]
-    pre = "_ZN2lz6k_stepINS_%s%sLi0EEEvNS_5KArgsE"
-    if mode == "rollout":  # one-wave workgroups below 2 x 256-lane groups per CU
-        pre = "_ZN2lz9k_rolloutINS_%%s%%sLi%dEEEvNS_5KArgsE" % (64 if n < 2 * 256 * 256 else 256)
-    return pre % ("7" if system == "pmsm" else "5", tag)
+    sysname = ("7" if system == "pmsm" else "5") + tag
+    if mode != "rollout":
+        return "_ZN2lz6k_stepINS_%sLi0EEEvNS_5KArgsE" % sysname
+    D = 7  # kDmaDist
+    if n < 2 * 256 * 256:  # one-wave workgroups; two lanes per env for LORENZ3 f32 >= 32,768
+        if system == "lorenz3" and n >= 32768:
+            return "_ZN2lz15k_rollout_splitINS_%sLi2ELi%dEEEvNS_5KArgsE" % (sysname, D)
+        return "_ZN2lz9k_rolloutINS_%sLi64ELi%dEEEvNS_5KArgsE" % (sysname, D)
+    return "_ZN2lz9k_rolloutINS_%sLi256ELi%dEEEvNS_5KArgsE" % (sysname, D)
 
 
 def policy_flops(O, A, H=128):

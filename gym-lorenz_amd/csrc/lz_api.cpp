@@ -85,7 +85,7 @@ struct lz_handle {
   void* planes[lz::kMaxPlanes];
   int32_t* counters;  // [2] compact-list cursors, ping-pong by call parity
   uint64_t* ticks;    // [2] device-resident call counter (RNG counter), ping-pong
-  float* bc;          // PMSM bias-correction tables [2][bc_len]
+  float* bc;          // PMSM bias-correction pairs [bc_len][2]
   int32_t bc_len;
   int parity;         // which slot of counters/ticks the next launch reads
   int count_steps;
@@ -253,9 +253,13 @@ lz_status lz_create(const lz_config* cfg_in, lz_handle** out) {
       lz_destroy(h);
       return fail(LZ_ERR_OOM, "bias table allocation failed");
     }
-    if (hipMemcpy(h->bc, t1.data(), t1.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(h->bc + t1.size(), t2.data(), t2.size() * sizeof(float), hipMemcpyHostToDevice) !=
-            hipSuccess) {
+    // interleaved pairs [k] = {1 - beta1**k, 1 - beta2**k}: one scalar load per step
+    std::vector<float> tb(2 * t1.size());
+    for (size_t j = 0; j < t1.size(); ++j) {
+      tb[2 * j] = t1[j];
+      tb[2 * j + 1] = t2[j];
+    }
+    if (hipMemcpy(h->bc, tb.data(), tb.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
       lz_destroy(h);
       return fail(LZ_ERR_HIP, "bias table upload failed");
     }
@@ -348,8 +352,7 @@ static void fill_common(const lz_handle* h, KArgs& a) {
   a.tick_in = h->ticks + h->parity;
   a.tick_out = h->ticks + (1 - h->parity);
   a.tick_adv = 1;
-  a.bc1 = h->bc;
-  a.bc2 = h->bc ? h->bc + h->bc_len : nullptr;
+  a.bc = h->bc;
   a.bc_len = h->bc_len;
   a.max_steps = h->max_steps;
   a.t_done_step = h->cfg.t_done_step;

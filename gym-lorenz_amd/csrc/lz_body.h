@@ -58,11 +58,13 @@ __device__ __forceinline__ void make_noise(const Sys& sys, const KArgs& a, int64
 // Shared by k_step (K = 1, state in HBM), k_rollout and k_rollout_policy (state in
 // VGPRs across K).  Returns the done byte; o[] holds the observation to emit
 // (post-reset if reset); with kKeepTerm, o_term[] receives the pre-reset observation.
+// lead = false: a lane that computes a copy of another lane's env (the split-lane
+// rollout) -- same arithmetic, but it takes no slot in the compact done list.
 template <class Sys, typename T, bool kRollout, bool kKeepTerm = false>
 __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KArgs& a, int64_t i,
                                              bool live, const float* act, uint64_t tick, int k,
                                              T* o, T& rew, bool& did_reset,
-                                             T* o_term = nullptr) {
+                                             T* o_term = nullptr, bool lead = true) {
   uint8_t dflag = 0;
   did_reset = false;
   if (live) {
@@ -85,7 +87,7 @@ __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KAr
   }
   // compact list of done envs: ballot + one atomic per wave (all lanes reach this)
   if (a.term_obs) {
-    const int32_t pos = wave_compact(dflag != 0, a.counter);
+    const int32_t pos = wave_compact(dflag != 0 && lead, a.counter);
     if (pos >= 0) {
       if constexpr (kRollout) {
         if (pos < a.term_cap) {

@@ -24,8 +24,7 @@ struct KArgs {
   int64_t term_cap;          // rollout capacity of the compact buffers
   int32_t* counter;          // compact-list cursor for this launch
   int32_t* counter_next;     // the other slot, zeroed by this launch for the next
-  const float* bc1;          // PMSM: (float)(1 - beta1**k), k < bc_len
-  const float* bc2;          // PMSM: (float)(1 - beta2**k)
+  const float* bc;           // PMSM: {(float)(1 - beta1**k), (float)(1 - beta2**k)}, k < bc_len
   const uint8_t* mask;       // reset: env selection (nullable)
   const void* init;          // reset: injected initial states (nullable)
   int64_t n;                 // envs in this handle

@@ -233,11 +233,29 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// Prefetch distance of the fused rollout's action DMA (steps in flight).
-constexpr int kDmaDist = 3;
-constexpr int kDmaSlots = kDmaDist + 1;
+// Prefetch distance D of the fused rollout's action DMA (steps in flight; D + 1 LDS
+// slots, a power of two).  vmcnt counts stores as well as loads, so D also bounds how
+// many steps of stores stay in flight behind the wait at the top of a step.
+// D = 7 measured against 3 (tools/ab_rollout.py, K = 2048): LORENZ3 f32 +5% at 32,768
+// envs (split lanes), +1.5% at 262,144; PMSM +4% at 32,768, even at 262,144.
+constexpr int kDmaDist = 7;
+template <int D>
+constexpr int dma_slots() { return D + 1; }
 
-template <class Sys, typename T, int B, bool FULL>
+// vmcnt wait at the top of step k < D: the vector-memory ops issued after step k's
+// DMA are the prologue's later DMAs ((D-1-k) * kA) and k earlier steps' DMA + stores
+template <int D, int kA, int kSt, int J = 0>
+__device__ __forceinline__ void ladder_wait(int k) {
+  if constexpr (J < D) {
+    if (k == J) {
+      wait_vmcnt<(D - 1 - J) * kA + J * (kA + kSt)>();
+      return;
+    }
+    ladder_wait<D, kA, kSt, J + 1>(k);
+  }
+}
+
+template <class Sys, typename T, int B, bool FULL, int D>
 __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any_reset,
                                              const KArgs& a, int64_t base, int tid, int nb,
                                              uint64_t tick, float* s_act, T* s_obs) {
@@ -258,19 +276,11 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   constexpr int kRowB = Sys::O * (int)sizeof(T);
   constexpr int kSt = 2 + (kDirect ? (kRowB + 15) / 16 : CO::N);
   constexpr int kA = Sys::A;  // DMA instructions per step
-  // vmcnt at the top of step k: vm ops issued after step k's DMA -- for k < D the
-  // prologue's later DMAs and k earlier steps' (DMA + stores); then one step's stores
-  // plus D-1 steps' (DMA + stores).  All lower bounds (see kSt).
-  constexpr int D = kDmaDist;
-  auto wait_for_step = [&](int k) __attribute__((always_inline)) {
-    constexpr int W0 = (D - 1) * kA, W1 = (D - 2) * kA + (kA + kSt);
-    constexpr int W2 = (D - 3) * kA + 2 * (kA + kSt), WN = kSt + (D - 1) * (kA + kSt);
-    if (k == 0) wait_vmcnt<W0>();
-    else if (D > 1 && k == 1) wait_vmcnt<(D > 1 ? W1 : 0)>();
-    else if (D > 2 && k == 2) wait_vmcnt<(D > 2 ? W2 : 0)>();
-    else wait_vmcnt<WN>();
-  };
-  static_assert(D >= 1 && D <= 3, "wait ladder covers distances 1..3");
+  // steady-state wait: step k's DMA has one step's stores plus D-1 steps' (DMA +
+  // stores) issued after it (lower bounds, see kSt)
+  constexpr int kSteady = kSt + (D - 1) * (kA + kSt);
+  static_assert(D >= 1 && kSteady <= 63, "vmcnt immediate (6 bits on gfx9)");
+  constexpr int kDmaSlots = dma_slots<D>();
   // DMA step kk's action slice into LDS slot `slot` (B*A floats):
   // direct: component-major [A][B]; staged: a verbatim copy of the row-major slice.
   // src = this lane's first source float of step kk (component j is j, resp. j*B, on).
@@ -295,11 +305,11 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   if constexpr (FULL) __builtin_amdgcn_s_waitcnt(0x0F70);
   if constexpr (FULL && Sys::kUsesAction) {
 #pragma unroll
-    for (int d = 0; d < kDmaDist; ++d) issue(dma_src(d < a.K ? d : a.K - 1), d);
+    for (int d = 0; d < D; ++d) issue(dma_src(d < a.K ? d : a.K - 1), d);
   }
   // running source of the DMA issued at step k (step min(k + D, K - 1)): advanced by
   // one step per step until it reaches the last (no per-step 64-bit multiply)
-  const float* dsrc = dma_src(kDmaDist < a.K ? kDmaDist : a.K - 1);
+  const float* dsrc = dma_src(D < a.K ? D : a.K - 1);
   // kLadder: one of the first D steps (its wait count depends on k); later steps all
   // wait with the steady-state count -- peeled so the hot loop carries no ladder
   auto run_step = [&](int k, auto ladder) __attribute__((always_inline)) {
@@ -307,16 +317,16 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
     float act[Sys::A];
     if constexpr (Sys::kUsesAction) {
       if constexpr (FULL) {
-        if constexpr (decltype(ladder)::value) wait_for_step(k);
-        else wait_vmcnt<kSt + (D - 1) * (kA + kSt)>();  // step k's DMA has >= N younger ops
+        if constexpr (decltype(ladder)::value) ladder_wait<D, kA, kSt>(k);
+        else wait_vmcnt<kSteady>();
         if constexpr (!kDirect) wg_barrier<false>();  // every wave's DMA has landed
         const float* slot = s_act + (k % kDmaSlots) * (B * Sys::A);
         if constexpr (kDirect) lds_read_act<Sys::A>(act, slot + tid, B);
         else lds_read_act<Sys::A>(act, slot + tid * Sys::A, 1);
         // prefetch step k+D into the slot step k-1 used (every reader is past this
         // point); near the end re-read step K-1: no branch, same op count
-        issue(dsrc, (k + kDmaDist) % kDmaSlots);
-        if (k + kDmaDist + 1 < a.K) dsrc += dstride;
+        issue(dsrc, (k + D) % kDmaSlots);
+        if (k + D + 1 < a.K) dsrc += dstride;
       } else {
         stage_in<true, float, Sys::A, B>(s_act, gact + (off + base) * Sys::A, nb, tid, false);
         wg_barrier<false>();
@@ -359,15 +369,15 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   };
   int k = 0;
   if constexpr (FULL && Sys::kUsesAction) {
-    const int kp = kDmaDist < a.K ? kDmaDist : a.K;
+    const int kp = D < a.K ? D : a.K;
     for (; k < kp; ++k) run_step(k, std::true_type{});
   }
   for (; k < a.K; ++k) run_step(k, std::false_type{});
 }
 
-template <class Sys, typename T, int B>
+template <class Sys, typename T, int B, int D>
 __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
-  __shared__ __attribute__((aligned(16))) float s_act[kDmaSlots * B * Sys::A];  // DMA ring
+  __shared__ __attribute__((aligned(16))) float s_act[dma_slots<D>() * B * Sys::A];  // DMA ring
   __shared__ __attribute__((aligned(16))) T s_obs[B * Sys::O];
   const int tid = (int)threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * B;
@@ -388,10 +398,147 @@ __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
     if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
   }
   if (nb == B && a.vec_ok)
-    rollout_loop<Sys, T, B, true>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
+    rollout_loop<Sys, T, B, true, D>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
   else
-    rollout_loop<Sys, T, B, false>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
+    rollout_loop<Sys, T, B, false, D>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
   if (live) {
+    sys.store(a, i);
+    if (any_reset) sys.store_autoreset_extra(a, i);
+    if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
+  }
+}
+
+// ------------------------------------------------------------------ split-lane rollout
+// Small N (cfg5: 32,768 envs per GPU): one env per lane gives 512 one-wave groups for
+// 1,024 SIMDs -- half the chip idles and every wave runs its step chain alone.  Here
+// R = 2 adjacent lanes carry the same env (lane 2e + q, q = 0/1): both run the whole
+// step (bit-identical arithmetic, same Philox draws), and the step's OUTPUT is split
+// between them -- lane q stores half of the obs row (the wave's obs store stays one
+// contiguous 64 x O/2-element instruction), q = 0 the reward, q = 1 the done byte, and
+// only q = 0 enters the compact done list and writes the state back.  Twice the waves
+// for the same per-wave instruction stream: pays where the step is cheap and the SIMDs
+// otherwise idle (rollout_split).
+typedef float f3v __attribute__((ext_vector_type(3)));
+typedef f3v f3v_a4 __attribute__((aligned(4)));
+
+// store W contiguous T's of v[] at p (p aligned to the row-half, W * sizeof(T) bytes)
+template <typename T, int W>
+__device__ __forceinline__ void store_half(T* p, const T* v) {
+  constexpr int RB = W * (int)sizeof(T);
+  if constexpr (RB == 12) {
+    const f3v x = {(float)v[0], (float)v[1], (float)v[2]};
+    __builtin_nontemporal_store(x, reinterpret_cast<f3v_a4*>(p));
+  } else {
+    using C = Chunk<RB>;
+    using ct = typename C::t;
+    const ct* src = reinterpret_cast<const ct*>(v);
+#pragma unroll
+    for (int j = 0; j < C::N; ++j) gstore<true>(reinterpret_cast<ct*>(p) + j, src[j]);
+  }
+}
+
+template <class Sys, typename T, int R, bool FULL, int D>
+__device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_reset,
+                                           const KArgs& a, int64_t base, int tid, int nb,
+                                           uint64_t tick, float* s_act) {
+  static_assert(R == 2 && Sys::O % 2 == 0, "split-lane rollout: two lanes per env");
+  constexpr int H = Sys::O / R;  // obs elements stored per lane
+  const int el = tid / R, q = tid % R;
+  const bool lead = q == 0;
+  const int64_t i = base + el;
+  const bool live = FULL || el < nb;
+  const float* gact = static_cast<const float*>(a.act);
+  // vector-memory ops every step issues after its DMA (lower bound): reward or done
+  // (two exec-masked stores) + at least one obs store
+  constexpr int kSt = 3;
+  constexpr int kA = Sys::A;
+  constexpr int kSteady = kSt + (D - 1) * (kA + kSt);
+  static_assert(D >= 1 && kSteady <= 63, "vmcnt immediate (6 bits on gfx9)");
+  constexpr int kDmaSlots = dma_slots<D>();
+  const uint32_t m0_wave = __builtin_amdgcn_readfirstlane(lds_off(s_act));
+  // component-major slot [A][64]: lane tid reads its env's action at slot[j*64 + tid]
+  // (both lanes of a pair load the same source float; the coalescer merges them)
+  auto issue = [&](const float* src, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < Sys::A; ++j) dma4_nt(src + j, m0_wave + (uint32_t)((slot * Sys::A + j) * 64) * 4u);
+  };
+  const int64_t dstride = a.n * Sys::A;
+  const float* dsrc = gact + i * Sys::A;
+  if constexpr (FULL) __builtin_amdgcn_s_waitcnt(0x0F70);
+  if constexpr (FULL && Sys::kUsesAction) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) issue(dsrc + (int64_t)(d < a.K ? d : a.K - 1) * dstride, d);
+    dsrc += (int64_t)(D < a.K ? D : a.K - 1) * dstride;
+  }
+  auto run_step = [&](int k, auto ladder) __attribute__((always_inline)) {
+    const int64_t off = (int64_t)k * a.n;
+    float act[Sys::A];
+    if constexpr (Sys::kUsesAction) {
+      if constexpr (FULL) {
+        if constexpr (decltype(ladder)::value) ladder_wait<D, kA, kSt>(k);
+        else wait_vmcnt<kSteady>();
+        lds_read_act<Sys::A>(act, s_act + (k % kDmaSlots) * (64 * Sys::A) + tid, 64);
+        issue(dsrc, (k + D) % kDmaSlots);
+        if (k + D + 1 < a.K) dsrc += dstride;
+      } else if (live) {
+#pragma unroll
+        for (int j = 0; j < Sys::A; ++j) act[j] = gload<true>(gact + (off + i) * Sys::A + j);
+      }
+    }
+    T o[Sys::O];
+    T rew = (T)0;
+    bool did_reset;
+    const uint8_t dflag = step_body<Sys, T, true>(sys, steps, a, i, live, act, tick + (uint64_t)k,
+                                                  k, o, rew, did_reset, nullptr, lead);
+    any_reset = any_reset || did_reset;
+    if (!live) return;
+    if (lead) gstore<true>(static_cast<T*>(a.rew) + off + i, rew);
+    else gstore<true>(a.done + off + i, dflag);
+    // this lane's half row: elements [q*H, q*H + H) of env i = elements tid*H of the
+    // block's contiguous obs slice
+    T* p = static_cast<T*>(a.obs) + (off + base) * Sys::O + (int64_t)tid * H;
+    T h[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) h[j] = q ? o[H + j] : o[j];
+    store_half<T, H>(p, h);
+  };
+  int k = 0;
+  if constexpr (FULL && Sys::kUsesAction) {
+    const int kp = D < a.K ? D : a.K;
+    for (; k < kp; ++k) run_step(k, std::true_type{});
+  }
+  for (; k < a.K; ++k) run_step(k, std::false_type{});
+}
+
+template <class Sys, typename T, int R, int D>
+__global__ __launch_bounds__(64) void k_rollout_split(KArgs a) {
+  constexpr int E = 64 / R;  // envs per one-wave workgroup
+  __shared__ __attribute__((aligned(16))) float s_act[dma_slots<D>() * 64 * Sys::A];
+  const int tid = (int)threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * E;
+  const int el = tid / R;
+  const int64_t i = base + el;
+  const int nb = (int)((a.n - base) < E ? (a.n - base) : E);
+  const bool live = el < nb;
+  const bool lead = (tid % R) == 0;
+  const uint64_t tick = *a.tick_in;
+  if (blockIdx.x == 0 && tid == 0) {
+    *a.counter_next = 0;
+    *a.tick_out = tick + a.tick_adv;
+  }
+  Sys sys;
+  sys.setup(a);
+  int32_t steps = 0;
+  bool any_reset = false;
+  if (live) {
+    sys.load(a, i);
+    if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
+  }
+  if (nb == E)
+    split_loop<Sys, T, R, true, D>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
+  else
+    split_loop<Sys, T, R, false, D>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
+  if (live && lead) {
     sys.store(a, i);
     if (any_reset) sys.store_autoreset_extra(a, i);
     if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
@@ -400,6 +547,35 @@ __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
 
 // ------------------------------------------------------------------ launchers
 static inline int64_t grid_for(int64_t n) { return (n + kBlock - 1) / kBlock; }
+
+// Two lanes per env in the small-N rollout (variant bit 256 forces one, 512 forces two):
+// by default for LORENZ3 f32 from 32,768 envs (below 131,072 the one-wave path runs).
+// Measured (profiles/r01/ab_rollout_*.json, K = 2048): +11% at 32,768 and +13% at
+// 65,536 envs; slower at 16,384 (the wave's step chain, not the SIMD count, bounds it
+// there) and for PMSM at any N (its step is 3-4x the instructions: doubling them costs
+// more than the extra waves recover).
+template <class Sys>
+static inline bool rollout_split(const KArgs& a) {
+  if constexpr (Sys::O % 2 != 0) return false;
+  if (a.variant & 256) return false;
+  if (a.variant & 512) return true;
+  return std::is_same<Sys, SysL3<float>>::value && a.n >= 32768;
+}
+
+template <class Sys, typename T, int D>
+static void launch_rollout_d(const KArgs& a, hipStream_t s) {
+  if (a.n < 2 * 256 * kBlock) {  // < 2 full workgroups per CU: one-wave groups
+    if (rollout_split<Sys>(a))
+      hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, D>), dim3((unsigned)((a.n + 31) / 32)),
+                         dim3(64), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_rollout<Sys, T, 64, D>), dim3((unsigned)((a.n + 63) / 64)), dim3(64),
+                         0, s, a);
+  } else {
+    hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D>), dim3((unsigned)grid_for(a.n)), dim3(kBlock),
+                       0, s, a);
+  }
+}
 
 // kVariants: instantiate the step-kernel tuning variants (A/B tools use LORENZ3 and
 // PMSM; the other systems always run the default variant)
@@ -423,11 +599,11 @@ static int launch_all(int which, const KArgs& a, hipStream_t s) {
 #undef LZ_STEP_V
       default: hipLaunchKernelGGL((k_step<Sys, T, 0>), grid, block, 0, s, a); break;
     }
-  } else if (a.n < 2 * 256 * kBlock) {  // < 2 full workgroups per CU: one-wave groups
-    hipLaunchKernelGGL((k_rollout<Sys, T, 64>), dim3((unsigned)((a.n + 63) / 64)), dim3(64), 0, s,
-                       a);
+  } else if constexpr (kVariants) {
+    if (a.variant & 1024) launch_rollout_d<Sys, T, 3>(a, s);  // A/B: prefetch distance 3
+    else launch_rollout_d<Sys, T, kDmaDist>(a, s);
   } else {
-    hipLaunchKernelGGL((k_rollout<Sys, T, kBlock>), grid, block, 0, s, a);
+    launch_rollout_d<Sys, T, kDmaDist>(a, s);
   }
   return (int)hipGetLastError();
 }

@@ -21,8 +21,11 @@ struct U4 {
 __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    // one 32x32->64 product per word (v_mad_u64_u32) instead of separate lo / hi
+    // multiplies (both quarter-rate)
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -46,47 +49,42 @@ __device__ __forceinline__ double u01d(uint32_t a, uint32_t b) {
   return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * 1.1102230246251565e-16;
 }
 
-// Three standard normals (Box-Muller on two word pairs) for per-step process noise.
+// One Box-Muller pair from two 32-bit words: u1 in (0, 1], u2 in [0, 1);
+// r = sqrt(-2 ln u1) = sqrt(-2 ln2 * log2 u1), (c, s) = r * (cos, sin)(2 pi u2).
+// Hardware transcendentals (v_log_f32, v_sqrt_f32, v_sin_f32 / v_cos_f32, which take
+// the angle in revolutions): a few ulp, far below what the N(0, sigma) draws are
+// checked for, and ~10 instructions instead of the ~150 of libm-accurate logf /
+// sincospif / sqrtf.  Tails are bounded by the 24-bit u1 (|z| <= 5.77) either way.
+__device__ __forceinline__ void box_muller(uint32_t wa, uint32_t wb, float& c, float& s) {
+  const float u1 = (float)((wa >> 8) + 1u) * 5.9604644775390625e-08f;
+  const float u2 = u01f(wb);
+  const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+  c = r * __builtin_amdgcn_cosf(u2);
+  s = r * __builtin_amdgcn_sinf(u2);
+}
+
+// Three standard normals (two Box-Muller pairs) for per-step process noise.
 __device__ __forceinline__ void normal3(uint64_t seed, uint64_t gid, uint64_t tick, float z[3]) {
   const U4 w = philox_block(seed, gid, kPurposeNoise, tick, 0);
-  const float u1 = (float)((w.x >> 8) + 1u) * 5.9604644775390625e-08f;  // (0,1]
-  const float u2 = u01f(w.y);
-  const float u3 = (float)((w.z >> 8) + 1u) * 5.9604644775390625e-08f;
-  const float u4 = u01f(w.w);
-  const float r1 = sqrtf(-2.0f * logf(u1)), r2 = sqrtf(-2.0f * logf(u3));
-  float s1, c1, s2, c2;
-  sincospif(2.0f * u2, &s1, &c1);
-  sincospif(2.0f * u4, &s2, &c2);
-  z[0] = r1 * c1;
-  z[1] = r1 * s1;
-  z[2] = r2 * c2;
+  float s1, s2;
+  box_muller(w.x, w.y, z[0], s1);
+  z[1] = s1;
+  box_muller(w.z, w.w, z[2], s2);
+  (void)s2;
 }
 
 // Two standard normals for the policy's Gaussian action sample (purpose 3): the first
 // Box-Muller pair of normal4 (identical values), for action dims <= 2.
 __device__ __forceinline__ void normal2(uint64_t seed, uint64_t gid, uint64_t tick, float z[4]) {
   const U4 w = philox_block(seed, gid, kPurposePolicy, tick, 0);
-  const float u1 = (float)((w.x >> 8) + 1u) * 5.9604644775390625e-08f;
-  const float r1 = sqrtf(-2.0f * logf(u1));
-  float s1, c1;
-  sincospif(2.0f * u01f(w.y), &s1, &c1);
-  z[0] = r1 * c1;
-  z[1] = r1 * s1;
+  box_muller(w.x, w.y, z[0], z[1]);
 }
 
 // Four standard normals for the policy's Gaussian action sample (purpose 3).
 __device__ __forceinline__ void normal4(uint64_t seed, uint64_t gid, uint64_t tick, float z[4]) {
   const U4 w = philox_block(seed, gid, kPurposePolicy, tick, 0);
-  const float u1 = (float)((w.x >> 8) + 1u) * 5.9604644775390625e-08f;
-  const float u3 = (float)((w.z >> 8) + 1u) * 5.9604644775390625e-08f;
-  const float r1 = sqrtf(-2.0f * logf(u1)), r2 = sqrtf(-2.0f * logf(u3));
-  float s1, c1, s2, c2;
-  sincospif(2.0f * u01f(w.y), &s1, &c1);
-  sincospif(2.0f * u01f(w.w), &s2, &c2);
-  z[0] = r1 * c1;
-  z[1] = r1 * s1;
-  z[2] = r2 * c2;
-  z[3] = r2 * s2;
+  box_muller(w.x, w.y, z[0], z[1]);
+  box_muller(w.z, w.w, z[2], z[3]);
 }
 
 }  // namespace lz

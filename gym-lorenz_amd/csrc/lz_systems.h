@@ -266,23 +266,23 @@ struct SysPMSM {
   __device__ static float bias(const float* tab, int32_t len, int32_t k) {
     return k < len ? tab[k] : 1.0f;
   }
-  // The two table values for this env's Adam step, by SCALAR loads issued from asm
-  // (waited on with lgkmcnt): a vector load would be waited on with vmcnt, which in the
+  // The two table values for this env's Adam step (one interleaved pair), by a SCALAR
+  // load issued from asm (waited on with lgkmcnt): a vector load would be waited on with vmcnt, which in the
   // fused rollouts also drains every store still in flight from the previous step.  A
   // waterfall over the distinct steps in the wave -- normally one: all envs of a batch
   // step their (never reset) Adam counters together.  The loads are asm so that hipcc
   // cannot rewrite the uniform index back into the lane's own (a vector load).
-  __device__ static float sload(const float* p) {
-    float v;
-    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
-    return v;
+  __device__ static void sload2(const float* p, float& x, float& y) {
+    uint64_t v;
+    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    x = __uint_as_float((uint32_t)v);
+    y = __uint_as_float((uint32_t)(v >> 32));
   }
   __device__ void bias_pair(const KArgs& a, float& bm, float& bv) const {
     for (;;) {
       const int32_t k0 = __builtin_amdgcn_readfirstlane(adam);
-      const bool in = k0 < a.bc_len;
-      const float m = in ? sload(a.bc1 + k0) : 1.0f;
-      const float v = in ? sload(a.bc2 + k0) : 1.0f;
+      float m = 1.0f, v = 1.0f;
+      if (k0 < a.bc_len) sload2(a.bc + 2 * (int64_t)k0, m, v);
       if (adam == k0) {
         bm = m;
         bv = v;

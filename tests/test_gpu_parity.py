@@ -291,9 +291,11 @@ def test_shard_invariance(gl):
 
 @pytest.mark.parametrize("system,dtype,n", [("lorenz3", "float32", 1000), ("pmsm", "float32", 1000),
                                             ("hr", "float64", 1000), ("lorenz4", "float32", 1000),
+                                            ("lorenz3", "float32", 40001),
                                             ("lorenz3", "float32", 140000)])
 def test_rollout_equals_steps(gl, system, dtype, n):
-    """Fused rollout (one-wave workgroups below 131,072 envs, 256-lane above) == K steps."""
+    """Fused rollout (one-wave workgroups below 131,072 envs -- two lanes per env for
+    LORENZ3 f32 from 32,768 -- 256-lane above) == K steps."""
     K = 33
     kw = {"add_noise": True} if system in ("pmsm", "hr") else {}
     a_be = gl.BatchedEnv(system, n, dtype=dtype, seed=4, max_episode_steps=10, **kw)
@@ -310,6 +312,37 @@ def test_rollout_equals_steps(gl, system, dtype, n):
         assert np.array_equal(_np(done[k]), _np(d)), k
     nd = int(nd.item())
     assert nd == int((_np(done) != 0).sum())
+
+
+@pytest.mark.parametrize("system,dtype", [("lorenz3", "float32"), ("pmsm", "float32"),
+                                          ("lorenz4", "float64"), ("hr", "float32")])
+@pytest.mark.parametrize("n", [2016, 1000])
+def test_rollout_split_lanes_bitexact(gl, system, dtype, n):
+    """Small-N rollout with two lanes per env (variant bit 512, the default up to 65,536
+    envs) == one lane per env (bit 256): outputs, final state and compact done list
+    (full one-wave groups at n=2016, a ragged last group at n=1000)."""
+    K = 40
+    kw = {"add_noise": True} if system in ("pmsm", "hr") else {}
+    res = []
+    A = None
+    for var in (256, 512):
+        be = gl.BatchedEnv(system, n, dtype=dtype, seed=6, max_episode_steps=7, variant=var, **kw)
+        if A is None:
+            A = torch.from_numpy(np.random.default_rng(9).uniform(
+                -1.5, 1.5, (K, n, be.action_dim)).astype(np.float32)).cuda()
+        be.reset()
+        be.rollout(A[:3])  # warm state (both kernels from the same start)
+        out = be.rollout(A, capture_terminal=K * n)
+        obs, rew, done, (didx, tobs, nd) = out
+        m = int(nd.item())
+        order = torch.argsort(didx[:m])
+        st = [_np(be.get_state(p)) for p in range(be.info.n_planes)]
+        res.append((_np(obs), _np(rew), _np(done), _np(didx[:m][order]), _np(tobs[:m][order]), st))
+    (o1, r1, d1, i1, t1, s1), (o2, r2, d2, i2, t2, s2) = res
+    assert bits_equal(o1, o2) and bits_equal(r1, r2) and np.array_equal(d1, d2)
+    assert len(i1) > 0 and np.array_equal(i1, i2) and bits_equal(t1, t2)
+    for a, b in zip(s1, s2):
+        assert bits_equal(a, b)
 
 
 def test_l3_1m_envs_vs_oracle(gl, orc):

@@ -53,8 +53,8 @@ def test_host_abi_under_asan_ubsan(tmp_path):
     subprocess.check_call(["gcc", "-g", "-fsanitize=address,undefined", "-I", INC, "-c",
                            os.path.join(ROOT, "tests", "c_abi", "host_sanitize.c"), "-o", drv])
     exe = str(tmp_path / "hsan")
-    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-fsanitize=address,undefined",
-                           "-fno-gpu-sanitize"] + objs + [drv, "-o", exe])
+    link = [HIPCC, "--offload-arch=gfx950", "-fno-gpu-sanitize", "-fsanitize=address,undefined"]
+    subprocess.check_call(link + objs + [drv, "-o", exe])
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=SAN_ENV)
     assert out.returncode == 0, out.stderr[-4000:]
     assert "clean" in out.stdout
