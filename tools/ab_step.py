@@ -1,5 +1,6 @@
 """Interleaved A/B of lz_step kernel variants (one process, hipGraph-replayed steps,
-HIP-event timing on the launch stream).  Usage: python tools/ab_step.py [envs...]"""
+HIP-event timing on the launch stream; order rotated every round, a variant listed twice
+is a noise control).  Usage: AB_VARIANTS=0,32,0 python tools/ab_step.py [envs...]"""
 import ctypes
 import json
 import os
@@ -57,18 +58,20 @@ def main():
     system = os.environ.get("AB_SYSTEM", "lorenz3")
     res = {}
     for n in envs:
-        runs = {v: make(v, n, system) for v in variants}
+        runs = [make(v, n, system) for v in variants]  # a variant may repeat (noise control)
         reps = max(4, int(2e5 / n * 4))
-        samples = {v: [] for v in variants}
-        for _ in range(7):
-            for v in variants:
-                samples[v].append(timeit(runs[v][0], runs[v][1], reps))
-        bps = runs[variants[0]][2][0].bytes_per_env_step
-        for v in variants:
-            s = sorted(samples[v])
+        samples = [[] for _ in variants]
+        V = len(variants)
+        for r in range(9):  # order rotated every round
+            for j in range(V):
+                k = (r + j) % V
+                samples[k].append(timeit(runs[k][0], runs[k][1], reps))
+        bps = runs[0][2][0].bytes_per_env_step
+        for k, v in enumerate(variants):
+            s = sorted(samples[k])
             med = s[len(s) // 2]
-            res["%s n=%d v=%d" % (system, n, v)] = {"us_med": med, "us_min": s[0],
-                                                    "GBps": bps * n / med / 1e3}
+            res["%s n=%d v=%d #%d" % (system, n, v, k)] = {"us_med": med, "us_min": s[0],
+                                                          "GBps": bps * n / med / 1e3}
         del runs
         torch.cuda.empty_cache()
     print(json.dumps(res, indent=1))
