@@ -94,6 +94,7 @@ struct lz_handle {
   int num_cus;         // compute units of the device (policy rollout grid)
   double* pol_part;    // policy rollout obs-moment partials (lazily allocated)
   int64_t pol_part_n;  // doubles allocated
+  uint8_t* vn_ws;      // lz_step_vecnorm moment partials (lazily allocated)
 };
 
 extern "C" {
@@ -277,6 +278,7 @@ lz_status lz_destroy(lz_handle* h) {
   if (h->ticks) (void)hipFree(h->ticks);
   if (h->bc) (void)hipFree(h->bc);
   if (h->pol_part) (void)hipFree(h->pol_part);
+  if (h->vn_ws) (void)hipFree(h->vn_ws);
   delete h;
   return LZ_OK;
 }
@@ -411,6 +413,97 @@ lz_status lz_step(lz_handle* h, const void* actions, const double* noise, void* 
   if (n_done_out)
     HIP_TRY(hipMemcpyAsync(n_done_out, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
   h->parity ^= 1;
+  return LZ_OK;
+}
+
+static lz_status check_vecnorm(const lz_handle* h, const lz_vecnorm* vn) {
+  if (!vn || !vn->obs_rms || !vn->ret_rms || !vn->returns)
+    return fail(LZ_ERR_INVALID, "vecnorm: obs_rms/ret_rms/returns must be non-NULL");
+  if (lz::rms_dim(vn->obs_rms) != h->desc.obs_dim || lz::rms_dim(vn->ret_rms) != 1)
+    return fail(LZ_ERR_INVALID, "vecnorm: obs_rms dim %d (obs_dim %d), ret_rms dim %d (1)",
+                lz::rms_dim(vn->obs_rms), h->desc.obs_dim, lz::rms_dim(vn->ret_rms));
+  if (lz::rms_device(vn->obs_rms) != h->cfg.device || lz::rms_device(vn->ret_rms) != h->cfg.device)
+    return fail(LZ_ERR_INVALID, "vecnorm: statistics live on another device");
+  if ((vn->flags & LZ_VN_DEFER) && !vn->moments)
+    return fail(LZ_ERR_INVALID, "vecnorm: LZ_VN_DEFER needs moments");
+  if (h->desc.obs_dim > lz::kVnMaxObs) return fail(LZ_ERR_UNSUPPORTED, "vecnorm: obs too wide");
+  return LZ_OK;
+}
+
+lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* actions, void* obs_out,
+                          void* rew_out, uint8_t* done_out, int32_t* done_idx_out,
+                          void* terminal_obs_out, int32_t* n_done_out) {
+  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_step_vecnorm before the first lz_reset");
+  const lz_status c = check_vecnorm(h, vn);
+  if (c != LZ_OK) return c;
+  const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4 && h->cfg.system != LZ_SYS_SC;
+  if ((needs_act && !actions) || !obs_out || !rew_out || !done_out || !done_idx_out ||
+      !terminal_obs_out || !n_done_out)
+    return fail(LZ_ERR_INVALID, "actions/obs/rew/done/done_idx/terminal_obs/n_done must be non-NULL");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  const int64_t n = h->cfg.num_envs;
+  const int64_t n_wg = (n + lz::kBlock - 1) / lz::kBlock;
+  if (!h->vn_ws) {  // column-major per-workgroup partials, W = 2 (kVnMaxObs + 1) at most
+    const size_t bytes = (size_t)n_wg * 2 * (lz::kVnMaxObs + 1) * sizeof(double);
+    if (hipMalloc(reinterpret_cast<void**>(&h->vn_ws), bytes) != hipSuccess)
+      return fail(LZ_ERR_OOM, "vecnorm workspace (%zu B)", bytes);
+  }
+  KArgs a;
+  fill_common(h, a);
+  a.act = actions;
+  a.obs = obs_out;
+  a.rew = rew_out;
+  a.done = done_out;
+  a.done_idx32 = done_idx_out;
+  a.term_obs = terminal_obs_out;
+  a.vec_ok = (!needs_act || aligned16(actions)) && aligned16(obs_out);
+  lz::VArgs v;
+  std::memset(&v, 0, sizeof v);
+  v.returns = vn->returns;
+  v.part = reinterpret_cast<double*>(h->vn_ws);
+  v.n_done_out = n_done_out;
+  v.obs_state = lz::rms_state(vn->obs_rms);
+  v.ret_state = lz::rms_state(vn->ret_rms);
+  v.moments = vn->moments;
+  v.gamma = vn->gamma;
+  v.flags = vn->flags;
+  v.n_wg = (int32_t)n_wg;
+  const int e = lz::launch_step_vecnorm(h->cfg.system, h->f64, a, v, h->stream);
+  if (e != 0) return fail(LZ_ERR_HIP, "step launch: %s", hipGetErrorString((hipError_t)e));
+  h->parity ^= 1;
+  return LZ_OK;
+}
+
+lz_status lz_vecnorm_apply(lz_handle* h, const lz_vecnorm* vn, const void* obs_raw,
+                           const void* rew_raw, const uint8_t* done, float* obs_norm,
+                           float* rew_norm, uint8_t* dones_out, const void* terminal_obs_raw,
+                           const int32_t* n_done, float* term_norm) {
+  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  const lz_status c = check_vecnorm(h, vn);
+  if (c != LZ_OK) return c;
+  if (!obs_raw || !rew_raw || !obs_norm || !rew_norm)
+    return fail(LZ_ERR_INVALID, "obs_raw/rew_raw/obs_norm/rew_norm must be non-NULL");
+  if ((done == nullptr) != (dones_out == nullptr))
+    return fail(LZ_ERR_INVALID, "done and dones_out go together");
+  const bool term = terminal_obs_raw != nullptr || term_norm != nullptr;
+  if (term && (!terminal_obs_raw || !term_norm || !n_done))
+    return fail(LZ_ERR_INVALID, "terminal_obs_raw, n_done and term_norm go together");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  const int O = h->desc.obs_dim;
+  if ((vn->flags & LZ_VN_DEFER) && (vn->flags & LZ_VN_TRAINING)) {
+    int e = 0;
+    if (vn->flags & LZ_VN_NORM_OBS) e = lz::launch_rms_update(vn->obs_rms, vn->moments, h->stream);
+    if (e == 0) e = lz::launch_rms_update(vn->ret_rms, vn->moments + 2 * O + 1, h->stream);
+    if (e != 0) return fail(LZ_ERR_HIP, "statistics update: %s", hipGetErrorString((hipError_t)e));
+  }
+  const int e = lz::launch_vn_apply(
+      h->f64, O, h->cfg.num_envs, obs_raw, rew_raw, done, term ? terminal_obs_raw : nullptr,
+      term ? n_done : nullptr, lz::rms_state(vn->obs_rms), lz::rms_state(vn->ret_rms),
+      (vn->flags & LZ_VN_NORM_OBS) != 0, (vn->flags & LZ_VN_NORM_REWARD) != 0, vn->epsilon,
+      vn->clip_obs, vn->clip_reward, obs_norm, rew_norm, dones_out, term ? term_norm : nullptr,
+      h->stream);
+  if (e != 0) return fail(LZ_ERR_HIP, "normalise launch: %s", hipGetErrorString((hipError_t)e));
   return LZ_OK;
 }
 

@@ -49,6 +49,23 @@ struct KArgs {
   double prm[LZ_MAX_PARAMS];
 };
 
+// VecNormalize epilogue of the step kernel (lz_step_vecnorm).  Per-workgroup float64
+// partials of the batch moments, column-major [W][n_wg] with W = 2 (O + 1) columns:
+// sums of obs column 0..O-1, of the returns, then the sums of squares likewise;
+// k_vn_reduce (the next launch) reduces them and updates the statistics.
+constexpr int kVnMaxObs = 8;
+struct VArgs {
+  double* returns;     // [N] VecNormalize.returns
+  double* part;        // [W][n_wg]
+  double* obs_state;   // obs_rms mean[O], var[O], count
+  double* ret_state;   // ret_rms mean, var, count
+  double* moments;     // LZ_VN_DEFER: [2O+1 obs][3 returns] batch moments out
+  int32_t* n_done_out; // the step's done count (device)
+  double gamma;
+  uint32_t flags;      // LZ_VN_*
+  int32_t n_wg;
+};
+
 // Policy-in-the-loop rollout (lz_policy.hip): SB3 ActorCriticPolicy (MlpPolicy,
 // net_arch pi=[128,128] vf=[128,128], Tanh, DiagGaussian) packed as bf16 MFMA
 // fragments.  Blob layout (bytes) -- produced by lz_policy_pack, read by the kernel:
@@ -86,6 +103,20 @@ struct PArgs {
   double* partials;        // [grid * waves][2 * O] obs moment partials (nullable)
 };
 
+// lz_rms internals for the fused VecNormalize step (lz_rms.hip)
+int rms_dim(const lz_rms* r);
+int rms_device(const lz_rms* r);
+double* rms_state(lz_rms* r);  // mean[dim], var[dim], count
+// RunningMeanStd.update_from_moments on `stream` (moments: count, sums, sums of squares)
+int launch_rms_update(lz_rms* r, const double* moments, void* stream);
+// normalised obs [n, O] / reward [n] / 0-1 dones [n] / terminal rows [*n_done, O]
+// (lz_vecnorm_apply)
+int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
+                    const uint8_t* done, const void* term, const int32_t* n_done,
+                    const double* obs_state, const double* ret_state, int norm_obs, int norm_rew,
+                    double eps, double clip_obs, double clip_rew, float* obs_n, float* rew_n,
+                    uint8_t* dones, float* term_n, void* stream);
+
 // record the thread-local message lz_last_error() returns; returns s
 lz_status set_error(lz_status s, const char* msg);
 
@@ -93,6 +124,7 @@ lz_status set_error(lz_status s, const char* msg);
 int launch_reset(int system, int f64, const KArgs& a, void* stream);
 int launch_step(int system, int f64, const KArgs& a, void* stream);
 int launch_rollout(int system, int f64, const KArgs& a, void* stream);
+int launch_step_vecnorm(int system, int f64, const KArgs& a, const VArgs& v, void* stream);
 // Launch shape of the policy rollout (one workgroup per CU: the weights fill LDS).
 //   >= 131,072 envs: 64 envs per wave (two 32-env MFMA column tiles, every lane steps
 //                    an env), 8 waves per workgroup (2 per SIMD);

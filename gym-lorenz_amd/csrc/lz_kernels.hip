@@ -18,6 +18,7 @@
 
 #include "lz_body.h"
 #include "lz_internal.h"
+#include "lz_rms_math.h"
 #include "lz_systems.h"
 
 namespace lz {
@@ -106,8 +107,130 @@ constexpr int step_block() {  // bits 3-4 of V: workgroup size
   return ((V >> 3) & 3) == 1 ? 512 : ((V >> 3) & 3) == 2 ? 128 : ((V >> 3) & 3) == 3 ? 1024 : 256;
 }
 
-template <class Sys, typename T, int V>
-__global__ __launch_bounds__(step_block<V>()) void k_step(KArgs a) {
+// ------------------------------------------------------------------ VecNormalize epilogue
+// (lz_step_vecnorm, lz_internal.h VArgs).  Per-workgroup float64 moments of the obs
+// columns (read back from the LDS obs tile) and of the updated returns: each column
+// summed by 32 lanes over strided rows, then a fixed xor tree; one plain store per
+// column into the column-major partials.  k_vn_reduce, the next launch on the stream,
+// sums them in a fixed order (no cross-workgroup synchronisation inside the step: an
+// in-kernel last-arriver reduction needs every workgroup to wait for its stores'
+// acknowledgements before taking a ticket, which measured 4x the step time at 1M envs).
+template <int O, typename T>
+__device__ __forceinline__ void vn_epilogue(const T* s_obs, const double* s_ret, int nb, int tid,
+                                            const VArgs& v) {
+  constexpr int C = O + 1;
+  __shared__ double red[2 * C][33];  // [column sums | sums of squares][lane], padded
+  const int j = tid & 31;
+  for (int c = tid >> 5; c < C; c += kBlock / 32) {
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 32; ++k) {  // rows j, j+32, ..., in order
+      const int r = j + 32 * k;
+      if (r < nb) {
+        const double x = c < O ? (double)(float)s_obs[r * O + c] : s_ret[r];
+        s += x;
+        q += x * x;
+      }
+    }
+    red[c][j] = s;
+    red[C + c][j] = q;
+  }
+  __syncthreads();
+  if (tid < 2 * C) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) t += red[tid][k];
+    v.part[(int64_t)tid * v.n_wg + blockIdx.x] = t;
+  }
+}
+
+// One workgroup of B lanes: the batch moments from the n_wg partials of every column
+// -- lane t sums workgroups t, t+B, ... in order, 8 rows of every column in flight per
+// round (coalesced column-major loads; one round at 1M envs), then a fixed LDS tree
+// over the lanes -- and the RunningMeanStd updates (lz_rms_math.h, as k_rms_update)
+// or, with LZ_VN_DEFER, the moments for the caller's all-reduce.  Also publishes the
+// step's done count.
+template <int O>
+constexpr int vn_reduce_block() {  // the LDS tree holds W x B doubles (<= 64 KiB)
+  return 2 * (O + 1) * 512 * 8 <= 65536 ? 512 : 256;
+}
+template <int O>
+__global__ __launch_bounds__(vn_reduce_block<O>()) void k_vn_reduce(VArgs v, int64_t n,
+                                                                   const int32_t* counter,
+                                                                   int32_t* n_done_out) {
+  constexpr int kVnReduceBlock = vn_reduce_block<O>();
+  constexpr int C = O + 1, W = 2 * C, U = 8;
+  __shared__ double red[W][kVnReduceBlock];
+  __shared__ double s_tot[W];
+  const int tid = (int)threadIdx.x;
+  if (tid == 0) *n_done_out = *counter;
+  if (!(v.flags & LZ_VN_TRAINING)) return;
+  double acc[W];
+#pragma unroll
+  for (int c = 0; c < W; ++c) acc[c] = 0.0;
+  for (int r = tid; r < v.n_wg; r += U * kVnReduceBlock) {
+    double x[U][W];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ru = r + u * kVnReduceBlock;
+#pragma unroll
+      for (int c = 0; c < W; ++c) x[u][c] = ru < v.n_wg ? v.part[(int64_t)c * v.n_wg + ru] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int c = 0; c < W; ++c) acc[c] += x[u][c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < W; ++c) red[c][tid] = acc[c];
+  __syncthreads();
+  for (int half = kVnReduceBlock / 2; half > 0; half >>= 1) {  // fixed pairing tree
+    for (int e = tid; e < W * half; e += kVnReduceBlock) {
+      const int c = e / half, k = e % half;
+      red[c][k] += red[c][k + half];
+    }
+    __syncthreads();
+  }
+  if (tid < W) s_tot[tid] = red[tid][0];
+  __syncthreads();
+  const double bc = (double)n;
+  if (v.flags & LZ_VN_DEFER) {  // (count, sums, sumsq) for obs, then for returns
+    if (tid < O) {
+      v.moments[1 + tid] = s_tot[tid];
+      v.moments[1 + O + tid] = s_tot[C + tid];
+    }
+    if (tid == 0) {
+      v.moments[0] = bc;
+      v.moments[2 * O + 1] = bc;
+      v.moments[2 * O + 2] = s_tot[O];
+      v.moments[2 * O + 3] = s_tot[C + O];
+    }
+    return;
+  }
+  const bool upd_obs = (v.flags & LZ_VN_NORM_OBS) && tid < O;
+  const bool upd_ret = tid == 64;
+  const double c_obs = v.obs_state[2 * O], c_ret = v.ret_state[2];
+  double nm = 0.0, nv = 0.0;
+  if (upd_obs)
+    rms_new(v.obs_state[tid], v.obs_state[O + tid], c_obs, bc, s_tot[tid], s_tot[C + tid], nm, nv);
+  if (upd_ret) rms_new(v.ret_state[0], v.ret_state[1], c_ret, bc, s_tot[O], s_tot[C + O], nm, nv);
+  __syncthreads();  // every lane has read the counts before they are rewritten
+  if (upd_obs) {
+    v.obs_state[tid] = nm;
+    v.obs_state[O + tid] = nv;
+    if (tid == 0) v.obs_state[2 * O] = c_obs + bc;
+  }
+  if (upd_ret) {
+    v.ret_state[0] = nm;
+    v.ret_state[1] = nv;
+    v.ret_state[2] = c_ret + bc;
+  }
+}
+
+// One 256-env tile of lz_step (k_step) or lz_step_vecnorm (k_step_vn, kVN).
+template <class Sys, typename T, int V, bool kVN>
+__device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
   constexpr int SB = step_block<V>();
   constexpr bool NT = (V & 1) == 0;
   constexpr bool kLds = (V & 2) == 0;
@@ -128,9 +251,11 @@ __global__ __launch_bounds__(step_block<V>()) void k_step(KArgs a) {
   Sys sys;
   sys.setup(a);
   int32_t steps = 0;
+  double ret_in = 0.0;  // kVN: VecNormalize.returns[i], loaded with the state
   if (live) {  // state loads first: in flight together with the action staging
     sys.load(a, i);
     if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
+    if constexpr (kVN) ret_in = v.returns[i];
   }
   float act[Sys::A];
   if constexpr (Sys::kUsesAction) {
@@ -150,8 +275,21 @@ __global__ __launch_bounds__(step_block<V>()) void k_step(KArgs a) {
   T o[Sys::O];
   T rew = (T)0;
   bool did_reset;
+  double* s_ret_p = nullptr;
   const uint8_t dflag =
       step_body<Sys, T, false>(sys, steps, a, i, live, act, tick, 0, o, rew, did_reset);
+  if constexpr (kVN) {  // VecNormalize.returns: r*gamma + reward, moments, then [done] = 0
+    __shared__ double s_ret[SB];
+    double rn = 0.0;
+    if (live) {
+      double r0 = ret_in;
+      if (v.flags & LZ_VN_TRAINING) r0 = r0 * v.gamma + (double)(float)rew;
+      rn = r0;
+      v.returns[i] = dflag ? 0.0 : r0;
+    }
+    s_ret[tid] = rn;
+    s_ret_p = s_ret;
+  }
   if (live) {
     sys.store(a, i);
     if (did_reset) sys.store_autoreset_extra(a, i);
@@ -170,7 +308,22 @@ __global__ __launch_bounds__(step_block<V>()) void k_step(KArgs a) {
     wg_barrier<kFullBar>();
     stage_out<NT, T, Sys::O, SB>(static_cast<T*>(a.obs) + base * Sys::O, s_obs, nb, tid, vec);
   }
+  if constexpr (kVN) {
+    static_assert(kLds && SB == kBlock, "the VecNormalize epilogue reads the LDS obs tile");
+    if (v.flags & LZ_VN_TRAINING) vn_epilogue<Sys::O, T>(s_obs, s_ret_p, nb, tid, v);
+  }
 }
+
+template <class Sys, typename T, int V>
+__global__ __launch_bounds__(step_block<V>()) void k_step(KArgs a) {
+  step_tile<Sys, T, V, false>(a, VArgs{});
+}
+
+template <class Sys, typename T>
+__global__ __launch_bounds__(kBlock) void k_step_vn(KArgs a, VArgs v) {
+  step_tile<Sys, T, 0, true>(a, v);
+}
+
 
 // ------------------------------------------------------------------ fused rollout
 // K steps in one launch, state in VGPRs.  B = envs per workgroup: 256, or 64 (one
@@ -634,6 +787,38 @@ static int dispatch(int which, int system, int f64, const KArgs& a, void* stream
     case LZ_SYS_SC:
       return f64 ? launch_all<SysSC<double>, double>(which, a, s)
                  : launch_all<SysSC<float>, float>(which, a, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+template <class Sys, typename T>
+static int launch_vn(const KArgs& a, const VArgs& v, hipStream_t s) {
+  static_assert(Sys::O <= kVnMaxObs, "obs too wide for the VecNormalize epilogue");
+  hipLaunchKernelGGL((k_step_vn<Sys, T>), dim3((unsigned)grid_for(a.n)), dim3(kBlock), 0, s, a, v);
+  hipLaunchKernelGGL((k_vn_reduce<Sys::O>), dim3(1), dim3(vn_reduce_block<Sys::O>()), 0, s, v, a.n,
+                     a.counter, v.n_done_out);
+  return (int)hipGetLastError();
+}
+
+int launch_step_vecnorm(int system, int f64, const KArgs& a, const VArgs& v, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (system) {
+    case LZ_SYS_LORENZ3:
+      return f64 ? launch_vn<SysL3<double>, double>(a, v, s) : launch_vn<SysL3<float>, float>(a, v, s);
+    case LZ_SYS_LORENZ4:
+      return f64 ? launch_vn<SysL4<double>, double>(a, v, s) : launch_vn<SysL4<float>, float>(a, v, s);
+    case LZ_SYS_PMSM:
+      return launch_vn<SysPMSM, float>(a, v, s);
+    case LZ_SYS_HR:
+      return f64 ? launch_vn<SysHR<double>, double>(a, v, s) : launch_vn<SysHR<float>, float>(a, v, s);
+    case LZ_SYS_T1:
+      return f64 ? launch_vn<SysT1<double>, double>(a, v, s) : launch_vn<SysT1<float>, float>(a, v, s);
+    case LZ_SYS_T2:
+      return f64 ? launch_vn<SysT2<double>, double>(a, v, s) : launch_vn<SysT2<float>, float>(a, v, s);
+    case LZ_SYS_TP:
+      return f64 ? launch_vn<SysTP<double>, double>(a, v, s) : launch_vn<SysTP<float>, float>(a, v, s);
+    case LZ_SYS_SC:
+      return f64 ? launch_vn<SysSC<double>, double>(a, v, s) : launch_vn<SysSC<float>, float>(a, v, s);
   }
   return (int)hipErrorInvalidValue;
 }

@@ -15,9 +15,11 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
 
 #include "lorenz_env.h"
 #include "lz_internal.h"
+#include "lz_rms_math.h"
 
 namespace {
 
@@ -107,18 +109,8 @@ __global__ void k_rms_update(double* mean, double* var, double* count, const dou
   const double c = *count;
   double new_mean = 0.0, new_var = 0.0;
   const bool act = d < D && bc > 0.0;
-  if (act) {
-    const double bm = moments[1 + d] / bc;
-    double bv = moments[1 + D + d] / bc - bm * bm;
-    if (bv < 0.0) bv = 0.0;
-    const double delta = bm - mean[d];
-    const double tot = c + bc;
-    new_mean = mean[d] + delta * bc / tot;
-    const double m_a = var[d] * c;
-    const double m_b = bv * bc;
-    const double m_2 = m_a + m_b + delta * delta * c * bc / tot;
-    new_var = m_2 / tot;
-  }
+  if (act)
+    lz::rms_new(mean[d], var[d], c, bc, moments[1 + d], moments[1 + D + d], new_mean, new_var);
   __syncthreads();  // every lane has read *count before lane 0 rewrites it
   if (act) {
     mean[d] = new_mean;
@@ -134,11 +126,7 @@ __global__ void k_rms_normalize(const void* x, int64_t n, int D, const double* m
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n * D) return;
   const int d = (int)(e % D);
-  double v = ldx<T>(x, e);
-  if (center) v = v - mean[d];
-  v = v / sqrt(var[d] + eps);
-  v = v < -clip ? -clip : (v > clip ? clip : v);  // np.clip (NaN-propagating)
-  y[e] = (float)v;
+  y[e] = lz::rms_norm(ldx<T>(x, e), mean[d], var[d], center != 0, eps, clip);
 }
 
 // VecNormalize._update_reward / step_wait: returns = returns * gamma + reward, then
@@ -150,6 +138,108 @@ __global__ void k_returns(double* ret, const void* rew, const uint8_t* done, int
   if (i >= n) return;
   if (phase == 0) ret[i] = ret[i] * gamma + ldx<T>(rew, i);
   else if (done[i]) ret[i] = 0.0;
+}
+
+// lz_vecnorm_apply: the normalised outputs of one VecNormalize.step_wait.  Threads of
+// the first row_blocks workgroups own R consecutive env rows each (R * O a multiple of
+// 4, so the obs columns of each element are compile-time constants and the rows move
+// as 16-B vectors when aligned): obs rows, rewards and the done flags as 0/1 bytes
+// (SB3's bool dones); the remaining workgroups grid-stride over the n_done terminal
+// rows.  Inputs are rounded to float32 first: SB3's VecNormalize sees DummyVecEnv's
+// float32 buffers.
+struct VnApplyArgs {
+  int64_t n;
+  const void* obs;
+  const void* rew;
+  const void* term;
+  const uint8_t* done;
+  const int32_t* n_done;
+  const double* os;  // obs_rms mean[O], var[O], count
+  const double* rs;  // ret_rms mean, var, count
+  double eps, clip_obs, clip_rew;
+  float* obs_n;
+  float* rew_n;
+  float* term_n;
+  uint8_t* dones;
+  int norm_obs, norm_rew, vec, row_blocks;
+};
+
+typedef float f4a __attribute__((ext_vector_type(4)));
+
+template <typename T, int O>
+__global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
+  constexpr int R = (O % 4 == 0) ? 1 : (O % 2 == 0 ? 2 : 4);
+  constexpr int E = R * O;
+  double mean[O], sd[O];
+#pragma unroll
+  for (int d = 0; d < O; ++d) {
+    mean[d] = p.os[d];
+    sd[d] = sqrt(p.os[O + d] + p.eps);
+  }
+  const T* obs = static_cast<const T*>(p.obs);
+  if ((int)blockIdx.x < p.row_blocks) {
+    const int64_t r0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * R;
+    if (r0 >= p.n) return;  // only in the last (partial, barrier-free) tile
+    const bool tile_full = ((int64_t)blockIdx.x + 1) * 256 * R <= p.n;  // uniform
+    float x[E], y[E];
+    if (std::is_same<T, float>::value && p.vec && tile_full) {
+      // the workgroup's [256 R, O] slice moves as contiguous float4s through LDS
+      __shared__ f4a tile[256 * E / 4];
+      const f4a* src = reinterpret_cast<const f4a*>(obs + (int64_t)blockIdx.x * 256 * E);
+#pragma unroll
+      for (int k = 0; k < E / 4; ++k) tile[threadIdx.x + 256 * k] = src[threadIdx.x + 256 * k];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < E / 4; ++k) {
+        const f4a q = tile[threadIdx.x * (E / 4) + k];
+        x[4 * k] = q[0]; x[4 * k + 1] = q[1]; x[4 * k + 2] = q[2]; x[4 * k + 3] = q[3];
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        y[e] = p.norm_obs ? lz::rms_norm_sd((double)x[e], mean[e % O], sd[e % O], true, p.clip_obs)
+                          : x[e];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < E / 4; ++k)
+        tile[threadIdx.x * (E / 4) + k] = (f4a){y[4 * k], y[4 * k + 1], y[4 * k + 2], y[4 * k + 3]};
+      __syncthreads();
+      f4a* dst = reinterpret_cast<f4a*>(p.obs_n + (int64_t)blockIdx.x * 256 * E);
+#pragma unroll
+      for (int k = 0; k < E / 4; ++k) dst[threadIdx.x + 256 * k] = tile[threadIdx.x + 256 * k];
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) x[e] = (r0 + e / O < p.n) ? (float)obs[r0 * O + e] : 0.0f;
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        y[e] = p.norm_obs ? lz::rms_norm_sd((double)x[e], mean[e % O], sd[e % O], true, p.clip_obs)
+                          : x[e];
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (r0 + e / O < p.n) p.obs_n[r0 * O + e] = y[e];
+    }
+    const T* rew = static_cast<const T*>(p.rew);
+    const double rsd = sqrt(p.rs[1] + p.eps);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if (r0 + k >= p.n) break;
+      const float r = (float)rew[r0 + k];
+      p.rew_n[r0 + k] = p.norm_rew ? lz::rms_norm_sd((double)r, 0.0, rsd, false, p.clip_rew) : r;
+      if (p.dones) p.dones[r0 + k] = p.done[r0 + k] != 0;
+    }
+    return;
+  }
+  if (p.term == nullptr) return;
+  const T* term = static_cast<const T*>(p.term);
+  const int64_t m = *p.n_done;
+  const int64_t stride = (int64_t)(gridDim.x - p.row_blocks) * 256;
+  for (int64_t j = (int64_t)(blockIdx.x - p.row_blocks) * 256 + threadIdx.x; j < m; j += stride) {
+#pragma unroll
+    for (int d = 0; d < O; ++d) {
+      const float x = (float)term[j * O + d];
+      p.term_n[j * O + d] =
+          p.norm_obs ? lz::rms_norm_sd((double)x, mean[d], sd[d], true, p.clip_obs) : x;
+    }
+  }
 }
 
 }  // namespace
@@ -168,7 +258,63 @@ struct lz_rms {
     if (e_ != hipSuccess) return rfail(LZ_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
+namespace lz {
+
+int rms_dim(const lz_rms* r) { return r->dim; }
+int rms_device(const lz_rms* r) { return r->device; }
+double* rms_state(lz_rms* r) { return r->state; }
+
+int launch_rms_update(lz_rms* r, const double* moments, void* stream) {
+  const int D = r->dim;
+  hipLaunchKernelGGL(k_rms_update, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     r->state, r->state + D, r->state + 2 * D, moments, D);
+  return (int)hipGetLastError();
+}
+
+int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
+                    const uint8_t* done, const void* term, const int32_t* n_done,
+                    const double* obs_state, const double* ret_state, int norm_obs, int norm_rew,
+                    double eps, double clip_obs, double clip_rew, float* obs_n, float* rew_n,
+                    uint8_t* dones, float* term_n, void* stream) {
+  if (n == 0) return 0;
+  const int R = (O % 4 == 0) ? 1 : (O % 2 == 0 ? 2 : 4);
+  VnApplyArgs p;
+  p.n = n;
+  p.obs = obs;
+  p.rew = rew;
+  p.term = term;
+  p.done = done;
+  p.n_done = n_done;
+  p.os = obs_state;
+  p.rs = ret_state;
+  p.eps = eps;
+  p.clip_obs = clip_obs;
+  p.clip_rew = clip_rew;
+  p.obs_n = obs_n;
+  p.rew_n = rew_n;
+  p.term_n = term_n;
+  p.dones = dones;
+  p.norm_obs = norm_obs;
+  p.norm_rew = norm_rew;
+  p.vec = !f64 && ((uintptr_t)obs % 16 == 0) && ((uintptr_t)obs_n % 16 == 0);
+  p.row_blocks = (int)((n + 256 * R - 1) / (256 * R));
+  const int tb = term ? (p.row_blocks < 64 ? p.row_blocks : 64) : 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)(p.row_blocks + tb)), block(256);
+  switch (O * 2 + (f64 ? 1 : 0)) {
+    case 12: hipLaunchKernelGGL((k_vn_apply<float, 6>), grid, block, 0, s, p); break;
+    case 13: hipLaunchKernelGGL((k_vn_apply<double, 6>), grid, block, 0, s, p); break;
+    case 16: hipLaunchKernelGGL((k_vn_apply<float, 8>), grid, block, 0, s, p); break;
+    case 17: hipLaunchKernelGGL((k_vn_apply<double, 8>), grid, block, 0, s, p); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace lz
+
 extern "C" {
+
 
 lz_status lz_rms_create(int32_t dim, int32_t device, double count_init, lz_rms** out) {
   if (!out) return rfail(LZ_ERR_INVALID, "out is NULL");

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgym_lorenz_amd.so")
+# LZ_LIB_AB: an alternative build of the same library, for A/B timing tools only
+LIB_PATH = os.environ.get("LZ_LIB_AB") or os.path.join(_HERE, "libgym_lorenz_amd.so")
 
 LZ_OK, LZ_ERR_INVALID, LZ_ERR_UNSUPPORTED, LZ_ERR_HIP, LZ_ERR_STATE, LZ_ERR_OOM = range(6)
 LORENZ3, LORENZ4, PMSM, HR = range(4)
@@ -104,6 +105,23 @@ class LzPolicyRolloutArgs(ctypes.Structure):
     ]
 
 
+class LzVecNorm(ctypes.Structure):
+    _fields_ = [
+        ("obs_rms", ctypes.c_void_p),
+        ("ret_rms", ctypes.c_void_p),
+        ("returns", ctypes.c_void_p),
+        ("moments", ctypes.c_void_p),
+        ("gamma", ctypes.c_double),
+        ("epsilon", ctypes.c_double),
+        ("clip_obs", ctypes.c_double),
+        ("clip_reward", ctypes.c_double),
+        ("flags", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+VN_TRAINING, VN_NORM_OBS, VN_NORM_REWARD, VN_DEFER = 1, 2, 4, 8
+
 VP = ctypes.c_void_p
 _SIGS = {
     "lz_config_init": (ctypes.c_int, [ctypes.POINTER(LzConfig), ctypes.c_int32]),
@@ -132,6 +150,9 @@ _SIGS = {
                                         ctypes.c_double, ctypes.c_double]),
     "lz_returns_update": (ctypes.c_int, [VP, VP, ctypes.c_int32, VP, ctypes.c_int64, ctypes.c_double,
                                          ctypes.c_int32, ctypes.c_int32, VP]),
+    "lz_step_vecnorm": (ctypes.c_int, [VP, ctypes.POINTER(LzVecNorm), VP, VP, VP, VP, VP, VP, VP]),
+    "lz_vecnorm_apply": (ctypes.c_int, [VP, ctypes.POINTER(LzVecNorm), VP, VP, VP, VP, VP, VP, VP,
+                                        VP, VP]),
     "lz_policy_blob_bytes": (ctypes.c_int64, []),
     "lz_policy_pack": (ctypes.c_int, [ctypes.POINTER(LzMlpPolicy), VP, ctypes.c_int64]),
     "lz_rollout_policy": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),

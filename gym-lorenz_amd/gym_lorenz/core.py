@@ -160,6 +160,26 @@ class BatchedEnv:
         self._last_actions = a  # keep alive until the stream consumed it
         return obs, rew, done
 
+    def step_vecnorm(self, actions, vn, out, compact_out):
+        """lz_step_vecnorm: one step plus VecNormalize's statistics bookkeeping
+        (`vn` an LzVecNorm).  out = (obs, rew, done) raw outputs, compact_out =
+        (done_idx, terminal_obs, n_done); all caller-owned device tensors."""
+        a = self._check_dev(actions, torch.float32, (self.num_envs, self.action_dim), "actions")
+        obs, rew, done = out
+        didx, tobs, ndone = compact_out
+        nat.check(nat.lib.lz_step_vecnorm(self._h, ctypes.byref(vn), _ptr(a), _ptr(obs), _ptr(rew),
+                                          _ptr(done), _ptr(didx), _ptr(tobs), _ptr(ndone)))
+        self._last_actions = a
+        return obs, rew, done
+
+    def vecnorm_apply(self, vn, obs, rew, obs_n, rew_n, term=None, n_done=None, term_n=None,
+                      done=None, dones=None):
+        """lz_vecnorm_apply: the normalised float32 obs / reward / terminal rows and,
+        with done / dones, the 0-1 done bytes (a torch.bool view)."""
+        nat.check(nat.lib.lz_vecnorm_apply(self._h, ctypes.byref(vn), _ptr(obs), _ptr(rew),
+                                           _ptr(done), _ptr(obs_n), _ptr(rew_n), _ptr(dones),
+                                           _ptr(term), _ptr(n_done), _ptr(term_n)))
+
     def done_list(self):
         """(env indices, terminal observations) of envs done in the last step,
         sorted by env index. Synchronises the stream."""

@@ -70,10 +70,11 @@ class DeviceLazyInfos(Sequence):
     first access synchronises once and materialises the done envs' dicts
     ("terminal_observation" as a device tensor row, "TimeLimit.truncated")."""
 
-    def __init__(self, n, done, done_idx, term_obs, n_done):
+    def __init__(self, n, done, done_idx, term_obs, n_done, host=False):
         self._n = n
         self._dev = (done, done_idx, term_obs, n_done)
         self._li = None
+        self._host = host  # terminal observations as NumPy float32 rows
 
     def _mat(self):
         if self._li is None:
@@ -82,6 +83,8 @@ class DeviceLazyInfos(Sequence):
             idx = didx[:m].cpu().numpy()
             flags = done.cpu().numpy()
             t = tobs[:m].float()
+            if self._host:
+                t = t.cpu().numpy()
             entries = {}
             for j, i in enumerate(idx):
                 f = int(flags[i])
@@ -176,16 +179,20 @@ class LorenzVecEnv(VecEnvBase):
     def step_async(self, actions):
         self._actions = actions
 
-    def step_wait(self):
-        acts = self._actions
+    def device_actions(self, acts):
+        """Host actions through the pinned staging buffer (one H2D copy); device
+        tensors pass through."""
         if not isinstance(acts, torch.Tensor) and self._pin_act is not None:
             np.copyto(self._pin_act.numpy(),
                       np.asarray(acts, dtype=np.float32).reshape(self.num_envs, -1))
             self._dev_act.copy_(self._pin_act, non_blocking=True)
-            acts = self._dev_act
-        elif not isinstance(acts, torch.Tensor):
-            acts = torch.from_numpy(np.asarray(acts, dtype=np.float32).reshape(
-                self.num_envs, -1))
+            return self._dev_act
+        if not isinstance(acts, torch.Tensor):
+            return torch.from_numpy(np.asarray(acts, dtype=np.float32).reshape(self.num_envs, -1))
+        return acts
+
+    def step_wait(self):
+        acts = self.device_actions(self._actions)
         if self.return_tensors and isinstance(self.backend, BatchedEnv):
             # sync-free: fresh output tensors per step (the caching allocator recycles
             # them) and the compact done list kept for DeviceLazyInfos

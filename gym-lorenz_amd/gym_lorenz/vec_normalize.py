@@ -14,6 +14,14 @@ vec_normalize.py) but runs it on the GPU over the LorenzVecEnv's device outputs
               terminal observations normalised; returns[dones] = 0
   reset:      returns = 0; obs_rms.update(obs); normalised obs
 
+step_wait over a LorenzVecEnv runs as three launches and no host synchronisation
+(lz_step_vecnorm + lz_vecnorm_apply): the env step kernel also produces float64
+per-workgroup moments of the observations and of the updated returns, a
+one-workgroup kernel reduces them in a fixed order and applies the two RunningMeanStd
+updates, and the third writes the normalised obs / rewards / terminal observations
+and the bool dones.  infos are materialised lazily (only done envs get dicts, on
+first access).
+
 Multi-GPU: pass `group` (a torch.distributed process group): the batch moments
 (count, sum, sum of squares) are all-reduced before every update, so all ranks hold
 the statistics of the whole env population (one 2*obs_dim+1 double all-reduce per
@@ -28,6 +36,8 @@ import torch
 import torch.distributed as dist
 
 from . import _native as nat
+from .core import BatchedEnv
+from .vec_env import DeviceLazyInfos, LazyInfos
 
 
 def _p(t):
@@ -133,6 +143,9 @@ class LorenzVecNormalize:
         self.norm_reward = norm_reward
         self.group = group
         self.returns = torch.zeros((self.num_envs,), dtype=torch.float64, device=self.device)
+        self._moments = torch.zeros((2 * obs_dim + 4,), dtype=torch.float64, device=self.device)
+        self._fused = isinstance(be, BatchedEnv) and be.compact
+        self._layout = self._vn = None
         self.old_obs = None
         self.old_reward = None
         self._actions = None
@@ -173,7 +186,7 @@ class LorenzVecNormalize:
         return be.step(acts)
 
     def reset(self):
-        obs = self.venv.backend.reset()
+        obs = self.venv.backend.reset().float()  # SB3 sees DummyVecEnv's float32 obs
         self.old_obs = obs.clone()
         self.returns.zero_()
         if self.training and self.norm_obs:
@@ -184,7 +197,67 @@ class LorenzVecNormalize:
     def step_async(self, actions):
         self._actions = actions
 
+    def _flags(self):
+        return ((nat.VN_TRAINING if self.training else 0) | (nat.VN_NORM_OBS if self.norm_obs else 0)
+                | (nat.VN_NORM_REWARD if self.norm_reward else 0)
+                | (nat.VN_DEFER if self.group is not None else 0))
+
+    def _vn_args(self):
+        vn = nat.LzVecNorm()
+        vn.obs_rms = self.obs_rms._h.value
+        vn.ret_rms = self.ret_rms._h.value
+        vn.returns = self.returns.data_ptr()
+        vn.moments = self._moments.data_ptr()
+        vn.gamma, vn.epsilon = float(self.gamma), float(self.epsilon)
+        vn.clip_obs, vn.clip_reward = float(self.clip_obs), float(self.clip_reward)
+        vn.flags = self._flags()
+        return vn
+
+    def _step_wait_fused(self):
+        venv, be = self.venv, self.venv.backend
+        n, o, dev, td = self.num_envs, be.obs_dim, self.device, be.tdtype
+        if self._layout is None:
+            # every output of a step in one fresh allocation per step (the caching
+            # allocator recycles it once the caller drops the views): raw obs and
+            # terminal obs, raw reward (old_obs, old_reward), normalised obs /
+            # terminal obs / reward, compact list + count, done bytes, 0-1 dones
+            es = torch.empty((), dtype=td).element_size()
+            spec = [(td, (n, o)), (td, (n, o)), (td, (n,)), (torch.float32, (n, o)),
+                    (torch.float32, (n, o)), (torch.float32, (n,)), (torch.int32, (n + 1,)),
+                    (torch.uint8, (n,)), (torch.uint8, (n,))]
+            offs, off = [], 0
+            for dt, shp in spec:
+                nb = int(np.prod(shp)) * (es if dt == td else torch.empty((), dtype=dt).element_size())
+                offs.append((off, nb, dt, shp))
+                off += (nb + 15) // 16 * 16
+            self._layout = (off, offs)
+        total, offs = self._layout
+        buf = torch.empty((total,), dtype=torch.uint8, device=dev)
+        obs, tobs, rew, obs_n, tn, rew_n, idx, done, dones = [
+            buf[a: a + b].view(dt).view(shp) for a, b, dt, shp in offs]
+        didx, ndone = idx[:n], idx[n:]
+        key = (self._flags(), self.gamma, self.epsilon, self.clip_obs, self.clip_reward)
+        if self._vn is None or self._vn[0] != key:
+            self._vn = (key, self._vn_args())
+        vn = self._vn[1]
+        be.step_vecnorm(venv.device_actions(self._actions), vn, (obs, rew, done), (didx, tobs, ndone))
+        if self.group is not None and self.training:
+            dist.all_reduce(self._moments, group=self.group)
+        be.vecnorm_apply(vn, obs, rew, obs_n, rew_n, tobs, ndone, tn, done, dones)
+        self.old_obs = obs if td == torch.float32 else obs.float()
+        self.old_reward = rew if td == torch.float32 else rew.float()
+        dones_b = dones.view(torch.bool)
+        if venv.return_tensors:
+            return obs_n, rew_n, dones_b, DeviceLazyInfos(n, done, didx, tn, ndone)
+        obs_h, rew_h, done_h = obs_n.cpu().numpy(), rew_n.cpu().numpy(), dones_b.cpu().numpy()
+        infos = DeviceLazyInfos(n, done, didx, tn, ndone, host=True)
+        if not venv.lazy_infos:
+            infos = [infos[i] for i in range(n)]
+        return obs_h, rew_h, done_h, infos
+
     def step_wait(self):
+        if self._fused:
+            return self._step_wait_fused()
         be = self.venv.backend
         obs, rew, done = self._dev_outputs(self._actions)
         self.old_obs = obs.clone()

@@ -30,6 +30,10 @@
  *   (legacy, unregistered: lorenz_env_transient1.py:18-104,
  *    lorenz_env_transient2.py:115-240, lorenz_env_transient_pmsm.py:17-133,
  *    lorenz_singlecontrol.py:97-172 -- LZ_SYS_T1 / T2 / TP / SC)
+ *   lz_step_vecnorm / lz_vecnorm_apply
+ *       -> VecNormalize(DummyVecEnv(...)).step() as the PMSM callers wrap the env
+ *          (code/lorenz_pmsm/train.py:118,170, optimize.py:52; SB3 2.7.1
+ *          common/vec_env/vec_normalize.py): step + statistics + normalisation
  *   lz_get_state / lz_set_state
  *       -> attribute access env.state1 / state2 / state_master / state_slave /
  *          lambda_coef ... used by code/lorenz_pmsm/test_evaluate.py:99-111
@@ -342,6 +346,62 @@ lz_status lz_rms_normalize(lz_rms* r, const void* x, int32_t dtype, int64_t n, f
 lz_status lz_returns_update(double* returns, const void* rew, int32_t dtype, const uint8_t* done,
                             int64_t n, double gamma, int32_t phase, int32_t device,
                             void* hip_stream);
+
+/* ------------------------------------------------------------------------------
+ * One VecNormalize(VecEnv).step() fused into the env step ("move the
+ * running mean/var and obs normalisation into the step kernel epilogue").  SB3 2.7.1
+ * VecNormalize.step_wait (common/vec_env/vec_normalize.py) over the outputs of
+ * lz_step, in its order:
+ *   obs_rms.update(obs)                       (if TRAINING and NORM_OBS)
+ *   returns = returns*gamma + reward; ret_rms.update(returns)      (if TRAINING)
+ *   obs_out  = NORM_OBS    ? clip((obs - mean)/sqrt(var + eps), +-clip_obs)  : obs
+ *   rew_out  = NORM_REWARD ? clip(reward/sqrt(ret_var + eps), +-clip_reward) : reward
+ *   terminal observations normalised like obs; returns[done] = 0
+ * lz_step_vecnorm runs the env step (its kernel also writes float64 per-workgroup
+ * moment partials of the obs and of the updated returns) and a one-workgroup
+ * reduction in a fixed order (deterministic, no float atomics) that applies the two
+ * RunningMeanStd updates -- two launches; lz_vecnorm_apply (one launch) writes the
+ * normalised outputs.  With LZ_VN_DEFER the reduction leaves the batch moments (obs:
+ * count, sums[O], sumsq[O]; then returns: count, sum, sumsq) in moments for a
+ * multi-GPU all-reduce and lz_vecnorm_apply performs the updates first.  Every
+ * pointer is device memory; the statistics are those of the two lz_rms objects (dims
+ * O and 1).
+ * ------------------------------------------------------------------------------ */
+enum {
+  LZ_VN_TRAINING = 1,
+  LZ_VN_NORM_OBS = 2,
+  LZ_VN_NORM_REWARD = 4,
+  LZ_VN_DEFER = 8
+};
+
+typedef struct lz_vecnorm {
+  lz_rms* obs_rms;     /* RunningMeanStd(shape=(obs_dim,)) */
+  lz_rms* ret_rms;     /* RunningMeanStd(shape=()) */
+  double* returns;     /* [num_envs] discounted returns (VecNormalize.returns) */
+  double* moments;     /* [2*obs_dim + 4] batch moments (LZ_VN_DEFER), else NULL */
+  double gamma;
+  double epsilon;
+  double clip_obs;
+  double clip_reward;
+  uint32_t flags;      /* LZ_VN_* */
+  uint32_t reserved;
+} lz_vecnorm;
+
+/* lz_step's contract for the raw outputs (obs_out/rew_out/done/compact list) plus the
+ * VecNormalize bookkeeping above.  n_done_out (device int32) is required: the compact
+ * list is how lz_vecnorm_apply finds the terminal rows to normalise. */
+lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* actions,
+                          void* obs_out, void* rew_out, uint8_t* done_out, int32_t* done_idx_out,
+                          void* terminal_obs_out, int32_t* n_done_out);
+/* The normalised views: obs_norm float32 [N, O], rew_norm float32 [N]; if done and
+ * dones_out are non-NULL, dones_out[i] = (done[i] != 0) (uint8 0/1, SB3's bool
+ * dones); if terminal_obs_raw and term_norm are non-NULL, term_norm float32
+ * [n_done, O] from terminal_obs_raw [n_done, O], n_done read on the device from
+ * n_done (the lz_step_vecnorm output). */
+lz_status lz_vecnorm_apply(lz_handle* h, const lz_vecnorm* vn, const void* obs_raw,
+                           const void* rew_raw, const uint8_t* done, float* obs_norm,
+                           float* rew_norm, uint8_t* dones_out, const void* terminal_obs_raw,
+                           const int32_t* n_done, float* term_norm);
 
 /* ------------------------------------------------------------------------------
  * VecFrameStack(venv, n_stack) on the device (SB3 2.7.1 common/vec_env/

@@ -57,6 +57,22 @@ def test_struct_layout_matches_header(nat, tmp_path):
     assert got == want
 
 
+def test_vecnorm_struct_layout_matches_header(nat, tmp_path):
+    c = tmp_path / "probe_vn.c"
+    c.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "lorenz_env.h"\n'
+        "int main(void){printf(\"%zu %zu %zu %zu %d %d %d %d\\n\", sizeof(lz_vecnorm),"
+        " offsetof(lz_vecnorm, gamma), offsetof(lz_vecnorm, clip_reward),"
+        " offsetof(lz_vecnorm, flags), LZ_VN_TRAINING, LZ_VN_NORM_OBS, LZ_VN_NORM_REWARD,"
+        " LZ_VN_DEFER);return 0;}\n")
+    exe = tmp_path / "probe_vn"
+    subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), str(c), "-o", str(exe)])
+    got = [int(v) for v in subprocess.check_output([str(exe)]).split()]
+    V = nat.LzVecNorm
+    assert got == [ctypes.sizeof(V), V.gamma.offset, V.clip_reward.offset, V.flags.offset,
+                   nat.VN_TRAINING, nat.VN_NORM_OBS, nat.VN_NORM_REWARD, nat.VN_DEFER]
+
+
 def test_config_init_reference_constants(nat, orc):
     for name, sysid in (("l3", nat.LORENZ3), ("l4", nat.LORENZ4), ("pmsm", nat.PMSM),
                         ("hr", nat.HR)):
@@ -85,6 +101,9 @@ def test_abi_version_and_errors(nat):
     # NULL handles are rejected, never dereferenced
     assert nat.lib.lz_step(None, None, None, None, None, None, None, None, None) == nat.LZ_ERR_INVALID
     assert nat.lib.lz_reset(None, None, None, None) == nat.LZ_ERR_INVALID
+    vn = nat.LzVecNorm()
+    assert nat.lib.lz_step_vecnorm(None, ctypes.byref(vn), *([None] * 7)) == nat.LZ_ERR_INVALID
+    assert nat.lib.lz_vecnorm_apply(None, ctypes.byref(vn), *([None] * 9)) == nat.LZ_ERR_INVALID
     assert nat.lib.lz_destroy(None) == nat.LZ_OK
     assert nat.lib.lz_plane_elem_size(None, 0) == 0
 
