@@ -7,6 +7,7 @@
 // arithmetic, so LORENZ3/4 are bit-identical to dynamic.py / lorenz_env_transient.py.
 // References are file:line in /root/reference/code/gym-lorenz/gym_lorenz/envs/.
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -344,6 +345,21 @@ __device__ __forceinline__ T cube_cr(T x) {
   return h + l;
 }
 
+// x / c for the HR obs scalings, exactly IEEE: in float32, for the reference constants
+// c = 50 and 20, as q = x*r, q' = fma(fma(-q, c, x), r, q) with r = RN(1/c) -- three
+// instructions instead of the ~10 of a correctly rounded divide.
+// tools/div_const_check.c verifies it bit-for-bit against x / c for all 2^32 floats
+// with 2^-100 <= |x| <= 2^100; zeros, subnormal quotients and inf/NaN are not covered
+// and take the divide (a wave-uniform branch, see SysHR::step).
+__device__ __forceinline__ float div_fast(float x, float c, float r) {
+  const float q = x * r;
+  return fmaf(fmaf(-q, c, x), r, q);
+}
+__device__ __forceinline__ bool div_fast_ok(float x) {
+  const float ax = fabsf(x);
+  return ax >= 0x1p-100f && ax <= 0x1p100f;
+}
+
 template <typename T>
 struct SysHR {
   static constexpr int A = 2, O = 6, NI = 7;
@@ -353,6 +369,7 @@ struct SysHR {
   float fa0, fa1;
   T pa, pb, pc, pd, pr, ps, pI, pxr, dt, h2, h6, sc, ms, tterm;
   float falpha, f1m;
+  bool fastdiv;
 
   __device__ void setup(const KArgs& a) {
     pa = (T)a.prm[0]; pb = (T)a.prm[1]; pc = (T)a.prm[2]; pd = (T)a.prm[3];
@@ -360,6 +377,7 @@ struct SysHR {
     dt = (T)a.prm[8]; h2 = (T)(a.prm[8] / 2); h6 = (T)(a.prm[8] / 6.0);   // :102-105
     sc = (T)a.prm[9]; ms = (T)a.prm[10]; tterm = (T)a.prm[12];
     falpha = (float)a.prm[11]; f1m = (float)(1.0 - a.prm[11]);            // :86
+    fastdiv = a.prm[9] == 50.0 && a.prm[10] == 20.0;  // the constants div_fast is verified for
   }
   __device__ void load(const KArgs& a, int64_t i) {
 #pragma unroll
@@ -404,6 +422,46 @@ struct SysHR {
 #pragma unroll
     for (int j = 0; j < 3; ++j) x[j] = x[j] + h6 * (((k1[j] + (T)2 * k2[j]) + (T)2 * k3[j]) + k4[j]);
   }
+  // float32: master (actions 0, 0) and slave (a1, a2) RK4 steps as one packed
+  // computation (lane pair = {master, slave}: v_pk_fma / v_pk_mul / v_pk_add), the
+  // same IEEE operations in the same order per element as rhs() / rk4() -- bit-identical.
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  __device__ static f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+  __device__ void rhs2(const f2* x, f2 act1, f2 act2, f2* d) const {
+    const f2 p = x[0] * x[0];                               // cube_cr, elementwise
+    const f2 e = fma2(x[0], x[0], -p);
+    const f2 h = p * x[0];
+    const f2 l = fma2(p, x[0], -h) + e * x[0];
+    const f2 x3 = h + l;
+    const f2 A = (f2)(float)pa, B = (f2)(float)pb, Cc = (f2)(float)pc, D = (f2)(float)pd;
+    const f2 R = (f2)(float)pr, S = (f2)(float)ps, I = (f2)(float)pI, XR = (f2)(float)pxr;
+    d[0] = (((x[1] - A * x3) + B * p) - x[2]) + I;
+    d[1] = ((Cc - D * p) - x[1]) + act1;
+    d[2] = R * (S * (x[0] - XR) - x[2]) + act2;
+  }
+  __device__ void rk4_pair(T* xm, T* xs, float a1, float a2) {
+    f2 x[3], k1[3], k2[3], k3[3], k4[3], y[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = (f2){(float)xm[j], (float)xs[j]};
+    const f2 u1 = {0.0f, a1}, u2 = {0.0f, a2};
+    const f2 H2 = (f2)(float)h2, DT = (f2)(float)dt, H6 = (f2)(float)h6, TWO = (f2)2.0f;
+    rhs2(x, u1, u2, k1);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) y[j] = x[j] + H2 * k1[j];
+    rhs2(y, u1, u2, k2);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) y[j] = x[j] + H2 * k2[j];
+    rhs2(y, u1, u2, k3);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) y[j] = x[j] + DT * k3[j];
+    rhs2(y, u1, u2, k4);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      x[j] = x[j] + H6 * (((k1[j] + TWO * k2[j]) + TWO * k3[j]) + k4[j]);
+      xm[j] = (T)x[j][0];
+      xs[j] = (T)x[j][1];
+    }
+  }
   __device__ static void draw(const KArgs& a, uint64_t gid, uint64_t tick, T* v) {
     for (int j = 0; j < 6; ++j) v[j] = Draw<T>::uniform(a.seed, gid, tick, j, (T)-10, (T)20);  // :55-57
     T sgm = (T)0;                                                                                  // :60-69
@@ -439,8 +497,12 @@ struct SysHR {
     }
     const float a1 = clip(f0, -1.0f, 1.0f) * 100.0f;       // :92-93 np.float32 * 100.0
     const float a2 = clip(f1, -1.0f, 1.0f) * 100.0f;
-    rk4(m, (T)0, (T)0);                                    // :100-105
-    rk4(s, (T)a1, (T)a2);                                  // :108-113
+    if constexpr (std::is_same<T, float>::value) {
+      rk4_pair(m, s, a1, a2);                              // both systems, packed f32
+    } else {
+      rk4(m, (T)0, (T)0);                                  // :100-105
+      rk4(s, (T)a1, (T)a2);                                // :108-113
+    }
     if (use_nz) {                                          // :135-137
 #pragma unroll
       for (int j = 0; j < 3; ++j) m[j] = m[j] + (T)nz[j] * dt;
@@ -448,10 +510,28 @@ struct SysHR {
     T e[3];
     bool te = false;
 #pragma unroll
+    for (int j = 0; j < 3; ++j) e[j] = m[j] - s[j];
+    bool slow = true;
+    if constexpr (std::is_same<T, float>::value) {  // div_fast: bit-identical to the divide
+      bool ok = fastdiv;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        ok = ok && div_fast_ok(e[j]) && div_fast_ok(m[j]);
+        o[j] = div_fast(e[j], 50.0f, 0x1.47ae14p-6f);      // RN(1/50)
+        o[3 + j] = div_fast(m[j], 20.0f, 0x1.99999ap-5f);  // RN(1/20)
+      }
+      slow = !__all(ok);  // wave-uniform: the divides run only if some lane needs them
+    }
+    if (slow) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        o[j] = e[j] / sc;
+        o[3 + j] = m[j] / ms;
+      }
+    }
+#pragma unroll
     for (int j = 0; j < 3; ++j) {                          // :150-156
-      e[j] = m[j] - s[j];
-      o[j] = e[j] / sc;
-      o[3 + j] = clip(m[j] / ms, (T)-1, (T)1);
+      o[3 + j] = clip(o[3 + j], (T)-1, (T)1);
       te = te || (fabs(e[j]) > tterm);                     // :174
     }
     const float q = act[0] * act[0] + act[1] * act[1];     // np.square + np.sum (f32)
