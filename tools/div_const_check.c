@@ -4,6 +4,7 @@
  * justify the 3-instruction division in SysHR<float> (lz_systems.h) in place of the
  * ~10-instruction v_div_scale / v_div_fmas / v_div_fixup sequence.
  *   gcc -O2 -fopenmp -ffp-contract=off tools/div_const_check.c -o /tmp/dcc -lm && /tmp/dcc 50 20
+ * (output: profiles/r01/div_const_check.txt)
  */
 #include <math.h>
 #include <stdint.h>
@@ -11,8 +12,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* The kernel's form: the FMA path only for 2^-100 <= |x| <= 2^100, else the divide.
+ * -DVARIANT='fmaf(e, r, q)' (unguarded) differs for -0, subnormal quotients and inf. */
 #ifndef VARIANT
-#define VARIANT fmaf(e, r, q)
+#define VARIANT ((fabsf(x) >= 0x1p-100f && fabsf(x) <= 0x1p100f) ? fmaf(e, r, q) : x / c)
 #endif
 
 static float f_of(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
