@@ -40,6 +40,24 @@ from .core import BatchedEnv
 from .vec_env import DeviceLazyInfos, LazyInfos
 
 
+class _FusedInfos(DeviceLazyInfos):
+    """DeviceLazyInfos over the views of a fused step's output buffer."""
+
+    def __init__(self, n, view, host=False):
+        self._n = n
+        self._view = view
+        self._li = None
+        self._host = host
+
+    def _mat(self):
+        if self._li is None:
+            v = self._view
+            idx = v(6)
+            self._dev = (v(7), idx[: self._n], v(4), idx[self._n:])
+            self._view = None
+        return super()._mat()
+
+
 def _p(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
@@ -145,7 +163,7 @@ class LorenzVecNormalize:
         self.returns = torch.zeros((self.num_envs,), dtype=torch.float64, device=self.device)
         self._moments = torch.zeros((2 * obs_dim + 4,), dtype=torch.float64, device=self.device)
         self._fused = isinstance(be, BatchedEnv) and be.compact
-        self._layout = self._vn = None
+        self._layout = self._vn = self._last = None
         self.old_obs = None
         self.old_reward = None
         self._actions = None
@@ -173,9 +191,15 @@ class LorenzVecNormalize:
         return (t * torch.sqrt(st[d:2 * d] + self.epsilon) + st[:d]).float()
 
     def get_original_obs(self):
+        if self._last is not None:  # fused step: the raw obs of the last step_wait
+            t = self._last[1](0)
+            return t if t.dtype == torch.float32 else t.float()
         return self.old_obs
 
     def get_original_reward(self):
+        if self._last is not None:
+            t = self._last[1](2)
+            return t if t.dtype == torch.float32 else t.float()
         return self.old_reward
 
     # --------------------------------------------------------------- VecEnv API
@@ -188,6 +212,7 @@ class LorenzVecNormalize:
     def reset(self):
         obs = self.venv.backend.reset().float()  # SB3 sees DummyVecEnv's float32 obs
         self.old_obs = obs.clone()
+        self._last = None
         self.returns.zero_()
         if self.training and self.norm_obs:
             self.obs_rms.update(obs, self.group)
@@ -220,7 +245,8 @@ class LorenzVecNormalize:
             # every output of a step in one fresh allocation per step (the caching
             # allocator recycles it once the caller drops the views): raw obs and
             # terminal obs, raw reward (old_obs, old_reward), normalised obs /
-            # terminal obs / reward, compact list + count, done bytes, 0-1 dones
+            # terminal obs / reward, compact list + count, done bytes, 0-1 dones.
+            # Views are only built for what is returned; the C calls take addresses.
             es = torch.empty((), dtype=td).element_size()
             spec = [(td, (n, o)), (td, (n, o)), (td, (n,)), (torch.float32, (n, o)),
                     (torch.float32, (n, o)), (torch.float32, (n,)), (torch.int32, (n + 1,)),
@@ -233,24 +259,33 @@ class LorenzVecNormalize:
             self._layout = (off, offs)
         total, offs = self._layout
         buf = torch.empty((total,), dtype=torch.uint8, device=dev)
-        obs, tobs, rew, obs_n, tn, rew_n, idx, done, dones = [
-            buf[a: a + b].view(dt).view(shp) for a, b, dt, shp in offs]
-        didx, ndone = idx[:n], idx[n:]
+        base = buf.data_ptr()
+        p_obs, p_tobs, p_rew, p_on, p_tn, p_rn, p_idx, p_done, p_dones = [base + a for a, _, _, _ in offs]
+        p_nd = p_idx + 4 * n
         key = (self._flags(), self.gamma, self.epsilon, self.clip_obs, self.clip_reward)
         if self._vn is None or self._vn[0] != key:
             self._vn = (key, self._vn_args())
         vn = self._vn[1]
-        be.step_vecnorm(venv.device_actions(self._actions), vn, (obs, rew, done), (didx, tobs, ndone))
+        acts = be._check_dev(venv.device_actions(self._actions), torch.float32,
+                             (n, be.action_dim), "actions")
+        nat.check(nat.lib.lz_step_vecnorm(be._h, vn, acts.data_ptr(), p_obs, p_rew, p_done, p_idx,
+                                          p_tobs, p_nd))
+        be._last_actions = acts
         if self.group is not None and self.training:
             dist.all_reduce(self._moments, group=self.group)
-        be.vecnorm_apply(vn, obs, rew, obs_n, rew_n, tobs, ndone, tn, done, dones)
-        self.old_obs = obs if td == torch.float32 else obs.float()
-        self.old_reward = rew if td == torch.float32 else rew.float()
-        dones_b = dones.view(torch.bool)
+        nat.check(nat.lib.lz_vecnorm_apply(be._h, vn, p_obs, p_rew, p_done, p_on, p_rn, p_dones,
+                                           p_tobs, p_nd, p_tn))
+
+        def view(k):
+            a, nb, dt, shp = offs[k]
+            return buf[a: a + nb].view(dt).view(shp)
+
+        self._last = (buf, view)  # old_obs / old_reward are built on request
+        infos = _FusedInfos(n, view, host=not venv.return_tensors)
+        dones = view(8).view(torch.bool)
         if venv.return_tensors:
-            return obs_n, rew_n, dones_b, DeviceLazyInfos(n, done, didx, tn, ndone)
-        obs_h, rew_h, done_h = obs_n.cpu().numpy(), rew_n.cpu().numpy(), dones_b.cpu().numpy()
-        infos = DeviceLazyInfos(n, done, didx, tn, ndone, host=True)
+            return view(3), view(5), dones, infos
+        obs_h, rew_h, done_h = view(3).cpu().numpy(), view(5).cpu().numpy(), dones.cpu().numpy()
         if not venv.lazy_infos:
             infos = [infos[i] for i in range(n)]
         return obs_h, rew_h, done_h, infos
