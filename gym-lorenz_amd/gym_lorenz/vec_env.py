@@ -106,6 +106,27 @@ class DeviceLazyInfos(Sequence):
         return self._mat().done_indices()
 
 
+class _StepInfos(DeviceLazyInfos):
+    """DeviceLazyInfos over one return_tensors step's output buffer (views built on
+    first access)."""
+
+    def __init__(self, n, buf, offs, sizes, td, o):
+        self._n = n
+        self._buf = (buf, offs, sizes, td, o)
+        self._li = None
+        self._host = False
+
+    def _mat(self):
+        if self._li is None:
+            buf, offs, sizes, td, o = self._buf
+            n = self._n
+            idx = buf[offs[3]: offs[3] + 4 * (n + 1)].view(torch.int32)
+            self._dev = (buf[offs[2]: offs[2] + n], idx[:n],
+                         buf[offs[4]: offs[4] + sizes[4]].view(td).view(n, o), idx[n:])
+            self._buf = None
+        return super()._mat()
+
+
 class LorenzVecEnv(VecEnvBase):
     def __init__(self, env_id="lorenz_dynamic-v0", num_envs=1, device=None, dtype="float32",
                  seed=0, max_episode_steps=None, return_tensors=False, lazy_infos=None,
@@ -136,6 +157,7 @@ class LorenzVecEnv(VecEnvBase):
             self.reset_infos = [{} for _ in range(num_envs)]
         self.metadata = {"render_modes": []}
         self._pin_act = self._pin_out = self._dev_act = None
+        self._layout = None
         if not return_tensors and isinstance(backend, BatchedEnv):
             # host-buffer path: pinned staging, one copy each way
             self._pin_act = torch.empty((num_envs, backend.action_dim), dtype=torch.float32,
@@ -194,19 +216,32 @@ class LorenzVecEnv(VecEnvBase):
     def step_wait(self):
         acts = self.device_actions(self._actions)
         if self.return_tensors and isinstance(self.backend, BatchedEnv):
-            # sync-free: fresh output tensors per step (the caching allocator recycles
-            # them) and the compact done list kept for DeviceLazyInfos
-            be, n, o = self.backend, self.num_envs, self.backend.obs_dim
-            dev, td = be.device, be.tdtype
-            out = (torch.empty((n, o), dtype=td, device=dev), torch.empty((n,), dtype=td, device=dev),
-                   torch.empty((n,), dtype=torch.uint8, device=dev))
-            comp = (torch.empty((n,), dtype=torch.int32, device=dev),
-                    torch.empty((n, o), dtype=td, device=dev),
-                    torch.empty((1,), dtype=torch.int32, device=dev))
-            obs, rew, done = be.step(acts, out=out, compact_out=comp)
-            obs_o = obs.float() if obs.dtype != torch.float32 else obs
-            rew_o = rew.float() if rew.dtype != torch.float32 else rew
-            return obs_o, rew_o, done.bool(), DeviceLazyInfos(n, done, *comp)
+            # sync-free: one fresh allocation per step for every output (the caching
+            # allocator recycles it once the caller drops the views), addresses straight
+            # into lz_step, views only for what is returned; the compact done list is
+            # viewed lazily by DeviceLazyInfos
+            be, n = self.backend, self.num_envs
+            if self._layout is None:
+                o, es = be.obs_dim, torch.empty((), dtype=be.tdtype).element_size()
+                sizes = [n * o * es, n * es, n, 4 * (n + 1), n * o * es]  # obs rew done idx tobs
+                offs = np.concatenate([[0], np.cumsum([(b + 15) // 16 * 16 for b in sizes])])
+                self._layout = (int(offs[-1]), [int(x) for x in offs[:-1]], sizes, o)
+            total, offs, sizes, o = self._layout
+            buf = torch.empty((total,), dtype=torch.uint8, device=be.device)
+            base = buf.data_ptr()
+            a = be._check_dev(acts, torch.float32, (n, be.action_dim), "actions")
+            nat.check(nat.lib.lz_step(be._h, a.data_ptr(), None, base + offs[0], base + offs[1],
+                                      base + offs[2], base + offs[3], base + offs[4],
+                                      base + offs[3] + 4 * n))
+            be._last_actions = a
+            td = be.tdtype
+            obs = buf[offs[0]: offs[0] + sizes[0]].view(td).view(n, o)
+            rew = buf[offs[1]: offs[1] + sizes[1]].view(td)
+            done = buf[offs[2]: offs[2] + n]
+            infos = _StepInfos(n, buf, offs, sizes, td, o)
+            obs_o = obs.float() if td != torch.float32 else obs
+            rew_o = rew.float() if td != torch.float32 else rew
+            return obs_o, rew_o, done.bool(), infos
         obs, rew, done = self.backend.step(acts)
         if self.return_tensors:
             obs_o = obs.float() if obs.dtype != torch.float32 else obs.clone()
