@@ -48,9 +48,11 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--system", choices=["lorenz3", "lorenz4", "pmsm", "hr"], default="lorenz3",
                    help="lorenz3 = the BASELINE headline (dynamic.py env); pmsm = cfg4")
-    p.add_argument("--mode", choices=["step", "rollout", "policy"], default="step",
+    p.add_argument("--mode", choices=["step", "rollout", "policy", "vecnorm"], default="step",
                    help="rollout = cfg5's fused K-step on-device rollout; policy = the fused "
-                        "SB3 actor-critic rollout (lz_rollout_policy + VecNormalize + GAE)")
+                        "SB3 actor-critic rollout (lz_rollout_policy + VecNormalize + GAE); "
+                        "vecnorm = VecNormalize(VecEnv).step fused (lz_step_vecnorm + "
+                        "lz_vecnorm_apply), 1 GPU")
     p.add_argument("--K", type=int, default=2048, help="rollout length (--mode rollout)")
     p.add_argument("--max-episode-steps", type=int, default=0,
                    help="TimeLimit truncation (auto-reset inside the kernel); 0 = none")
@@ -149,6 +151,105 @@ def kernel_name(system, mode, n):
             return "_ZN2lz15k_rollout_splitINS_%sLi2ELi%dEEEvNS_5KArgsE" % (sysname, D)
         return "_ZN2lz9k_rolloutINS_%sLi64ELi%dEEEvNS_5KArgsE" % (sysname, D)
     return "_ZN2lz9k_rolloutINS_%sLi256ELi%dEEEvNS_5KArgsE" % (sysname, D)
+
+
+def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
+    """--mode vecnorm: one SB3 VecNormalize(norm_obs, norm_reward, clip_obs=10) step per
+    step (code/lorenz_pmsm/train.py:170), fused: lz_step_vecnorm (step + float64 moments
+    + fixed-order reduction + RunningMeanStd updates) and lz_vecnorm_apply (normalised
+    obs / reward / terminal rows, bool dones); actions / outputs in a 16-slot ring, a
+    hipGraph of 64 steps.  Per-rank statistics (the all-reduce of the multi-GPU path,
+    LZ_VN_DEFER, is not captured here)."""
+    A, O = env.action_dim, env.obs_dim
+    R, L = 16, 64
+    g = torch.Generator(device=device).manual_seed(1000)
+    arange = SYSTEM_INFO[args.system][2]
+    acts = (torch.rand((R, n, A), generator=g, device=device) * 2 - 1) * arange
+    raw_o = torch.empty((R, n, O), device=device)
+    raw_r = torch.empty((R, n), device=device)
+    done = torch.empty((R, n), dtype=torch.uint8, device=device)
+    obs_n = torch.empty((R, n, O), device=device)
+    rew_n = torch.empty((R, n), device=device)
+    dones = torch.empty((R, n), dtype=torch.uint8, device=device)
+    didx = torch.empty((n + 1,), dtype=torch.int32, device=device)
+    tobs, tn = torch.empty((n, O), device=device), torch.empty((n, O), device=device)
+    from gym_lorenz.vec_normalize import DeviceRunningMeanStd
+
+    stream = torch.cuda.Stream(device)
+    obs_rms = DeviceRunningMeanStd(O, device, stream=stream)
+    ret_rms = DeviceRunningMeanStd(1, device, stream=stream)
+    returns = torch.zeros((n,), dtype=torch.float64, device=device)
+    vn = nat.LzVecNorm()
+    vn.obs_rms, vn.ret_rms = obs_rms._h.value, ret_rms._h.value
+    vn.returns = returns.data_ptr()
+    vn.gamma, vn.epsilon, vn.clip_obs, vn.clip_reward = 0.99, 1e-8, 10.0, 10.0
+    vn.flags = nat.VN_TRAINING | nat.VN_NORM_OBS | nat.VN_NORM_REWARD
+    h = env._h
+    env.reset()
+    nd = didx.data_ptr() + 4 * n
+
+    def one(k):
+        r = k % R
+        nat.check(nat.lib.lz_step_vecnorm(h, vn, acts[r].data_ptr(), raw_o[r].data_ptr(),
+                                          raw_r[r].data_ptr(), done[r].data_ptr(), didx.data_ptr(),
+                                          tobs.data_ptr(), nd))
+        nat.check(nat.lib.lz_vecnorm_apply(h, vn, raw_o[r].data_ptr(), raw_r[r].data_ptr(),
+                                           done[r].data_ptr(), obs_n[r].data_ptr(),
+                                           rew_n[r].data_ptr(), dones[r].data_ptr(),
+                                           tobs.data_ptr(), nd, tn.data_ptr()))
+
+    with torch.cuda.stream(stream):
+        nat.check(nat.lib.lz_set_stream(h, ctypes.c_void_p(stream.cuda_stream)))
+        for k in range(4):
+            one(k)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            for k in range(L):
+                one(k)
+        for _ in range(max(1, args.warmup // L)):
+            graph.replay()
+        torch.cuda.synchronize(device)
+        reps = max(1, args.steps // L)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(reps):
+            graph.replay()
+        ev1.record(stream)
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+    steps = reps * L
+    elapsed = t1 - t0
+    step_s = ev0.elapsed_time(ev1) / 1e3 / steps
+    info = env.info
+    es = 4
+    bytes_step = info.bytes_per_env_step + 16 + 2 * (O * es + es + 1)
+    achieved = bytes_step * n / step_s / 1e9
+    obs_rms.close()
+    ret_rms.close()
+    return {
+        "metric": METRIC, "value": total * steps / elapsed, "unit": "env-steps/s",
+        "n_gpus": world, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True,
+        "scaling": args.scaling, "vs_baseline": None, "dtype": "f32 env, f64 statistics",
+        "data": "synthetic: on-device Philox initial states; actions ~ U(-%g,%g) f32 "
+                "pre-generated on device" % (arange, arange),
+        "config": {
+            "workload": "VecNormalize(norm_obs, norm_reward, clip_obs=10) over %s, fused step "
+                        "(lz_step_vecnorm + lz_vecnorm_apply: 3 kernels, no host sync), %d envs"
+                        % (SYSTEM_INFO[args.system][0], n),
+            "system": args.system, "envs_total": total, "envs_per_gpu": n, "mode": "vecnorm",
+            "parallelism": "env shard x%d (per-rank statistics)" % world,
+            "launch": "hipGraph of %d steps" % L},
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "kernel": "k_step_vn + k_vn_reduce + k_vn_apply (one fused VecNormalize step)",
+            "avg_launch_us": step_s * 1e6, "bytes_per_env_step": bytes_step,
+            "note": "achieved = algorithmic bytes of the whole fused step (lz_step's + 16 B of "
+                    "float64 returns + the normalise pass: raw obs/reward/done read, normalised "
+                    "obs/reward/dones written) / HIP-event time per step"},
+    }
 
 
 def policy_flops(O, A, H=128):
@@ -293,6 +394,15 @@ def main():
                         **kw)
     if args.mode == "policy":
         out = bench_policy(args, gl, nat, torch, env, device, world, rank, total, n)
+        env.close()
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        return
+    if args.mode == "vecnorm":
+        out = bench_vecnorm(args, gl, nat, torch, env, device, world, total, n)
         env.close()
         if world > 1:
             dist.barrier()
