@@ -54,6 +54,10 @@ def parse():
                         "vecnorm = VecNormalize(VecEnv).step fused (lz_step_vecnorm + "
                         "lz_vecnorm_apply), 1 GPU")
     p.add_argument("--K", type=int, default=2048, help="rollout length (--mode rollout)")
+    p.add_argument("--policy", choices=["mlp", "attn"], default="mlp",
+                   help="--mode policy: mlp = SB3 MlpPolicy behind VecNormalize (the PMSM A2C "
+                        "learner, code/lorenz_pmsm/train.py); attn = code/train.py's PPO policy "
+                        "with the AttentionFeaturesExtractor (no VecNormalize, as there)")
     p.add_argument("--max-episode-steps", type=int, default=0,
                    help="TimeLimit truncation (auto-reset inside the kernel); 0 = none")
     return p.parse_args()
@@ -257,6 +261,15 @@ def policy_flops(O, A, H=128):
     return 2 * (O * H + H * H + H * A) + 2 * (O * H + H * H + H)
 
 
+def attn_policy_flops(O, A, H=128, F=64):
+    """Useful FLOP per env-step of code/train.py's attention actor-critic as SB3 runs it:
+    fc1, in_proj (8 tokens x 48 x 16), scores and weights @ v (4 heads, 8 x 8 x 4),
+    out_proj (8 x 16 x 16), post_attention_fc (128 -> 64), then the pi and vf nets on
+    the 64 features."""
+    ext = 2 * (O * H + 8 * 48 * 16 + 2 * 4 * 8 * 8 * 4 + 8 * 16 * 16 + H * F)
+    return ext + 2 * (F * H + H * H + H * A) + 2 * (F * H + H * H + H)
+
+
 def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
     """--mode policy: the reference's PMSM learner loop (code/lorenz_pmsm/train.py:155-178:
     A2C MlpPolicy pi/vf [128,128] Tanh, VecNormalize(norm_obs, clip_obs=10), n_steps=16)
@@ -265,19 +278,22 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
     lz_gae.  One "step" = one env step of every env (policy forward included)."""
     import torch.distributed as dist
 
-    from gym_lorenz.policy import ActorCriticMlp, FusedRolloutCollector
+    from gym_lorenz.policy import ActorCriticAttn, ActorCriticMlp, FusedRolloutCollector
     from gym_lorenz.vec_normalize import DeviceRunningMeanStd
 
     K = args.K
     O, A = env.obs_dim, env.action_dim
-    net = ActorCriticMlp(O, A, seed=0)  # SB3 init (orthogonal, log_std 0): random weights
-    rms = DeviceRunningMeanStd(O, device)
+    attn = args.policy == "attn"
+    # SB3 init (orthogonal, log_std 0): random weights
+    net = ActorCriticAttn(O, A, seed=0) if attn else ActorCriticMlp(O, A, seed=0)
+    rms = None if attn else DeviceRunningMeanStd(O, device)
     col = FusedRolloutCollector(env, net.state_dict(), gamma=0.99, gae_lambda=0.95, obs_rms=rms,
                                 clip_obs=10.0, training=True, bootstrap=True)
     stream = torch.cuda.Stream(device)
     with torch.cuda.stream(stream):
         nat.check(nat.lib.lz_set_stream(env._h, ctypes.c_void_p(stream.cuda_stream)))
-        nat.check(nat.lib.lz_rms_set_stream(rms._h, ctypes.c_void_p(stream.cuda_stream)))
+        if rms is not None:
+            nat.check(nat.lib.lz_rms_set_stream(rms._h, ctypes.c_void_p(stream.cuda_stream)))
         col.reset()
         launches = max(2, args.steps // K)
         warm = 2
@@ -314,7 +330,7 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         t = torch.tensor([elapsed, launch_s], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, launch_s = float(t[0]), float(t[1])
-    fl = policy_flops(O, A)
+    fl = attn_policy_flops(O, A) if attn else policy_flops(O, A)
     achieved = fl * n * K / launch_s / 1e12
     mangled = {"pmsm": "7SysPMSME", "lorenz3": "5SysL3IfEE", "lorenz4": "5SysL4IfEE",
                "hr": "5SysHRIfEE"}[args.system]
@@ -333,23 +349,35 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         "data": "synthetic: on-device Philox initial states and Gaussian action samples; "
                 "SB3-initialised (orthogonal) random policy weights",
         "config": {
-            "workload": "%s with the SB3 A2C/PPO MlpPolicy (pi/vf [128,128] Tanh) in the loop: "
-                        "%d-step fused rollout (lz_rollout_policy: policy forward + DiagGaussian "
-                        "sample + clip + env step + truncation bootstrap + VecNormalize obs), "
-                        "obs_rms update, GAE (lz_gae); %d envs total, %d per GPU"
+            "workload": ("%s with code/train.py's PPO actor-critic (AttentionFeaturesExtractor "
+                         "fc1 + 4-head self-attention over 8 tokens + post_fc 64, then pi/vf "
+                         "[128,128] Tanh) in the loop: %d-step fused rollout "
+                         "(lz_rollout_policy_attn: extractor + nets + DiagGaussian sample + clip "
+                         "+ env step + truncation bootstrap), GAE (lz_gae); %d envs total, %d per "
+                         "GPU" if attn else
+                         "%s with the SB3 A2C/PPO MlpPolicy (pi/vf [128,128] Tanh) in the loop: "
+                         "%d-step fused rollout (lz_rollout_policy: policy forward + DiagGaussian "
+                         "sample + clip + env step + truncation bootstrap + VecNormalize obs), "
+                         "obs_rms update, GAE (lz_gae); %d envs total, %d per GPU")
                         % (SYSTEM_INFO[args.system][0], K, total, n),
             "system": args.system, "envs_total": total, "envs_per_gpu": n, "mode": "policy",
+            "policy": args.policy,
             "K": K, "parallelism": "env shard x%d (no collective on step; obs_rms moments "
                                    "all-reduced once per rollout when N>1)" % world,
         },
         "roofline": {
             "bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS, "traffic": None,
-            "kernel": "_ZN2lz16k_rollout_policyINS_%sLi8EEEvNS_5KArgsENS_5PArgsE" % mangled,
+            "kernel": ("_ZN2lz16k_rollout_policyINS_%sLi4ELi32ELi3EEEvNS_5KArgsENS_5PArgsE"
+                       if attn else "_ZN2lz16k_rollout_policyINS_%sLi8EEEvNS_5KArgsENS_5PArgsE")
+                      % mangled,
             "avg_launch_us": launch_s * 1e6, "flop_per_env_step": fl,
-            "note": "achieved = useful MLP FLOP (pi + vf, %d per env-step) x envs x K / HIP-event "
-                    "time of one collect() (policy kernel + a 1-block moments reduction + the "
-                    "obs_rms update)" % fl,
+            "note": ("achieved = useful FLOP of the attention actor-critic as SB3 computes it "
+                     "(extractor + pi + vf, %d per env-step) x envs x K / HIP-event time of one "
+                     "collect() (one policy-rollout launch)" if attn else
+                     "achieved = useful MLP FLOP (pi + vf, %d per env-step) x envs x K / HIP-event "
+                     "time of one collect() (policy kernel + a 1-block moments reduction + the "
+                     "obs_rms update)") % fl,
         },
     }
 

@@ -540,7 +540,7 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
   return LZ_OK;
 }
 
-lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r) {
+static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, bool attn) {
   if (!h || !r) return fail(LZ_ERR_INVALID, "handle/args is NULL");
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_rollout_policy before the first lz_reset");
   if (h->f64) return fail(LZ_ERR_UNSUPPORTED, "the policy rollout runs float32 handles only");
@@ -554,7 +554,8 @@ lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r) {
   if (!(r->act_low <= r->act_high)) return fail(LZ_ERR_INVALID, "act_low > act_high");
   HIP_TRY(hipSetDevice(h->cfg.device));
   const int64_t n = h->cfg.num_envs;
-  const lz::PolShape sh = lz::policy_shape(n, h->cfg.reserved[0], h->num_cus);
+  const lz::PolShape sh = attn ? lz::attn_policy_shape(n, h->num_cus)
+                              : lz::policy_shape(n, h->cfg.reserved[0], h->num_cus);
   const int W = sh.waves, grid = sh.grid;
   const int O = h->desc.obs_dim;
   const int64_t need = (int64_t)grid * W * 2 * O;
@@ -593,7 +594,8 @@ lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r) {
   p.val = r->val_buf;
   p.last_val = r->last_values;
   p.partials = r->obs_moments ? h->pol_part : nullptr;
-  int e = lz::launch_rollout_policy(h->cfg.system, a, p, sh, h->stream);
+  int e = attn ? lz::launch_rollout_policy_attn(h->cfg.system, a, p, sh, h->stream)
+               : lz::launch_rollout_policy(h->cfg.system, a, p, sh, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "policy rollout launch: %s", hipGetErrorString((hipError_t)e));
   if (r->obs_moments) {
     e = lz::launch_policy_moments_final(h->pol_part, grid * W, 2 * O, (double)r->K * (double)n,
@@ -604,6 +606,14 @@ lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r) {
     HIP_TRY(hipMemcpyAsync(r->n_done, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
   h->parity ^= 1;
   return LZ_OK;
+}
+
+lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r) {
+  return rollout_policy(h, r, false);
+}
+
+lz_status lz_rollout_policy_attn(lz_handle* h, const lz_policy_rollout_args* r) {
+  return rollout_policy(h, r, true);
 }
 
 int32_t lz_plane_elem_size(const lz_handle* h, int32_t plane) {

@@ -87,6 +87,39 @@ constexpr int kPolLogStd = 2 * kPolNet;
 constexpr int kPolBlobBytes = kPolLogStd + 64;     // 92480 B (resident in LDS)
 constexpr int kPolMaxObs = 8, kPolMaxAct = 4;
 
+// The same actor-critic behind code/train.py:52-95's AttentionFeaturesExtractor
+// (shared features extractor: fc1 obs->128 ReLU, 8 tokens x 16, 4-head self-attention,
+// post_attention_fc 128->64 ReLU; then pi/vf [128,128] Tanh on the 64 features).
+// Blob layout (lz_attn_policy_pack; fragment maps in lz_policy.hip):
+//   extractor: fc1 A-fragments [4 tiles][64] bf16x8 + bias [4][2][16] f32;
+//              K|V projection [64] bf16x8 + bias [2][16]; Q projection (pre-scaled by
+//              log2(e)/sqrt(4)) [64] + bias [2][16];
+//              out_proj folded into post_attention_fc: per token [8][2 tiles][64] +
+//              bias [2][2][16]
+//   net 0 (pi) / net 1 (vf): W1 [4 out tiles][4 k-steps][64], W2 [4][8][64], W3 [8][64],
+//              b1 / b2 [4][2][16], b3 [2][16]
+//   log_std / Normal constants float[16]
+constexpr int kAttTokens = 8, kAttTokDim = 16, kAttFeat = 64;
+constexpr int kAttFc1W = 0;
+constexpr int kAttFc1B = kAttFc1W + 4 * 64 * 16;
+constexpr int kAttKvW = kAttFc1B + 4 * 2 * 16 * 4;
+constexpr int kAttKvB = kAttKvW + 64 * 16;
+constexpr int kAttQW = kAttKvB + 2 * 16 * 4;
+constexpr int kAttQB = kAttQW + 64 * 16;
+constexpr int kAttPostW = kAttQB + 2 * 16 * 4;
+constexpr int kAttPostB = kAttPostW + kAttTokens * 2 * 64 * 16;
+constexpr int kAttExt = kAttPostB + 2 * 2 * 16 * 4;  // 23552 B
+constexpr int kAttW1 = 0;
+constexpr int kAttW2 = kAttW1 + 4 * 4 * 64 * 16;
+constexpr int kAttW3 = kAttW2 + 4 * 8 * 64 * 16;
+constexpr int kAttB1 = kAttW3 + 8 * 64 * 16;
+constexpr int kAttB2 = kAttB1 + 4 * 2 * 16 * 4;
+constexpr int kAttB3 = kAttB2 + 4 * 2 * 16 * 4;
+constexpr int kAttNet = kAttB3 + 2 * 16 * 4;       // 58496 B
+constexpr int kAttPi = kAttExt, kAttVf = kAttExt + kAttNet;
+constexpr int kAttLogStd = kAttExt + 2 * kAttNet;
+constexpr int kAttBlobBytes = kAttLogStd + 64;     // 140608 B (resident in LDS)
+
 struct PArgs {
   const uint8_t* blob;     // device copy of the packed policy
   const float* obs_in;     // [N, O] raw observation at rollout start
@@ -155,6 +188,11 @@ inline PolShape policy_shape(int64_t n, int variant, int num_cus) {
 }
 int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, const PolShape& sh,
                           void* stream);
+// the attention-extractor policy (kAtt* blob): one shape, 32 envs per wave, 4 waves
+// (one per SIMD: the 137 KB blob leaves room for one workgroup per CU)
+PolShape attn_policy_shape(int64_t n, int num_cus);
+int launch_rollout_policy_attn(int system, const KArgs& a, const PArgs& p, const PolShape& sh,
+                               void* stream);
 int launch_policy_moments_final(const double* partials, int nparts, int width, double count,
                                 double* out, void* stream);
 

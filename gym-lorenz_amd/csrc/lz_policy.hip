@@ -237,6 +237,216 @@ __device__ __forceinline__ void mlp_pair_pipe(const uint8_t* na, const uint8_t* 
   }
 }
 
+// ------------------------------------------------------------------ attention extractor
+// code/train.py:52-95 AttentionFeaturesExtractor, shared by pi and vf (SB3
+// share_features_extractor=True):
+//   x = relu(fc1(obs))                      [128] = 8 tokens x 16
+//   q, k, v = in_proj(token)                nn.MultiheadAttention(16, 4 heads of 4)
+//   a_i = sum_j softmax_j(q_i . k_j / 2) v_j   per head
+//   features = relu(post_fc(concat_i out_proj(a_i)))   [64]
+// MI355X mapping (one wave = 32 envs, lanes l and l + 32 = the same env):
+// - fc1 is one 32x32x16 MFMA per 32 units.  Its accumulator registers 0..7 / 8..15 of
+//   lane half h hold units 32t + 16S + 8(j>>2) + 4h + (j&3): after ReLU and bf16
+//   packing they ARE token 2t + S's B fragment (token dim (j&3) + 8(j>>2) + 4h at k =
+//   8h + j), so the per-token projections need no data movement.
+// - K|V: one MFMA per token with the rows permuted so that lane half h receives the
+//   keys and values of heads 2h and 2h+1 (registers 0-3 k of head 2h, 4-7 k of 2h+1,
+//   8-11 v of 2h, 12-15 v of 2h+1).  Q: one MFMA per token, rows 0-7 of each half the
+//   queries of the same two heads, pre-scaled by log2(e) / sqrt(4) so the softmax is an
+//   exp2.  Each lane then runs its two heads' attention in fp32 VALU for all 8 query
+//   tokens (keys and values of the 8 tokens live in registers).
+// - The head outputs of token i (half h: dims 8h..8h+7, heads 2h, 2h+1) are, packed to
+//   bf16, the B fragment of a K=16 MFMA in natural order; out_proj is folded into
+//   post_attention_fc on the host (W_post[:, 16i:16i+16] W_out per token, the biases
+//   likewise), so post_fc is 2 tiles x 8 tokens of accumulation.
+// - ReLU keeps NaN (torch.relu), as the env's own non-finite states reach the policy.
+template <int S>
+__device__ __forceinline__ bf16x8 relu8(const f32x16& c) {  // registers 8S..8S+7
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const float u = c[8 * S + j], w = c[8 * S + j + 1];
+    const f32x2 t = {u < 0.0f ? 0.0f : u, w < 0.0f ? 0.0f : w};
+    const bf16x2 b = __builtin_convertvector(t, bf16x2);
+    r[j] = b[0];
+    r[j + 1] = b[1];
+  }
+  return r;
+}
+
+__device__ __forceinline__ void attn_extract(const uint8_t* ext, bf16x8 x, int lane, bf16x8* feat) {
+  asm volatile("" ::: "memory");
+  const int h = lane >> 5;
+  const bf16x8* w1 = reinterpret_cast<const bf16x8*>(ext + kAttFc1W) + lane;
+  const f32x16* b1 = reinterpret_cast<const f32x16*>(ext + kAttFc1B) + h;
+  bf16x8 tok[kAttTokens];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f32x16 c = mfma(w1[t * 64], x, b1[2 * t]);
+    tok[2 * t] = relu8<0>(c);
+    tok[2 * t + 1] = relu8<1>(c);
+  }
+  const bf16x8 wkv = reinterpret_cast<const bf16x8*>(ext + kAttKvW)[lane];
+  const f32x16 bkv = reinterpret_cast<const f32x16*>(ext + kAttKvB)[h];
+  f32x16 kv[kAttTokens];
+#pragma unroll
+  for (int t = 0; t < kAttTokens; ++t) kv[t] = mfma(wkv, tok[t], bkv);
+  const bf16x8 wq = reinterpret_cast<const bf16x8*>(ext + kAttQW)[lane];
+  const f32x16 bq = reinterpret_cast<const f32x16*>(ext + kAttQB)[h];
+  const bf16x8* wp = reinterpret_cast<const bf16x8*>(ext + kAttPostW) + lane;
+  f32x16 f0 = reinterpret_cast<const f32x16*>(ext + kAttPostB)[h];
+  f32x16 f1 = reinterpret_cast<const f32x16*>(ext + kAttPostB)[2 + h];
+#pragma unroll
+  for (int i = 0; i < kAttTokens; ++i) {
+    const f32x16 q = mfma(wq, tok[i], bq);
+    float o[8];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      // scores q . k (log2 domain): the 4-term dots as two packed-f32 lanes
+      // (v_pk_mul_f32 + v_pk_fma_f32) and one add
+      const f32x2 q01 = {q[4 * hh], q[4 * hh + 1]}, q23 = {q[4 * hh + 2], q[4 * hh + 3]};
+      float s[kAttTokens];
+      float m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < kAttTokens; ++j) {
+        const f32x2 k01 = {kv[j][4 * hh], kv[j][4 * hh + 1]};
+        const f32x2 k23 = {kv[j][4 * hh + 2], kv[j][4 * hh + 3]};
+        const f32x2 t = __builtin_elementwise_fma(q23, k23, q01 * k01);
+        s[j] = t[0] + t[1];
+        m = fmaxf(m, s[j]);
+      }
+      // softmax numerators, their sum, then sum_j p_j v_j (packed FMAs over the 4 dims)
+      // normalised once by 1 / sum
+      float sum = 0.0f;
+      f32x2 o01, o23;
+#pragma unroll
+      for (int j = 0; j < kAttTokens; ++j) {
+        const float p = __builtin_amdgcn_exp2f(s[j] - m);
+        sum = j == 0 ? p : sum + p;
+        const f32x2 pp = {p, p};
+        const f32x2 v01 = {kv[j][8 + 4 * hh], kv[j][9 + 4 * hh]};
+        const f32x2 v23 = {kv[j][10 + 4 * hh], kv[j][11 + 4 * hh]};
+        o01 = j == 0 ? pp * v01 : __builtin_elementwise_fma(pp, v01, o01);
+        o23 = j == 0 ? pp * v23 : __builtin_elementwise_fma(pp, v23, o23);
+      }
+      const float rs = __builtin_amdgcn_rcpf(sum);
+      const f32x2 rr = {rs, rs};
+      o01 = o01 * rr;
+      o23 = o23 * rr;
+      o[4 * hh] = o01[0];
+      o[4 * hh + 1] = o01[1];
+      o[4 * hh + 2] = o23[0];
+      o[4 * hh + 3] = o23[1];
+    }
+    bf16x8 a;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 t = {o[j], o[j + 1]};
+      const bf16x2 b = __builtin_convertvector(t, bf16x2);
+      a[j] = b[0];
+      a[j + 1] = b[1];
+    }
+    f0 = mfma(wp[(2 * i) * 64], a, f0);
+    f1 = mfma(wp[(2 * i + 1) * 64], a, f1);
+  }
+  feat[0] = relu8<0>(f0);
+  feat[1] = relu8<1>(f0);
+  feat[2] = relu8<0>(f1);
+  feat[3] = relu8<1>(f1);
+}
+
+// One [128,128] Tanh net + head on the 64 features (layer 1: 4 k-steps of 16 features,
+// columns in the relu8 order unit_of(s, h, j)).
+__device__ __forceinline__ f32x16 attn_net(const uint8_t* net, const bf16x8* feat, int lane) {
+  asm volatile("" ::: "memory");
+  const int h = lane >> 5;
+  const bf16x8* w1 = reinterpret_cast<const bf16x8*>(net + kAttW1) + lane;
+  const bf16x8* w2 = reinterpret_cast<const bf16x8*>(net + kAttW2) + lane;
+  const bf16x8* w3 = reinterpret_cast<const bf16x8*>(net + kAttW3) + lane;
+  const f32x16* b1 = reinterpret_cast<const f32x16*>(net + kAttB1) + h;
+  const f32x16* b2 = reinterpret_cast<const f32x16*>(net + kAttB2) + h;
+  bf16x8 h1[8];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x16 c = b1[2 * t];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) c = mfma(w1[(t * 4 + s) * 64], feat[s], c);
+    h1[2 * t] = act8<0>(c);
+    h1[2 * t + 1] = act8<1>(c);
+  }
+  f32x16 head = reinterpret_cast<const f32x16*>(net + kAttB3)[h];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    asm volatile("" ::: "memory");
+    bf16x8 wf[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) wf[kk] = w2[(t * 8 + kk) * 64];
+    f32x16 c = b2[2 * t];
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) c = mfma(wf[kk], h1[kk], c);
+    head = mfma(w3[(2 * t) * 64], act8<0>(c), head);
+    head = mfma(w3[(2 * t + 1) * 64], act8<1>(c), head);
+  }
+  return head;
+}
+
+// pi and vf nets on the same features, interleaved layer by layer (two independent
+// MFMA / tanh chains for the one-wave-per-SIMD shape)
+__device__ __forceinline__ void attn_nets_pair(const uint8_t* na, const uint8_t* nb,
+                                               const bf16x8* feat, int lane, f32x16& head_a,
+                                               f32x16& head_b) {
+  asm volatile("" ::: "memory");
+  const int h = lane >> 5;
+  const bf16x8* w1a = reinterpret_cast<const bf16x8*>(na + kAttW1) + lane;
+  const bf16x8* w1b = reinterpret_cast<const bf16x8*>(nb + kAttW1) + lane;
+  const bf16x8* w2a = reinterpret_cast<const bf16x8*>(na + kAttW2) + lane;
+  const bf16x8* w2b = reinterpret_cast<const bf16x8*>(nb + kAttW2) + lane;
+  const bf16x8* w3a = reinterpret_cast<const bf16x8*>(na + kAttW3) + lane;
+  const bf16x8* w3b = reinterpret_cast<const bf16x8*>(nb + kAttW3) + lane;
+  const f32x16* b1a = reinterpret_cast<const f32x16*>(na + kAttB1) + h;
+  const f32x16* b1b = reinterpret_cast<const f32x16*>(nb + kAttB1) + h;
+  const f32x16* b2a = reinterpret_cast<const f32x16*>(na + kAttB2) + h;
+  const f32x16* b2b = reinterpret_cast<const f32x16*>(nb + kAttB2) + h;
+  bf16x8 h1a[8], h1b[8];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x16 ca = b1a[2 * t], cb = b1b[2 * t];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      ca = mfma(w1a[(t * 4 + s) * 64], feat[s], ca);
+      cb = mfma(w1b[(t * 4 + s) * 64], feat[s], cb);
+    }
+    h1a[2 * t] = act8<0>(ca);
+    h1b[2 * t] = act8<0>(cb);
+    h1a[2 * t + 1] = act8<1>(ca);
+    h1b[2 * t + 1] = act8<1>(cb);
+  }
+  head_a = reinterpret_cast<const f32x16*>(na + kAttB3)[h];
+  head_b = reinterpret_cast<const f32x16*>(nb + kAttB3)[h];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    asm volatile("" ::: "memory");
+    bf16x8 wfa[8], wfb[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      wfa[kk] = w2a[(t * 8 + kk) * 64];
+      wfb[kk] = w2b[(t * 8 + kk) * 64];
+    }
+    f32x16 ca = b2a[2 * t], cb = b2b[2 * t];
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      ca = mfma(wfa[kk], h1a[kk], ca);
+      cb = mfma(wfb[kk], h1b[kk], cb);
+    }
+    head_a = mfma(w3a[(2 * t) * 64], act8<0>(ca), head_a);
+    head_b = mfma(w3b[(2 * t) * 64], act8<0>(cb), head_b);
+    head_a = mfma(w3a[(2 * t + 1) * 64], act8<1>(ca), head_a);
+    head_b = mfma(w3b[(2 * t + 1) * 64], act8<1>(cb), head_b);
+  }
+}
+
 // VecNormalize.normalize_obs (float64, then float32 for the policy: obs_as_tensor)
 template <int O>
 __device__ __forceinline__ void normalize(const float* o, float* x, bool on, const double* mu,
@@ -292,15 +502,31 @@ __device__ __forceinline__ void net_fwd(const uint8_t* net, const float* x, bool
   }
 }
 
+// V(x) alone (truncation bootstrap, last values): the value net, after the shared
+// attention extractor for kPair == 3
+template <int E, int O, int kPair>
+__device__ __forceinline__ void value_fwd(const uint8_t* blob, const uint8_t* vf_net, const float* x,
+                                          bool use, int lane, float* out) {
+  if constexpr (kPair == 3) {
+    bf16x8 f[4];
+    attn_extract(blob, obs_frag<O>(x, use), lane, f);
+    out[0] = attn_net(blob + kAttVf, f, lane)[0];
+  } else {
+    net_fwd<E, O, 1>(vf_net, x, use, lane, out);
+  }
+}
+
 // kPair: 0 = the nets one after the other, 1 = interleaved (mlp_pair),
-// 2 = interleaved + pipelined weight loads (mlp_pair_pipe)
+// 2 = interleaved + pipelined weight loads (mlp_pair_pipe), 3 = the attention-extractor
+// actor-critic (kAtt* blob: attn_extract + attn_nets_pair)
 template <class Sys, int W, int E, int kPair>
 __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   static_assert(!kPair || E == 32, "the interleaved pair runs 32-env tiles");
+  constexpr int kBlob = kPair == 3 ? kAttBlobBytes : kPolBlobBytes;
   constexpr int O = Sys::O, A = Sys::A;
   static_assert(O <= kPolMaxObs && A <= kPolMaxAct, "policy tile shape");
   static_assert(E == 32 || E == 64, "envs per wave");
-  __shared__ __attribute__((aligned(64))) uint8_t s_blob[kPolBlobBytes];
+  __shared__ __attribute__((aligned(64))) uint8_t s_blob[kBlob];
   __shared__ double s_norm[2 * kPolMaxObs];
   __shared__ double s_mom[W * E * 2 * O];
   const int tid = (int)threadIdx.x;
@@ -310,7 +536,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   {
     const f4v* src = reinterpret_cast<const f4v*>(p.blob);
     f4v* dst = reinterpret_cast<f4v*>(s_blob);
-    for (int v = tid; v < kPolBlobBytes / 16; v += W * 64) dst[v] = src[v];
+    for (int v = tid; v < kBlob / 16; v += W * 64) dst[v] = src[v];
   }
   if (tid < O) {  // VecNormalize: mean and sqrt(var + eps) per obs dim
     s_norm[tid] = p.norm ? p.norm[tid] : 0.0;
@@ -322,11 +548,12 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
     *a.tick_out = tick + a.tick_adv;
   }
   __syncthreads();
-  const uint8_t* pi_net = s_blob;
-  const uint8_t* vf_net = s_blob + kPolNet;
+  const uint8_t* pi_net = s_blob + (kPair == 3 ? kAttPi : 0);
+  const uint8_t* vf_net = s_blob + (kPair == 3 ? kAttVf : kPolNet);
   // torch.distributions.Normal constants, computed by the packer: scale = exp(log_std),
   // 2 * scale**2, log(scale) (LDS, wave-uniform broadcast reads)
-  const float* g_scale = reinterpret_cast<const float*>(s_blob + kPolLogStd) + 4;
+  const float* g_scale =
+      reinterpret_cast<const float*>(s_blob + (kPair == 3 ? kAttLogStd : kPolLogStd)) + 4;
   const float* g_var2 = g_scale + 4;
   const float* g_lscale = g_scale + 8;
   const bool norm = p.norm != nullptr;
@@ -374,7 +601,15 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
         for (int j = 0; j < O; ++j) obs_buf[off * O + j] = x[j];
       }
       float mean[A], val[1];
-      if constexpr (kPair) {
+      if constexpr (kPair == 3) {
+        f32x16 hp, hv;
+        bf16x8 f[4];
+        attn_extract(s_blob, obs_frag<O>(x, live), lane, f);
+        attn_nets_pair(pi_net, vf_net, f, lane, hp, hv);
+#pragma unroll
+        for (int j = 0; j < A; ++j) mean[j] = hp[j];
+        val[0] = hv[0];
+      } else if constexpr (kPair) {
         f32x16 hp, hv;
         if constexpr (kPair == 2) mlp_pair_pipe(pi_net, vf_net, obs_frag<O>(x, live), lane, hp, hv);
         else mlp_pair(pi_net, vf_net, obs_frag<O>(x, live), lane, hp, hv);
@@ -417,7 +652,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
         if (__ballot(bt) != 0ull) {  // wave-uniform branch
           float xt[O], vt[1];
           normalize<O>(ot, xt, norm, mu, sd, p.clip);
-          net_fwd<E, O, 1>(vf_net, xt, bt, lane, vt);
+          value_fwd<E, O, kPair>(s_blob, vf_net, xt, bt, lane, vt);
           if (bt) rew = rew + gamma * vt[0];
         }
       }
@@ -438,7 +673,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
     }
     float x[O], vl[1];
     normalize<O>(o, x, norm, mu, sd, p.clip);
-    net_fwd<E, O, 1>(vf_net, x, live, lane, vl);
+    value_fwd<E, O, kPair>(s_blob, vf_net, x, live, lane, vl);
     if (live) {
       p.last_val[i] = vl[0];
 #pragma unroll
@@ -533,6 +768,36 @@ int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, const PolS
   return (int)hipErrorInvalidValue;
 }
 
+PolShape attn_policy_shape(int64_t n, int num_cus) {
+  PolShape s = {32, 4, 3, 0};
+  const int64_t groups = ((n + 31) / 32 + 3) / 4;
+  s.grid = (int)(groups < num_cus ? groups : num_cus);
+  return s;
+}
+
+template <class Sys>
+static int launch_pol_attn(const KArgs& a, const PArgs& p, const PolShape& sh, hipStream_t s) {
+  hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, 3>), dim3((unsigned)sh.grid), dim3(4 * 64), 0, s,
+                     a, p);
+  return (int)hipGetLastError();
+}
+
+int launch_rollout_policy_attn(int system, const KArgs& a, const PArgs& p, const PolShape& grid,
+                               void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (system) {
+    case LZ_SYS_LORENZ3: return launch_pol_attn<SysL3<float>>(a, p, grid, s);
+    case LZ_SYS_LORENZ4: return launch_pol_attn<SysL4<float>>(a, p, grid, s);
+    case LZ_SYS_PMSM: return launch_pol_attn<SysPMSM>(a, p, grid, s);
+    case LZ_SYS_HR: return launch_pol_attn<SysHR<float>>(a, p, grid, s);
+    case LZ_SYS_T1: return launch_pol_attn<SysT1<float>>(a, p, grid, s);
+    case LZ_SYS_T2: return launch_pol_attn<SysT2<float>>(a, p, grid, s);
+    case LZ_SYS_TP: return launch_pol_attn<SysTP<float>>(a, p, grid, s);
+    case LZ_SYS_SC: return launch_pol_attn<SysSC<float>>(a, p, grid, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
 int launch_policy_moments_final(const double* partials, int nparts, int width, double count,
                                 double* out, void* stream) {
   hipLaunchKernelGGL(k_pol_moments_final, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream),
@@ -600,6 +865,132 @@ void pack_net(uint8_t* net, int O, int rows3, const float* w1, const float* b1, 
     }
 }
 
+// Attention-extractor actor-critic (kAtt* layout, see lz_internal.h / attn_extract).
+// log2(e) / sqrt(head_dim 4): the Q projection is stored pre-scaled so that the
+// kernel's softmax is exp2(s - max) on q.k directly.
+constexpr double kAttQScale = 1.4426950408889634 / 2.0;
+
+// row of a 32-row K|V or Q tile -> in_proj row (-1: zero padding).  A tile row r lands
+// in lane half h = (r >> 2) & 1, register g = (r & 3) + 4 (r >> 3): group g >> 2 = r >> 3.
+inline int kv_row(int r) {
+  const int h = (r >> 2) & 1, grp = r >> 3, d = r & 3;
+  return (grp < 2 ? 16 : 32) + 4 * (2 * h + (grp & 1)) + d;  // k heads 2h, 2h+1, then v
+}
+inline int q_row(int r) {
+  const int h = (r >> 2) & 1, grp = r >> 3, d = r & 3;
+  return grp < 2 ? 4 * (2 * h + grp) + d : -1;
+}
+
+void pack_attn(uint8_t* b, const lz_attn_policy* p) {
+  using lz::kPolHidden;
+  const int O = p->obs_dim;
+  uint16_t* f1 = reinterpret_cast<uint16_t*>(b + lz::kAttFc1W);
+  uint16_t* fkv = reinterpret_cast<uint16_t*>(b + lz::kAttKvW);
+  uint16_t* fq = reinterpret_cast<uint16_t*>(b + lz::kAttQW);
+  uint16_t* fp = reinterpret_cast<uint16_t*>(b + lz::kAttPostW);
+  float* c1 = reinterpret_cast<float*>(b + lz::kAttFc1B);
+  float* ckv = reinterpret_cast<float*>(b + lz::kAttKvB);
+  float* cq = reinterpret_cast<float*>(b + lz::kAttQB);
+  float* cp = reinterpret_cast<float*>(b + lz::kAttPostB);
+  // out_proj folded into post_attention_fc (float64): per token i
+  //   Wf_i = W_post[:, 16i:16i+16] W_out,  b_f = b_post + sum_i W_post[:, 16i:16i+16] b_out
+  static_assert(lz::kAttTokens * lz::kAttTokDim == kPolHidden, "token split");
+  double wf[lz::kAttTokens][lz::kAttFeat][lz::kAttTokDim];
+  double bfold[lz::kAttFeat];
+  for (int f = 0; f < lz::kAttFeat; ++f) {
+    double acc = p->post_b[f];
+    for (int i = 0; i < lz::kAttTokens; ++i)
+      for (int d = 0; d < lz::kAttTokDim; ++d) {
+        double w = 0.0;
+        for (int e = 0; e < lz::kAttTokDim; ++e)
+          w += (double)p->post_w[f * kPolHidden + 16 * i + e] * (double)p->out_proj_w[e * 16 + d];
+        wf[i][f][d] = w;
+      }
+    for (int i = 0; i < lz::kAttTokens; ++i)
+      for (int e = 0; e < lz::kAttTokDim; ++e)
+        acc += (double)p->post_w[f * kPolHidden + 16 * i + e] * (double)p->out_proj_b[e];
+    bfold[f] = acc;
+  }
+  for (int lane = 0; lane < 64; ++lane) {
+    const int r = lane & 31, h = lane >> 5;
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * h + j;                              // natural k (obs, head outputs)
+      const int td = (j & 3) + 8 * (j >> 2) + 4 * h;        // token dim of a relu8 fragment
+      for (int t = 0; t < 4; ++t)
+        f1[(t * 64 + lane) * 8 + j] = bf16_rne(k < O ? p->fc1_w[(32 * t + r) * O + k] : 0.0f);
+      fkv[lane * 8 + j] = bf16_rne(p->in_proj_w[kv_row(r) * 16 + td]);
+      const int qr = q_row(r);
+      fq[lane * 8 + j] =
+          bf16_rne(qr < 0 ? 0.0f : (float)(kAttQScale * (double)p->in_proj_w[qr * 16 + td]));
+      for (int i = 0; i < lz::kAttTokens; ++i)
+        for (int T = 0; T < 2; ++T)
+          fp[((2 * i + T) * 64 + lane) * 8 + j] = bf16_rne((float)wf[i][32 * T + r][k]);
+    }
+  }
+  for (int h = 0; h < 2; ++h)
+    for (int g = 0; g < 16; ++g) {
+      const int r = row_of(g, h);
+      for (int t = 0; t < 4; ++t) c1[(2 * t + h) * 16 + g] = p->fc1_b[32 * t + r];
+      ckv[h * 16 + g] = p->in_proj_b[kv_row(r)];
+      cq[h * 16 + g] = q_row(r) < 0 ? 0.0f : (float)(kAttQScale * (double)p->in_proj_b[q_row(r)]);
+      for (int T = 0; T < 2; ++T) cp[(2 * T + h) * 16 + g] = (float)bfold[32 * T + r];
+    }
+  // the two [128,128] Tanh nets: layer 1 reads the 64 features as 4 k-steps of relu8
+  // fragments (feature unit_of(s, h, j)); layers 2 and 3 as in pack_net
+  const float* W1[2] = {p->pi_w1, p->vf_w1};
+  const float* B1[2] = {p->pi_b1, p->vf_b1};
+  const float* W2[2] = {p->pi_w2, p->vf_w2};
+  const float* B2[2] = {p->pi_b2, p->vf_b2};
+  const float* W3[2] = {p->act_w, p->val_w};
+  const float* B3[2] = {p->act_b, p->val_b};
+  const int rows3[2] = {p->act_dim, 1};
+  for (int n = 0; n < 2; ++n) {
+    uint8_t* net = b + (n == 0 ? lz::kAttPi : lz::kAttVf);
+    uint16_t* g1 = reinterpret_cast<uint16_t*>(net + lz::kAttW1);
+    uint16_t* g2 = reinterpret_cast<uint16_t*>(net + lz::kAttW2);
+    uint16_t* g3 = reinterpret_cast<uint16_t*>(net + lz::kAttW3);
+    float* d1 = reinterpret_cast<float*>(net + lz::kAttB1);
+    float* d2 = reinterpret_cast<float*>(net + lz::kAttB2);
+    float* d3 = reinterpret_cast<float*>(net + lz::kAttB3);
+    for (int lane = 0; lane < 64; ++lane) {
+      const int r = lane & 31, h = lane >> 5;
+      for (int j = 0; j < 8; ++j) {
+        for (int t = 0; t < 4; ++t) {
+          for (int s = 0; s < 4; ++s)
+            g1[((t * 4 + s) * 64 + lane) * 8 + j] =
+                bf16_rne(kTanhScale * W1[n][(32 * t + r) * lz::kAttFeat + unit_of(s, h, j)]);
+          for (int kk = 0; kk < 8; ++kk)
+            g2[((t * 8 + kk) * 64 + lane) * 8 + j] =
+                bf16_rne(kTanhScale * W2[n][(32 * t + r) * kPolHidden + unit_of(kk, h, j)]);
+        }
+        for (int kk = 0; kk < 8; ++kk)
+          g3[(kk * 64 + lane) * 8 + j] =
+              bf16_rne(r < rows3[n] ? W3[n][r * kPolHidden + unit_of(kk, h, j)] : 0.0f);
+      }
+    }
+    for (int h = 0; h < 2; ++h)
+      for (int g = 0; g < 16; ++g) {
+        for (int t = 0; t < 4; ++t) {
+          d1[(2 * t + h) * 16 + g] = kTanhScale * B1[n][32 * t + row_of(g, h)];
+          d2[(2 * t + h) * 16 + g] = kTanhScale * B2[n][32 * t + row_of(g, h)];
+        }
+        d3[h * 16 + g] = row_of(g, h) < rows3[n] ? B3[n][row_of(g, h)] : 0.0f;
+      }
+  }
+}
+
+void pack_gauss(float* ls, int act_dim, const float* log_std) {
+  // [log_std(4)][scale(4)][2 scale^2 (4)][log scale (4)]: torch Normal's
+  // scale = exp(log_std), var = scale**2 (the kernel divides by 2 * var), log(scale)
+  for (int j = 0; j < act_dim; ++j) {
+    const float sc = std::exp(log_std[j]);
+    ls[j] = log_std[j];
+    ls[4 + j] = sc;
+    ls[8 + j] = 2.0f * (sc * sc);
+    ls[12 + j] = std::log(sc);
+  }
+}
+
 lz_status pfail(lz_status s, const char* msg) {
   return lz::set_error(s, msg);
 }
@@ -624,16 +1015,27 @@ lz_status lz_policy_pack(const lz_mlp_policy* p, void* host_blob, int64_t cap) {
   pack_net(b, p->obs_dim, p->act_dim, p->pi_w1, p->pi_b1, p->pi_w2, p->pi_b2, p->act_w, p->act_b);
   pack_net(b + lz::kPolNet, p->obs_dim, 1, p->vf_w1, p->vf_b1, p->vf_w2, p->vf_b2, p->val_w,
            p->val_b);
-  // [log_std(4)][scale(4)][2 scale^2 (4)][log scale (4)]: torch Normal's
-  // scale = exp(log_std), var = scale**2 (the kernel divides by 2 * var), log(scale)
-  float* ls = reinterpret_cast<float*>(b + lz::kPolLogStd);
-  for (int j = 0; j < p->act_dim; ++j) {
-    const float sc = std::exp(p->log_std[j]);
-    ls[j] = p->log_std[j];
-    ls[4 + j] = sc;
-    ls[8 + j] = 2.0f * (sc * sc);
-    ls[12 + j] = std::log(sc);
-  }
+  pack_gauss(reinterpret_cast<float*>(b + lz::kPolLogStd), p->act_dim, p->log_std);
+  return LZ_OK;
+}
+
+int64_t lz_attn_policy_blob_bytes(void) { return lz::kAttBlobBytes; }
+
+lz_status lz_attn_policy_pack(const lz_attn_policy* p, void* host_blob, int64_t cap) {
+  if (!p || !host_blob) return pfail(LZ_ERR_INVALID, "policy/blob is NULL");
+  if (cap < lz::kAttBlobBytes) return pfail(LZ_ERR_INVALID, "blob capacity too small");
+  if (p->obs_dim < 1 || p->obs_dim > lz::kPolMaxObs || p->act_dim < 1 || p->act_dim > lz::kPolMaxAct)
+    return pfail(LZ_ERR_UNSUPPORTED, "policy supports obs_dim 1..8 and act_dim 1..4");
+  const float* req[] = {p->fc1_w, p->fc1_b, p->in_proj_w, p->in_proj_b, p->out_proj_w,
+                        p->out_proj_b, p->post_w, p->post_b, p->pi_w1, p->pi_b1, p->pi_w2,
+                        p->pi_b2, p->vf_w1, p->vf_b1, p->vf_w2, p->vf_b2, p->act_w, p->act_b,
+                        p->val_w, p->val_b, p->log_std};
+  for (const float* q : req)
+    if (!q) return pfail(LZ_ERR_INVALID, "a policy weight pointer is NULL");
+  uint8_t* b = static_cast<uint8_t*>(host_blob);
+  std::memset(b, 0, lz::kAttBlobBytes);
+  pack_attn(b, p);
+  pack_gauss(reinterpret_cast<float*>(b + lz::kAttLogStd), p->act_dim, p->log_std);
   return LZ_OK;
 }
 

@@ -77,6 +77,14 @@ class LzMlpPolicy(ctypes.Structure):
             "act_w", "act_b", "val_w", "val_b", "log_std")]
 
 
+class LzAttnPolicy(ctypes.Structure):
+    _fields_ = [("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32)] + [
+        (name, ctypes.c_void_p) for name in (
+            "fc1_w", "fc1_b", "in_proj_w", "in_proj_b", "out_proj_w", "out_proj_b", "post_w",
+            "post_b", "pi_w1", "pi_b1", "pi_w2", "pi_b2", "vf_w1", "vf_b1", "vf_w2", "vf_b2",
+            "act_w", "act_b", "val_w", "val_b", "log_std")]
+
+
 class LzPolicyRolloutArgs(ctypes.Structure):
     _fields_ = [
         ("K", ctypes.c_int32),
@@ -156,6 +164,9 @@ _SIGS = {
     "lz_policy_blob_bytes": (ctypes.c_int64, []),
     "lz_policy_pack": (ctypes.c_int, [ctypes.POINTER(LzMlpPolicy), VP, ctypes.c_int64]),
     "lz_rollout_policy": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
+    "lz_attn_policy_blob_bytes": (ctypes.c_int64, []),
+    "lz_attn_policy_pack": (ctypes.c_int, [ctypes.POINTER(LzAttnPolicy), VP, ctypes.c_int64]),
+    "lz_rollout_policy_attn": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
     "lz_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, ctypes.c_double,
                               ctypes.c_double, VP, VP, ctypes.c_int32, VP]),
     "lz_frame_stack": (ctypes.c_int, [VP, VP, VP, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,

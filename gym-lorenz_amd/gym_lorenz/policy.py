@@ -88,6 +88,62 @@ class ActorCriticMlp(nn.Module):
         return mean, value
 
 
+class AttentionFeaturesExtractor(nn.Module):
+    """code/train.py:52-95 restated in plain torch (same submodule names, so the same
+    state_dict keys under ``features_extractor.``): fc1 obs->128 + ReLU, the 128 units
+    as 8 tokens of 16, nn.MultiheadAttention(16, 4 heads, batch_first) self-attention,
+    flatten, post_attention_fc 128->features_dim + ReLU."""
+
+    def __init__(self, obs_dim, features_dim=64):
+        super().__init__()
+        self.hidden_dim, self.seq_len, self.token_dim = 128, 8, 16
+        self.features_dim = features_dim
+        self.fc1 = nn.Linear(obs_dim, self.hidden_dim)
+        self.attention_layer = nn.MultiheadAttention(embed_dim=self.token_dim, num_heads=4,
+                                                     batch_first=True)
+        self.post_attention_fc = nn.Sequential(nn.Linear(self.hidden_dim, features_dim), nn.ReLU())
+
+    def forward(self, observations):
+        x = torch.relu(self.fc1(observations))
+        x_seq = x.view(-1, self.seq_len, self.token_dim)
+        attn_output, _ = self.attention_layer(x_seq, x_seq, x_seq)
+        return self.post_attention_fc(attn_output.reshape(-1, self.hidden_dim))
+
+
+class ActorCriticAttn(nn.Module):
+    """SB3 ActorCriticPolicy as code/train.py:101-112 builds it: the shared
+    AttentionFeaturesExtractor (features_dim=64), net_arch pi=[128,128] vf=[128,128]
+    Tanh, DiagGaussian (log_std_init=0), SB3's orthogonal init (gain sqrt(2) for the
+    extractor and the nets, 0.01 / 1 for the heads, zero biases; init_weights touches
+    nn.Linear modules only, so in_proj keeps torch's xavier init)."""
+
+    def __init__(self, obs_dim, act_dim, features_dim=64, hidden=HIDDEN, log_std_init=0.0,
+                 seed=None):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed) if seed is not None else None
+        if seed is not None:
+            torch.manual_seed(seed)  # nn.MultiheadAttention's own xavier init
+        self.features_extractor = AttentionFeaturesExtractor(obs_dim, features_dim)
+        self.mlp_extractor = _MlpExtractor(features_dim, hidden)
+        self.action_net = nn.Linear(hidden, act_dim)
+        self.value_net = nn.Linear(hidden, 1)
+        self.log_std = nn.Parameter(torch.ones(act_dim) * log_std_init)
+        with torch.no_grad():
+            for mod, gain in ((self.features_extractor, math.sqrt(2)),
+                              (self.mlp_extractor, math.sqrt(2)), (self.action_net, 0.01),
+                              (self.value_net, 1.0)):
+                for m in mod.modules():
+                    if isinstance(m, nn.Linear):
+                        nn.init.orthogonal_(m.weight, gain=gain, generator=g)
+                        m.bias.zero_()
+
+    def forward(self, obs):
+        f = self.features_extractor(obs)
+        mean = self.action_net(self.mlp_extractor.policy_net(f))
+        value = self.value_net(self.mlp_extractor.value_net(f)).flatten()
+        return mean, value
+
+
 def _bf(t):
     return t.to(torch.bfloat16).to(torch.float32)
 
@@ -119,6 +175,92 @@ def reference_forward_bf16(state_dict, obs):
     return mean, value
 
 
+# log2(e) / sqrt(head dim 4): lz_attn_policy_pack stores the Q projection pre-scaled by
+# it (bf16(c W_q), c b_q) so the kernel's softmax is exp2(q.k - max)
+ATTN_Q_SCALE = 1.4426950408889634 / 2.0
+FE = "features_extractor."
+ATTN_FE_KEYS = ("fc1.weight", "fc1.bias", "attention_layer.in_proj_weight",
+                "attention_layer.in_proj_bias", "attention_layer.out_proj.weight",
+                "attention_layer.out_proj.bias", "post_attention_fc.0.weight",
+                "post_attention_fc.0.bias")
+_ATTN_FE_FIELDS = ("fc1_w", "fc1_b", "in_proj_w", "in_proj_b", "out_proj_w", "out_proj_b",
+                   "post_w", "post_b")
+
+
+def is_attention_policy(state_dict):
+    """True for a state_dict of code/train.py's AttentionFeaturesExtractor policy."""
+    return any(k.endswith("features_extractor.fc1.weight") for k in state_dict)
+
+
+def _fe_key(state_dict, name):
+    # SB3 (share_features_extractor=True) stores the shared extractor under
+    # features_extractor. and aliases it as pi_features_extractor. / vf_features_extractor.
+    for pre in (FE, "pi_" + FE):
+        if pre + name in state_dict:
+            return pre + name
+    raise KeyError("policy state_dict lacks %r (expected code/train.py's "
+                   "AttentionFeaturesExtractor)" % (FE + name))
+
+
+def attn_folded_post(sd):
+    """out_proj folded into post_attention_fc, float64 (as lz_attn_policy_pack):
+    Wf [8 tokens, 64, 16] and the folded bias [64]."""
+    g = {k: torch.as_tensor(np.asarray(_np(sd[_fe_key(sd, k)])), dtype=torch.float64)
+         for k in ATTN_FE_KEYS[4:]}
+    wo, bo = g["attention_layer.out_proj.weight"], g["attention_layer.out_proj.bias"]
+    wp, bp = g["post_attention_fc.0.weight"], g["post_attention_fc.0.bias"]
+    blocks = wp.view(wp.shape[0], 8, 16).permute(1, 0, 2)  # [8, 64, 16]
+    wf = blocks @ wo
+    bf = bp + (blocks @ bo).sum(0)
+    return wf, bf
+
+
+def reference_forward_attn_bf16(state_dict, obs):
+    """lz_rollout_policy_attn's arithmetic restated in torch: bf16 obs / weights /
+    tokens / head outputs / features (RNE), fp32 accumulation and attention, the Q
+    projection pre-scaled by ATTN_Q_SCALE and a base-2 softmax, out_proj folded into
+    post_attention_fc in float64, the Tanh nets as reference_forward_bf16.  Differs
+    from the kernel in fp32 summation order and the exp2 / rcp / tanh implementations.
+    Returns (mean, value)."""
+    sd = state_dict
+    f32 = torch.float32
+
+    def t(k):
+        return torch.as_tensor(np.asarray(_np(sd[k])), dtype=f32)
+
+    x = _bf(torch.as_tensor(obs, dtype=f32))
+    n = x.shape[0]
+    tok = _bf(torch.relu(x @ _bf(t(_fe_key(sd, "fc1.weight"))).T + t(_fe_key(sd, "fc1.bias"))))
+    tok = tok.view(n, 8, 16)
+    w_in, b_in = t(_fe_key(sd, ATTN_FE_KEYS[2])), t(_fe_key(sd, ATTN_FE_KEYS[3]))
+    c = torch.tensor(np.float64(ATTN_Q_SCALE))
+    wq = _bf((c.double() * w_in[:16].double()).to(f32))
+    bq = (c.double() * b_in[:16].double()).to(f32)
+    q = tok @ wq.T + bq
+    k = tok @ _bf(w_in[16:32]).T + b_in[16:32]
+    v = tok @ _bf(w_in[32:48]).T + b_in[32:48]
+    q, k, v = (z.view(n, 8, 4, 4).transpose(1, 2) for z in (q, k, v))  # [n, head, token, 4]
+    s = q @ k.transpose(-1, -2)
+    p = torch.exp2(s - s.amax(-1, keepdim=True))
+    o = (p @ v) * (1.0 / p.sum(-1, keepdim=True))  # normalised after the weighted sum
+    a = _bf(o.transpose(1, 2).reshape(n, 8, 16))
+    wf, bfold = attn_folded_post(sd)
+    feat = bfold.to(f32) + torch.einsum("nid,ifd->nf", a, _bf(wf.to(f32)))
+    feat = _bf(torch.relu(feat))
+    s_t = torch.tensor(TANH_SCALE)
+
+    def net(prefix, w3, b3):
+        h = feat
+        for layer in (".0", ".2"):
+            acc = h @ _bf(s_t * t(prefix + layer + ".weight")).T + s_t * t(prefix + layer + ".bias")
+            h = _bf(torch.tanh(acc / s_t))
+        return h @ _bf(t(w3)).T + t(b3)
+
+    mean = net("mlp_extractor.policy_net", "action_net.weight", "action_net.bias")
+    value = net("mlp_extractor.value_net", "value_net.weight", "value_net.bias").flatten()
+    return mean, value
+
+
 def _np(v):
     if isinstance(v, torch.Tensor):
         return v.detach().to("cpu", torch.float32).numpy()
@@ -144,6 +286,32 @@ def pack_policy(state_dict, obs_dim, act_dim):
         setattr(p, f, a.ctypes.data)
     blob = np.zeros(int(nat.lib.lz_policy_blob_bytes()), np.uint8)
     nat.check(nat.lib.lz_policy_pack(ctypes.byref(p), blob.ctypes.data, blob.size))
+    return blob
+
+
+def pack_attn_policy(state_dict, obs_dim, act_dim, features_dim=64):
+    """lz_attn_policy_pack: SB3 state_dict of code/train.py's attention actor-critic ->
+    uint8 numpy blob (host; needs no GPU)."""
+    if features_dim != 64:
+        raise ValueError("the fused kernel implements features_dim=64 (code/train.py:100)")
+    keys = [_fe_key(state_dict, k) for k in ATTN_FE_KEYS] + list(KEYS)
+    for key in KEYS:
+        if key not in state_dict:
+            raise KeyError("policy state_dict lacks %r" % key)
+    arrs = [np.ascontiguousarray(_np(state_dict[k]), dtype=np.float32) for k in keys]
+    F = features_dim
+    shapes = [(HIDDEN, obs_dim), (HIDDEN,), (48, 16), (48,), (16, 16), (16,), (F, HIDDEN), (F,)] + [
+        (HIDDEN, F), (HIDDEN,), (HIDDEN, HIDDEN), (HIDDEN,)] * 2 + [
+        (act_dim, HIDDEN), (act_dim,), (1, HIDDEN), (1,), (act_dim,)]
+    for key, a, shp in zip(keys, arrs, shapes):
+        if a.shape != shp:
+            raise ValueError("%s has shape %s, expected %s" % (key, a.shape, shp))
+    p = nat.LzAttnPolicy()
+    p.obs_dim, p.act_dim = int(obs_dim), int(act_dim)
+    for f, a in zip(_ATTN_FE_FIELDS + _FIELDS, arrs):
+        setattr(p, f, a.ctypes.data)
+    blob = np.zeros(int(nat.lib.lz_attn_policy_blob_bytes()), np.uint8)
+    nat.check(nat.lib.lz_attn_policy_pack(ctypes.byref(p), blob.ctypes.data, blob.size))
     return blob
 
 
@@ -195,14 +363,19 @@ class FusedRolloutCollector:
         self.group = group
         self.act_low, self.act_high = action_bounds(backend.system_name)
         self.blob = None
+        self.attention = False
         self.last_obs = None
         self.last_episode_starts = torch.ones((self.n,), dtype=torch.float32, device=self.device)
         if state_dict is not None:
             self.set_params(state_dict)
 
     def set_params(self, state_dict):
-        """Pack and upload the actor-critic weights (call after every optimizer step)."""
-        blob = pack_policy(state_dict, self.O, self.A)
+        """Pack and upload the actor-critic weights (call after every optimizer step).
+        A state_dict with code/train.py's AttentionFeaturesExtractor selects the
+        attention kernel (lz_rollout_policy_attn), any other the MlpPolicy kernel."""
+        self.attention = is_attention_policy(state_dict)
+        pack = pack_attn_policy if self.attention else pack_policy
+        blob = pack(state_dict, self.O, self.A)
         self.blob = torch.from_numpy(blob).to(self.device)
 
     def reset(self):
@@ -248,7 +421,8 @@ class FusedRolloutCollector:
         r.rew_buf, r.done_buf, r.last_values = _p(rew), _p(done), _p(last_val)
         r.obs_moments = _p(mom)
         r.done_idx, r.terminal_obs, r.cap, r.n_done = _p(didx), _p(tobs), self.capture_terminal, _p(ndone)
-        nat.check(nat.lib.lz_rollout_policy(self.env._h, ctypes.byref(r)))
+        launch = nat.lib.lz_rollout_policy_attn if self.attention else nat.lib.lz_rollout_policy
+        nat.check(launch(self.env._h, ctypes.byref(r)))
         starts = torch.empty((K, n), dtype=f32, device=dev)
         starts[0] = self.last_episode_starts
         if K > 1:

@@ -301,6 +301,51 @@ typedef struct lz_policy_rollout_args {
  * a small scratch buffer for obs_moments (do not capture that first call). */
 lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r);
 
+/* The actor-critic of the reference's flagship PPO script, code/train.py:52-112:
+ * policy_kwargs = dict(features_extractor_class=AttentionFeaturesExtractor,
+ * features_extractor_kwargs=dict(features_dim=64), net_arch=dict(pi=[128, 128],
+ * vf=[128, 128])), Tanh nets, one features extractor shared by pi and vf (SB3
+ * share_features_extractor=True).  The extractor (code/train.py:56-95): fc1
+ * Linear(obs_dim, 128) + ReLU, the 128 units viewed as 8 tokens of 16, a 4-head
+ * nn.MultiheadAttention(16) self-attention, the 8 outputs flattened,
+ * post_attention_fc Linear(128, 64) + ReLU.  Names are SB3 state_dict keys
+ * (prefix features_extractor.). */
+typedef struct lz_attn_policy {
+  int32_t obs_dim;        /* 1..8 */
+  int32_t act_dim;        /* 1..4 */
+  const float* fc1_w;     /* features_extractor.fc1.weight [128, obs_dim] */
+  const float* fc1_b;     /* features_extractor.fc1.bias [128] */
+  const float* in_proj_w; /* features_extractor.attention_layer.in_proj_weight [48, 16] */
+  const float* in_proj_b; /* features_extractor.attention_layer.in_proj_bias [48] */
+  const float* out_proj_w; /* features_extractor.attention_layer.out_proj.weight [16, 16] */
+  const float* out_proj_b; /* features_extractor.attention_layer.out_proj.bias [16] */
+  const float* post_w;    /* features_extractor.post_attention_fc.0.weight [64, 128] */
+  const float* post_b;    /* features_extractor.post_attention_fc.0.bias [64] */
+  const float* pi_w1;     /* mlp_extractor.policy_net.0.weight [128, 64] */
+  const float* pi_b1;
+  const float* pi_w2;     /* mlp_extractor.policy_net.2.weight [128, 128] */
+  const float* pi_b2;
+  const float* vf_w1;     /* mlp_extractor.value_net.0.weight [128, 64] */
+  const float* vf_b1;
+  const float* vf_w2;     /* mlp_extractor.value_net.2.weight [128, 128] */
+  const float* vf_b2;
+  const float* act_w;     /* action_net.weight [act_dim, 128] */
+  const float* act_b;
+  const float* val_w;     /* value_net.weight [1, 128] */
+  const float* val_b;
+  const float* log_std;   /* log_std [act_dim] */
+} lz_attn_policy;
+
+/* Size of the packed attention policy blob (bf16 MFMA fragments + f32 biases;
+ * out_proj folded into post_attention_fc in float64). */
+int64_t lz_attn_policy_blob_bytes(void);
+/* Pack *p into host_blob (cap >= lz_attn_policy_blob_bytes()).  Host-only. */
+lz_status lz_attn_policy_pack(const lz_attn_policy* p, void* host_blob, int64_t cap);
+/* lz_rollout_policy with an lz_attn_policy_pack blob: the same K-step fused rollout
+ * with the attention features extractor in front of the two nets (32 envs per wave,
+ * one wave per SIMD; the blob is resident in LDS). */
+lz_status lz_rollout_policy_attn(lz_handle* h, const lz_policy_rollout_args* r);
+
 /* SB3 RolloutBuffer.compute_returns_and_advantage over time-major [K, N] float32
  * buffers (float32 arithmetic in NumPy's order): advantages and returns out.
  * done = the done bytes of each step (episode_starts shifted by one). */

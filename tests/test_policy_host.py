@@ -178,6 +178,22 @@ def test_policy_structs_match_header(tmp_path):
     assert nat.lib.lz_policy_blob_bytes() == 92480
 
 
+def test_attn_policy_struct_matches_header(tmp_path):
+    from gym_lorenz import _native as nat
+
+    c = tmp_path / "probe.c"
+    c.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "lorenz_env.h"\n'
+        'int main(void){printf("%zu %zu %zu\\n", sizeof(lz_attn_policy),'
+        " offsetof(lz_attn_policy, post_b), offsetof(lz_attn_policy, log_std));return 0;}\n")
+    exe = tmp_path / "probe"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)])
+    got = [int(v) for v in subprocess.check_output([str(exe)]).split()]
+    P = nat.LzAttnPolicy
+    assert got == [ctypes.sizeof(P), P.post_b.offset, P.log_std.offset]
+    assert nat.lib.lz_attn_policy_blob_bytes() == 140608
+
+
 def test_sb3_framestack_restatement_hand_case():
     from oracle.sb3_framestack import StackedObservations
 
@@ -188,3 +204,157 @@ def test_sb3_framestack_restatement_hand_case():
     st, infos = so.update(np.array([[5, 6], [7, 8]], np.float32), np.array([False, True]), infos)
     assert st.tolist() == [[0, 0, 1, 2, 5, 6], [0, 0, 0, 0, 7, 8]]
     assert infos[1]["terminal_observation"].tolist() == [0, 0, 3, 4, 9, 9]
+
+
+# ---------------------------------------------------------------- attention extractor
+# lz_internal.h kAtt* layout (bytes)
+def _attn_layout():
+    L = {"Fc1W": 0}
+    L["Fc1B"] = L["Fc1W"] + 4 * 64 * 16
+    L["KvW"] = L["Fc1B"] + 4 * 2 * 16 * 4
+    L["KvB"] = L["KvW"] + 64 * 16
+    L["QW"] = L["KvB"] + 2 * 16 * 4
+    L["QB"] = L["QW"] + 64 * 16
+    L["PostW"] = L["QB"] + 2 * 16 * 4
+    L["PostB"] = L["PostW"] + 8 * 2 * 64 * 16
+    L["Ext"] = L["PostB"] + 2 * 2 * 16 * 4
+    N = {"W1": 0}
+    N["W2"] = N["W1"] + 4 * 4 * 64 * 16
+    N["W3"] = N["W2"] + 4 * 8 * 64 * 16
+    N["B1"] = N["W3"] + 8 * 64 * 16
+    N["B2"] = N["B1"] + 512
+    N["B3"] = N["B2"] + 512
+    N["Net"] = N["B3"] + 128
+    return L, N
+
+
+def _relu_frag(c):
+    t = _bf16(np.where(c < 0, np.float32(0), c))  # torch.relu keeps NaN
+    return [t[:, 0:8], t[:, 8:16]]
+
+
+def _emulate_attn(blob, obs):
+    """lz_rollout_policy_attn's forward on one 32-env tile over the packed blob."""
+    L, N = _attn_layout()
+    f32 = lambda off, n: blob[off: off + 4 * n].view(np.float32)  # noqa: E731
+    lane_h = np.arange(64) >> 5
+    O = obs.shape[1]
+    x = np.zeros((64, 8), np.float32)
+    x[:32, :O] = _bf16(obs)
+    fc1 = _unpack(blob, L["Fc1W"], 4)
+    b1 = f32(L["Fc1B"], 128).reshape(4, 2, 16)
+    tok = []
+    for t in range(4):
+        tok += _relu_frag(_mfma(fc1[t], x, b1[t][lane_h]))
+    wkv = _unpack(blob, L["KvW"], 1)[0]
+    bkv = f32(L["KvB"], 32).reshape(2, 16)[lane_h]
+    kv = np.stack([_mfma(wkv, tok[t], bkv) for t in range(8)], 1)  # [64, token, 16]
+    wq = _unpack(blob, L["QW"], 1)[0]
+    bq = f32(L["QB"], 32).reshape(2, 16)[lane_h]
+    wp = _unpack(blob, L["PostW"], 16)
+    bp = f32(L["PostB"], 64).reshape(2, 2, 16)
+    f0, f1 = bp[0][lane_h], bp[1][lane_h]
+    for i in range(8):
+        q = _mfma(wq, tok[i], bq)
+        o = np.zeros((64, 8), np.float32)
+        for hh in range(2):
+            s = np.einsum("ld,ljd->lj", q[:, 4 * hh: 4 * hh + 4], kv[:, :, 4 * hh: 4 * hh + 4])
+            p = np.exp2(s - s.max(1, keepdims=True))
+            o[:, 4 * hh: 4 * hh + 4] = np.einsum("lj,ljd->ld", p, kv[:, :, 8 + 4 * hh: 12 + 4 * hh]) * (
+                np.float32(1) / p.sum(1, keepdims=True))
+        a = _bf16(o)
+        f0 = _mfma(wp[2 * i], a, f0)
+        f1 = _mfma(wp[2 * i + 1], a, f1)
+    feat = _relu_frag(f0) + _relu_frag(f1)
+    outs = []
+    for net in (L["Ext"], L["Ext"] + N["Net"]):
+        w1 = _unpack(blob, net + N["W1"], 16)
+        w2 = _unpack(blob, net + N["W2"], 32)
+        w3 = _unpack(blob, net + N["W3"], 8)
+        nb1 = f32(net + N["B1"], 128).reshape(4, 2, 16)
+        nb2 = f32(net + N["B2"], 128).reshape(4, 2, 16)
+        nb3 = f32(net + N["B3"], 32).reshape(2, 16)
+        h1 = []
+        for t in range(4):
+            c = nb1[t][lane_h]
+            for s in range(4):
+                c = _mfma(w1[t * 4 + s], feat[s], c)
+            h1 += _act(c)
+        h2 = []
+        for t in range(4):
+            c = nb2[t][lane_h]
+            for kk in range(8):
+                c = _mfma(w2[t * 8 + kk], h1[kk], c)
+            h2 += _act(c)
+        c = nb3[lane_h]
+        for kk in range(8):
+            c = _mfma(w3[kk], h2[kk], c)
+        outs.append(c)
+    return outs[0][:32, :4], outs[1][:32, 0]
+
+
+def _random_attn_policy(pol, O, A, seed, scale=0.4):
+    net = pol.ActorCriticAttn(O, A, seed=seed)
+    g = torch.Generator().manual_seed(seed + 1)
+    with torch.no_grad():
+        for p in net.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * (scale if p.dim() > 1 else 0.3))
+    return net, {k: v.detach().clone() for k, v in net.state_dict().items()}
+
+
+@pytest.mark.parametrize("O,A", [(6, 2), (3, 3), (8, 1)])
+def test_attn_pack_layout_matches_mfma_dataflow(pol, O, A):
+    _, sd = _random_attn_policy(pol, O, A, seed=O * 10 + A)
+    blob = pol.pack_attn_policy(sd, O, A)
+    assert blob.size == 140608
+    obs = np.random.default_rng(O + A).normal(0, 1.5, size=(32, O)).astype(np.float32)
+    mean, value = _emulate_attn(blob, obs)
+    ref_mean, ref_value = pol.reference_forward_attn_bf16(sd, obs)
+    # same bf16 roundings; fp32 summation order may flip a rounding boundary
+    np.testing.assert_allclose(mean[:, :A], ref_mean.numpy(), rtol=0, atol=5e-3)
+    np.testing.assert_allclose(value, ref_value.numpy(), rtol=0, atol=5e-3)
+    assert np.median(np.abs(mean[:, :A] - ref_mean.numpy())) < 1e-4
+    assert np.all(mean[:, A:] == 0)
+
+
+@pytest.mark.parametrize("sb3_init", [False, True])
+def test_attn_restatement_vs_fp32_module(pol, sb3_init):
+    """The bf16 restatement (q pre-scale, base-2 softmax, out_proj folded into
+    post_attention_fc) against the plain fp32 module of code/train.py:52-95 under
+    nn.MultiheadAttention: agreement to bf16 accuracy."""
+    if sb3_init:
+        net = pol.ActorCriticAttn(6, 2, seed=3)
+        net.log_std.data.zero_()
+        sd = net.state_dict()
+    else:
+        net, sd = _random_attn_policy(pol, 6, 2, seed=7, scale=0.25)
+    obs = np.random.default_rng(5).normal(0, 1.0, size=(512, 6)).astype(np.float32)
+    with torch.no_grad():
+        m32, v32 = net(torch.from_numpy(obs))
+    mb, vb = pol.reference_forward_attn_bf16(sd, obs)
+    for got, want in ((mb, m32), (vb, v32)):
+        err = (got - want).abs()
+        scale = want.abs().max().item()
+        assert err.max().item() <= 0.03 * scale + 1e-4, (err.max().item(), scale)
+        assert err.mean().item() <= 0.006 * scale + 1e-5
+
+
+def test_attn_state_dict_keys_match_sb3(pol):
+    """The module's state_dict keys are SB3's for code/train.py's policy (the shared
+    extractor under features_extractor.); pi_features_extractor. aliases are accepted."""
+    net = pol.ActorCriticAttn(6, 2, seed=0)
+    sd = net.state_dict()
+    for k in pol.ATTN_FE_KEYS:
+        assert pol.FE + k in sd
+    for k in pol.KEYS:
+        assert k in sd
+    assert pol.is_attention_policy(sd) and not pol.is_attention_policy(
+        pol.ActorCriticMlp(6, 2, seed=0).state_dict())
+    alias = {("pi_" + k if k.startswith(pol.FE) else k): v for k, v in sd.items()}
+    assert np.array_equal(pol.pack_attn_policy(alias, 6, 2), pol.pack_attn_policy(sd, 6, 2))
+    bad = dict(sd)
+    del bad[pol.FE + "attention_layer.in_proj_bias"]
+    with pytest.raises(KeyError):
+        pol.pack_attn_policy(bad, 6, 2)
+    with pytest.raises(ValueError):
+        pol.pack_attn_policy(sd, 6, 3)

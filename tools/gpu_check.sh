@@ -53,6 +53,14 @@ for step in "$@"; do
     policy_prof)
       export TMPDIR=/tmp
       run policy_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/policy_prof -o run --output-format csv -- python bench.py --mode policy --system pmsm --envs 262144 --K 16 --steps 2048 ;;
+    attn_tests) run gpu_attn_tests 600 python -u -m pytest tests/test_gpu_policy_attn.py -v -s -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    attn_bench)
+      run attn_hr_32k_K2048 300 python bench.py --mode policy --policy attn --system hr --envs 32768 --K 2048 --steps 4096
+      run attn_hr_262k_K16 300 python bench.py --mode policy --policy attn --system hr --envs 262144 --K 16 --steps 1024
+      run attn_pmsm_262k_K16 300 python bench.py --mode policy --policy attn --system pmsm --envs 262144 --K 16 --steps 1024 ;;
+    attn_prof)
+      export TMPDIR=/tmp
+      run attn_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/attn_prof -o run --output-format csv -- python bench.py --mode policy --policy attn --system hr --envs 32768 --K 2048 --steps 4096 ;;
     split) run ab_split 600 python tools/ab_split.py 131072 1048576 ;;
     dist2) LZ_BENCH_BACKEND=gloo run dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 500 --warmup 64 --envs 262144 ;;
     pmc)
