@@ -298,6 +298,8 @@ __device__ __forceinline__ void attn_extract(const uint8_t* ext, bf16x8 x, int l
   f32x16 f1 = reinterpret_cast<const f32x16*>(ext + kAttPostB)[2 + h];
 #pragma unroll
   for (int i = 0; i < kAttTokens; ++i) {
+    // token i's two post_fc fragments, issued ahead of the attention math they wait on
+    const bf16x8 wpa = wp[(2 * i) * 64], wpb = wp[(2 * i + 1) * 64];
     const f32x16 q = mfma(wq, tok[i], bq);
     float o[8];
 #pragma unroll
@@ -346,8 +348,8 @@ __device__ __forceinline__ void attn_extract(const uint8_t* ext, bf16x8 x, int l
       a[j] = b[0];
       a[j + 1] = b[1];
     }
-    f0 = mfma(wp[(2 * i) * 64], a, f0);
-    f1 = mfma(wp[(2 * i + 1) * 64], a, f1);
+    f0 = mfma(wpa, a, f0);
+    f1 = mfma(wpb, a, f1);
   }
   feat[0] = relu8<0>(f0);
   feat[1] = relu8<1>(f0);
@@ -396,6 +398,8 @@ __device__ __forceinline__ f32x16 attn_net(const uint8_t* net, const bf16x8* fea
 __device__ __forceinline__ void attn_nets_pair(const uint8_t* na, const uint8_t* nb,
                                                const bf16x8* feat, int lane, f32x16& head_a,
                                                f32x16& head_b) {
+  // weight fragments software-pipelined one tile ahead (as mlp_pair_pipe): with one
+  // wave per SIMD nothing else hides the LDS latency of a tile's loads
   asm volatile("" ::: "memory");
   const int h = lane >> 5;
   const bf16x8* w1a = reinterpret_cast<const bf16x8*>(na + kAttW1) + lane;
@@ -408,42 +412,69 @@ __device__ __forceinline__ void attn_nets_pair(const uint8_t* na, const uint8_t*
   const f32x16* b1b = reinterpret_cast<const f32x16*>(nb + kAttB1) + h;
   const f32x16* b2a = reinterpret_cast<const f32x16*>(na + kAttB2) + h;
   const f32x16* b2b = reinterpret_cast<const f32x16*>(nb + kAttB2) + h;
+  bf16x8 c1a[4], c1b[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) { c1a[s] = w1a[s * 64]; c1b[s] = w1b[s * 64]; }
+  asm volatile("" ::: "memory");
   bf16x8 h1a[8], h1b[8];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
+    bf16x8 n1a[4], n1b[4];
+    if (t < 3) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        n1a[s] = w1a[((t + 1) * 4 + s) * 64];
+        n1b[s] = w1b[((t + 1) * 4 + s) * 64];
+      }
+    }
     f32x16 ca = b1a[2 * t], cb = b1b[2 * t];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      ca = mfma(w1a[(t * 4 + s) * 64], feat[s], ca);
-      cb = mfma(w1b[(t * 4 + s) * 64], feat[s], cb);
+      ca = mfma(c1a[s], feat[s], ca);
+      cb = mfma(c1b[s], feat[s], cb);
     }
     h1a[2 * t] = act8<0>(ca);
     h1b[2 * t] = act8<0>(cb);
     h1a[2 * t + 1] = act8<1>(ca);
     h1b[2 * t + 1] = act8<1>(cb);
+    if (t < 3) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) { c1a[s] = n1a[s]; c1b[s] = n1b[s]; }
+    }
   }
+  bf16x8 cur_a[8], cur_b[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) { cur_a[kk] = w2a[kk * 64]; cur_b[kk] = w2b[kk * 64]; }
+  asm volatile("" ::: "memory");
   head_a = reinterpret_cast<const f32x16*>(na + kAttB3)[h];
   head_b = reinterpret_cast<const f32x16*>(nb + kAttB3)[h];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    asm volatile("" ::: "memory");
-    bf16x8 wfa[8], wfb[8];
+    bf16x8 nxt_a[8], nxt_b[8], h3a[2], h3b[2];
+    if (t < 3) {
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      wfa[kk] = w2a[(t * 8 + kk) * 64];
-      wfb[kk] = w2b[(t * 8 + kk) * 64];
+      for (int kk = 0; kk < 8; ++kk) {
+        nxt_a[kk] = w2a[((t + 1) * 8 + kk) * 64];
+        nxt_b[kk] = w2b[((t + 1) * 8 + kk) * 64];
+      }
     }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) { h3a[q] = w3a[(2 * t + q) * 64]; h3b[q] = w3b[(2 * t + q) * 64]; }
     f32x16 ca = b2a[2 * t], cb = b2b[2 * t];
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      ca = mfma(wfa[kk], h1a[kk], ca);
-      cb = mfma(wfb[kk], h1b[kk], cb);
+      ca = mfma(cur_a[kk], h1a[kk], ca);
+      cb = mfma(cur_b[kk], h1b[kk], cb);
     }
-    head_a = mfma(w3a[(2 * t) * 64], act8<0>(ca), head_a);
-    head_b = mfma(w3b[(2 * t) * 64], act8<0>(cb), head_b);
-    head_a = mfma(w3a[(2 * t + 1) * 64], act8<1>(ca), head_a);
-    head_b = mfma(w3b[(2 * t + 1) * 64], act8<1>(cb), head_b);
+    head_a = mfma(h3a[0], act8<0>(ca), head_a);
+    head_b = mfma(h3b[0], act8<0>(cb), head_b);
+    head_a = mfma(h3a[1], act8<1>(ca), head_a);
+    head_b = mfma(h3b[1], act8<1>(cb), head_b);
+    if (t < 3) {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) { cur_a[kk] = nxt_a[kk]; cur_b[kk] = nxt_b[kk]; }
+    }
   }
 }
 
