@@ -54,10 +54,12 @@ def parse():
                         "vecnorm = VecNormalize(VecEnv).step fused (lz_step_vecnorm + "
                         "lz_vecnorm_apply), 1 GPU")
     p.add_argument("--K", type=int, default=2048, help="rollout length (--mode rollout)")
-    p.add_argument("--policy", choices=["mlp", "attn"], default="mlp",
+    p.add_argument("--policy", choices=["mlp", "attn", "attn_ln"], default="mlp",
                    help="--mode policy: mlp = SB3 MlpPolicy behind VecNormalize (the PMSM A2C "
                         "learner, code/lorenz_pmsm/train.py); attn = code/train.py's PPO policy "
-                        "with the AttentionFeaturesExtractor (no VecNormalize, as there)")
+                        "with the AttentionFeaturesExtractor (no VecNormalize, as there); "
+                        "attn_ln = code/lorenz_filter/train.py's residual + LayerNorm extractor "
+                        "on VecFrameStack(4)")
     p.add_argument("--max-episode-steps", type=int, default=0,
                    help="TimeLimit truncation (auto-reset inside the kernel); 0 = none")
     return p.parse_args()
@@ -283,12 +285,15 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
 
     K = args.K
     O, A = env.obs_dim, env.action_dim
-    attn = args.policy == "attn"
+    attn = args.policy in ("attn", "attn_ln")
+    ln = args.policy == "attn_ln"
+    stack = 4 if ln else 1
     # SB3 init (orthogonal, log_std 0): random weights
-    net = ActorCriticAttn(O, A, seed=0) if attn else ActorCriticMlp(O, A, seed=0)
+    net = (ActorCriticAttn(stack * O, A, seed=0, layer_norm=ln) if attn
+           else ActorCriticMlp(O, A, seed=0))
     rms = None if attn else DeviceRunningMeanStd(O, device)
     col = FusedRolloutCollector(env, net.state_dict(), gamma=0.99, gae_lambda=0.95, obs_rms=rms,
-                                clip_obs=10.0, training=True, bootstrap=True)
+                                clip_obs=10.0, training=True, bootstrap=True, frame_stack=stack)
     stream = torch.cuda.Stream(device)
     with torch.cuda.stream(stream):
         nat.check(nat.lib.lz_set_stream(env._h, ctypes.c_void_p(stream.cuda_stream)))
@@ -330,7 +335,7 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         t = torch.tensor([elapsed, launch_s], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, launch_s = float(t[0]), float(t[1])
-    fl = attn_policy_flops(O, A) if attn else policy_flops(O, A)
+    fl = attn_policy_flops(stack * O, A) if attn else policy_flops(O, A)
     achieved = fl * n * K / launch_s / 1e12
     mangled = {"pmsm": "7SysPMSME", "lorenz3": "5SysL3IfEE", "lorenz4": "5SysL4IfEE",
                "hr": "5SysHRIfEE"}[args.system]
@@ -349,7 +354,12 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         "data": "synthetic: on-device Philox initial states and Gaussian action samples; "
                 "SB3-initialised (orthogonal) random policy weights",
         "config": {
-            "workload": ("%s with code/train.py's PPO actor-critic (AttentionFeaturesExtractor "
+            "workload": ("%s with code/lorenz_filter/train.py's PPO actor-critic on "
+                         "VecFrameStack(4) (attention + residual + LayerNorm extractor, pi/vf "
+                         "[128,128] Tanh): %d-step fused rollout (lz_rollout_policy_attn_stack: "
+                         "frame stack + extractor + nets + sample + clip + env step + bootstrap), "
+                         "GAE (lz_gae); %d envs total, %d per GPU" if ln else
+                         "%s with code/train.py's PPO actor-critic (AttentionFeaturesExtractor "
                          "fc1 + 4-head self-attention over 8 tokens + post_fc 64, then pi/vf "
                          "[128,128] Tanh) in the loop: %d-step fused rollout "
                          "(lz_rollout_policy_attn: extractor + nets + DiagGaussian sample + clip "
@@ -368,7 +378,9 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         "roofline": {
             "bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS, "traffic": None,
-            "kernel": ("_ZN2lz16k_rollout_policyINS_%sLi4ELi32ELi3EEEvNS_5KArgsENS_5PArgsE"
+            "kernel": ("_ZN2lz16k_rollout_policyINS_%sLi4ELi32ELi4ELi4EEEvNS_5KArgsENS_5PArgsE"
+                       if ln else
+                       "_ZN2lz16k_rollout_policyINS_%sLi4ELi32ELi3EEEvNS_5KArgsENS_5PArgsE"
                        if attn else "_ZN2lz16k_rollout_policyINS_%sLi8EEEvNS_5KArgsENS_5PArgsE")
                       % mangled,
             "avg_launch_us": launch_s * 1e6, "flop_per_env_step": fl,

@@ -540,8 +540,23 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
   return LZ_OK;
 }
 
-static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, bool attn) {
+// arch: 0 = MlpPolicy, 1 = attention extractor, 2 = residual + LayerNorm attention on
+// VecFrameStack(n_stack) observations
+static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, int arch,
+                                int n_stack = 1, const float* stack_in = nullptr,
+                                float* stack_out = nullptr) {
   if (!h || !r) return fail(LZ_ERR_INVALID, "handle/args is NULL");
+  const bool attn = arch != 0;
+  if (arch == 2) {
+    if (n_stack != 1 && n_stack != 4) return fail(LZ_ERR_UNSUPPORTED, "n_stack must be 1 or 4");
+    if (!stack_in || !stack_out) return fail(LZ_ERR_INVALID, "stack_in / stack_out must be non-NULL");
+    if (r->obs_norm || r->obs_moments)
+      return fail(LZ_ERR_UNSUPPORTED, "the frame-stacked rollout takes no VecNormalize statistics");
+    const int sys = h->cfg.system;
+    if (sys != LZ_SYS_LORENZ3 && sys != LZ_SYS_PMSM && sys != LZ_SYS_HR)
+      return fail(LZ_ERR_UNSUPPORTED, "the frame-stacked rollout runs LORENZ3 / PMSM / HR");
+    if (n_stack * h->desc.obs_dim > lz::kLnMaxIn) return fail(LZ_ERR_UNSUPPORTED, "stacked obs > 32 dims");
+  }
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_rollout_policy before the first lz_reset");
   if (h->f64) return fail(LZ_ERR_UNSUPPORTED, "the policy rollout runs float32 handles only");
   if (r->K <= 0) return fail(LZ_ERR_INVALID, "K must be >= 1");
@@ -594,8 +609,11 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, b
   p.val = r->val_buf;
   p.last_val = r->last_values;
   p.partials = r->obs_moments ? h->pol_part : nullptr;
-  int e = attn ? lz::launch_rollout_policy_attn(h->cfg.system, a, p, sh, h->stream)
-               : lz::launch_rollout_policy(h->cfg.system, a, p, sh, h->stream);
+  p.stack_in = stack_in;
+  p.stack_out = stack_out;
+  int e = arch == 2 ? lz::launch_rollout_policy_attn_ln(h->cfg.system, n_stack, a, p, sh, h->stream)
+          : attn    ? lz::launch_rollout_policy_attn(h->cfg.system, a, p, sh, h->stream)
+                    : lz::launch_rollout_policy(h->cfg.system, a, p, sh, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "policy rollout launch: %s", hipGetErrorString((hipError_t)e));
   if (r->obs_moments) {
     e = lz::launch_policy_moments_final(h->pol_part, grid * W, 2 * O, (double)r->K * (double)n,
@@ -609,11 +627,16 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, b
 }
 
 lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r) {
-  return rollout_policy(h, r, false);
+  return rollout_policy(h, r, 0);
 }
 
 lz_status lz_rollout_policy_attn(lz_handle* h, const lz_policy_rollout_args* r) {
-  return rollout_policy(h, r, true);
+  return rollout_policy(h, r, 1);
+}
+
+lz_status lz_rollout_policy_attn_stack(lz_handle* h, const lz_policy_rollout_args* r,
+                                       int32_t n_stack, const float* stack_in, float* stack_out) {
+  return rollout_policy(h, r, 2, n_stack, stack_in, stack_out);
 }
 
 int32_t lz_plane_elem_size(const lz_handle* h, int32_t plane) {

@@ -120,6 +120,32 @@ constexpr int kAttPi = kAttExt, kAttVf = kAttExt + kAttNet;
 constexpr int kAttLogStd = kAttExt + 2 * kAttNet;
 constexpr int kAttBlobBytes = kAttLogStd + 64;     // 140608 B (resident in LDS)
 
+// code/lorenz_filter/train.py:54-103's variant of the extractor: the attention output
+// goes through out_proj, a residual connection and LayerNorm(16) per token before
+// post_attention_fc (so out_proj cannot be folded), on VecFrameStack(n_stack) inputs of
+// up to 32 stacked dims (fc1 K = 2 x 16).  Blob (lz_attn_ln_policy_pack):
+//   fc1 [4 tiles][2 k-steps][64] + bias; K|V and Q as kAtt*; out_proj [64] (rows 16-31
+//   zero) + bias [2][16]; LayerNorm weight / bias [2 halves][8] f32 each; post_fc
+//   [8][2][64] (columns in the token-fragment order) + bias [2][2][16]; nets and
+//   log_std as kAtt*.
+constexpr int kLnMaxIn = 32, kLnMaxStack = 4;
+constexpr int kLnFc1W = 0;
+constexpr int kLnFc1B = kLnFc1W + 4 * 2 * 64 * 16;
+constexpr int kLnKvW = kLnFc1B + 4 * 2 * 16 * 4;
+constexpr int kLnKvB = kLnKvW + 64 * 16;
+constexpr int kLnQW = kLnKvB + 2 * 16 * 4;
+constexpr int kLnQB = kLnQW + 64 * 16;
+constexpr int kLnOutW = kLnQB + 2 * 16 * 4;
+constexpr int kLnOutB = kLnOutW + 64 * 16;
+constexpr int kLnGamma = kLnOutB + 2 * 16 * 4;
+constexpr int kLnBeta = kLnGamma + 16 * 4;
+constexpr int kLnPostW = kLnBeta + 16 * 4;
+constexpr int kLnPostB = kLnPostW + kAttTokens * 2 * 64 * 16;
+constexpr int kLnExt = kLnPostB + 2 * 2 * 16 * 4;   // 28928 B
+constexpr int kLnPi = kLnExt, kLnVf = kLnExt + kAttNet;
+constexpr int kLnLogStd = kLnExt + 2 * kAttNet;
+constexpr int kLnBlobBytes = kLnLogStd + 64;       // 145984 B (resident in LDS)
+
 struct PArgs {
   const uint8_t* blob;     // device copy of the packed policy
   const float* obs_in;     // [N, O] raw observation at rollout start
@@ -134,6 +160,8 @@ struct PArgs {
   float* val;              // [K, N]
   float* last_val;         // [N]
   double* partials;        // [grid * waves][2 * O] obs moment partials (nullable)
+  const float* stack_in;   // kPair 4: [N, n_stack * O] VecFrameStack obs at rollout start
+  float* stack_out;        // kPair 4: [N, n_stack * O] after the K steps
 };
 
 // lz_rms internals for the fused VecNormalize step (lz_rms.hip)
@@ -193,6 +221,10 @@ int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, const PolS
 PolShape attn_policy_shape(int64_t n, int num_cus);
 int launch_rollout_policy_attn(int system, const KArgs& a, const PArgs& p, const PolShape& sh,
                                void* stream);
+// the residual + LayerNorm extractor on VecFrameStack(n_stack) obs (kLn* blob);
+// n_stack 1 or 4, same shape as attn_policy_shape
+int launch_rollout_policy_attn_ln(int system, int n_stack, const KArgs& a, const PArgs& p,
+                                  const PolShape& sh, void* stream);
 int launch_policy_moments_final(const double* partials, int nparts, int width, double count,
                                 double* out, void* stream);
 

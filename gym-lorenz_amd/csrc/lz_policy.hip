@@ -33,6 +33,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 #include "lz_body.h"
 #include "lz_internal.h"
@@ -393,6 +394,143 @@ __device__ __forceinline__ f32x16 attn_net(const uint8_t* net, const bf16x8* fea
   return head;
 }
 
+// code/lorenz_filter/train.py:54-103: the same extractor with out_proj, a residual
+// connection and LayerNorm(16) per token before post_attention_fc, on up to 32 stacked
+// input dims (VecFrameStack): fc1 is KS k-steps of 16.  Per query token i: attention
+// as attn_extract, out_proj (one MFMA: rows 0-15 = W_out, so registers 0..7 of lane
+// half h hold the token dims (g&3) + 8(g>>2) + 4h -- exactly the order of the token's
+// own fragment, so the residual adds register to register), LayerNorm over the 16
+// dims (8 per half, the two halves' partial sums exchanged with a lane-32 swap), the
+// affine, bf16, and post_fc's two MFMAs.  The residual uses the bf16 token values the
+// projections consumed (the torch restatement does the same).
+template <int KS>
+__device__ __forceinline__ void attn_ln_extract(const uint8_t* ext, const bf16x8* x, int lane,
+                                                bf16x8* feat) {
+  asm volatile("" ::: "memory");
+  const int h = lane >> 5;
+  const bf16x8* w1 = reinterpret_cast<const bf16x8*>(ext + kLnFc1W) + lane;
+  const f32x16* b1 = reinterpret_cast<const f32x16*>(ext + kLnFc1B) + h;
+  bf16x8 tok[kAttTokens];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x16 c = b1[2 * t];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) c = mfma(w1[(t * 2 + s) * 64], x[s], c);
+    tok[2 * t] = relu8<0>(c);
+    tok[2 * t + 1] = relu8<1>(c);
+  }
+  const bf16x8 wkv = reinterpret_cast<const bf16x8*>(ext + kLnKvW)[lane];
+  const f32x16 bkv = reinterpret_cast<const f32x16*>(ext + kLnKvB)[h];
+  f32x16 kv[kAttTokens];
+#pragma unroll
+  for (int t = 0; t < kAttTokens; ++t) kv[t] = mfma(wkv, tok[t], bkv);
+  const bf16x8 wq = reinterpret_cast<const bf16x8*>(ext + kLnQW)[lane];
+  const f32x16 bq = reinterpret_cast<const f32x16*>(ext + kLnQB)[h];
+  const bf16x8 wo = reinterpret_cast<const bf16x8*>(ext + kLnOutW)[lane];
+  const f32x16 bo = reinterpret_cast<const f32x16*>(ext + kLnOutB)[h];
+  const float* gam = reinterpret_cast<const float*>(ext + kLnGamma) + 8 * h;
+  const float* bet = reinterpret_cast<const float*>(ext + kLnBeta) + 8 * h;
+  const bf16x8* wp = reinterpret_cast<const bf16x8*>(ext + kLnPostW) + lane;
+  f32x16 f0 = reinterpret_cast<const f32x16*>(ext + kLnPostB)[h];
+  f32x16 f1 = reinterpret_cast<const f32x16*>(ext + kLnPostB)[2 + h];
+#pragma unroll
+  for (int i = 0; i < kAttTokens; ++i) {
+    const bf16x8 wpa = wp[(2 * i) * 64], wpb = wp[(2 * i + 1) * 64];
+    const f32x16 q = mfma(wq, tok[i], bq);
+    float o[8];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const f32x2 q01 = {q[4 * hh], q[4 * hh + 1]}, q23 = {q[4 * hh + 2], q[4 * hh + 3]};
+      float sc[kAttTokens];
+      float m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < kAttTokens; ++j) {
+        const f32x2 k01 = {kv[j][4 * hh], kv[j][4 * hh + 1]};
+        const f32x2 k23 = {kv[j][4 * hh + 2], kv[j][4 * hh + 3]};
+        const f32x2 t = __builtin_elementwise_fma(q23, k23, q01 * k01);
+        sc[j] = t[0] + t[1];
+        m = fmaxf(m, sc[j]);
+      }
+      float sum = 0.0f;
+      f32x2 o01, o23;
+#pragma unroll
+      for (int j = 0; j < kAttTokens; ++j) {
+        const float pj = __builtin_amdgcn_exp2f(sc[j] - m);
+        sum = j == 0 ? pj : sum + pj;
+        const f32x2 pp = {pj, pj};
+        const f32x2 v01 = {kv[j][8 + 4 * hh], kv[j][9 + 4 * hh]};
+        const f32x2 v23 = {kv[j][10 + 4 * hh], kv[j][11 + 4 * hh]};
+        o01 = j == 0 ? pp * v01 : __builtin_elementwise_fma(pp, v01, o01);
+        o23 = j == 0 ? pp * v23 : __builtin_elementwise_fma(pp, v23, o23);
+      }
+      const float rs = __builtin_amdgcn_rcpf(sum);
+      const f32x2 rr = {rs, rs};
+      o01 = o01 * rr;
+      o23 = o23 * rr;
+      o[4 * hh] = o01[0];
+      o[4 * hh + 1] = o01[1];
+      o[4 * hh + 2] = o23[0];
+      o[4 * hh + 3] = o23[1];
+    }
+    bf16x8 a;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 t = {o[j], o[j + 1]};
+      const bf16x2 b = __builtin_convertvector(t, bf16x2);
+      a[j] = b[0];
+      a[j + 1] = b[1];
+    }
+    const f32x16 y = mfma(wo, a, bo);  // out_proj
+    float z[8];
+    float s1 = 0.0f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      z[g] = y[g] + (float)tok[i][g];  // residual
+      s1 = g == 0 ? z[g] : s1 + z[g];
+    }
+    s1 = s1 + __shfl_xor(s1, 32, 64);
+    const float mean = s1 * 0.0625f;
+    float s2 = 0.0f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      z[g] = z[g] - mean;
+      s2 = g == 0 ? z[g] * z[g] : s2 + z[g] * z[g];
+    }
+    s2 = s2 + __shfl_xor(s2, 32, 64);
+    const float r = __builtin_amdgcn_rsqf(s2 * 0.0625f + 1e-5f);  // LayerNorm eps 1e-5
+    bf16x8 u;
+#pragma unroll
+    for (int g = 0; g < 8; g += 2) {
+      const f32x2 t = {(z[g] * r) * gam[g] + bet[g], (z[g + 1] * r) * gam[g + 1] + bet[g + 1]};
+      const bf16x2 b = __builtin_convertvector(t, bf16x2);
+      u[g] = b[0];
+      u[g + 1] = b[1];
+    }
+    f0 = mfma(wpa, u, f0);
+    f1 = mfma(wpb, u, f1);
+  }
+  feat[0] = relu8<0>(f0);
+  feat[1] = relu8<1>(f0);
+  feat[2] = relu8<0>(f1);
+  feat[3] = relu8<1>(f1);
+}
+
+// the KS fc1 B fragments of a VecFrameStack obs of SO dims held by both lane halves:
+// k-step s, half h, element j = stacked dim 16s + 8h + j (zero past SO or if !use)
+template <int SO, int KS>
+__device__ __forceinline__ void stack_frags(const float* st, int h, bool use, bf16x8* xs) {
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d0 = 16 * s + j, d1 = 16 * s + 8 + j;
+      const float v0 = d0 < SO ? st[d0 < SO ? d0 : 0] : 0.0f;
+      const float v1 = d1 < SO ? st[d1 < SO ? d1 : 0] : 0.0f;
+      xs[s][j] = (__bf16)(use ? (h ? v1 : v0) : 0.0f);
+    }
+  }
+}
+
 // pi and vf nets on the same features, interleaved layer by layer (two independent
 // MFMA / tanh chains for the one-wave-per-SIMD shape)
 __device__ __forceinline__ void attn_nets_pair(const uint8_t* na, const uint8_t* nb,
@@ -550,16 +688,22 @@ __device__ __forceinline__ void value_fwd(const uint8_t* blob, const uint8_t* vf
 // kPair: 0 = the nets one after the other, 1 = interleaved (mlp_pair),
 // 2 = interleaved + pipelined weight loads (mlp_pair_pipe), 3 = the attention-extractor
 // actor-critic (kAtt* blob: attn_extract + attn_nets_pair)
-template <class Sys, int W, int E, int kPair>
+// 4 = the residual + LayerNorm attention actor-critic on VecFrameStack(S) observations
+// (kLn* blob: attn_ln_extract + attn_nets_pair; the S-frame stack lives in the
+// registers of both lane halves of the env)
+template <class Sys, int W, int E, int kPair, int S = 1>
 __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   static_assert(!kPair || E == 32, "the interleaved pair runs 32-env tiles");
-  constexpr int kBlob = kPair == 3 ? kAttBlobBytes : kPolBlobBytes;
+  constexpr int kBlob = kPair == 4 ? kLnBlobBytes : kPair == 3 ? kAttBlobBytes : kPolBlobBytes;
   constexpr int O = Sys::O, A = Sys::A;
+  constexpr int SO = S * O, KS = (SO + 15) / 16;  // kPair 4: stacked dims, fc1 k-steps
+  static_assert(kPair == 4 || S == 1, "frame stacking is the kPair 4 path");
+  static_assert(SO <= kLnMaxIn, "stacked obs dims");
   static_assert(O <= kPolMaxObs && A <= kPolMaxAct, "policy tile shape");
   static_assert(E == 32 || E == 64, "envs per wave");
   __shared__ __attribute__((aligned(64))) uint8_t s_blob[kBlob];
   __shared__ double s_norm[2 * kPolMaxObs];
-  __shared__ double s_mom[W * E * 2 * O];
+  __shared__ double s_mom[kPair == 4 ? 1 : W * E * 2 * O];  // kPair 4: no obs moments
   const int tid = (int)threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int slot = E == 64 ? lane : (lane & 31);  // this lane's env within the tile
@@ -579,12 +723,13 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
     *a.tick_out = tick + a.tick_adv;
   }
   __syncthreads();
-  const uint8_t* pi_net = s_blob + (kPair == 3 ? kAttPi : 0);
-  const uint8_t* vf_net = s_blob + (kPair == 3 ? kAttVf : kPolNet);
+  const uint8_t* pi_net = s_blob + (kPair == 4 ? kLnPi : kPair == 3 ? kAttPi : 0);
+  const uint8_t* vf_net = s_blob + (kPair == 4 ? kLnVf : kPair == 3 ? kAttVf : kPolNet);
   // torch.distributions.Normal constants, computed by the packer: scale = exp(log_std),
   // 2 * scale**2, log(scale) (LDS, wave-uniform broadcast reads)
   const float* g_scale =
-      reinterpret_cast<const float*>(s_blob + (kPair == 3 ? kAttLogStd : kPolLogStd)) + 4;
+      reinterpret_cast<const float*>(
+          s_blob + (kPair == 4 ? kLnLogStd : kPair == 3 ? kAttLogStd : kPolLogStd)) + 4;
   const float* g_var2 = g_scale + 4;
   const float* g_lscale = g_scale + 8;
   const bool norm = p.norm != nullptr;
@@ -594,10 +739,12 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   const bool boot = (p.pflags & LZ_POLICY_BOOTSTRAP) != 0;
   const float gamma = p.gamma;
   // per-lane float64 obs-moment accumulators of the env-owning lanes, in LDS
-  double* mom = s_mom + (wave * E + slot) * (2 * O);
-  if (owner) {
+  double* mom = s_mom + (kPair == 4 ? 0 : (wave * E + slot) * (2 * O));
+  if constexpr (kPair != 4) {
+    if (owner) {
 #pragma unroll
-    for (int j = 0; j < 2 * O; ++j) mom[j] = 0.0;
+      for (int j = 0; j < 2 * O; ++j) mom[j] = 0.0;
+    }
   }
 
   Sys sys;
@@ -619,6 +766,12 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
 #pragma unroll
       for (int j = 0; j < O; ++j) o[j] = p.obs_in[i * O + j];
     }
+    const bool valid = i < a.n;  // kPair 4: both halves of the env's lanes
+    float st[kPair == 4 ? SO : 1];
+    if constexpr (kPair == 4) {
+#pragma unroll
+      for (int j = 0; j < SO; ++j) st[j] = valid ? p.stack_in[i * SO + j] : 0.0f;
+    }
     // settle the tile's loads (state planes, obs_in) here: otherwise
     // hipcc places their first-use waits inside the step loop, where a vmcnt(0) also
     // drains every store of the previous step -- a store round trip per step
@@ -626,13 +779,29 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
     for (int k = 0; k < a.K; ++k) {
       const int64_t off = (int64_t)k * a.n + i;
       float x[O];
-      normalize<O>(o, x, norm, mu, sd, p.clip);
-      if (live) {  // the observation the policy sees (SB3 rollout_buffer.add(_last_obs))
+      if constexpr (kPair == 4) {
+        if (live) {  // the stacked observation the policy sees
 #pragma unroll
-        for (int j = 0; j < O; ++j) obs_buf[off * O + j] = x[j];
+          for (int j = 0; j < SO; ++j) obs_buf[off * SO + j] = st[j];
+        }
+      } else {
+        normalize<O>(o, x, norm, mu, sd, p.clip);
+        if (live) {  // the observation the policy sees (SB3 rollout_buffer.add(_last_obs))
+#pragma unroll
+          for (int j = 0; j < O; ++j) obs_buf[off * O + j] = x[j];
+        }
       }
       float mean[A], val[1];
-      if constexpr (kPair == 3) {
+      if constexpr (kPair == 4) {
+        f32x16 hp, hv;
+        bf16x8 xs[KS], f[4];
+        stack_frags<SO, KS>(st, h, valid, xs);
+        attn_ln_extract<KS>(s_blob, xs, lane, f);
+        attn_nets_pair(pi_net, vf_net, f, lane, hp, hv);
+#pragma unroll
+        for (int j = 0; j < A; ++j) mean[j] = hp[j];
+        val[0] = hv[0];
+      } else if constexpr (kPair == 3) {
         f32x16 hp, hv;
         bf16x8 f[4];
         attn_extract(s_blob, obs_frag<O>(x, live), lane, f);
@@ -678,7 +847,39 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
                                                            tick + (uint64_t)k, k, on, rew,
                                                            did_reset, ot);
       any_reset = any_reset || did_reset;
-      if (boot) {  // SB3: truncated (not terminated) -> rewards += gamma * V(terminal obs)
+      if constexpr (kPair == 4) {
+        // VecFrameStack (SB3 StackedObservations.update): the partner half receives the
+        // env's new / terminal frames and done byte; both halves roll the stack; a done
+        // env's terminal observation is [rolled stack, terminal frame], its stack
+        // restarts from zeros; the new frame goes last
+        const int src = lane & 31;
+        const uint8_t db = (uint8_t)__shfl((int)df, src, 64);
+        float nb[O], tb[O];
+#pragma unroll
+        for (int j = 0; j < O; ++j) {
+          nb[j] = __shfl(on[j], src, 64);
+          tb[j] = __shfl(ot[j], src, 64);
+        }
+        float stt[SO];
+#pragma unroll
+        for (int j = 0; j < SO - O; ++j) stt[j] = st[j + O];
+#pragma unroll
+        for (int j = 0; j < O; ++j) stt[SO - O + j] = tb[j];
+        if (boot) {
+          const bool bt = valid && (db & LZ_DONE_TRUNCATED) && !(db & LZ_DONE_TERMINATED);
+          if (__ballot(bt) != 0ull) {
+            bf16x8 xs[KS], f[4];
+            stack_frags<SO, KS>(stt, h, bt, xs);
+            attn_ln_extract<KS>(s_blob, xs, lane, f);
+            const float vt = attn_net(vf_net, f, lane)[0];
+            if (bt) rew = rew + gamma * vt;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < SO - O; ++j) st[j] = db ? 0.0f : stt[j];
+#pragma unroll
+        for (int j = 0; j < O; ++j) st[SO - O + j] = nb[j];
+      } else if (boot) {  // SB3: truncated (not terminated) -> rewards += gamma * V(terminal obs)
         const bool bt = live && (df & LZ_DONE_TRUNCATED) && !(df & LZ_DONE_TERMINATED);
         if (__ballot(bt) != 0ull) {  // wave-uniform branch
           float xt[O], vt[1];
@@ -690,7 +891,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       if (live) {
         rew_buf[off] = rew;
         a.done[off] = df;
-        if (p.partials) {
+        if (kPair != 4 && p.partials) {
 #pragma unroll
           for (int j = 0; j < O; ++j) {
             const double v = (double)on[j];
@@ -702,9 +903,21 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
 #pragma unroll
       for (int j = 0; j < O; ++j) o[j] = on[j];
     }
-    float x[O], vl[1];
-    normalize<O>(o, x, norm, mu, sd, p.clip);
-    value_fwd<E, O, kPair>(s_blob, vf_net, x, live, lane, vl);
+    float vl[1];
+    if constexpr (kPair == 4) {
+      bf16x8 xs[KS], f[4];
+      stack_frags<SO, KS>(st, h, valid, xs);
+      attn_ln_extract<KS>(s_blob, xs, lane, f);
+      vl[0] = attn_net(vf_net, f, lane)[0];
+      if (live) {
+#pragma unroll
+        for (int j = 0; j < SO; ++j) p.stack_out[i * SO + j] = st[j];
+      }
+    } else {
+      float x[O];
+      normalize<O>(o, x, norm, mu, sd, p.clip);
+      value_fwd<E, O, kPair>(s_blob, vf_net, x, live, lane, vl);
+    }
     if (live) {
       p.last_val[i] = vl[0];
 #pragma unroll
@@ -714,7 +927,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
     }
   }
-  if (p.partials) {  // fixed-order butterfly over the wave: deterministic for a given grid
+  if (kPair != 4 && p.partials) {  // fixed-order butterfly over the wave: deterministic
     double* dst = p.partials + ((int64_t)blockIdx.x * W + wave) * (2 * O);
 #pragma unroll
     for (int j = 0; j < 2 * O; ++j) {
@@ -829,6 +1042,27 @@ int launch_rollout_policy_attn(int system, const KArgs& a, const PArgs& p, const
   return (int)hipErrorInvalidValue;
 }
 
+template <class Sys>
+static int launch_pol_attn_ln(int n_stack, const KArgs& a, const PArgs& p, const PolShape& sh,
+                              hipStream_t s) {
+  const dim3 grid((unsigned)sh.grid), block(4 * 64);
+  if (n_stack == 4) hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, 4, 4>), grid, block, 0, s, a, p);
+  else if (n_stack == 1) hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, 4, 1>), grid, block, 0, s, a, p);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+int launch_rollout_policy_attn_ln(int system, int n_stack, const KArgs& a, const PArgs& p,
+                                  const PolShape& grid, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (system) {  // the reference's frame-stacked learner is HR (lorenz_filter/train.py)
+    case LZ_SYS_LORENZ3: return launch_pol_attn_ln<SysL3<float>>(n_stack, a, p, grid, s);
+    case LZ_SYS_PMSM: return launch_pol_attn_ln<SysPMSM>(n_stack, a, p, grid, s);
+    case LZ_SYS_HR: return launch_pol_attn_ln<SysHR<float>>(n_stack, a, p, grid, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
 int launch_policy_moments_final(const double* partials, int nparts, int width, double count,
                                 double* out, void* stream) {
   hipLaunchKernelGGL(k_pol_moments_final, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream),
@@ -912,50 +1146,78 @@ inline int q_row(int r) {
   return grp < 2 ? 4 * (2 * h + grp) + d : -1;
 }
 
-void pack_attn(uint8_t* b, const lz_attn_policy* p) {
+// token dim held by element j of lane half h of a relu8 token fragment
+inline int tok_dim(int h, int j) { return (j & 3) + 8 * (j >> 2) + 4 * h; }
+
+// The attention actor-critics.  ln_w == nullptr: code/train.py's extractor (kAtt*
+// layout, out_proj folded into post_fc, obs_dim <= 8); otherwise code/lorenz_filter/
+// train.py's residual + LayerNorm extractor (kLn* layout, fc1 over <= 32 stacked dims).
+void pack_attn(uint8_t* b, const lz_attn_policy* p, const float* ln_w, const float* ln_b) {
   using lz::kPolHidden;
-  const int O = p->obs_dim;
-  uint16_t* f1 = reinterpret_cast<uint16_t*>(b + lz::kAttFc1W);
-  uint16_t* fkv = reinterpret_cast<uint16_t*>(b + lz::kAttKvW);
-  uint16_t* fq = reinterpret_cast<uint16_t*>(b + lz::kAttQW);
-  uint16_t* fp = reinterpret_cast<uint16_t*>(b + lz::kAttPostW);
-  float* c1 = reinterpret_cast<float*>(b + lz::kAttFc1B);
-  float* ckv = reinterpret_cast<float*>(b + lz::kAttKvB);
-  float* cq = reinterpret_cast<float*>(b + lz::kAttQB);
-  float* cp = reinterpret_cast<float*>(b + lz::kAttPostB);
-  // out_proj folded into post_attention_fc (float64): per token i
-  //   Wf_i = W_post[:, 16i:16i+16] W_out,  b_f = b_post + sum_i W_post[:, 16i:16i+16] b_out
+  const bool ln = ln_w != nullptr;
+  const int I = p->obs_dim;
+  uint16_t* f1 = reinterpret_cast<uint16_t*>(b + (ln ? lz::kLnFc1W : lz::kAttFc1W));
+  uint16_t* fkv = reinterpret_cast<uint16_t*>(b + (ln ? lz::kLnKvW : lz::kAttKvW));
+  uint16_t* fq = reinterpret_cast<uint16_t*>(b + (ln ? lz::kLnQW : lz::kAttQW));
+  uint16_t* fp = reinterpret_cast<uint16_t*>(b + (ln ? lz::kLnPostW : lz::kAttPostW));
+  float* c1 = reinterpret_cast<float*>(b + (ln ? lz::kLnFc1B : lz::kAttFc1B));
+  float* ckv = reinterpret_cast<float*>(b + (ln ? lz::kLnKvB : lz::kAttKvB));
+  float* cq = reinterpret_cast<float*>(b + (ln ? lz::kLnQB : lz::kAttQB));
+  float* cp = reinterpret_cast<float*>(b + (ln ? lz::kLnPostB : lz::kAttPostB));
   static_assert(lz::kAttTokens * lz::kAttTokDim == kPolHidden, "token split");
-  double wf[lz::kAttTokens][lz::kAttFeat][lz::kAttTokDim];
+  // post_fc per token i: folded with out_proj (code/train.py, float64)
+  //   Wf_i = W_post[:, 16i:16i+16] W_out,  b_f = b_post + sum_i W_post[:, 16i:16i+16] b_out
+  // or, after the LayerNorm (lorenz_filter), W_post[:, 16i + tok_dim] itself
+  std::vector<double> wf_buf((size_t)lz::kAttTokens * lz::kAttFeat * lz::kAttTokDim);
+  auto wf = reinterpret_cast<double (*)[lz::kAttFeat][lz::kAttTokDim]>(wf_buf.data());
   double bfold[lz::kAttFeat];
   for (int f = 0; f < lz::kAttFeat; ++f) {
     double acc = p->post_b[f];
     for (int i = 0; i < lz::kAttTokens; ++i)
       for (int d = 0; d < lz::kAttTokDim; ++d) {
         double w = 0.0;
-        for (int e = 0; e < lz::kAttTokDim; ++e)
-          w += (double)p->post_w[f * kPolHidden + 16 * i + e] * (double)p->out_proj_w[e * 16 + d];
+        if (ln) {
+          w = p->post_w[f * kPolHidden + 16 * i + d];
+        } else {
+          for (int e = 0; e < lz::kAttTokDim; ++e)
+            w += (double)p->post_w[f * kPolHidden + 16 * i + e] * (double)p->out_proj_w[e * 16 + d];
+        }
         wf[i][f][d] = w;
       }
-    for (int i = 0; i < lz::kAttTokens; ++i)
-      for (int e = 0; e < lz::kAttTokDim; ++e)
-        acc += (double)p->post_w[f * kPolHidden + 16 * i + e] * (double)p->out_proj_b[e];
+    if (!ln)
+      for (int i = 0; i < lz::kAttTokens; ++i)
+        for (int e = 0; e < lz::kAttTokDim; ++e)
+          acc += (double)p->post_w[f * kPolHidden + 16 * i + e] * (double)p->out_proj_b[e];
     bfold[f] = acc;
   }
   for (int lane = 0; lane < 64; ++lane) {
     const int r = lane & 31, h = lane >> 5;
     for (int j = 0; j < 8; ++j) {
-      const int k = 8 * h + j;                              // natural k (obs, head outputs)
-      const int td = (j & 3) + 8 * (j >> 2) + 4 * h;        // token dim of a relu8 fragment
-      for (int t = 0; t < 4; ++t)
-        f1[(t * 64 + lane) * 8 + j] = bf16_rne(k < O ? p->fc1_w[(32 * t + r) * O + k] : 0.0f);
+      const int k = 8 * h + j;       // natural k (obs, head outputs)
+      const int td = tok_dim(h, j);  // token dim of a relu8 / LayerNorm fragment
+      for (int t = 0; t < 4; ++t) {
+        if (ln) {
+          for (int s = 0; s < 2; ++s) {
+            const int kk = 16 * s + k;  // stacked input dim
+            f1[((t * 2 + s) * 64 + lane) * 8 + j] =
+                bf16_rne(kk < I ? p->fc1_w[(32 * t + r) * I + kk] : 0.0f);
+          }
+        } else {
+          f1[(t * 64 + lane) * 8 + j] = bf16_rne(k < I ? p->fc1_w[(32 * t + r) * I + k] : 0.0f);
+        }
+      }
       fkv[lane * 8 + j] = bf16_rne(p->in_proj_w[kv_row(r) * 16 + td]);
       const int qr = q_row(r);
       fq[lane * 8 + j] =
           bf16_rne(qr < 0 ? 0.0f : (float)(kAttQScale * (double)p->in_proj_w[qr * 16 + td]));
       for (int i = 0; i < lz::kAttTokens; ++i)
         for (int T = 0; T < 2; ++T)
-          fp[((2 * i + T) * 64 + lane) * 8 + j] = bf16_rne((float)wf[i][32 * T + r][k]);
+          fp[((2 * i + T) * 64 + lane) * 8 + j] =
+              bf16_rne((float)wf[i][32 * T + r][ln ? td : k]);
+      if (ln) {  // out_proj: rows 0-15 = W_out, natural k (the head outputs)
+        uint16_t* fo = reinterpret_cast<uint16_t*>(b + lz::kLnOutW);
+        fo[lane * 8 + j] = bf16_rne(r < 16 ? p->out_proj_w[r * 16 + k] : 0.0f);
+      }
     }
   }
   for (int h = 0; h < 2; ++h)
@@ -965,6 +1227,14 @@ void pack_attn(uint8_t* b, const lz_attn_policy* p) {
       ckv[h * 16 + g] = p->in_proj_b[kv_row(r)];
       cq[h * 16 + g] = q_row(r) < 0 ? 0.0f : (float)(kAttQScale * (double)p->in_proj_b[q_row(r)]);
       for (int T = 0; T < 2; ++T) cp[(2 * T + h) * 16 + g] = (float)bfold[32 * T + r];
+      if (ln) {
+        float* co = reinterpret_cast<float*>(b + lz::kLnOutB);
+        co[h * 16 + g] = r < 16 ? p->out_proj_b[r] : 0.0f;
+        if (g < 8) {
+          reinterpret_cast<float*>(b + lz::kLnGamma)[h * 8 + g] = ln_w[tok_dim(h, g)];
+          reinterpret_cast<float*>(b + lz::kLnBeta)[h * 8 + g] = ln_b[tok_dim(h, g)];
+        }
+      }
     }
   // the two [128,128] Tanh nets: layer 1 reads the 64 features as 4 k-steps of relu8
   // fragments (feature unit_of(s, h, j)); layers 2 and 3 as in pack_net
@@ -976,7 +1246,7 @@ void pack_attn(uint8_t* b, const lz_attn_policy* p) {
   const float* B3[2] = {p->act_b, p->val_b};
   const int rows3[2] = {p->act_dim, 1};
   for (int n = 0; n < 2; ++n) {
-    uint8_t* net = b + (n == 0 ? lz::kAttPi : lz::kAttVf);
+    uint8_t* net = b + (ln ? (n == 0 ? lz::kLnPi : lz::kLnVf) : (n == 0 ? lz::kAttPi : lz::kAttVf));
     uint16_t* g1 = reinterpret_cast<uint16_t*>(net + lz::kAttW1);
     uint16_t* g2 = reinterpret_cast<uint16_t*>(net + lz::kAttW2);
     uint16_t* g3 = reinterpret_cast<uint16_t*>(net + lz::kAttW3);
@@ -1065,8 +1335,29 @@ lz_status lz_attn_policy_pack(const lz_attn_policy* p, void* host_blob, int64_t 
     if (!q) return pfail(LZ_ERR_INVALID, "a policy weight pointer is NULL");
   uint8_t* b = static_cast<uint8_t*>(host_blob);
   std::memset(b, 0, lz::kAttBlobBytes);
-  pack_attn(b, p);
+  pack_attn(b, p, nullptr, nullptr);
   pack_gauss(reinterpret_cast<float*>(b + lz::kAttLogStd), p->act_dim, p->log_std);
+  return LZ_OK;
+}
+
+int64_t lz_attn_ln_policy_blob_bytes(void) { return lz::kLnBlobBytes; }
+
+lz_status lz_attn_ln_policy_pack(const lz_attn_ln_policy* q, void* host_blob, int64_t cap) {
+  if (!q || !host_blob) return pfail(LZ_ERR_INVALID, "policy/blob is NULL");
+  if (cap < lz::kLnBlobBytes) return pfail(LZ_ERR_INVALID, "blob capacity too small");
+  const lz_attn_policy* p = &q->attn;
+  if (p->obs_dim < 1 || p->obs_dim > lz::kLnMaxIn || p->act_dim < 1 || p->act_dim > lz::kPolMaxAct)
+    return pfail(LZ_ERR_UNSUPPORTED, "policy supports input dims 1..32 and act_dim 1..4");
+  const float* req[] = {p->fc1_w, p->fc1_b, p->in_proj_w, p->in_proj_b, p->out_proj_w,
+                        p->out_proj_b, p->post_w, p->post_b, p->pi_w1, p->pi_b1, p->pi_w2,
+                        p->pi_b2, p->vf_w1, p->vf_b1, p->vf_w2, p->vf_b2, p->act_w, p->act_b,
+                        p->val_w, p->val_b, p->log_std, q->ln_w, q->ln_b};
+  for (const float* r : req)
+    if (!r) return pfail(LZ_ERR_INVALID, "a policy weight pointer is NULL");
+  uint8_t* b = static_cast<uint8_t*>(host_blob);
+  std::memset(b, 0, lz::kLnBlobBytes);
+  pack_attn(b, p, q->ln_w, q->ln_b);
+  pack_gauss(reinterpret_cast<float*>(b + lz::kLnLogStd), p->act_dim, p->log_std);
   return LZ_OK;
 }
 

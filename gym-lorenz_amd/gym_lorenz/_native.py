@@ -85,6 +85,10 @@ class LzAttnPolicy(ctypes.Structure):
             "act_w", "act_b", "val_w", "val_b", "log_std")]
 
 
+class LzAttnLnPolicy(ctypes.Structure):
+    _fields_ = [("attn", LzAttnPolicy), ("ln_w", ctypes.c_void_p), ("ln_b", ctypes.c_void_p)]
+
+
 class LzPolicyRolloutArgs(ctypes.Structure):
     _fields_ = [
         ("K", ctypes.c_int32),
@@ -167,6 +171,10 @@ _SIGS = {
     "lz_attn_policy_blob_bytes": (ctypes.c_int64, []),
     "lz_attn_policy_pack": (ctypes.c_int, [ctypes.POINTER(LzAttnPolicy), VP, ctypes.c_int64]),
     "lz_rollout_policy_attn": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
+    "lz_attn_ln_policy_blob_bytes": (ctypes.c_int64, []),
+    "lz_attn_ln_policy_pack": (ctypes.c_int, [ctypes.POINTER(LzAttnLnPolicy), VP, ctypes.c_int64]),
+    "lz_rollout_policy_attn_stack": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs),
+                                                    ctypes.c_int32, VP, VP]),
     "lz_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, ctypes.c_double,
                               ctypes.c_double, VP, VP, ctypes.c_int32, VP]),
     "lz_frame_stack": (ctypes.c_int, [VP, VP, VP, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,

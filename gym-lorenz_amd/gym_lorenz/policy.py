@@ -110,6 +110,23 @@ class AttentionFeaturesExtractor(nn.Module):
         return self.post_attention_fc(attn_output.reshape(-1, self.hidden_dim))
 
 
+class AttentionFeaturesExtractorLN(AttentionFeaturesExtractor):
+    """code/lorenz_filter/train.py:54-103: the same extractor with a residual connection
+    and LayerNorm(16) per token after the attention (x_seq = layer_norm(x_seq +
+    attn_output)) before post_attention_fc; used there on VecFrameStack(n_stack=4)."""
+
+    def __init__(self, obs_dim, features_dim=64):
+        super().__init__(obs_dim, features_dim)
+        self.layer_norm = nn.LayerNorm(self.token_dim)
+
+    def forward(self, observations):
+        x = torch.relu(self.fc1(observations))
+        x_seq = x.view(-1, self.seq_len, self.token_dim)
+        attn_output, _ = self.attention_layer(x_seq, x_seq, x_seq)
+        x_seq = self.layer_norm(x_seq + attn_output)
+        return self.post_attention_fc(x_seq.reshape(-1, self.hidden_dim))
+
+
 class ActorCriticAttn(nn.Module):
     """SB3 ActorCriticPolicy as code/train.py:101-112 builds it: the shared
     AttentionFeaturesExtractor (features_dim=64), net_arch pi=[128,128] vf=[128,128]
@@ -118,12 +135,13 @@ class ActorCriticAttn(nn.Module):
     nn.Linear modules only, so in_proj keeps torch's xavier init)."""
 
     def __init__(self, obs_dim, act_dim, features_dim=64, hidden=HIDDEN, log_std_init=0.0,
-                 seed=None):
+                 seed=None, layer_norm=False):
         super().__init__()
         g = torch.Generator().manual_seed(seed) if seed is not None else None
         if seed is not None:
             torch.manual_seed(seed)  # nn.MultiheadAttention's own xavier init
-        self.features_extractor = AttentionFeaturesExtractor(obs_dim, features_dim)
+        ext = AttentionFeaturesExtractorLN if layer_norm else AttentionFeaturesExtractor
+        self.features_extractor = ext(obs_dim, features_dim)
         self.mlp_extractor = _MlpExtractor(features_dim, hidden)
         self.action_net = nn.Linear(hidden, act_dim)
         self.value_net = nn.Linear(hidden, 1)
@@ -190,6 +208,11 @@ _ATTN_FE_FIELDS = ("fc1_w", "fc1_b", "in_proj_w", "in_proj_b", "out_proj_w", "ou
 def is_attention_policy(state_dict):
     """True for a state_dict of code/train.py's AttentionFeaturesExtractor policy."""
     return any(k.endswith("features_extractor.fc1.weight") for k in state_dict)
+
+
+def is_attention_ln_policy(state_dict):
+    """True for code/lorenz_filter/train.py's residual + LayerNorm extractor."""
+    return any(k.endswith("features_extractor.layer_norm.weight") for k in state_dict)
 
 
 def _fe_key(state_dict, name):
@@ -261,6 +284,58 @@ def reference_forward_attn_bf16(state_dict, obs):
     return mean, value
 
 
+def reference_forward_attn_ln_bf16(state_dict, obs):
+    """lz_rollout_policy_attn_stack's arithmetic restated in torch (code/lorenz_filter/
+    train.py's extractor): as reference_forward_attn_bf16 up to the head outputs, then
+    out_proj (bf16 operands, fp32 accumulate), the residual with the bf16 token values,
+    LayerNorm(16) in fp32 (biased variance, eps 1e-5), bf16, post_attention_fc (bf16
+    operands) + ReLU, the Tanh nets.  obs: the (stacked) policy input.  Returns
+    (mean, value)."""
+    sd = state_dict
+    f32 = torch.float32
+
+    def t(k):
+        return torch.as_tensor(np.asarray(_np(sd[k])), dtype=f32)
+
+    x = _bf(torch.as_tensor(obs, dtype=f32))
+    n = x.shape[0]
+    tok = _bf(torch.relu(x @ _bf(t(_fe_key(sd, "fc1.weight"))).T + t(_fe_key(sd, "fc1.bias"))))
+    tok = tok.view(n, 8, 16)
+    w_in, b_in = t(_fe_key(sd, ATTN_FE_KEYS[2])), t(_fe_key(sd, ATTN_FE_KEYS[3]))
+    c = torch.tensor(np.float64(ATTN_Q_SCALE))
+    wq = _bf((c.double() * w_in[:16].double()).to(f32))
+    bq = (c.double() * b_in[:16].double()).to(f32)
+    q = tok @ wq.T + bq
+    k = tok @ _bf(w_in[16:32]).T + b_in[16:32]
+    v = tok @ _bf(w_in[32:48]).T + b_in[32:48]
+    q, k, v = (z.view(n, 8, 4, 4).transpose(1, 2) for z in (q, k, v))
+    s = q @ k.transpose(-1, -2)
+    p = torch.exp2(s - s.amax(-1, keepdim=True))
+    o = (p @ v) * (1.0 / p.sum(-1, keepdim=True))
+    a = _bf(o.transpose(1, 2).reshape(n, 8, 16))
+    y = a @ _bf(t(_fe_key(sd, ATTN_FE_KEYS[4]))).T + t(_fe_key(sd, ATTN_FE_KEYS[5]))
+    z = y + tok
+    mu = z.mean(-1, keepdim=True)
+    z = z - mu
+    var = (z * z).mean(-1, keepdim=True)
+    u = _bf(z * torch.rsqrt(var + 1e-5) * t(_fe_key(sd, "layer_norm.weight"))
+            + t(_fe_key(sd, "layer_norm.bias")))
+    feat = _bf(torch.relu(u.reshape(n, 128) @ _bf(t(_fe_key(sd, ATTN_FE_KEYS[6]))).T
+                          + t(_fe_key(sd, ATTN_FE_KEYS[7]))))
+    s_t = torch.tensor(TANH_SCALE)
+
+    def net(prefix, w3, b3):
+        h = feat
+        for layer in (".0", ".2"):
+            acc = h @ _bf(s_t * t(prefix + layer + ".weight")).T + s_t * t(prefix + layer + ".bias")
+            h = _bf(torch.tanh(acc / s_t))
+        return h @ _bf(t(w3)).T + t(b3)
+
+    mean = net("mlp_extractor.policy_net", "action_net.weight", "action_net.bias")
+    value = net("mlp_extractor.value_net", "value_net.weight", "value_net.bias").flatten()
+    return mean, value
+
+
 def _np(v):
     if isinstance(v, torch.Tensor):
         return v.detach().to("cpu", torch.float32).numpy()
@@ -315,6 +390,34 @@ def pack_attn_policy(state_dict, obs_dim, act_dim, features_dim=64):
     return blob
 
 
+def pack_attn_ln_policy(state_dict, in_dim, act_dim, features_dim=64):
+    """lz_attn_ln_policy_pack: code/lorenz_filter/train.py's policy (in_dim = the
+    stacked observation width) -> uint8 numpy blob (host; needs no GPU)."""
+    if features_dim != 64:
+        raise ValueError("the fused kernel implements features_dim=64")
+    keys = [_fe_key(state_dict, k) for k in ATTN_FE_KEYS] + list(KEYS) + [
+        _fe_key(state_dict, "layer_norm.weight"), _fe_key(state_dict, "layer_norm.bias")]
+    for key in KEYS:
+        if key not in state_dict:
+            raise KeyError("policy state_dict lacks %r" % key)
+    arrs = [np.ascontiguousarray(_np(state_dict[k]), dtype=np.float32) for k in keys]
+    F = features_dim
+    shapes = [(HIDDEN, in_dim), (HIDDEN,), (48, 16), (48,), (16, 16), (16,), (F, HIDDEN), (F,)] + [
+        (HIDDEN, F), (HIDDEN,), (HIDDEN, HIDDEN), (HIDDEN,)] * 2 + [
+        (act_dim, HIDDEN), (act_dim,), (1, HIDDEN), (1,), (act_dim,), (16,), (16,)]
+    for key, a, shp in zip(keys, arrs, shapes):
+        if a.shape != shp:
+            raise ValueError("%s has shape %s, expected %s" % (key, a.shape, shp))
+    p = nat.LzAttnLnPolicy()
+    p.attn.obs_dim, p.attn.act_dim = int(in_dim), int(act_dim)
+    for f, a in zip(_ATTN_FE_FIELDS + _FIELDS, arrs):
+        setattr(p.attn, f, a.ctypes.data)
+    p.ln_w, p.ln_b = arrs[-2].ctypes.data, arrs[-1].ctypes.data
+    blob = np.zeros(int(nat.lib.lz_attn_ln_policy_blob_bytes()), np.uint8)
+    nat.check(nat.lib.lz_attn_ln_policy_pack(ctypes.byref(p), blob.ctypes.data, blob.size))
+    return blob
+
+
 @dataclass
 class RolloutBatch:
     """SB3 RolloutBuffer contents, time-major device tensors."""
@@ -331,6 +434,7 @@ class RolloutBatch:
     done_idx: torch.Tensor = None     # compact list k*N + env
     terminal_obs: torch.Tensor = None
     n_done: torch.Tensor = None
+    last_stack: torch.Tensor = None   # [N, n_stack * O] VecFrameStack obs after the rollout
     advantages: torch.Tensor = None
     returns: torch.Tensor = None
 
@@ -350,7 +454,7 @@ class FusedRolloutCollector:
 
     def __init__(self, backend, state_dict=None, gamma=0.99, gae_lambda=0.95, obs_rms=None,
                  clip_obs=10.0, norm_eps=1e-8, training=True, bootstrap=True,
-                 deterministic=False, capture_terminal=0, group=None):
+                 deterministic=False, capture_terminal=0, group=None, frame_stack=1):
         if backend.tdtype != torch.float32:
             raise ValueError("the fused policy rollout runs float32 env handles")
         self.env = backend
@@ -364,6 +468,15 @@ class FusedRolloutCollector:
         self.act_low, self.act_high = action_bounds(backend.system_name)
         self.blob = None
         self.attention = False
+        self.attention_ln = False
+        # SB3 VecFrameStack(n_stack) between the env and the policy
+        # (code/lorenz_filter/train.py:115): the stack is carried on the device
+        self.frame_stack = int(frame_stack)
+        if self.frame_stack not in (1, 4):
+            raise ValueError("frame_stack must be 1 or 4 (the fused kernel's instantiations)")
+        if self.frame_stack > 1 and obs_rms is not None:
+            raise ValueError("the frame-stacked rollout stacks raw observations (no VecNormalize)")
+        self.last_stack = None
         self.last_obs = None
         self.last_episode_starts = torch.ones((self.n,), dtype=torch.float32, device=self.device)
         if state_dict is not None:
@@ -374,14 +487,27 @@ class FusedRolloutCollector:
         A state_dict with code/train.py's AttentionFeaturesExtractor selects the
         attention kernel (lz_rollout_policy_attn), any other the MlpPolicy kernel."""
         self.attention = is_attention_policy(state_dict)
-        pack = pack_attn_policy if self.attention else pack_policy
-        blob = pack(state_dict, self.O, self.A)
+        self.attention_ln = is_attention_ln_policy(state_dict)
+        if self.frame_stack > 1 and not self.attention_ln:
+            raise ValueError("frame_stack > 1 runs code/lorenz_filter/train.py's policy "
+                             "(the residual + LayerNorm attention extractor)")
+        if self.attention_ln:
+            if self.obs_rms is not None:
+                raise ValueError("the LayerNorm attention rollout takes raw observations")
+            blob = pack_attn_ln_policy(state_dict, self.frame_stack * self.O, self.A)
+        else:
+            pack = pack_attn_policy if self.attention else pack_policy
+            blob = pack(state_dict, self.O, self.A)
         self.blob = torch.from_numpy(blob).to(self.device)
 
     def reset(self):
         """VecEnv.reset(): fresh episodes; the next rollout starts from their obs."""
         obs = self.env.reset()
         self.last_obs = obs.clone()
+        # StackedObservations.reset: zeros, the first frame last
+        self.last_stack = torch.zeros((self.n, self.frame_stack * self.O), dtype=torch.float32,
+                                      device=self.device)
+        self.last_stack[:, -self.O:] = obs
         self.last_episode_starts.fill_(1.0)
         if self.obs_rms is not None and self.training:
             self.obs_rms.update(self.last_obs, self.group)
@@ -394,7 +520,8 @@ class FusedRolloutCollector:
             self.reset()
         n, O, A, dev = self.n, self.O, self.A, self.device
         f32 = torch.float32
-        obs_buf = torch.empty((K, n, O), dtype=f32, device=dev)
+        SO = self.frame_stack * O if self.attention_ln else O
+        obs_buf = torch.empty((K, n, SO), dtype=f32, device=dev)
         act_buf = torch.empty((K, n, A), dtype=f32, device=dev)
         logp = torch.empty((K, n), dtype=f32, device=dev)
         val = torch.empty((K, n), dtype=f32, device=dev)
@@ -421,21 +548,30 @@ class FusedRolloutCollector:
         r.rew_buf, r.done_buf, r.last_values = _p(rew), _p(done), _p(last_val)
         r.obs_moments = _p(mom)
         r.done_idx, r.terminal_obs, r.cap, r.n_done = _p(didx), _p(tobs), self.capture_terminal, _p(ndone)
-        launch = nat.lib.lz_rollout_policy_attn if self.attention else nat.lib.lz_rollout_policy
-        nat.check(launch(self.env._h, ctypes.byref(r)))
+        stack_out = None
+        if self.attention_ln:
+            stack_out = torch.empty((n, SO), dtype=f32, device=dev)
+            nat.check(nat.lib.lz_rollout_policy_attn_stack(self.env._h, ctypes.byref(r),
+                                                           self.frame_stack, _p(self.last_stack),
+                                                           _p(stack_out)))
+        else:
+            launch = nat.lib.lz_rollout_policy_attn if self.attention else nat.lib.lz_rollout_policy
+            nat.check(launch(self.env._h, ctypes.byref(r)))
         starts = torch.empty((K, n), dtype=f32, device=dev)
         starts[0] = self.last_episode_starts
         if K > 1:
             starts[1:] = (done[:-1] != 0).to(f32)
         self.last_episode_starts = (done[-1] != 0).to(f32)
-        self._keep = (self.blob, self.last_obs)  # alive until the stream consumed them
+        self._keep = (self.blob, self.last_obs, self.last_stack)  # alive until consumed
         self.last_obs = obs_last
+        if stack_out is not None:
+            self.last_stack = stack_out
         if want_mom:
             if self.group is not None:
                 dist.all_reduce(mom, group=self.group)
             nat.check(nat.lib.lz_rms_update(self.obs_rms._h, ctypes.c_void_p(mom.data_ptr())))
         return RolloutBatch(obs_buf, act_buf, logp, val, rew, done, starts, last_val, obs_last,
-                            mom, didx, tobs, ndone)
+                            mom, didx, tobs, ndone, stack_out)
 
     def compute_returns_and_advantage(self, batch):
         """RolloutBuffer.compute_returns_and_advantage(last_values, dones) on device."""

@@ -346,6 +346,31 @@ lz_status lz_attn_policy_pack(const lz_attn_policy* p, void* host_blob, int64_t 
  * one wave per SIMD; the blob is resident in LDS). */
 lz_status lz_rollout_policy_attn(lz_handle* h, const lz_policy_rollout_args* r);
 
+/* code/lorenz_filter/train.py:54-132: PPO on VecFrameStack(HR, n_stack=4) with the
+ * extractor variant that adds a residual connection and LayerNorm(16) after the
+ * attention (x_seq = layer_norm(x_seq + out_proj(attn))) before post_attention_fc.
+ * attn.obs_dim is the policy's input width = n_stack * env obs_dim (1..32). */
+typedef struct lz_attn_ln_policy {
+  lz_attn_policy attn;
+  const float* ln_w;      /* features_extractor.layer_norm.weight [16] */
+  const float* ln_b;      /* features_extractor.layer_norm.bias [16] */
+} lz_attn_ln_policy;
+
+int64_t lz_attn_ln_policy_blob_bytes(void);
+lz_status lz_attn_ln_policy_pack(const lz_attn_ln_policy* p, void* host_blob, int64_t cap);
+
+/* The fused rollout with an lz_attn_ln_policy_pack blob on SB3 VecFrameStack(n_stack)
+ * observations (n_stack 1 or 4; systems LORENZ3 / PMSM / HR).  The stack of every env
+ * lives in registers for the K steps and follows SB3 StackedObservations.update: roll
+ * by obs_dim, the new frame last, zeros before the post-reset frame of a done env; the
+ * truncation bootstrap values the stacked terminal observation [rolled stack, terminal
+ * frame].  r->obs_buf is [K, N, n_stack*O] (the stacked observations the policy saw);
+ * r->obs_in / obs_last stay the raw [N, O] frames, r->terminal_obs the raw terminal
+ * frames; r->obs_norm and r->obs_moments must be NULL (the reference stacks raw obs).
+ * stack_in / stack_out: [N, n_stack*O] float32 device (may alias). */
+lz_status lz_rollout_policy_attn_stack(lz_handle* h, const lz_policy_rollout_args* r,
+                                       int32_t n_stack, const float* stack_in, float* stack_out);
+
 /* SB3 RolloutBuffer.compute_returns_and_advantage over time-major [K, N] float32
  * buffers (float32 arithmetic in NumPy's order): advantages and returns out.
  * done = the done bytes of each step (episode_starts shifted by one). */

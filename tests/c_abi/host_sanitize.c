@@ -89,6 +89,38 @@ int main(void) {
       for (size_t i = 0; i < sizeof all / sizeof all[0]; ++i) free((void*)all[i]);
     }
   if (lz_rollout_policy_attn(NULL, NULL) != LZ_ERR_INVALID) return 16;
+  /* the residual + LayerNorm packer (code/lorenz_filter/train.py), input dims 1..32 */
+  const int64_t lbytes = lz_attn_ln_policy_blob_bytes();
+  for (int I = 1; I <= 32; I += 3)
+    for (int A = 1; A <= 4; A += 3) {
+      const int H = LZ_POLICY_HIDDEN, F = 64;
+      lz_attn_ln_policy q;
+      lz_attn_policy* p = &q.attn;
+      p->obs_dim = I;
+      p->act_dim = A;
+      p->fc1_w = w((size_t)H * I, 0.1f); p->fc1_b = w(H, 0.01f);
+      p->in_proj_w = w(48 * 16, 0.1f); p->in_proj_b = w(48, 0.01f);
+      p->out_proj_w = w(16 * 16, 0.1f); p->out_proj_b = w(16, 0.01f);
+      p->post_w = w((size_t)F * H, 0.05f); p->post_b = w(F, 0.01f);
+      p->pi_w1 = w((size_t)H * F, 0.1f); p->pi_b1 = w(H, 0.01f);
+      p->pi_w2 = w((size_t)H * H, 0.05f); p->pi_b2 = w(H, 0.01f);
+      p->vf_w1 = w((size_t)H * F, 0.1f); p->vf_b1 = w(H, 0.01f);
+      p->vf_w2 = w((size_t)H * H, 0.05f); p->vf_b2 = w(H, 0.01f);
+      p->act_w = w((size_t)A * H, 0.02f); p->act_b = w(A, 0.01f);
+      p->val_w = w(H, 0.02f); p->val_b = w(1, 0.01f);
+      p->log_std = w(A, 0.1f);
+      q.ln_w = w(16, 0.1f); q.ln_b = w(16, 0.01f);
+      void* blob = malloc((size_t)lbytes);
+      if (lz_attn_ln_policy_pack(&q, blob, lbytes) != LZ_OK) return 17;
+      if (lz_attn_ln_policy_pack(&q, blob, lbytes - 1) != LZ_ERR_INVALID) return 18;
+      free(blob);
+      const float* all[] = {p->fc1_w, p->fc1_b, p->in_proj_w, p->in_proj_b, p->out_proj_w,
+                            p->out_proj_b, p->post_w, p->post_b, p->pi_w1, p->pi_b1, p->pi_w2,
+                            p->pi_b2, p->vf_w1, p->vf_b1, p->vf_w2, p->vf_b2, p->act_w, p->act_b,
+                            p->val_w, p->val_b, p->log_std, q.ln_w, q.ln_b};
+      for (size_t i = 0; i < sizeof all / sizeof all[0]; ++i) free((void*)all[i]);
+    }
+  if (lz_rollout_policy_attn_stack(NULL, NULL, 4, NULL, NULL) != LZ_ERR_INVALID) return 19;
   lz_mlp_policy bad;
   memset(&bad, 0, sizeof bad);
   bad.obs_dim = 9;

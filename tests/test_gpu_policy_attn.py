@@ -178,3 +178,137 @@ def test_attn_bootstrap_and_log_prob(gl, pol):
     act = ba.actions.reshape(-1, 2).cpu()
     lp_ref = torch.distributions.Normal(mean_ref, torch.exp(sd["log_std"])).log_prob(act).sum(-1)
     np.testing.assert_allclose(_np(ba.log_probs).reshape(-1), lp_ref.numpy(), atol=8e-2, rtol=3e-2)
+
+
+# --------------------------- code/lorenz_filter/train.py: LayerNorm extractor on VecFrameStack(4)
+def _random_attn_ln(pol, I, A, seed, scale=0.3):
+    net = pol.ActorCriticAttn(I, A, seed=seed, layer_norm=True)
+    g = torch.Generator().manual_seed(seed + 1)
+    with torch.no_grad():
+        for name, p in net.named_parameters():
+            if "layer_norm" in name:
+                p.copy_((1.0 if name.endswith("weight") else 0.0)
+                        + 0.2 * torch.randn(p.shape, generator=g))
+            else:
+                p.copy_(torch.randn(p.shape, generator=g) * (scale if p.dim() > 1 else 0.3))
+    return net, {k: v.detach().clone() for k, v in net.state_dict().items()}
+
+
+def _sb3_stacks(obs0, obs_r, done_r, didx, tobs, n, n_stack):
+    """SB3 VecFrameStack over the replayed raw frames (oracle/sb3_framestack.py): the
+    stacked obs the policy sees at every step, the stacked terminal observations
+    {(k, env): stack} and the final stack."""
+    from oracle.sb3_framestack import StackedObservations
+
+    K, O = obs_r.shape[0], obs_r.shape[2]
+    term = {int(i): tobs[m] for m, i in enumerate(didx)}
+    so = StackedObservations(n, n_stack, O)
+    seen = [so.reset(obs0).copy()]
+    stacked_term = {}
+    for k in range(K):
+        d = done_r[k] != 0
+        infos = [{"terminal_observation": term[k * n + e]} if d[e] else {} for e in range(n)]
+        st, infos = so.update(obs_r[k], d, infos)
+        for e in np.nonzero(d)[0]:
+            stacked_term[(k, int(e))] = infos[e]["terminal_observation"]
+        seen.append(st.copy())
+    return np.stack(seen[:-1]), stacked_term, seen[-1]
+
+
+@pytest.mark.parametrize("system,n,K,kw", [
+    ("hr", 777, 11, dict(add_noise=True, add_filter=True, max_episode_steps=4)),
+    ("lorenz3", 300, 7, dict(max_episode_steps=3)),
+])
+def test_attn_ln_framestack_rollout_bitexact(gl, pol, system, n, K, kw):
+    """code/lorenz_filter/train.py's collection: VecFrameStack(4) + the LayerNorm
+    extractor.  Env part bit-exact vs lz_rollout replaying the policy's own actions;
+    the stacked observations the policy saw, and the final stack, bit-exact vs the SB3
+    StackedObservations restatement (incl. zeroed stacks after a done)."""
+    envp = gl.BatchedEnv(system, n, seed=11, **kw)
+    envr = gl.BatchedEnv(system, n, seed=11, **kw)
+    O, A = envp.obs_dim, envp.action_dim
+    _, sd = _random_attn_ln(pol, 4 * O, A, seed=3)
+    col = pol.FusedRolloutCollector(envp, sd, bootstrap=False, capture_terminal=K * n,
+                                    frame_stack=4)
+    assert col.attention_ln
+    obs0 = _np(col.reset())
+    assert np.array_equal(obs0, _np(envr.reset()))
+    b = col.collect(K)
+    lo, hi = pol.action_bounds(envp.system_name)
+    acts = torch.clamp(b.actions, lo, hi).contiguous()
+    obs_r, rew_r, done_r, (didx, tobs, nd) = envr.rollout(acts, capture_terminal=K * n)
+    assert np.array_equal(_np(b.rewards), _np(rew_r))
+    assert np.array_equal(_np(b.dones), _np(done_r))
+    assert np.array_equal(_np(b.last_obs), _np(obs_r[-1]))
+    m = int(nd.item())
+    assert m > 0 and int(b.n_done.item()) == m
+    seen, _, final = _sb3_stacks(obs0, _np(obs_r), _np(done_r), _np(didx[:m]), _np(tobs[:m]), n, 4)
+    assert b.observations.shape == (K, n, 4 * O)
+    assert np.array_equal(_np(b.observations), seen)
+    assert np.array_equal(_np(b.last_stack), final)
+    assert torch.isfinite(b.values).all()
+
+
+def test_attn_ln_forward_and_bootstrap(gl, pol):
+    """Deterministic actions / values vs the torch restatement on the stacked obs; the
+    truncation bootstrap values the STACKED terminal observation (SB3 VecFrameStack
+    rewrites infos['terminal_observation'])."""
+    n, K, gamma = 1500, 9, 0.97
+    ea = gl.BatchedEnv("hr", n, seed=21, max_episode_steps=4, add_filter=True)
+    eb = gl.BatchedEnv("hr", n, seed=21, max_episode_steps=4, add_filter=True)
+    _, sd = _random_attn_ln(pol, 24, 2, seed=4)
+    ca = pol.FusedRolloutCollector(ea, sd, gamma=gamma, bootstrap=True, deterministic=True,
+                                   capture_terminal=K * n, frame_stack=4)
+    cb = pol.FusedRolloutCollector(eb, sd, gamma=gamma, bootstrap=False, deterministic=True,
+                                   frame_stack=4)
+    obs0 = _np(ca.reset())
+    cb.reset()
+    ba, bb = ca.collect(K), cb.collect(K)
+    assert torch.equal(ba.actions, bb.actions)
+    obs = ba.observations.reshape(-1, 24).cpu()
+    mean_ref, val_ref = pol.reference_forward_attn_ln_bf16(sd, obs)
+    ea_ = (ba.actions.reshape(-1, 2).cpu() - mean_ref).abs()
+    ev_ = (ba.values.reshape(-1).cpu() - val_ref).abs()
+    print("LN max |kernel - restatement|: mean %.3g value %.3g (median %.3g / %.3g)"
+          % (ea_.max(), ev_.max(), ea_.median(), ev_.median()))
+    np.testing.assert_allclose(_np(ba.actions).reshape(-1, 2), _np(mean_ref), atol=TOL_A, rtol=TOL_R)
+    np.testing.assert_allclose(_np(ba.values).reshape(-1), _np(val_ref), atol=TOL_A, rtol=TOL_R)
+    assert ev_.median().item() < 2e-3 and ea_.median().item() < 2e-3
+    _, vl = pol.reference_forward_attn_ln_bf16(sd, ba.last_stack.cpu())
+    np.testing.assert_allclose(_np(ba.last_values), _np(vl), atol=TOL_A, rtol=TOL_R)
+    # bootstrap on the stacked terminal observations
+    d = _np(ba.dones)
+    trunc = (d & 2 != 0) & (d & 1 == 0)
+    assert trunc.sum() > 0
+    diff = _np(ba.rewards) - _np(bb.rewards)
+    assert np.all(diff[~trunc] == 0)
+    m = int(ba.n_done.item())
+    obs_r = ba.observations.cpu().numpy()[:, :, -6:]  # raw frames the policy saw
+    raw = np.concatenate([obs_r[1:], _np(ba.last_obs)[None]], 0)  # frame after step k
+    _, sterm, _ = _sb3_stacks(obs0, raw, d, _np(ba.done_idx[:m]), _np(ba.terminal_obs[:m]), n, 4)
+    keys = [(k, e) for (k, e) in sterm if trunc[k, e]]
+    st = np.stack([sterm[key] for key in keys])
+    _, vt = pol.reference_forward_attn_ln_bf16(sd, st)
+    got = np.array([diff[k, e] for (k, e) in keys])
+    np.testing.assert_allclose(got, np.float32(gamma) * _np(vt), atol=TOL_A, rtol=TOL_R)
+
+
+def test_attn_ln_sb3_init_vs_fp32(gl, pol):
+    n, K = 8192, 4
+    env = gl.BatchedEnv("hr", n, seed=15, add_filter=True)
+    net = pol.ActorCriticAttn(24, 2, seed=3, layer_norm=True)
+    col = pol.FusedRolloutCollector(env, net.state_dict(), bootstrap=False, deterministic=True,
+                                    frame_stack=4)
+    col.reset()
+    b = col.collect(K)
+    obs = b.observations.reshape(-1, 24).cpu()
+    with torch.no_grad():
+        mean32, val32 = net(obs)
+    dv = (b.values.reshape(-1).cpu() - val32).abs()
+    dm = (b.actions.reshape(-1, 2).cpu() - mean32).abs()
+    sv, sm = val32.abs().mean().item(), mean32.abs().mean().item()
+    print("attn-LN bf16 vs fp32: value max %.3g mean %.3g (|V| ~ %.3g); action max %.3g mean "
+          "%.3g (|mu| ~ %.3g)" % (dv.max(), dv.mean(), sv, dm.max(), dm.mean(), sm))
+    assert dv.mean().item() < 0.02 * max(sv, 1e-3) + 1e-3
+    assert dm.mean().item() < 0.02 * max(sm, 1e-3) + 1e-4
+    assert dv.max().item() < 0.1 * max(sv, 1.0)

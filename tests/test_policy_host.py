@@ -184,14 +184,18 @@ def test_attn_policy_struct_matches_header(tmp_path):
     c = tmp_path / "probe.c"
     c.write_text(
         '#include <stdio.h>\n#include <stddef.h>\n#include "lorenz_env.h"\n'
-        'int main(void){printf("%zu %zu %zu\\n", sizeof(lz_attn_policy),'
-        " offsetof(lz_attn_policy, post_b), offsetof(lz_attn_policy, log_std));return 0;}\n")
+        'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(lz_attn_policy),'
+        " offsetof(lz_attn_policy, post_b), offsetof(lz_attn_policy, log_std),"
+        " sizeof(lz_attn_ln_policy), offsetof(lz_attn_ln_policy, ln_b));return 0;}\n")
     exe = tmp_path / "probe"
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)])
     got = [int(v) for v in subprocess.check_output([str(exe)]).split()]
     P = nat.LzAttnPolicy
-    assert got == [ctypes.sizeof(P), P.post_b.offset, P.log_std.offset]
+    Q = nat.LzAttnLnPolicy
+    assert got == [ctypes.sizeof(P), P.post_b.offset, P.log_std.offset, ctypes.sizeof(Q),
+                   Q.ln_b.offset]
     assert nat.lib.lz_attn_policy_blob_bytes() == 140608
+    assert nat.lib.lz_attn_ln_policy_blob_bytes() == 145984
 
 
 def test_sb3_framestack_restatement_hand_case():
@@ -358,3 +362,161 @@ def test_attn_state_dict_keys_match_sb3(pol):
         pol.pack_attn_policy(bad, 6, 2)
     with pytest.raises(ValueError):
         pol.pack_attn_policy(sd, 6, 3)
+
+
+# ------------------------------------------- residual + LayerNorm variant (lorenz_filter)
+def _ln_layout():
+    L = {"Fc1W": 0}
+    L["Fc1B"] = L["Fc1W"] + 4 * 2 * 64 * 16
+    L["KvW"] = L["Fc1B"] + 512
+    L["KvB"] = L["KvW"] + 1024
+    L["QW"] = L["KvB"] + 128
+    L["QB"] = L["QW"] + 1024
+    L["OutW"] = L["QB"] + 128
+    L["OutB"] = L["OutW"] + 1024
+    L["Gamma"] = L["OutB"] + 128
+    L["Beta"] = L["Gamma"] + 64
+    L["PostW"] = L["Beta"] + 64
+    L["PostB"] = L["PostW"] + 8 * 2 * 64 * 16
+    L["Ext"] = L["PostB"] + 256
+    return L
+
+
+def _emulate_attn_ln(blob, x_in):
+    """lz_rollout_policy_attn_stack's forward on one 32-env tile (x_in: [32, <=32] the
+    stacked policy input) over the packed kLn blob."""
+    L = _ln_layout()
+    _, N = _attn_layout()
+    f32 = lambda off, n: blob[off: off + 4 * n].view(np.float32)  # noqa: E731
+    lane_h = np.arange(64) >> 5
+    I = x_in.shape[1]
+    xin = np.zeros((32, 32), np.float32)
+    xin[:, :I] = _bf16(x_in)
+    xs = []
+    for s in range(2):  # k-step s: half h holds stacked dims 16s + 8h + j
+        f = np.zeros((64, 8), np.float32)
+        f[:32] = xin[:, 16 * s: 16 * s + 8]
+        f[32:] = xin[:, 16 * s + 8: 16 * s + 16]
+        xs.append(f)
+    fc1 = _unpack(blob, L["Fc1W"], 8)
+    b1 = f32(L["Fc1B"], 128).reshape(4, 2, 16)
+    tok = []
+    for t in range(4):
+        c = b1[t][lane_h]
+        for s in range(2):
+            c = _mfma(fc1[t * 2 + s], xs[s], c)
+        tok += _relu_frag(c)
+    wkv = _unpack(blob, L["KvW"], 1)[0]
+    kv = np.stack([_mfma(wkv, tok[t], f32(L["KvB"], 32).reshape(2, 16)[lane_h]) for t in range(8)], 1)
+    wq = _unpack(blob, L["QW"], 1)[0]
+    bq = f32(L["QB"], 32).reshape(2, 16)[lane_h]
+    wo = _unpack(blob, L["OutW"], 1)[0]
+    bo = f32(L["OutB"], 32).reshape(2, 16)[lane_h]
+    gam = f32(L["Gamma"], 16).reshape(2, 8)[lane_h]
+    bet = f32(L["Beta"], 16).reshape(2, 8)[lane_h]
+    wp = _unpack(blob, L["PostW"], 16)
+    bp = f32(L["PostB"], 64).reshape(2, 2, 16)
+    f0, f1 = bp[0][lane_h], bp[1][lane_h]
+    for i in range(8):
+        q = _mfma(wq, tok[i], bq)
+        o = np.zeros((64, 8), np.float32)
+        for hh in range(2):
+            s_ = np.einsum("ld,ljd->lj", q[:, 4 * hh: 4 * hh + 4], kv[:, :, 4 * hh: 4 * hh + 4])
+            p = np.exp2(s_ - s_.max(1, keepdims=True))
+            o[:, 4 * hh: 4 * hh + 4] = np.einsum("lj,ljd->ld", p, kv[:, :, 8 + 4 * hh: 12 + 4 * hh]) * (
+                np.float32(1) / p.sum(1, keepdims=True))
+        y = _mfma(wo, _bf16(o), bo)[:, :8]
+        z = y + tok[i]
+        tot = z.sum(1) + np.roll(z.sum(1), 32)  # the two halves' partial sums
+        z = z - (tot * np.float32(0.0625))[:, None]
+        sq = (z * z).sum(1)
+        var = (sq + np.roll(sq, 32)) * np.float32(0.0625)
+        u = _bf16(z / np.sqrt(var + np.float32(1e-5))[:, None] * gam + bet)
+        f0 = _mfma(wp[2 * i], u, f0)
+        f1 = _mfma(wp[2 * i + 1], u, f1)
+    feat = _relu_frag(f0) + _relu_frag(f1)
+    outs = []
+    for net in (L["Ext"], L["Ext"] + N["Net"]):
+        w1 = _unpack(blob, net + N["W1"], 16)
+        w2 = _unpack(blob, net + N["W2"], 32)
+        w3 = _unpack(blob, net + N["W3"], 8)
+        nb1 = f32(net + N["B1"], 128).reshape(4, 2, 16)
+        nb2 = f32(net + N["B2"], 128).reshape(4, 2, 16)
+        nb3 = f32(net + N["B3"], 32).reshape(2, 16)
+        h1 = []
+        for t in range(4):
+            c = nb1[t][lane_h]
+            for s in range(4):
+                c = _mfma(w1[t * 4 + s], feat[s], c)
+            h1 += _act(c)
+        h2 = []
+        for t in range(4):
+            c = nb2[t][lane_h]
+            for kk in range(8):
+                c = _mfma(w2[t * 8 + kk], h1[kk], c)
+            h2 += _act(c)
+        c = nb3[lane_h]
+        for kk in range(8):
+            c = _mfma(w3[kk], h2[kk], c)
+        outs.append(c)
+    return outs[0][:32, :4], outs[1][:32, 0]
+
+
+def _random_attn_ln_policy(pol, I, A, seed, scale=0.3):
+    net = pol.ActorCriticAttn(I, A, seed=seed, layer_norm=True)
+    g = torch.Generator().manual_seed(seed + 1)
+    with torch.no_grad():
+        for name, p in net.named_parameters():
+            if "layer_norm" in name:  # gains around 1, offsets small
+                p.copy_((1.0 if name.endswith("weight") else 0.0)
+                        + 0.2 * torch.randn(p.shape, generator=g))
+            else:
+                p.copy_(torch.randn(p.shape, generator=g) * (scale if p.dim() > 1 else 0.3))
+    return net, {k: v.detach().clone() for k, v in net.state_dict().items()}
+
+
+@pytest.mark.parametrize("I,A", [(24, 2), (6, 2), (32, 3), (13, 1)])
+def test_attn_ln_pack_layout_matches_mfma_dataflow(pol, I, A):
+    _, sd = _random_attn_ln_policy(pol, I, A, seed=I + A)
+    blob = pol.pack_attn_ln_policy(sd, I, A)
+    assert blob.size == 145984
+    x = np.random.default_rng(I).normal(0, 1.0, size=(32, I)).astype(np.float32)
+    mean, value = _emulate_attn_ln(blob, x)
+    ref_mean, ref_value = pol.reference_forward_attn_ln_bf16(sd, x)
+    np.testing.assert_allclose(mean[:, :A], ref_mean.numpy(), rtol=0, atol=5e-3)
+    np.testing.assert_allclose(value, ref_value.numpy(), rtol=0, atol=5e-3)
+    assert np.median(np.abs(mean[:, :A] - ref_mean.numpy())) < 1e-4
+    assert np.all(mean[:, A:] == 0)
+
+
+@pytest.mark.parametrize("sb3_init", [False, True])
+def test_attn_ln_restatement_vs_fp32_module(pol, sb3_init):
+    """The bf16 restatement of code/lorenz_filter/train.py's extractor (residual on the
+    bf16 tokens, fp32 LayerNorm) against the plain fp32 module: bf16 accuracy."""
+    if sb3_init:
+        net = pol.ActorCriticAttn(24, 2, seed=3, layer_norm=True)
+        sd = net.state_dict()
+    else:
+        net, sd = _random_attn_ln_policy(pol, 24, 2, seed=9)
+    x = np.random.default_rng(5).normal(0, 1.0, size=(512, 24)).astype(np.float32)
+    with torch.no_grad():
+        m32, v32 = net(torch.from_numpy(x))
+    mb, vb = pol.reference_forward_attn_ln_bf16(sd, x)
+    for got, want in ((mb, m32), (vb, v32)):
+        err = (got - want).abs()
+        scale = want.abs().max().item()
+        assert err.max().item() <= 0.04 * scale + 1e-4, (err.max().item(), scale)
+        assert err.mean().item() <= 0.008 * scale + 1e-5, (err.mean().item(), scale)
+
+
+def test_attn_ln_keys_and_errors(pol):
+    net = pol.ActorCriticAttn(24, 2, seed=0, layer_norm=True)
+    sd = net.state_dict()
+    assert pol.is_attention_ln_policy(sd) and pol.is_attention_policy(sd)
+    assert not pol.is_attention_ln_policy(pol.ActorCriticAttn(6, 2, seed=0).state_dict())
+    with pytest.raises(ValueError):
+        pol.pack_attn_ln_policy(sd, 6, 2)  # fc1 is [128, 24]
+    from gym_lorenz import _native as nat
+    big = pol.ActorCriticAttn(40, 2, seed=0, layer_norm=True).state_dict()
+    with pytest.raises(nat.LorenzEnvError):
+        pol.pack_attn_ln_policy(big, 40, 2)

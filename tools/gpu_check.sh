@@ -58,6 +58,9 @@ for step in "$@"; do
       run attn_hr_32k_K2048 300 python bench.py --mode policy --policy attn --system hr --envs 32768 --K 2048 --steps 4096
       run attn_hr_262k_K16 300 python bench.py --mode policy --policy attn --system hr --envs 262144 --K 16 --steps 1024
       run attn_pmsm_262k_K16 300 python bench.py --mode policy --policy attn --system pmsm --envs 262144 --K 16 --steps 1024 ;;
+    attn_ln_bench)
+      run attn_ln_hr_32k_K2048 300 python bench.py --mode policy --policy attn_ln --system hr --envs 32768 --K 2048 --steps 4096
+      run attn_ln_hr_262k_K16 300 python bench.py --mode policy --policy attn_ln --system hr --envs 262144 --K 16 --steps 1024 ;;
     attn_prof)
       export TMPDIR=/tmp
       run attn_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/attn_prof -o run --output-format csv -- python bench.py --mode policy --policy attn --system hr --envs 32768 --K 2048 --steps 4096 ;;
