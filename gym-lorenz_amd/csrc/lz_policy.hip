@@ -1320,6 +1320,45 @@ lz_status lz_policy_pack(const lz_mlp_policy* p, void* host_blob, int64_t cap) {
   return LZ_OK;
 }
 
+lz_status lz_policy_pack_hidden(const lz_mlp_policy* p, int32_t hidden, void* host_blob,
+                                int64_t cap) {
+  // a [hidden, hidden] net zero-padded to 128 units: a padded unit's pre-activation is
+  // exactly 0, tanh(0) = 0, and its zero weights add exact zeros downstream -- the
+  // 128-wide kernel computes the narrower net unchanged
+  if (!p) return pfail(LZ_ERR_INVALID, "policy is NULL");
+  if (hidden == lz::kPolHidden) return lz_policy_pack(p, host_blob, cap);
+  if (hidden < 1 || hidden > lz::kPolHidden)
+    return pfail(LZ_ERR_UNSUPPORTED, "hidden width must be 1..128");
+  if (p->obs_dim < 1 || p->obs_dim > lz::kPolMaxObs || p->act_dim < 1 || p->act_dim > lz::kPolMaxAct)
+    return pfail(LZ_ERR_UNSUPPORTED, "policy supports obs_dim 1..8 and act_dim 1..4");
+  const float* req[] = {p->pi_w1, p->pi_b1, p->pi_w2, p->pi_b2, p->vf_w1, p->vf_b1, p->vf_w2,
+                        p->vf_b2, p->act_w, p->act_b, p->val_w, p->val_b, p->log_std};
+  for (const float* q : req)
+    if (!q) return pfail(LZ_ERR_INVALID, "a policy weight pointer is NULL");
+  const int H = lz::kPolHidden, O = p->obs_dim, A = p->act_dim;
+  std::vector<float> buf((size_t)2 * (H * O + H + H * H + H) + (size_t)(A + 1) * H, 0.0f);
+  float* q = buf.data();
+  auto pad = [&](const float* src, int rows, int cols, int prow, int pcol) {
+    float* dst = q;
+    for (int r = 0; r < rows; ++r)
+      for (int c = 0; c < cols; ++c) dst[r * pcol + c] = src[r * cols + c];
+    q += (size_t)prow * pcol;
+    return dst;
+  };
+  lz_mlp_policy w = *p;
+  w.pi_w1 = pad(p->pi_w1, hidden, O, H, O);
+  w.pi_b1 = pad(p->pi_b1, 1, hidden, 1, H);
+  w.pi_w2 = pad(p->pi_w2, hidden, hidden, H, H);
+  w.pi_b2 = pad(p->pi_b2, 1, hidden, 1, H);
+  w.vf_w1 = pad(p->vf_w1, hidden, O, H, O);
+  w.vf_b1 = pad(p->vf_b1, 1, hidden, 1, H);
+  w.vf_w2 = pad(p->vf_w2, hidden, hidden, H, H);
+  w.vf_b2 = pad(p->vf_b2, 1, hidden, 1, H);
+  w.act_w = pad(p->act_w, A, hidden, A, H);
+  w.val_w = pad(p->val_w, 1, hidden, 1, H);
+  return lz_policy_pack(&w, host_blob, cap);
+}
+
 int64_t lz_attn_policy_blob_bytes(void) { return lz::kAttBlobBytes; }
 
 lz_status lz_attn_policy_pack(const lz_attn_policy* p, void* host_blob, int64_t cap) {

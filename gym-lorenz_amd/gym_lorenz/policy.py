@@ -343,15 +343,17 @@ def _np(v):
 
 
 def pack_policy(state_dict, obs_dim, act_dim):
-    """lz_policy_pack: SB3 state_dict -> uint8 numpy blob (host; needs no GPU)."""
+    """lz_policy_pack / lz_policy_pack_hidden: SB3 state_dict (net_arch pi=[H,H]
+    vf=[H,H], H <= 128) -> uint8 numpy blob (host; needs no GPU)."""
     arrs = []
     for key in KEYS:
         if key not in state_dict:
             raise KeyError("policy state_dict lacks %r (expected SB3 MlpPolicy with "
-                           "net_arch pi=[128,128] vf=[128,128])" % key)
+                           "net_arch pi=[H,H] vf=[H,H], H <= 128)" % key)
         arrs.append(np.ascontiguousarray(_np(state_dict[key]), dtype=np.float32))
-    shapes = [(HIDDEN, obs_dim), (HIDDEN,), (HIDDEN, HIDDEN), (HIDDEN,)] * 2 + [
-        (act_dim, HIDDEN), (act_dim,), (1, HIDDEN), (1,), (act_dim,)]
+    H = arrs[0].shape[0]
+    shapes = [(H, obs_dim), (H,), (H, H), (H,)] * 2 + [
+        (act_dim, H), (act_dim,), (1, H), (1,), (act_dim,)]
     for key, a, shp in zip(KEYS, arrs, shapes):
         if a.shape != shp:
             raise ValueError("%s has shape %s, expected %s" % (key, a.shape, shp))
@@ -360,7 +362,7 @@ def pack_policy(state_dict, obs_dim, act_dim):
     for f, a in zip(_FIELDS, arrs):
         setattr(p, f, a.ctypes.data)
     blob = np.zeros(int(nat.lib.lz_policy_blob_bytes()), np.uint8)
-    nat.check(nat.lib.lz_policy_pack(ctypes.byref(p), blob.ctypes.data, blob.size))
+    nat.check(nat.lib.lz_policy_pack_hidden(ctypes.byref(p), H, blob.ctypes.data, blob.size))
     return blob
 
 

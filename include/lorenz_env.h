@@ -265,6 +265,12 @@ int64_t lz_policy_blob_bytes(void);
  * copies the blob to the device (e.g. torch.uint8 CUDA tensor) for lz_rollout_policy.
  * Host-only: needs no GPU. */
 lz_status lz_policy_pack(const lz_mlp_policy* p, void* host_blob, int64_t cap);
+/* lz_policy_pack for net_arch pi=[hidden, hidden] vf=[hidden, hidden], hidden 1..128
+ * (code/lorenz_pmsm/optimize.py:36-41 searches 64 and 128): weights [hidden, obs_dim],
+ * [hidden, hidden], [act_dim, hidden] ...; zero-padded to the kernel's 128 units, which
+ * is exact (padded units are tanh(0) = 0 and carry zero weights). */
+lz_status lz_policy_pack_hidden(const lz_mlp_policy* p, int32_t hidden, void* host_blob,
+                                int64_t cap);
 
 typedef struct lz_policy_rollout_args {
   int32_t K;                /* steps (SB3 n_steps) */

@@ -325,3 +325,28 @@ def test_policy_launch_shapes_agree_bitwise(gl, pol, n):
                   "last_values", "last_obs"):
             assert torch.equal(getattr(b, f), getattr(outs[0], f)), f
         np.testing.assert_allclose(_np(b.obs_moments), _np(outs[0].obs_moments), rtol=1e-12)
+
+
+def test_policy_narrow_net_optuna_setting(gl, pol):
+    """code/lorenz_pmsm/optimize.py:36-52: A2C MlpPolicy net_arch [64, 64] Tanh behind
+    VecNormalize(norm_obs, clip_obs=10) on PMSM -- zero-padded into the 128-unit kernel."""
+    from gym_lorenz.vec_normalize import DeviceRunningMeanStd
+
+    n, K = 4099, 8
+    env = gl.BatchedEnv("pmsm", n, seed=5)
+    net = pol.ActorCriticMlp(6, 2, hidden=64, seed=1)
+    g = torch.Generator().manual_seed(2)
+    with torch.no_grad():
+        for p in net.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * (0.4 if p.dim() > 1 else 0.3))
+    sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    rms = DeviceRunningMeanStd(6, env.device)
+    col = pol.FusedRolloutCollector(env, sd, bootstrap=False, deterministic=True, obs_rms=rms)
+    col.reset()
+    col.collect(K)
+    b = col.collect(K)
+    obs = b.observations.reshape(-1, 6).cpu()
+    mean_ref, val_ref = pol.reference_forward_bf16(sd, obs)
+    np.testing.assert_allclose(_np(b.actions).reshape(-1, 2), _np(mean_ref), atol=TOL_A, rtol=TOL_R)
+    np.testing.assert_allclose(_np(b.values).reshape(-1), _np(val_ref), atol=TOL_A, rtol=TOL_R)
+    assert np.median(np.abs(_np(b.values).reshape(-1) - _np(val_ref))) < 2e-3

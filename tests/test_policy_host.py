@@ -520,3 +520,25 @@ def test_attn_ln_keys_and_errors(pol):
     big = pol.ActorCriticAttn(40, 2, seed=0, layer_norm=True).state_dict()
     with pytest.raises(nat.LorenzEnvError):
         pol.pack_attn_ln_policy(big, 40, 2)
+
+
+@pytest.mark.parametrize("H", [64, 32, 100])
+def test_pack_narrow_nets_zero_padded(pol, H):
+    """net_arch [H, H] (code/lorenz_pmsm/optimize.py:36-41 searches 64 and 128):
+    zero-padded to the kernel's 128 units, the MFMA dataflow computes the narrow net."""
+    net = pol.ActorCriticMlp(6, 2, hidden=H, seed=H)
+    g = torch.Generator().manual_seed(H)
+    with torch.no_grad():
+        for p in net.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * (0.4 if p.dim() > 1 else 0.3))
+    sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    blob = pol.pack_policy(sd, 6, 2)
+    obs = np.random.default_rng(H).normal(0, 1.5, size=(32, 6)).astype(np.float32)
+    mean, value = _emulate(pol, blob, obs)
+    ref_mean, ref_value = pol.reference_forward_bf16(sd, obs)
+    np.testing.assert_allclose(mean[:, :2], ref_mean.numpy(), rtol=0, atol=2e-4)
+    np.testing.assert_allclose(value, ref_value.numpy(), rtol=0, atol=2e-4)
+    from gym_lorenz import _native as nat
+    big = pol.ActorCriticMlp(6, 2, hidden=129, seed=0).state_dict()
+    with pytest.raises(nat.LorenzEnvError):
+        pol.pack_policy(big, 6, 2)
