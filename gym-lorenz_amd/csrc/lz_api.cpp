@@ -444,8 +444,9 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
   HIP_TRY(hipSetDevice(h->cfg.device));
   const int64_t n = h->cfg.num_envs;
   const int64_t n_wg = (n + lz::kBlock - 1) / lz::kBlock;
-  if (!h->vn_ws) {  // column-major per-workgroup partials, W = 2 (kVnMaxObs + 1) at most
-    const size_t bytes = (size_t)n_wg * 2 * (lz::kVnMaxObs + 1) * sizeof(double);
+  if (!h->vn_ws) {  // column-major per-workgroup partials, W = 2 (kVnMaxObs + 1) at most,
+                    // then the W column totals
+    const size_t bytes = (size_t)(n_wg + 1) * 2 * (lz::kVnMaxObs + 1) * sizeof(double);
     if (hipMalloc(reinterpret_cast<void**>(&h->vn_ws), bytes) != hipSuccess)
       return fail(LZ_ERR_OOM, "vecnorm workspace (%zu B)", bytes);
   }
@@ -462,6 +463,7 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
   std::memset(&v, 0, sizeof v);
   v.returns = vn->returns;
   v.part = reinterpret_cast<double*>(h->vn_ws);
+  v.tot = v.part + (size_t)n_wg * 2 * (lz::kVnMaxObs + 1);
   v.n_done_out = n_done_out;
   v.obs_state = lz::rms_state(vn->obs_rms);
   v.ret_state = lz::rms_state(vn->ret_rms);

@@ -57,6 +57,7 @@ constexpr int kVnMaxObs = 8;
 struct VArgs {
   double* returns;     // [N] VecNormalize.returns
   double* part;        // [W][n_wg]
+  double* tot;         // [W] column totals (k_vn_colsum -> k_vn_update)
   double* obs_state;   // obs_rms mean[O], var[O], count
   double* ret_state;   // ret_rms mean, var, count
   double* moments;     // LZ_VN_DEFER: [2O+1 obs][3 returns] batch moments out

@@ -111,8 +111,8 @@ constexpr int step_block() {  // bits 3-4 of V: workgroup size
 // (lz_step_vecnorm, lz_internal.h VArgs).  Per-workgroup float64 moments of the obs
 // columns (read back from the LDS obs tile) and of the updated returns: each column
 // summed by 32 lanes over strided rows, then a fixed xor tree; one plain store per
-// column into the column-major partials.  k_vn_reduce, the next launch on the stream,
-// sums them in a fixed order (no cross-workgroup synchronisation inside the step: an
+// column into the column-major partials.  k_vn_colsum / k_vn_update, the next launches
+// on the stream, sum them in a fixed order (no cross-workgroup synchronisation inside the step: an
 // in-kernel last-arriver reduction needs every workgroup to wait for its stores'
 // acknowledgements before taking a ticket, which measured 4x the step time at 1M envs).
 template <int O, typename T>
@@ -144,56 +144,46 @@ __device__ __forceinline__ void vn_epilogue(const T* s_obs, const double* s_ret,
   }
 }
 
-// One workgroup of B lanes: the batch moments from the n_wg partials of every column
-// -- lane t sums workgroups t, t+B, ... in order, 8 rows of every column in flight per
-// round (coalesced column-major loads; one round at 1M envs), then a fixed LDS tree
-// over the lanes -- and the RunningMeanStd updates (lz_rms_math.h, as k_rms_update)
-// or, with LZ_VN_DEFER, the moments for the caller's all-reduce.  Also publishes the
-// step's done count.
-template <int O>
-constexpr int vn_reduce_block() {  // the LDS tree holds W x B doubles (<= 64 KiB)
-  return 2 * (O + 1) * 512 * 8 <= 65536 ? 512 : 256;
-}
-template <int O>
-__global__ __launch_bounds__(vn_reduce_block<O>()) void k_vn_reduce(VArgs v, int64_t n,
-                                                                   const int32_t* counter,
-                                                                   int32_t* n_done_out) {
-  constexpr int kVnReduceBlock = vn_reduce_block<O>();
-  constexpr int C = O + 1, W = 2 * C, U = 8;
-  __shared__ double red[W][kVnReduceBlock];
-  __shared__ double s_tot[W];
-  const int tid = (int)threadIdx.x;
-  if (tid == 0) *n_done_out = *counter;
+// The batch moments from the n_wg per-workgroup partials: one workgroup per partial
+// column (2 (O + 1) of them) sums it in a fixed order -- lane t adds rows t, t + 1024,
+// ... into accumulator u of rows t + 256 u (mod 1024), the 4 accumulators in order,
+// then a fixed LDS tree -- and stores the column total.  (A single workgroup for all
+// columns measured 11.5 us per 1M-env step; a column per workgroup spreads the 458 KB
+// of partials over 14 CUs.)  Block 0 also publishes the step's done count.
+constexpr int kVnColBlock = 256;
+__global__ __launch_bounds__(kVnColBlock) void k_vn_colsum(VArgs v, const int32_t* counter,
+                                                          int32_t* n_done_out) {
+  __shared__ double red[kVnColBlock];
+  const int tid = (int)threadIdx.x, c = (int)blockIdx.x;
+  if (c == 0 && tid == 0) *n_done_out = *counter;
   if (!(v.flags & LZ_VN_TRAINING)) return;
-  double acc[W];
+  const double* col = v.part + (int64_t)c * v.n_wg;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int r = tid; r < v.n_wg; r += 4 * kVnColBlock) {
 #pragma unroll
-  for (int c = 0; c < W; ++c) acc[c] = 0.0;
-  for (int r = tid; r < v.n_wg; r += U * kVnReduceBlock) {
-    double x[U][W];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int ru = r + u * kVnReduceBlock;
-#pragma unroll
-      for (int c = 0; c < W; ++c) x[u][c] = ru < v.n_wg ? v.part[(int64_t)c * v.n_wg + ru] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int c = 0; c < W; ++c) acc[c] += x[u][c];
+    for (int u = 0; u < 4; ++u) {
+      const int ru = r + u * kVnColBlock;
+      if (ru < v.n_wg) acc[u] += col[ru];
     }
   }
-#pragma unroll
-  for (int c = 0; c < W; ++c) red[c][tid] = acc[c];
+  red[tid] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
-  for (int half = kVnReduceBlock / 2; half > 0; half >>= 1) {  // fixed pairing tree
-    for (int e = tid; e < W * half; e += kVnReduceBlock) {
-      const int c = e / half, k = e % half;
-      red[c][k] += red[c][k + half];
-    }
+#pragma unroll
+  for (int half = kVnColBlock / 2; half > 0; half >>= 1) {  // fixed pairing tree
+    if (tid < half) red[tid] += red[tid + half];
     __syncthreads();
   }
-  if (tid < W) s_tot[tid] = red[tid][0];
-  __syncthreads();
+  if (tid == 0) v.tot[c] = red[0];
+}
+
+// The RunningMeanStd updates from the column totals (lz_rms_math.h, as k_rms_update)
+// or, with LZ_VN_DEFER, the moments for the caller's all-reduce.  One wave.
+template <int O>
+__global__ __launch_bounds__(64) void k_vn_update(VArgs v, int64_t n) {
+  constexpr int C = O + 1;
+  if (!(v.flags & LZ_VN_TRAINING)) return;
+  const int tid = (int)threadIdx.x;
+  const double* s_tot = v.tot;
   const double bc = (double)n;
   if (v.flags & LZ_VN_DEFER) {  // (count, sums, sumsq) for obs, then for returns
     if (tid < O) {
@@ -209,7 +199,7 @@ __global__ __launch_bounds__(vn_reduce_block<O>()) void k_vn_reduce(VArgs v, int
     return;
   }
   const bool upd_obs = (v.flags & LZ_VN_NORM_OBS) && tid < O;
-  const bool upd_ret = tid == 64;
+  const bool upd_ret = tid == 32;
   const double c_obs = v.obs_state[2 * O], c_ret = v.ret_state[2];
   double nm = 0.0, nv = 0.0;
   if (upd_obs)
@@ -795,8 +785,9 @@ template <class Sys, typename T>
 static int launch_vn(const KArgs& a, const VArgs& v, hipStream_t s) {
   static_assert(Sys::O <= kVnMaxObs, "obs too wide for the VecNormalize epilogue");
   hipLaunchKernelGGL((k_step_vn<Sys, T>), dim3((unsigned)grid_for(a.n)), dim3(kBlock), 0, s, a, v);
-  hipLaunchKernelGGL((k_vn_reduce<Sys::O>), dim3(1), dim3(vn_reduce_block<Sys::O>()), 0, s, v, a.n,
-                     a.counter, v.n_done_out);
+  hipLaunchKernelGGL(k_vn_colsum, dim3(2 * (Sys::O + 1)), dim3(kVnColBlock), 0, s, v, a.counter,
+                     v.n_done_out);
+  hipLaunchKernelGGL((k_vn_update<Sys::O>), dim3(1), dim3(64), 0, s, v, a.n);
   return (int)hipGetLastError();
 }
 

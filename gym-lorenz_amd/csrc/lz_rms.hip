@@ -187,7 +187,8 @@ __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
       __shared__ f4a tile[256 * E / 4];
       const f4a* src = reinterpret_cast<const f4a*>(obs + (int64_t)blockIdx.x * 256 * E);
 #pragma unroll
-      for (int k = 0; k < E / 4; ++k) tile[threadIdx.x + 256 * k] = src[threadIdx.x + 256 * k];
+      for (int k = 0; k < E / 4; ++k)  // raw obs: read once (non-temporal)
+        tile[threadIdx.x + 256 * k] = __builtin_nontemporal_load(src + threadIdx.x + 256 * k);
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < E / 4; ++k) {
@@ -205,7 +206,8 @@ __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
       __syncthreads();
       f4a* dst = reinterpret_cast<f4a*>(p.obs_n + (int64_t)blockIdx.x * 256 * E);
 #pragma unroll
-      for (int k = 0; k < E / 4; ++k) dst[threadIdx.x + 256 * k] = tile[threadIdx.x + 256 * k];
+      for (int k = 0; k < E / 4; ++k)  // normalised obs: written once (non-temporal)
+        __builtin_nontemporal_store(tile[threadIdx.x + 256 * k], dst + threadIdx.x + 256 * k);
     } else {
 #pragma unroll
       for (int e = 0; e < E; ++e) x[e] = (r0 + e / O < p.n) ? (float)obs[r0 * O + e] : 0.0f;
