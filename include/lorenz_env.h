@@ -37,6 +37,19 @@
  *   lz_get_state / lz_set_state
  *       -> attribute access env.state1 / state2 / state_master / state_slave /
  *          lambda_coef ... used by code/lorenz_pmsm/test_evaluate.py:99-111
+ *   lz_policy_pack[_hidden] / lz_rollout_policy / lz_gae
+ *       -> SB3 OnPolicyAlgorithm.collect_rollouts + RolloutBuffer.compute_returns_and_
+ *          advantage for the MlpPolicy learners (code/lorenz_pmsm/train.py:155-178,
+ *          optimize.py:36-60 ([64,64] / [128,128]), code/gym_run.py:83 (PPO default
+ *          net_arch [64,64]))
+ *   lz_attn_policy_pack / lz_rollout_policy_attn
+ *       -> the same for code/train.py:52-112 and code/gym_try.py:52-116 (PPO with the
+ *          AttentionFeaturesExtractor)
+ *   lz_attn_ln_policy_pack / lz_rollout_policy_attn_stack
+ *       -> the same for code/lorenz_filter/train.py:54-132 (VecFrameStack(4) + the
+ *          residual/LayerNorm extractor)
+ *   lz_frame_stack
+ *       -> SB3 VecFrameStack.step_wait (code/lorenz_filter/train.py:115)
  *
  * Conventions
  *   - Every function returns an lz_status (0 == LZ_OK).  Nothing throws across
