@@ -304,8 +304,21 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
   }
 }
 
+// Occupancy hint per system (Sys::kStepWaves, default none): a register-heavy step body
+// compiled for more resident waves, so that the 4096 workgroups of a 1M-env step need
+// fewer rounds over the CUs (HR f32: 82 VGPRs = 5 waves/SIMD unconstrained).
+template <class Sys, class = void>
+struct step_waves {
+  static constexpr int value = 1;
+};
+template <class Sys>
+struct step_waves<Sys, std::void_t<decltype(Sys::kStepWaves)>> {
+  static constexpr int value = Sys::kStepWaves;
+};
+
 template <class Sys, typename T, int V>
-__global__ __launch_bounds__(step_block<V>()) void k_step(KArgs a) {
+__global__ __launch_bounds__(step_block<V>())
+__attribute__((amdgpu_waves_per_eu(step_waves<Sys>::value))) void k_step(KArgs a) {
   step_tile<Sys, T, V, false>(a, VArgs{});
 }
 

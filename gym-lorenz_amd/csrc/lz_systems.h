@@ -365,6 +365,13 @@ struct SysHR {
   static constexpr int A = 2, O = 6, NI = 7;
   static constexpr bool kUsesAction = true, kNoise = true;
   static constexpr int kStepPlane = LZ_HR_STEP;
+#ifndef LZ_HR_PACKED
+#define LZ_HR_PACKED 1
+#endif
+#ifndef LZ_HR_STEP_WAVES
+#define LZ_HR_STEP_WAVES 6
+#endif
+  static constexpr int kStepWaves = sizeof(T) == 4 ? LZ_HR_STEP_WAVES : 1;  // k_step occupancy hint
   T m[3], s[3], sigma;
   float fa0, fa1;
   T pa, pb, pc, pd, pr, ps, pI, pxr, dt, h2, h6, sc, ms, tterm;
@@ -407,20 +414,22 @@ struct SysHR {
     d[1] = ((pc - pd * x2) - x[1]) + a1;
     d[2] = pr * (ps * (x[0] - pxr) - x[2]) + a2;
   }
+  // The stage sum ((k1 + 2 k2) + 2 k3) + k4 is accumulated as the stages complete --
+  // the same operations in the same order, with one stage live instead of four.
   __device__ void rk4(T* x, T a1, T a2) const {  // :100-113
-    T k1[3], k2[3], k3[3], k4[3], y[3];
-    rhs(x, a1, a2, k1);
+    T k[3], acc[3], y[3];
+    rhs(x, a1, a2, k);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) y[j] = x[j] + h2 * k1[j];
-    rhs(y, a1, a2, k2);
+    for (int j = 0; j < 3; ++j) { acc[j] = k[j]; y[j] = x[j] + h2 * k[j]; }
+    rhs(y, a1, a2, k);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) y[j] = x[j] + h2 * k2[j];
-    rhs(y, a1, a2, k3);
+    for (int j = 0; j < 3; ++j) { acc[j] = acc[j] + (T)2 * k[j]; y[j] = x[j] + h2 * k[j]; }
+    rhs(y, a1, a2, k);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) y[j] = x[j] + dt * k3[j];
-    rhs(y, a1, a2, k4);
+    for (int j = 0; j < 3; ++j) { acc[j] = acc[j] + (T)2 * k[j]; y[j] = x[j] + dt * k[j]; }
+    rhs(y, a1, a2, k);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) x[j] = x[j] + h6 * (((k1[j] + (T)2 * k2[j]) + (T)2 * k3[j]) + k4[j]);
+    for (int j = 0; j < 3; ++j) x[j] = x[j] + h6 * (acc[j] + k[j]);
   }
   // float32: master (actions 0, 0) and slave (a1, a2) RK4 steps as one packed
   // computation (lane pair = {master, slave}: v_pk_fma / v_pk_mul / v_pk_add), the
@@ -440,24 +449,24 @@ struct SysHR {
     d[2] = R * (S * (x[0] - XR) - x[2]) + act2;
   }
   __device__ void rk4_pair(T* xm, T* xs, float a1, float a2) {
-    f2 x[3], k1[3], k2[3], k3[3], k4[3], y[3];
+    f2 x[3], k[3], acc[3], y[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) x[j] = (f2){(float)xm[j], (float)xs[j]};
     const f2 u1 = {0.0f, a1}, u2 = {0.0f, a2};
     const f2 H2 = (f2)(float)h2, DT = (f2)(float)dt, H6 = (f2)(float)h6, TWO = (f2)2.0f;
-    rhs2(x, u1, u2, k1);
+    rhs2(x, u1, u2, k);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) y[j] = x[j] + H2 * k1[j];
-    rhs2(y, u1, u2, k2);
+    for (int j = 0; j < 3; ++j) { acc[j] = k[j]; y[j] = x[j] + H2 * k[j]; }
+    rhs2(y, u1, u2, k);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) y[j] = x[j] + H2 * k2[j];
-    rhs2(y, u1, u2, k3);
+    for (int j = 0; j < 3; ++j) { acc[j] = acc[j] + TWO * k[j]; y[j] = x[j] + H2 * k[j]; }
+    rhs2(y, u1, u2, k);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) y[j] = x[j] + DT * k3[j];
-    rhs2(y, u1, u2, k4);
+    for (int j = 0; j < 3; ++j) { acc[j] = acc[j] + TWO * k[j]; y[j] = x[j] + DT * k[j]; }
+    rhs2(y, u1, u2, k);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      x[j] = x[j] + H6 * (((k1[j] + TWO * k2[j]) + TWO * k3[j]) + k4[j]);
+      x[j] = x[j] + H6 * (acc[j] + k[j]);
       xm[j] = (T)x[j][0];
       xs[j] = (T)x[j][1];
     }
@@ -497,7 +506,7 @@ struct SysHR {
     }
     const float a1 = clip(f0, -1.0f, 1.0f) * 100.0f;       // :92-93 np.float32 * 100.0
     const float a2 = clip(f1, -1.0f, 1.0f) * 100.0f;
-    if constexpr (std::is_same<T, float>::value) {
+    if constexpr (std::is_same<T, float>::value && LZ_HR_PACKED) {
       rk4_pair(m, s, a1, a2);                              // both systems, packed f32
     } else {
       rk4(m, (T)0, (T)0);                                  // :100-105
