@@ -64,6 +64,10 @@ for step in "$@"; do
     attn_prof)
       export TMPDIR=/tmp
       run attn_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/attn_prof -o run --output-format csv -- python bench.py --mode policy --policy attn --system hr --envs 32768 --K 2048 --steps 4096 ;;
+    vecnorm_bench)
+      run vn_l3_1M 300 python bench.py --mode vecnorm --envs 1048576 --steps 2000 --warmup 200
+      run vn_pmsm_262k 300 python bench.py --mode vecnorm --system pmsm --envs 262144 --steps 2000 --warmup 200
+      run vn_pmsm_1M 300 python bench.py --mode vecnorm --system pmsm --envs 1048576 --steps 2000 --warmup 200 ;;
     split) run ab_split 600 python tools/ab_split.py 131072 1048576 ;;
     dist2) LZ_BENCH_BACKEND=gloo run dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 500 --warmup 64 --envs 262144 ;;
     pmc)
