@@ -53,6 +53,7 @@ def _random_attn(pol, O, A, seed, scale=0.3):
     ("hr", 1000, 12, dict(add_noise=True, add_filter=True, max_episode_steps=5)),
     ("pmsm", 777, 10, dict(add_noise=True, max_episode_steps=4)),
     ("lorenz3", 40000, 3, dict(max_episode_steps=2)),  # grid-stride: 313 groups > 256 CUs
+    ("hr", 5, 6, dict(max_episode_steps=2)),            # a single partial 32-env tile
 ])
 def test_attn_rollout_env_part_bitexact(gl, pol, system, n, K, kw):
     envp = gl.BatchedEnv(system, n, seed=11, **kw)
@@ -218,6 +219,8 @@ def _sb3_stacks(obs0, obs_r, done_r, didx, tobs, n, n_stack):
 @pytest.mark.parametrize("system,n,K,kw", [
     ("hr", 777, 11, dict(add_noise=True, add_filter=True, max_episode_steps=4)),
     ("lorenz3", 300, 7, dict(max_episode_steps=3)),
+    ("pmsm", 3, 5, dict(max_episode_steps=2)),          # a single partial 32-env tile
+    ("hr", 33000, 3, dict(max_episode_steps=2)),        # grid-stride: 258 groups > 256 CUs
 ])
 def test_attn_ln_framestack_rollout_bitexact(gl, pol, system, n, K, kw):
     """code/lorenz_filter/train.py's collection: VecFrameStack(4) + the LayerNorm
