@@ -85,10 +85,41 @@ def cpu_baseline(seconds):
         for k in range(steps):
             oracle.l3_step(st, acts[k % 8])
         dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": "oracle/lz_oracle.c orc_l3_step_float (scalar C restatement of "
-                      "dynamic.py:86-115), 65,536 envs x %d steps = %.2e env-steps in %.1f s, "
-                      "1 thread, GPU box host CPU" % (steps, n * steps, dt)}
+    out = {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+           "sample": "oracle/lz_oracle.c orc_l3_step_float (scalar C restatement of "
+                     "dynamic.py:86-115), 65,536 envs x %d steps = %.2e env-steps in %.1f s, "
+                     "1 thread, GPU box host CPU" % (steps, n * steps, dt)}
+    out["reference_loop"] = reference_loop_baseline(min(4.0, seconds / 3))
+    return out
+
+
+def reference_loop_baseline(seconds):
+    """The reference's own cost model on the same host core: dynamic.py's step() per env
+    object, driven by a DummyVecEnv-style Python loop (oracle/ref_loop.py restates it;
+    the reference itself does not travel to the GPU box)."""
+    import numpy as np
+
+    from oracle.ref_loop import LorenzRefEnv, dummy_vec_step
+
+    n = 1024
+    x0 = np.random.default_rng(0).uniform(-30, 30, (n, 3))
+    envs = [LorenzRefEnv(x) for x in x0]
+    acts = np.random.default_rng(1).uniform(-1, 1, (n, 3)).astype(np.float32)
+    bo, br = np.zeros((n, 6), np.float32), np.zeros(n, np.float32)
+    with np.errstate(all="ignore"):
+        t0 = time.perf_counter()
+        dummy_vec_step(envs, acts, bo, br)
+        per = time.perf_counter() - t0
+        steps = max(2, int(seconds / max(per, 1e-9)))
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            dummy_vec_step(envs, acts, bo, br)
+        dt = time.perf_counter() - t0
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1,
+            "kind": "reference-semantics Python loop",
+            "sample": "oracle/ref_loop.py: dynamic.py:61-90 step() per env object in a "
+                      "DummyVecEnv-style loop, %d envs x %d steps in %.1f s, 1 thread, GPU box "
+                      "host CPU" % (n, steps, dt)}
 
 
 def fp32_drift(gl, torch, device):

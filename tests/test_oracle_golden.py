@@ -190,3 +190,22 @@ def test_legacy_done_accumulators_never_fire(orc):
     for key in ("t1", "t2", "tp", "sc"):
         p = orc.PARAMS[key]
         assert orc.t_done_step(p[3], p[5]) == -1, key
+
+
+def test_ref_loop_restatement_matches_reference_fixture():
+    """oracle/ref_loop.py (bench.py's reference-semantics CPU baseline) reproduces the
+    reference's dynamic.py trajectories bit for bit (fixture from the reference)."""
+    import numpy as np
+
+    from conftest import golden
+    from oracle.ref_loop import LorenzRefEnv
+
+    g = golden("l3")
+    for e in range(g["x0"].shape[0]):
+        env = LorenzRefEnv(g["x0"][e])
+        with np.errstate(all="ignore"):
+            for k in range(200):
+                obs, rew, done, _ = env.step(g["actions"][e, k])
+                assert np.array_equal(obs, g["obs"][e, k], equal_nan=True)
+                assert (rew == g["reward"][e, k]) or (np.isnan(rew) and np.isnan(g["reward"][e, k]))
+                assert done == g["done"][e, k]
