@@ -193,7 +193,7 @@ def kernel_name(system, mode, n):
 def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
     """--mode vecnorm: one SB3 VecNormalize(norm_obs, norm_reward, clip_obs=10) step per
     step (code/lorenz_pmsm/train.py:170), fused: lz_step_vecnorm (step + float64 moments
-    + fixed-order reduction + RunningMeanStd updates) and lz_vecnorm_apply (normalised
+    + fixed-order reduction) and lz_vecnorm_apply (RunningMeanStd updates + normalised
     obs / reward / terminal rows, bool dones); actions / outputs in a 16-slot ring, a
     hipGraph of 64 steps.  Per-rank statistics (the all-reduce of the multi-GPU path,
     LZ_VN_DEFER, is not captured here)."""
@@ -281,7 +281,7 @@ def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": "k_step_vn + k_vn_reduce + k_vn_apply (one fused VecNormalize step)",
+            "kernel": "k_step_vn + k_vn_colsum + k_vn_apply (one fused VecNormalize step)",
             "avg_launch_us": step_s * 1e6, "bytes_per_env_step": bytes_step,
             "note": "achieved = algorithmic bytes of the whole fused step (lz_step's + 16 B of "
                     "float64 returns + the normalise pass: raw obs/reward/done read, normalised "

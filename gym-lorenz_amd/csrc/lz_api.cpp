@@ -95,6 +95,7 @@ struct lz_handle {
   double* pol_part;    // policy rollout obs-moment partials (lazily allocated)
   int64_t pol_part_n;  // doubles allocated
   uint8_t* vn_ws;      // lz_step_vecnorm moment partials (lazily allocated)
+  int vn_pending;      // lz_step_vecnorm left totals for lz_vecnorm_apply's updates
 };
 
 extern "C" {
@@ -445,8 +446,8 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
   const int64_t n = h->cfg.num_envs;
   const int64_t n_wg = (n + lz::kBlock - 1) / lz::kBlock;
   if (!h->vn_ws) {  // column-major per-workgroup partials, W = 2 (kVnMaxObs + 1) at most,
-                    // then the W column totals
-    const size_t bytes = (size_t)(n_wg + 1) * 2 * (lz::kVnMaxObs + 1) * sizeof(double);
+                    // then the W column totals and the statistics snapshot
+    const size_t bytes = (size_t)(n_wg + 2) * 2 * (lz::kVnMaxObs + 1) * sizeof(double);
     if (hipMalloc(reinterpret_cast<void**>(&h->vn_ws), bytes) != hipSuccess)
       return fail(LZ_ERR_OOM, "vecnorm workspace (%zu B)", bytes);
   }
@@ -464,6 +465,7 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
   v.returns = vn->returns;
   v.part = reinterpret_cast<double*>(h->vn_ws);
   v.tot = v.part + (size_t)n_wg * 2 * (lz::kVnMaxObs + 1);
+  v.old = v.tot + 2 * (lz::kVnMaxObs + 1);
   v.n_done_out = n_done_out;
   v.obs_state = lz::rms_state(vn->obs_rms);
   v.ret_state = lz::rms_state(vn->ret_rms);
@@ -474,6 +476,7 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
   const int e = lz::launch_step_vecnorm(h->cfg.system, h->f64, a, v, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "step launch: %s", hipGetErrorString((hipError_t)e));
   h->parity ^= 1;
+  h->vn_pending = (vn->flags & LZ_VN_TRAINING) && !(vn->flags & LZ_VN_DEFER);
   return LZ_OK;
 }
 
@@ -499,12 +502,24 @@ lz_status lz_vecnorm_apply(lz_handle* h, const lz_vecnorm* vn, const void* obs_r
     if (e == 0) e = lz::launch_rms_update(vn->ret_rms, vn->moments + 2 * O + 1, h->stream);
     if (e != 0) return fail(LZ_ERR_HIP, "statistics update: %s", hipGetErrorString((hipError_t)e));
   }
+  // the RunningMeanStd updates of the preceding lz_step_vecnorm (training, not
+  // deferred) are applied by this normalise pass
+  lz::VnUpdate upd{};
+  if (h->vn_pending && (vn->flags & LZ_VN_TRAINING) && !(vn->flags & LZ_VN_DEFER)) {
+    const int64_t n_wg = (h->cfg.num_envs + lz::kBlock - 1) / lz::kBlock;
+    const double* tot = reinterpret_cast<const double*>(h->vn_ws) + (size_t)n_wg * 2 * (lz::kVnMaxObs + 1);
+    upd.tot = tot;
+    upd.old = tot + 2 * (lz::kVnMaxObs + 1);
+    upd.batch = (double)h->cfg.num_envs;
+    upd.upd_obs = (vn->flags & LZ_VN_NORM_OBS) != 0;
+  }
+  h->vn_pending = 0;
   const int e = lz::launch_vn_apply(
       h->f64, O, h->cfg.num_envs, obs_raw, rew_raw, done, term ? terminal_obs_raw : nullptr,
       term ? n_done : nullptr, lz::rms_state(vn->obs_rms), lz::rms_state(vn->ret_rms),
       (vn->flags & LZ_VN_NORM_OBS) != 0, (vn->flags & LZ_VN_NORM_REWARD) != 0, vn->epsilon,
       vn->clip_obs, vn->clip_reward, obs_norm, rew_norm, dones_out, term ? term_norm : nullptr,
-      h->stream);
+      upd, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "normalise launch: %s", hipGetErrorString((hipError_t)e));
   return LZ_OK;
 }

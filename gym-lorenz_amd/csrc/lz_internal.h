@@ -52,12 +52,14 @@ struct KArgs {
 // VecNormalize epilogue of the step kernel (lz_step_vecnorm).  Per-workgroup float64
 // partials of the batch moments, column-major [W][n_wg] with W = 2 (O + 1) columns:
 // sums of obs column 0..O-1, of the returns, then the sums of squares likewise;
-// k_vn_reduce (the next launch) reduces them and updates the statistics.
+// k_vn_colsum (the next launch) reduces them; the normalise pass of lz_vecnorm_apply
+// applies the statistics updates.
 constexpr int kVnMaxObs = 8;
 struct VArgs {
   double* returns;     // [N] VecNormalize.returns
   double* part;        // [W][n_wg]
-  double* tot;         // [W] column totals (k_vn_colsum -> k_vn_update)
+  double* tot;         // [W] column totals (k_vn_colsum -> the normalise pass)
+  double* old;         // [2O+1 obs][3 returns] statistics snapshot taken by k_vn_colsum
   double* obs_state;   // obs_rms mean[O], var[O], count
   double* ret_state;   // ret_rms mean, var, count
   double* moments;     // LZ_VN_DEFER: [2O+1 obs][3 returns] batch moments out
@@ -171,13 +173,22 @@ int rms_device(const lz_rms* r);
 double* rms_state(lz_rms* r);  // mean[dim], var[dim], count
 // RunningMeanStd.update_from_moments on `stream` (moments: count, sums, sums of squares)
 int launch_rms_update(lz_rms* r, const double* moments, void* stream);
+// The RunningMeanStd updates folded into the normalise pass (training, not deferred):
+// every workgroup derives the new statistics from the snapshot + column totals the
+// step's k_vn_colsum left, workgroup 0 writes them back.
+struct VnUpdate {
+  const double* tot;   // [2 (O + 1)] column totals (nullptr: no update in this pass)
+  const double* old;   // [2O+1 obs][3 returns] snapshot of the statistics
+  double batch;        // batch count n
+  int upd_obs;         // obs_rms.update (TRAINING and NORM_OBS)
+};
 // normalised obs [n, O] / reward [n] / 0-1 dones [n] / terminal rows [*n_done, O]
 // (lz_vecnorm_apply)
 int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
                     const uint8_t* done, const void* term, const int32_t* n_done,
-                    const double* obs_state, const double* ret_state, int norm_obs, int norm_rew,
+                    double* obs_state, double* ret_state, int norm_obs, int norm_rew,
                     double eps, double clip_obs, double clip_rew, float* obs_n, float* rew_n,
-                    uint8_t* dones, float* term_n, void* stream);
+                    uint8_t* dones, float* term_n, const VnUpdate& upd, void* stream);
 
 // record the thread-local message lz_last_error() returns; returns s
 lz_status set_error(lz_status s, const char* msg);

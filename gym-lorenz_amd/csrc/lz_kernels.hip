@@ -111,8 +111,8 @@ constexpr int step_block() {  // bits 3-4 of V: workgroup size
 // (lz_step_vecnorm, lz_internal.h VArgs).  Per-workgroup float64 moments of the obs
 // columns (read back from the LDS obs tile) and of the updated returns: each column
 // summed by 32 lanes over strided rows, then a fixed xor tree; one plain store per
-// column into the column-major partials.  k_vn_colsum / k_vn_update, the next launches
-// on the stream, sum them in a fixed order (no cross-workgroup synchronisation inside the step: an
+// column into the column-major partials.  k_vn_colsum, the next launch on the stream,
+// sums them in a fixed order (no cross-workgroup synchronisation inside the step: an
 // in-kernel last-arriver reduction needs every workgroup to wait for its stores'
 // acknowledgements before taking a ticket, which measured 4x the step time at 1M envs).
 template <int O, typename T>
@@ -149,14 +149,25 @@ __device__ __forceinline__ void vn_epilogue(const T* s_obs, const double* s_ret,
 // ... into accumulator u of rows t + 256 u (mod 1024), the 4 accumulators in order,
 // then a fixed LDS tree -- and stores the column total.  (A single workgroup for all
 // columns measured 11.5 us per 1M-env step; a column per workgroup spreads the 458 KB
-// of partials over 14 CUs.)  Block 0 also publishes the step's done count.
+// of partials over 14 CUs.)  With LZ_VN_DEFER each total goes to its slot of the
+// moments vector for the caller's all-reduce; otherwise workgroup 0 snapshots the
+// statistics, and lz_vecnorm_apply's normalise pass applies the RunningMeanStd updates
+// (no separate update launch).  Block 0 also publishes the step's done count.
 constexpr int kVnColBlock = 256;
-__global__ __launch_bounds__(kVnColBlock) void k_vn_colsum(VArgs v, const int32_t* counter,
+template <int O>
+__global__ __launch_bounds__(kVnColBlock) void k_vn_colsum(VArgs v, int64_t n,
+                                                          const int32_t* counter,
                                                           int32_t* n_done_out) {
+  constexpr int C = O + 1;
   __shared__ double red[kVnColBlock];
   const int tid = (int)threadIdx.x, c = (int)blockIdx.x;
   if (c == 0 && tid == 0) *n_done_out = *counter;
   if (!(v.flags & LZ_VN_TRAINING)) return;
+  const bool defer = (v.flags & LZ_VN_DEFER) != 0;
+  if (c == 0 && !defer) {  // statistics as they were before this step
+    if (tid < 2 * O + 1) v.old[tid] = v.obs_state[tid];
+    if (tid < 3) v.old[2 * O + 1 + tid] = v.ret_state[tid];
+  }
   const double* col = v.part + (int64_t)c * v.n_wg;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   for (int r = tid; r < v.n_wg; r += 4 * kVnColBlock) {
@@ -173,48 +184,15 @@ __global__ __launch_bounds__(kVnColBlock) void k_vn_colsum(VArgs v, const int32_
     if (tid < half) red[tid] += red[tid + half];
     __syncthreads();
   }
-  if (tid == 0) v.tot[c] = red[0];
-}
-
-// The RunningMeanStd updates from the column totals (lz_rms_math.h, as k_rms_update)
-// or, with LZ_VN_DEFER, the moments for the caller's all-reduce.  One wave.
-template <int O>
-__global__ __launch_bounds__(64) void k_vn_update(VArgs v, int64_t n) {
-  constexpr int C = O + 1;
-  if (!(v.flags & LZ_VN_TRAINING)) return;
-  const int tid = (int)threadIdx.x;
-  const double* s_tot = v.tot;
-  const double bc = (double)n;
-  if (v.flags & LZ_VN_DEFER) {  // (count, sums, sumsq) for obs, then for returns
-    if (tid < O) {
-      v.moments[1 + tid] = s_tot[tid];
-      v.moments[1 + O + tid] = s_tot[C + tid];
+  if (tid != 0) return;
+  v.tot[c] = red[0];
+  if (defer) {  // (count, sums[O], sumsq[O]) for obs, then (count, sum, sumsq) for returns
+    const int slot = c < O ? 1 + c : c == O ? 2 * O + 2 : c < C + O ? 1 + O + (c - C) : 2 * O + 3;
+    v.moments[slot] = red[0];
+    if (c == 0) {
+      v.moments[0] = (double)n;
+      v.moments[2 * O + 1] = (double)n;
     }
-    if (tid == 0) {
-      v.moments[0] = bc;
-      v.moments[2 * O + 1] = bc;
-      v.moments[2 * O + 2] = s_tot[O];
-      v.moments[2 * O + 3] = s_tot[C + O];
-    }
-    return;
-  }
-  const bool upd_obs = (v.flags & LZ_VN_NORM_OBS) && tid < O;
-  const bool upd_ret = tid == 32;
-  const double c_obs = v.obs_state[2 * O], c_ret = v.ret_state[2];
-  double nm = 0.0, nv = 0.0;
-  if (upd_obs)
-    rms_new(v.obs_state[tid], v.obs_state[O + tid], c_obs, bc, s_tot[tid], s_tot[C + tid], nm, nv);
-  if (upd_ret) rms_new(v.ret_state[0], v.ret_state[1], c_ret, bc, s_tot[O], s_tot[C + O], nm, nv);
-  __syncthreads();  // every lane has read the counts before they are rewritten
-  if (upd_obs) {
-    v.obs_state[tid] = nm;
-    v.obs_state[O + tid] = nv;
-    if (tid == 0) v.obs_state[2 * O] = c_obs + bc;
-  }
-  if (upd_ret) {
-    v.ret_state[0] = nm;
-    v.ret_state[1] = nv;
-    v.ret_state[2] = c_ret + bc;
   }
 }
 
@@ -798,9 +776,8 @@ template <class Sys, typename T>
 static int launch_vn(const KArgs& a, const VArgs& v, hipStream_t s) {
   static_assert(Sys::O <= kVnMaxObs, "obs too wide for the VecNormalize epilogue");
   hipLaunchKernelGGL((k_step_vn<Sys, T>), dim3((unsigned)grid_for(a.n)), dim3(kBlock), 0, s, a, v);
-  hipLaunchKernelGGL(k_vn_colsum, dim3(2 * (Sys::O + 1)), dim3(kVnColBlock), 0, s, v, a.counter,
-                     v.n_done_out);
-  hipLaunchKernelGGL((k_vn_update<Sys::O>), dim3(1), dim3(64), 0, s, v, a.n);
+  hipLaunchKernelGGL((k_vn_colsum<Sys::O>), dim3(2 * (Sys::O + 1)), dim3(kVnColBlock), 0, s, v,
+                     a.n, a.counter, v.n_done_out);
   return (int)hipGetLastError();
 }
 

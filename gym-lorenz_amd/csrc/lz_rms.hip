@@ -154,8 +154,9 @@ struct VnApplyArgs {
   const void* term;
   const uint8_t* done;
   const int32_t* n_done;
-  const double* os;  // obs_rms mean[O], var[O], count
-  const double* rs;  // ret_rms mean, var, count
+  double* os;        // obs_rms mean[O], var[O], count
+  double* rs;        // ret_rms mean, var, count
+  lz::VnUpdate upd;  // statistics updates folded into this pass (upd.tot != nullptr)
   double eps, clip_obs, clip_rew;
   float* obs_n;
   float* rew_n;
@@ -170,11 +171,52 @@ template <typename T, int O>
 __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
   constexpr int R = (O % 4 == 0) ? 1 : (O % 2 == 0 ? 2 : 4);
   constexpr int E = R * O;
-  double mean[O], sd[O];
+  double mean[O], sd[O], rsd;
+  if (p.upd.tot) {
+    // RunningMeanStd.update_from_moments for every obs column (lanes 0..O-1) and the
+    // returns (lane 64), from the pre-step snapshot -- so no workgroup reads statistics
+    // that workgroup 0 is rewriting -- then broadcast through LDS
+    __shared__ double s_st[2 * O + 1];
+    const int t = (int)threadIdx.x;
+    const double* old = p.upd.old;
+    const double bc = p.upd.batch;
+    if (t < O) {
+      double nm = old[t], nv = old[O + t];
+      if (p.upd.upd_obs)
+        lz::rms_new(old[t], old[O + t], old[2 * O], bc, p.upd.tot[t], p.upd.tot[O + 1 + t], nm, nv);
+      s_st[t] = nm;
+      s_st[O + t] = sqrt(nv + p.eps);
+      if (blockIdx.x == 0 && p.upd.upd_obs) {
+        p.os[t] = nm;
+        p.os[O + t] = nv;
+        if (t == 0) p.os[2 * O] = old[2 * O] + bc;
+      }
+    }
+    if (t == 64) {
+      const double* r = old + 2 * O + 1;
+      double nm, nv;
+      lz::rms_new(r[0], r[1], r[2], bc, p.upd.tot[O], p.upd.tot[2 * O + 1], nm, nv);
+      s_st[2 * O] = sqrt(nv + p.eps);
+      if (blockIdx.x == 0) {
+        p.rs[0] = nm;
+        p.rs[1] = nv;
+        p.rs[2] = r[2] + bc;
+      }
+    }
+    __syncthreads();
 #pragma unroll
-  for (int d = 0; d < O; ++d) {
-    mean[d] = p.os[d];
-    sd[d] = sqrt(p.os[O + d] + p.eps);
+    for (int d = 0; d < O; ++d) {
+      mean[d] = s_st[d];
+      sd[d] = s_st[O + d];
+    }
+    rsd = s_st[2 * O];
+  } else {
+#pragma unroll
+    for (int d = 0; d < O; ++d) {
+      mean[d] = p.os[d];
+      sd[d] = sqrt(p.os[O + d] + p.eps);
+    }
+    rsd = sqrt(p.rs[1] + p.eps);
   }
   const T* obs = static_cast<const T*>(p.obs);
   if ((int)blockIdx.x < p.row_blocks) {
@@ -220,7 +262,6 @@ __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
         if (r0 + e / O < p.n) p.obs_n[r0 * O + e] = y[e];
     }
     const T* rew = static_cast<const T*>(p.rew);
-    const double rsd = sqrt(p.rs[1] + p.eps);
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       if (r0 + k >= p.n) break;
@@ -275,9 +316,9 @@ int launch_rms_update(lz_rms* r, const double* moments, void* stream) {
 
 int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
                     const uint8_t* done, const void* term, const int32_t* n_done,
-                    const double* obs_state, const double* ret_state, int norm_obs, int norm_rew,
+                    double* obs_state, double* ret_state, int norm_obs, int norm_rew,
                     double eps, double clip_obs, double clip_rew, float* obs_n, float* rew_n,
-                    uint8_t* dones, float* term_n, void* stream) {
+                    uint8_t* dones, float* term_n, const VnUpdate& upd, void* stream) {
   if (n == 0) return 0;
   const int R = (O % 4 == 0) ? 1 : (O % 2 == 0 ? 2 : 4);
   VnApplyArgs p;
@@ -289,6 +330,7 @@ int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
   p.n_done = n_done;
   p.os = obs_state;
   p.rs = ret_state;
+  p.upd = upd;
   p.eps = eps;
   p.clip_obs = clip_obs;
   p.clip_rew = clip_rew;

@@ -447,10 +447,12 @@ lz_status lz_returns_update(double* returns, const void* rew, int32_t dtype, con
  *   rew_out  = NORM_REWARD ? clip(reward/sqrt(ret_var + eps), +-clip_reward) : reward
  *   terminal observations normalised like obs; returns[done] = 0
  * lz_step_vecnorm runs the env step (its kernel also writes float64 per-workgroup
- * moment partials of the obs and of the updated returns) and a one-workgroup
- * reduction in a fixed order (deterministic, no float atomics) that applies the two
- * RunningMeanStd updates -- two launches; lz_vecnorm_apply (one launch) writes the
- * normalised outputs.  With LZ_VN_DEFER the reduction leaves the batch moments (obs:
+ * moment partials of the obs and of the updated returns) and a column-per-workgroup
+ * reduction in a fixed order (deterministic, no float atomics) -- two launches;
+ * lz_vecnorm_apply (one launch) applies the two RunningMeanStd updates (every
+ * workgroup derives them from the step's totals; workgroup 0 writes them back) and
+ * writes the normalised outputs: the statistics are updated once lz_vecnorm_apply has
+ * run, so call the two as a pair.  With LZ_VN_DEFER the reduction leaves the batch moments (obs:
  * count, sums[O], sumsq[O]; then returns: count, sum, sumsq) in moments for a
  * multi-GPU all-reduce and lz_vecnorm_apply performs the updates first.  Every
  * pointer is device memory; the statistics are those of the two lz_rms objects (dims
