@@ -671,12 +671,18 @@ __device__ __forceinline__ void net_fwd(const uint8_t* net, const float* x, bool
   }
 }
 
+// The kernel variants (template parameter kPair of k_rollout_policy): the MlpPolicy
+// nets one after the other / interleaved / interleaved with pipelined weight loads,
+// code/train.py's attention actor-critic, code/lorenz_filter/train.py's residual +
+// LayerNorm attention actor-critic on VecFrameStack observations.
+constexpr int kMlpSerial = 0, kMlpPair = 1, kMlpPairPipe = 2, kAttn = 3, kAttnLn = 4;
+
 // V(x) alone (truncation bootstrap, last values): the value net, after the shared
-// attention extractor for kPair == 3
+// attention extractor for kPair == kAttn
 template <int E, int O, int kPair>
 __device__ __forceinline__ void value_fwd(const uint8_t* blob, const uint8_t* vf_net, const float* x,
                                           bool use, int lane, float* out) {
-  if constexpr (kPair == 3) {
+  if constexpr (kPair == kAttn) {
     bf16x8 f[4];
     attn_extract(blob, obs_frag<O>(x, use), lane, f);
     out[0] = attn_net(blob + kAttVf, f, lane)[0];
@@ -685,25 +691,24 @@ __device__ __forceinline__ void value_fwd(const uint8_t* blob, const uint8_t* vf
   }
 }
 
-// kPair: 0 = the nets one after the other, 1 = interleaved (mlp_pair),
-// 2 = interleaved + pipelined weight loads (mlp_pair_pipe), 3 = the attention-extractor
-// actor-critic (kAtt* blob: attn_extract + attn_nets_pair)
-// 4 = the residual + LayerNorm attention actor-critic on VecFrameStack(S) observations
-// (kLn* blob: attn_ln_extract + attn_nets_pair; the S-frame stack lives in the
-// registers of both lane halves of the env)
+// kPair (see kMlpSerial ...): kMlpPair = mlp_pair, kMlpPairPipe = mlp_pair_pipe,
+// kAttn = attn_extract + attn_nets_pair (kAtt* blob), kAttnLn = attn_ln_extract +
+// attn_nets_pair (kLn* blob) with the S-frame stack in the registers of both lane
+// halves of the env
 template <class Sys, int W, int E, int kPair, int S = 1>
 __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
-  static_assert(!kPair || E == 32, "the interleaved pair runs 32-env tiles");
-  constexpr int kBlob = kPair == 4 ? kLnBlobBytes : kPair == 3 ? kAttBlobBytes : kPolBlobBytes;
+  static_assert(kPair == kMlpSerial || E == 32, "the paired / attention kernels run 32-env tiles");
+  constexpr int kBlob =
+      kPair == kAttnLn ? kLnBlobBytes : kPair == kAttn ? kAttBlobBytes : kPolBlobBytes;
   constexpr int O = Sys::O, A = Sys::A;
-  constexpr int SO = S * O, KS = (SO + 15) / 16;  // kPair 4: stacked dims, fc1 k-steps
-  static_assert(kPair == 4 || S == 1, "frame stacking is the kPair 4 path");
+  constexpr int SO = S * O, KS = (SO + 15) / 16;  // kAttnLn: stacked dims, fc1 k-steps
+  static_assert(kPair == kAttnLn || S == 1, "frame stacking is the kAttnLn path");
   static_assert(SO <= kLnMaxIn, "stacked obs dims");
   static_assert(O <= kPolMaxObs && A <= kPolMaxAct, "policy tile shape");
   static_assert(E == 32 || E == 64, "envs per wave");
   __shared__ __attribute__((aligned(64))) uint8_t s_blob[kBlob];
   __shared__ double s_norm[2 * kPolMaxObs];
-  __shared__ double s_mom[kPair == 4 ? 1 : W * E * 2 * O];  // kPair 4: no obs moments
+  __shared__ double s_mom[kPair == kAttnLn ? 1 : W * E * 2 * O];  // kAttnLn: no obs moments
   const int tid = (int)threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int slot = E == 64 ? lane : (lane & 31);  // this lane's env within the tile
@@ -723,13 +728,13 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
     *a.tick_out = tick + a.tick_adv;
   }
   __syncthreads();
-  const uint8_t* pi_net = s_blob + (kPair == 4 ? kLnPi : kPair == 3 ? kAttPi : 0);
-  const uint8_t* vf_net = s_blob + (kPair == 4 ? kLnVf : kPair == 3 ? kAttVf : kPolNet);
+  const uint8_t* pi_net = s_blob + (kPair == kAttnLn ? kLnPi : kPair == kAttn ? kAttPi : 0);
+  const uint8_t* vf_net = s_blob + (kPair == kAttnLn ? kLnVf : kPair == kAttn ? kAttVf : kPolNet);
   // torch.distributions.Normal constants, computed by the packer: scale = exp(log_std),
   // 2 * scale**2, log(scale) (LDS, wave-uniform broadcast reads)
   const float* g_scale =
       reinterpret_cast<const float*>(
-          s_blob + (kPair == 4 ? kLnLogStd : kPair == 3 ? kAttLogStd : kPolLogStd)) + 4;
+          s_blob + (kPair == kAttnLn ? kLnLogStd : kPair == kAttn ? kAttLogStd : kPolLogStd)) + 4;
   const float* g_var2 = g_scale + 4;
   const float* g_lscale = g_scale + 8;
   const bool norm = p.norm != nullptr;
@@ -739,8 +744,8 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   const bool boot = (p.pflags & LZ_POLICY_BOOTSTRAP) != 0;
   const float gamma = p.gamma;
   // per-lane float64 obs-moment accumulators of the env-owning lanes, in LDS
-  double* mom = s_mom + (kPair == 4 ? 0 : (wave * E + slot) * (2 * O));
-  if constexpr (kPair != 4) {
+  double* mom = s_mom + (kPair == kAttnLn ? 0 : (wave * E + slot) * (2 * O));
+  if constexpr (kPair != kAttnLn) {
     if (owner) {
 #pragma unroll
       for (int j = 0; j < 2 * O; ++j) mom[j] = 0.0;
@@ -766,9 +771,9 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
 #pragma unroll
       for (int j = 0; j < O; ++j) o[j] = p.obs_in[i * O + j];
     }
-    const bool valid = i < a.n;  // kPair 4: both halves of the env's lanes
-    float st[kPair == 4 ? SO : 1];
-    if constexpr (kPair == 4) {
+    const bool valid = i < a.n;  // kAttnLn: both halves of the env's lanes
+    float st[kPair == kAttnLn ? SO : 1];
+    if constexpr (kPair == kAttnLn) {
 #pragma unroll
       for (int j = 0; j < SO; ++j) st[j] = valid ? p.stack_in[i * SO + j] : 0.0f;
     }
@@ -779,7 +784,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
     for (int k = 0; k < a.K; ++k) {
       const int64_t off = (int64_t)k * a.n + i;
       float x[O];
-      if constexpr (kPair == 4) {
+      if constexpr (kPair == kAttnLn) {
         if (live) {  // the stacked observation the policy sees
 #pragma unroll
           for (int j = 0; j < SO; ++j) obs_buf[off * SO + j] = st[j];
@@ -792,7 +797,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
         }
       }
       float mean[A], val[1];
-      if constexpr (kPair == 4) {
+      if constexpr (kPair == kAttnLn) {
         f32x16 hp, hv;
         bf16x8 xs[KS], f[4];
         stack_frags<SO, KS>(st, h, valid, xs);
@@ -801,7 +806,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
 #pragma unroll
         for (int j = 0; j < A; ++j) mean[j] = hp[j];
         val[0] = hv[0];
-      } else if constexpr (kPair == 3) {
+      } else if constexpr (kPair == kAttn) {
         f32x16 hp, hv;
         bf16x8 f[4];
         attn_extract(s_blob, obs_frag<O>(x, live), lane, f);
@@ -809,9 +814,10 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
 #pragma unroll
         for (int j = 0; j < A; ++j) mean[j] = hp[j];
         val[0] = hv[0];
-      } else if constexpr (kPair) {
+      } else if constexpr (kPair == kMlpPair || kPair == kMlpPairPipe) {
         f32x16 hp, hv;
-        if constexpr (kPair == 2) mlp_pair_pipe(pi_net, vf_net, obs_frag<O>(x, live), lane, hp, hv);
+        if constexpr (kPair == kMlpPairPipe)
+          mlp_pair_pipe(pi_net, vf_net, obs_frag<O>(x, live), lane, hp, hv);
         else mlp_pair(pi_net, vf_net, obs_frag<O>(x, live), lane, hp, hv);
 #pragma unroll
         for (int j = 0; j < A; ++j) mean[j] = hp[j];
@@ -847,7 +853,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
                                                            tick + (uint64_t)k, k, on, rew,
                                                            did_reset, ot);
       any_reset = any_reset || did_reset;
-      if constexpr (kPair == 4) {
+      if constexpr (kPair == kAttnLn) {
         // VecFrameStack (SB3 StackedObservations.update): the partner half receives the
         // env's new / terminal frames and done byte; both halves roll the stack; a done
         // env's terminal observation is [rolled stack, terminal frame], its stack
@@ -891,7 +897,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       if (live) {
         rew_buf[off] = rew;
         a.done[off] = df;
-        if (kPair != 4 && p.partials) {
+        if (kPair != kAttnLn && p.partials) {
 #pragma unroll
           for (int j = 0; j < O; ++j) {
             const double v = (double)on[j];
@@ -904,7 +910,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       for (int j = 0; j < O; ++j) o[j] = on[j];
     }
     float vl[1];
-    if constexpr (kPair == 4) {
+    if constexpr (kPair == kAttnLn) {
       bf16x8 xs[KS], f[4];
       stack_frags<SO, KS>(st, h, valid, xs);
       attn_ln_extract<KS>(s_blob, xs, lane, f);
@@ -927,7 +933,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
     }
   }
-  if (kPair != 4 && p.partials) {  // fixed-order butterfly over the wave: deterministic
+  if (kPair != kAttnLn && p.partials) {  // fixed-order butterfly over the wave: deterministic
     double* dst = p.partials + ((int64_t)blockIdx.x * W + wave) * (2 * O);
 #pragma unroll
     for (int j = 0; j < 2 * O; ++j) {
@@ -986,13 +992,13 @@ template <class Sys>
 static int launch_pol(const KArgs& a, const PArgs& p, const PolShape& sh, hipStream_t s) {
   const dim3 grid((unsigned)sh.grid);
   if (sh.envs_per_wave == 64)
-    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 64, 0>), grid, dim3(8 * 64), 0, s, a, p);
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 64, kMlpSerial>), grid, dim3(8 * 64), 0, s, a, p);
   else if (sh.pair == 2)
-    hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, 2>), grid, dim3(4 * 64), 0, s, a, p);
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, kMlpPairPipe>), grid, dim3(4 * 64), 0, s, a, p);
   else if (sh.pair)
-    hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, 1>), grid, dim3(4 * 64), 0, s, a, p);
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, kMlpPair>), grid, dim3(4 * 64), 0, s, a, p);
   else
-    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 32, 0>), grid, dim3(8 * 64), 0, s, a, p);
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 32, kMlpSerial>), grid, dim3(8 * 64), 0, s, a, p);
   return (int)hipGetLastError();
 }
 
@@ -1021,7 +1027,7 @@ PolShape attn_policy_shape(int64_t n, int num_cus) {
 
 template <class Sys>
 static int launch_pol_attn(const KArgs& a, const PArgs& p, const PolShape& sh, hipStream_t s) {
-  hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, 3>), dim3((unsigned)sh.grid), dim3(4 * 64), 0, s,
+  hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, kAttn>), dim3((unsigned)sh.grid), dim3(4 * 64), 0, s,
                      a, p);
   return (int)hipGetLastError();
 }
@@ -1046,8 +1052,8 @@ template <class Sys>
 static int launch_pol_attn_ln(int n_stack, const KArgs& a, const PArgs& p, const PolShape& sh,
                               hipStream_t s) {
   const dim3 grid((unsigned)sh.grid), block(4 * 64);
-  if (n_stack == 4) hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, 4, 4>), grid, block, 0, s, a, p);
-  else if (n_stack == 1) hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, 4, 1>), grid, block, 0, s, a, p);
+  if (n_stack == 4) hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, kAttnLn, 4>), grid, block, 0, s, a, p);
+  else if (n_stack == 1) hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, kAttnLn, 1>), grid, block, 0, s, a, p);
   else return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
