@@ -96,6 +96,9 @@ struct lz_handle {
   int64_t pol_part_n;  // doubles allocated
   uint8_t* vn_ws;      // lz_step_vecnorm moment partials (lazily allocated)
   int vn_pending;      // lz_step_vecnorm left totals for lz_vecnorm_apply's updates
+  uint8_t* hs_pin;     // lz_step_host: mapped host staging (actions | noise || obs | rew | done)
+  uint8_t* hs_dev;     // lz_step_host: its device address
+  size_t hs_in, hs_out;  // bytes of the input / output parts
 };
 
 extern "C" {
@@ -280,6 +283,7 @@ lz_status lz_destroy(lz_handle* h) {
   if (h->bc) (void)hipFree(h->bc);
   if (h->pol_part) (void)hipFree(h->pol_part);
   if (h->vn_ws) (void)hipFree(h->vn_ws);
+  if (h->hs_pin) (void)hipHostFree(h->hs_pin);  // hs_dev is its mapped device address
   delete h;
   return LZ_OK;
 }
@@ -414,6 +418,49 @@ lz_status lz_step(lz_handle* h, const void* actions, const double* noise, void* 
   if (n_done_out)
     HIP_TRY(hipMemcpyAsync(n_done_out, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
   h->parity ^= 1;
+  return LZ_OK;
+}
+
+static size_t align16(size_t b) { return (b + 15) & ~(size_t)15; }
+
+lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, void* obs_out,
+                       void* rew_out, uint8_t* done_out) {
+  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_step_host before the first lz_reset");
+  const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4 && h->cfg.system != LZ_SYS_SC;
+  if ((needs_act && !actions) || !obs_out || !rew_out || !done_out)
+    return fail(LZ_ERR_INVALID, "actions/obs_out/rew_out/done_out must be non-NULL");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  const int64_t n = h->cfg.num_envs;
+  const size_t es = h->f64 ? 8 : 4;
+  const size_t b_act = (size_t)n * h->desc.action_dim * 4, b_nz = (size_t)n * 3 * 8;
+  const size_t b_obs = (size_t)n * h->desc.obs_dim * es, b_rew = (size_t)n * es;
+  const size_t o_nz = align16(b_act), in = align16(o_nz + b_nz);
+  const size_t o_rew = align16(b_obs), o_done = align16(o_rew + b_rew), out = o_done + (size_t)n;
+  if (!h->hs_pin) {
+    // host memory mapped into the device's address space: the step kernel reads the
+    // actions and writes its outputs over PCIe, no copy launches
+    if (hipHostMalloc(reinterpret_cast<void**>(&h->hs_pin), in + out,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return fail(LZ_ERR_OOM, "lz_step_host: mapped staging (%zu B)", in + out);
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, h->hs_pin, 0) != hipSuccess || !dp)
+      return fail(LZ_ERR_HIP, "lz_step_host: no device address for the mapped staging");
+    h->hs_dev = static_cast<uint8_t*>(dp);
+    h->hs_in = in;
+    h->hs_out = out;
+  }
+  if (needs_act) std::memcpy(h->hs_pin, actions, b_act);
+  if (noise) std::memcpy(h->hs_pin + o_nz, noise, b_nz);
+  uint8_t* d_out = h->hs_dev + in;
+  const lz_status st = lz_step(h, needs_act ? h->hs_dev : nullptr,
+                               noise ? reinterpret_cast<const double*>(h->hs_dev + o_nz) : nullptr,
+                               d_out, d_out + o_rew, d_out + o_done, nullptr, nullptr, nullptr);
+  if (st != LZ_OK) return st;
+  HIP_TRY(hipStreamSynchronize(h->stream));  // (a hipStreamQuery spin measured no faster)
+  std::memcpy(obs_out, h->hs_pin + in, b_obs);
+  std::memcpy(rew_out, h->hs_pin + in + o_rew, b_rew);
+  std::memcpy(done_out, h->hs_pin + in + o_done, (size_t)n);
   return LZ_OK;
 }
 

@@ -7,6 +7,14 @@ fails with LZ_ERR_HIP / LZ_ERR_INVALID and LorenzEnvError is raised.
 import ctypes
 import os
 
+# torch first: its ROCm wheel brings its own libamdhip64 / libhsa-runtime64, and the
+# process must end up with torch's HSA runtime shared by both HIP runtimes.  Loading
+# this library before torch (i.e. `import gym_lorenz` before `import torch`) leaves
+# /opt/rocm's HSA runtime in the process, under which this library's hipGetDeviceCount
+# finds no device on the MI355X boxes (measured; tests/test_gpu_parity.py::
+# test_import_order_gym_lorenz_first).
+import torch  # noqa: F401
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # LZ_LIB_AB: an alternative build of the same library, for A/B timing tools only
 LIB_PATH = os.environ.get("LZ_LIB_AB") or os.path.join(_HERE, "libgym_lorenz_amd.so")
@@ -147,6 +155,7 @@ _SIGS = {
     "lz_reset": (ctypes.c_int, [VP, VP, VP, VP]),
     "lz_step": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, VP, VP, VP]),
     "lz_rollout": (ctypes.c_int, [VP, ctypes.c_int32, VP, VP, VP, VP, VP, VP, ctypes.c_int64, VP]),
+    "lz_step_host": (ctypes.c_int, [VP, VP, VP, VP, VP, VP]),
     "lz_get_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
     "lz_set_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
     "lz_plane_elem_size": (ctypes.c_int32, [VP, ctypes.c_int32]),

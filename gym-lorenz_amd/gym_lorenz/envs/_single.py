@@ -21,10 +21,13 @@ class SingleEnvCore:
         self.be = BatchedEnv(system, 1, dtype=dtype, device=device, autoreset=False,
                              compact=False, max_episode_steps=0, **kw)
         self._np_dtype = np.float64 if self.be.tdtype == torch.float64 else np.float32
-        self._act = torch.zeros((1, self.be.action_dim), dtype=torch.float32,
-                                device=self.be.device)
-        self._noise = torch.zeros((1, 3), dtype=torch.float64, device=self.be.device)
+        # host-side inputs / outputs of lz_step_host (pinned staging lives in the library)
         o = self.be.obs_dim
+        self._obs_h = np.zeros((1, o), self._np_dtype)
+        self._rew_h = np.zeros((1,), self._np_dtype)
+        self._done_h = np.zeros((1,), np.uint8)
+        self._act_h = np.zeros((1, self.be.action_dim), np.float32)
+        self._noise_h = np.zeros((1, 3), np.float64)
         es = np.dtype(self._np_dtype).itemsize
         self._o_end = o * es
         self._r_end = (o + 1) * es
@@ -42,14 +45,17 @@ class SingleEnvCore:
         return self._unpack()[0]
 
     def step(self, action, noise=None):
-        a = np.asarray(action, dtype=np.float32).reshape(1, -1)
-        self._act.copy_(torch.from_numpy(a))
+        # lz_step_host: actions (+ injected noise) in, obs | reward | done out, host
+        # memory, one synchronous library call (pinned staging inside the library)
+        self._act_h[...] = np.asarray(action, dtype=np.float32).reshape(1, -1)
         nz = None
         if noise is not None:
-            self._noise.copy_(torch.from_numpy(np.asarray(noise, dtype=np.float64).reshape(1, 3)))
-            nz = self._noise
-        self.be.step(self._act, nz, want_n_done=False)
-        return self._unpack()
+            self._noise_h[...] = np.asarray(noise, dtype=np.float64).reshape(1, 3)
+            nz = self._noise_h.ctypes.data
+        nat.check(nat.lib.lz_step_host(self.be._h, self._act_h.ctypes.data, nz,
+                                       self._obs_h.ctypes.data, self._rew_h.ctypes.data,
+                                       self._done_h.ctypes.data))
+        return self._obs_h[0].copy(), self._rew_h[0], int(self._done_h[0])
 
     def plane(self, p):
         return self.be.get_state(p).cpu().numpy()[0]

@@ -226,6 +226,16 @@ lz_status lz_step(lz_handle* h, const void* actions, const double* noise, void* 
                   void* rew_out, uint8_t* done_out, int32_t* done_idx_out,
                   void* terminal_obs_out, int32_t* n_done_out);
 
+/* One step of a small handle from / to HOST memory, synchronous: actions (float32
+ * [N, A]) and optional injected noise (double [N, 3]) are copied into the handle's
+ * host staging buffer, which is mapped into the device address space (hipHostMalloc
+ * mapped + coherent), lz_step reads them and writes obs | reward | done there over
+ * PCIe (no copy launches), the stream is synchronised and the outputs copied out.  The per-env drop-in classes use it -- one call per
+ * env.step() of a reference caller that keeps DummyVecEnv([lambda: gymnasium.make(..)])
+ * (code/train.py:98-100).  The handle's first call allocates the staging buffers. */
+lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, void* obs_out,
+                       void* rew_out, uint8_t* done_out);
+
 /* K fused steps in ONE launch, state held in registers.  Time-major buffers:
  *   actions T [K, N, action_dim]; obs_out T [K, N, obs_dim]; rew_out T [K, N];
  *   done_out uint8 [K, N]; done_idx_out int64 [cap] (k * N + env) and

@@ -31,6 +31,7 @@ int main(void) {
   if (lz_create(&cfg, &h) != LZ_ERR_INVALID) return 5;
   if (lz_step(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL) != LZ_ERR_INVALID) return 6;
   if (lz_rollout_policy(NULL, NULL) != LZ_ERR_INVALID) return 7;
+  if (lz_step_host(NULL, NULL, NULL, NULL, NULL, NULL) != LZ_ERR_INVALID) return 20;
   if (lz_gae(10, 2, NULL, NULL, NULL, NULL, 0.99, 0.95, NULL, NULL, 0, NULL) != LZ_ERR_INVALID) return 8;
   if (lz_frame_stack(NULL, NULL, NULL, 1, 4, 6, 0, 0, NULL) != LZ_ERR_INVALID) return 9;
   lz_rms* r = NULL;

@@ -547,3 +547,21 @@ def test_vecenv_return_tensors_matches_numpy(gl):
             seen += 1
         assert len(ia) == n and ia[0] is not None
     assert seen > 0
+
+
+def test_import_order_gym_lorenz_first():
+    """A fresh interpreter that imports gym_lorenz before anything touches torch /
+    HIP (the order of a script that starts with `import gym_lorenz`) can create and
+    step envs: _native.py loads torch's HIP runtime first."""
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import gym_lorenz as gl\n"
+            "e = gl.make('lorenz_dynamic-v0'); o = e.reset(); o2 = e.step([0.0, 0.0, 0.0])[0]\n"
+            "assert o.shape == (6,) and o2.shape == (6,)\n"
+            "print('ok')\n" % (ROOT + "/gym-lorenz_amd"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
