@@ -970,21 +970,48 @@ __global__ __launch_bounds__(256) void k_pol_moments_final(const double* part, i
 //   last_gae_lam = delta + gamma * gae_lambda * next_non_terminal * last_gae_lam
 //   returns = advantages + values
 // with next_non_terminal = 1 - episode_starts[t+1] = 1 - done[t].
-__global__ __launch_bounds__(256) void k_gae(int64_t n, int K, const float* rew, const float* val,
-                                            const uint8_t* done, const float* last_val, float gamma,
-                                            float gl, float* adv, float* ret) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// One lane per env walks k = K-1 .. 0 (the recursion runs backwards in time).  The
+// loads of U steps are issued ahead of their arithmetic (restrict pointers: the
+// outputs never alias the inputs), the next value is carried in a register instead of
+// re-read, and one-wave workgroups spread a small batch (cfg5: 32,768 envs) over all
+// CUs.  Same expressions, same order: bit-identical to the straightforward loop.
+constexpr int kGaeBlock = 64;
+__global__ __launch_bounds__(kGaeBlock) void k_gae(int64_t n, int K, const float* __restrict__ rew,
+                                                  const float* __restrict__ val,
+                                                  const uint8_t* __restrict__ done,
+                                                  const float* __restrict__ last_val, float gamma,
+                                                  float gl, float* __restrict__ adv,
+                                                  float* __restrict__ ret) {
+  const int64_t i = (int64_t)blockIdx.x * kGaeBlock + threadIdx.x;
   if (i >= n) return;
   float last = 0.0f;
-  for (int k = K - 1; k >= 0; --k) {
-    const int64_t off = (int64_t)k * n + i;
-    const float nnt = 1.0f - (done[off] ? 1.0f : 0.0f);
-    const float nv = k == K - 1 ? last_val[i] : val[off + n];
-    const float v = val[off];
-    const float delta = (rew[off] + (gamma * nv) * nnt) - v;
+  float nv = last_val[i];  // next step's value: V(last obs) for k = K-1
+  auto one = [&](int64_t off, float r, float v, uint8_t d) __attribute__((always_inline)) {
+    const float nnt = 1.0f - (d ? 1.0f : 0.0f);
+    const float delta = (r + (gamma * nv) * nnt) - v;
     last = delta + (gl * nnt) * last;
-    adv[off] = last;
-    ret[off] = last + v;
+    __builtin_nontemporal_store(last, adv + off);
+    __builtin_nontemporal_store(last + v, ret + off);
+    nv = v;
+  };
+  constexpr int U = 8;
+  int k = K - 1;
+  for (; k >= U - 1; k -= U) {
+    float r[U], v[U];
+    uint8_t d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t off = (int64_t)(k - u) * n + i;
+      r[u] = __builtin_nontemporal_load(rew + off);
+      v[u] = __builtin_nontemporal_load(val + off);
+      d[u] = __builtin_nontemporal_load(done + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one((int64_t)(k - u) * n + i, r[u], v[u], d[u]);
+  }
+  for (; k >= 0; --k) {
+    const int64_t off = (int64_t)k * n + i;
+    one(off, rew[off], val[off], done[off]);
   }
 }
 
@@ -1416,7 +1443,8 @@ lz_status lz_gae(int64_t n, int32_t K, const float* rew, const float* values, co
   if (hipSetDevice(device) != hipSuccess) return pfail(LZ_ERR_HIP, "hipSetDevice failed");
   // NumPy: python-float gamma * float32 array -> float32(gamma); gamma * gae_lambda is a
   // python-float product rounded once to float32
-  hipLaunchKernelGGL(lz::k_gae, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(lz::k_gae, dim3((unsigned)((n + lz::kGaeBlock - 1) / lz::kGaeBlock)),
+                     dim3(lz::kGaeBlock), 0,
                      static_cast<hipStream_t>(stream), n, K, rew, values, done, last_values,
                      (float)gamma, (float)(gamma * gae_lambda), advantages, returns);
   const hipError_t e = hipGetLastError();
