@@ -970,12 +970,19 @@ __global__ __launch_bounds__(256) void k_pol_moments_final(const double* part, i
 //   last_gae_lam = delta + gamma * gae_lambda * next_non_terminal * last_gae_lam
 //   returns = advantages + values
 // with next_non_terminal = 1 - episode_starts[t+1] = 1 - done[t].
-// One lane per env walks k = K-1 .. 0 (the recursion runs backwards in time).  The
-// loads of U steps are issued ahead of their arithmetic (restrict pointers: the
-// outputs never alias the inputs), the next value is carried in a register instead of
-// re-read, and one-wave workgroups spread a small batch (cfg5: 32,768 envs) over all
-// CUs.  Same expressions, same order: bit-identical to the straightforward loop.
+// One lane per env walks k = K-1 .. 0 (the recursion runs backwards in time); the next
+// value is carried in a register instead of re-read, and one-wave workgroups spread a
+// small batch (cfg5: 32,768 envs) over all CUs.  Loads are issued in batches of U steps
+// ahead of their arithmetic (restrict pointers: the outputs never alias the inputs).
+// Two schedules, picked by batch size (profiles/r01/policy/gae_ab.json):
+//   DB = true : double-buffered, batch j+1 issued before batch j's arithmetic (U = 4):
+//               a latency-bound small batch (32,768 envs = 512 waves) keeps loads in
+//               flight across batches -- 830 -> 450 us at 32,768 envs x 2048 steps;
+//   DB = false: one batch of U = 8 at a time: with >= 2,048 waves the other waves hide
+//               the gaps, and this schedule runs 5.4 TB/s at 262,144 envs (DB: 4.8).
+// Same expressions, same order: bit-identical to the straightforward loop either way.
 constexpr int kGaeBlock = 64;
+template <int U, bool DB>
 __global__ __launch_bounds__(kGaeBlock) void k_gae(int64_t n, int K, const float* __restrict__ rew,
                                                   const float* __restrict__ val,
                                                   const uint8_t* __restrict__ done,
@@ -994,20 +1001,55 @@ __global__ __launch_bounds__(kGaeBlock) void k_gae(int64_t n, int K, const float
     __builtin_nontemporal_store(last + v, ret + off);
     nv = v;
   };
-  constexpr int U = 8;
-  int k = K - 1;
-  for (; k >= U - 1; k -= U) {
-    float r[U], v[U];
-    uint8_t d[U];
+  float ra[U], va[U], rb[U], vb[U];
+  uint8_t da[U], db[U];
+  auto load = [&](int k0, float* r, float* v, uint8_t* d) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t off = (int64_t)(k - u) * n + i;
+      const int64_t off = (int64_t)(k0 - u) * n + i;
       r[u] = __builtin_nontemporal_load(rew + off);
       v[u] = __builtin_nontemporal_load(val + off);
       d[u] = __builtin_nontemporal_load(done + off);
     }
+  };
+  auto run = [&](int k0, const float* r, const float* v, const uint8_t* d)
+      __attribute__((always_inline)) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) one((int64_t)(k - u) * n + i, r[u], v[u], d[u]);
+    for (int u = 0; u < U; ++u) one((int64_t)(k0 - u) * n + i, r[u], v[u], d[u]);
+  };
+  int k = K - 1;
+  if (!DB) {
+    for (; k >= U - 1; k -= U) {
+      float r[U], v[U];  // batch-local arrays: the scheduler interleaves the next
+      uint8_t d[U];      // batch's loads with this one's stores
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t off = (int64_t)(k - u) * n + i;
+        r[u] = __builtin_nontemporal_load(rew + off);
+        v[u] = __builtin_nontemporal_load(val + off);
+        d[u] = __builtin_nontemporal_load(done + off);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) one((int64_t)(k - u) * n + i, r[u], v[u], d[u]);
+    }
+  } else if (k >= U - 1) {
+    load(k, ra, va, da);
+    // two batches per iteration (a, b) so the buffers swap by name, not by moves
+    for (; k >= 3 * U - 1; k -= 2 * U) {
+      load(k - U, rb, vb, db);
+      run(k, ra, va, da);
+      load(k - 2 * U, ra, va, da);
+      run(k - U, rb, vb, db);
+    }
+    if (k >= 2 * U - 1) {
+      load(k - U, rb, vb, db);
+      run(k, ra, va, da);
+      run(k - U, rb, vb, db);
+      k -= 2 * U;
+    } else {
+      run(k, ra, va, da);
+      k -= U;
+    }
   }
   for (; k >= 0; --k) {
     const int64_t off = (int64_t)k * n + i;
@@ -1443,7 +1485,9 @@ lz_status lz_gae(int64_t n, int32_t K, const float* rew, const float* values, co
   if (hipSetDevice(device) != hipSuccess) return pfail(LZ_ERR_HIP, "hipSetDevice failed");
   // NumPy: python-float gamma * float32 array -> float32(gamma); gamma * gae_lambda is a
   // python-float product rounded once to float32
-  hipLaunchKernelGGL(lz::k_gae, dim3((unsigned)((n + lz::kGaeBlock - 1) / lz::kGaeBlock)),
+  // below 2,048 one-wave groups the batch is latency-bound: double-buffered loads
+  auto kern = n < 131072 ? lz::k_gae<4, true> : lz::k_gae<8, false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)((n + lz::kGaeBlock - 1) / lz::kGaeBlock)),
                      dim3(lz::kGaeBlock), 0,
                      static_cast<hipStream_t>(stream), n, K, rew, values, done, last_values,
                      (float)gamma, (float)(gamma * gae_lambda), advantages, returns);

@@ -260,11 +260,14 @@ def test_policy_vecnormalize(gl, pol):
     assert rms.count == ref.count
 
 
-def test_gae_bitexact_vs_sb3_restatement(gl, pol):
+# (K, n): both load schedules of k_gae (double-buffered U=4 below 131,072 envs, single
+# batches of U=8 above) with K below one batch, exactly 2 and 3 batches, and ragged tails
+@pytest.mark.parametrize("K,n", [(37, 5003), (3, 70), (8, 100), (12, 64), (9, 131075),
+                                 (37, 131072)])
+def test_gae_bitexact_vs_sb3_restatement(gl, pol, K, n):
     from oracle.sb3_buffer import compute_returns_and_advantage
 
     rng = np.random.default_rng(1)
-    K, n = 37, 5003
     rew = rng.normal(0, 3, (K, n)).astype(np.float32)
     val = rng.normal(0, 3, (K, n)).astype(np.float32)
     done = (rng.random((K, n)) < 0.05).astype(np.uint8) * rng.integers(1, 4, (K, n)).astype(np.uint8)
