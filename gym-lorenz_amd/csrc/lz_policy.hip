@@ -1060,6 +1060,24 @@ __global__ __launch_bounds__(kGaeBlock) void k_gae(int64_t n, int K, const float
   }
 }
 
+// RolloutBuffer.episode_starts of one collect, from the done codes the rollout wrote
+// (SB3 collect_rollouts: episode_starts[0] = the previous collect's last dones,
+// episode_starts[k] = dones[k-1]): one pass instead of the compare + convert + copy
+// torch launches it replaces.  Thread e of the grid-stride loop writes element e of
+// the [K, N] float32 buffer; the first N lanes also write the next collect's carry.
+__global__ __launch_bounds__(256) void k_episode_starts(int64_t n, int K, const uint8_t* __restrict__ done,
+                                                        const float* __restrict__ last_in,
+                                                        float* __restrict__ starts,
+                                                        float* __restrict__ last_out) {
+  const int64_t total = (int64_t)K * n;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const float v = e < n ? last_in[e] : (done[e - n] != 0 ? 1.0f : 0.0f);
+    __builtin_nontemporal_store(v, starts + e);
+    if (e < n) last_out[e] = done[(int64_t)(K - 1) * n + e] != 0 ? 1.0f : 0.0f;
+  }
+}
+
 template <class Sys>
 static int launch_pol(const KArgs& a, const PArgs& p, const PolShape& sh, hipStream_t s) {
   const dim3 grid((unsigned)sh.grid);
@@ -1494,6 +1512,23 @@ lz_status lz_gae(int64_t n, int32_t K, const float* rew, const float* values, co
                      dim3(lz::kGaeBlock), 0,
                      static_cast<hipStream_t>(stream), n, K, rew, values, done, last_values,
                      (float)gamma, (float)(gamma * gae_lambda), advantages, returns);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pfail(LZ_ERR_HIP, hipGetErrorString(e));
+  return LZ_OK;
+}
+
+lz_status lz_episode_starts(int64_t n, int32_t K, const uint8_t* done, const float* last_in,
+                            float* starts, float* last_out, int32_t device, void* stream) {
+  if (!done || !last_in || !starts || !last_out) return pfail(LZ_ERR_INVALID, "NULL buffer");
+  if (n < 0 || K < 1) return pfail(LZ_ERR_INVALID, "n >= 0 and K >= 1 required");
+  if (last_in == last_out) return pfail(LZ_ERR_INVALID, "last_in and last_out must not alias");
+  if (n == 0) return LZ_OK;
+  if (hipSetDevice(device) != hipSuccess) return pfail(LZ_ERR_HIP, "hipSetDevice failed");
+  const int64_t total = (int64_t)K * n;
+  const int64_t want = (total + 255) / 256;
+  const unsigned grid = (unsigned)(want < 8192 ? want : 8192);  // grid-stride beyond 2M
+  hipLaunchKernelGGL(lz::k_episode_starts, dim3(grid), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), n, K, done, last_in, starts, last_out);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pfail(LZ_ERR_HIP, hipGetErrorString(e));
   return LZ_OK;

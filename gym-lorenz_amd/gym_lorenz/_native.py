@@ -188,6 +188,8 @@ _SIGS = {
                                                     ctypes.c_int32, VP, VP]),
     "lz_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, ctypes.c_double,
                               ctypes.c_double, VP, VP, ctypes.c_int32, VP]),
+    "lz_episode_starts": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP,
+                                         ctypes.c_int32, VP]),
     "lz_frame_stack": (ctypes.c_int, [VP, VP, VP, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                       ctypes.c_int32, ctypes.c_int32, VP]),
     "lz_last_error": (ctypes.c_char_p, []),

@@ -560,10 +560,11 @@ class FusedRolloutCollector:
             launch = nat.lib.lz_rollout_policy_attn if self.attention else nat.lib.lz_rollout_policy
             nat.check(launch(self.env._h, ctypes.byref(r)))
         starts = torch.empty((K, n), dtype=f32, device=dev)
-        starts[0] = self.last_episode_starts
-        if K > 1:
-            starts[1:] = (done[:-1] != 0).to(f32)
-        self.last_episode_starts = (done[-1] != 0).to(f32)
+        carry = torch.empty((n,), dtype=f32, device=dev)
+        nat.check(nat.lib.lz_episode_starts(n, K, _p(done), _p(self.last_episode_starts),
+                                            _p(starts), _p(carry), dev.index,
+                                            ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+        self.last_episode_starts = carry
         self._keep = (self.blob, self.last_obs, self.last_stack)  # alive until consumed
         self.last_obs = obs_last
         if stack_out is not None:

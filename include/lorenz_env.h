@@ -37,7 +37,7 @@
  *   lz_get_state / lz_set_state
  *       -> attribute access env.state1 / state2 / state_master / state_slave /
  *          lambda_coef ... used by code/lorenz_pmsm/test_evaluate.py:99-111
- *   lz_policy_pack[_hidden] / lz_rollout_policy / lz_gae
+ *   lz_policy_pack[_hidden] / lz_rollout_policy / lz_gae / lz_episode_starts
  *       -> SB3 OnPolicyAlgorithm.collect_rollouts + RolloutBuffer.compute_returns_and_
  *          advantage for the MlpPolicy learners (code/lorenz_pmsm/train.py:155-178,
  *          optimize.py:36-60 ([64,64] / [128,128]), code/gym_run.py:83 (PPO default
@@ -407,6 +407,14 @@ lz_status lz_gae(int64_t n, int32_t K, const float* rew, const float* values,
                  const uint8_t* done, const float* last_values, double gamma,
                  double gae_lambda, float* advantages, float* returns, int32_t device,
                  void* hip_stream);
+
+/* RolloutBuffer.episode_starts of one collect (SB3 2.7.1 OnPolicyAlgorithm.
+ * collect_rollouts: rollout_buffer.add(..., self._last_episode_starts, ...), then
+ * _last_episode_starts = dones): starts[0] = last_in, starts[k] = (done[k-1] != 0)
+ * as float32 [K, N]; last_out = (done[K-1] != 0), the next collect's last_in (must
+ * not alias last_in). */
+lz_status lz_episode_starts(int64_t n, int32_t K, const uint8_t* done, const float* last_in,
+                            float* starts, float* last_out, int32_t device, void* hip_stream);
 
 /* Copy one SoA state plane (N elements, T or int32 / float32 as listed above)
  * between the handle and a device buffer. */

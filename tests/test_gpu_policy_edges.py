@@ -94,3 +94,39 @@ def test_errors(pol):
     env.reset()
     assert nat.lib.lz_rollout_policy(env._h, ctypes.byref(r64)) == nat.LZ_ERR_UNSUPPORTED
     del c
+
+
+# lz_episode_starts: SB3's episode_starts buffer of one collect from the done codes,
+# exact vs the torch expression it replaced; grid-stride beyond 2,097,152 elements
+@pytest.mark.parametrize("n,K", [(1, 1), (5, 1), (300, 7), (4099, 16), (200003, 16)])
+def test_episode_starts_exact(pol, n, K):
+    from gym_lorenz import _native as nat
+
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(n + K)
+    done = torch.randint(0, 4, (K, n), device=dev, dtype=torch.uint8, generator=g)
+    done[torch.rand((K, n), device=dev, generator=g) < 0.7] = 0
+    last_in = (torch.rand(n, device=dev, generator=g) < 0.5).float()
+    starts = torch.full((K, n), -7.0, device=dev)
+    last_out = torch.full((n,), -7.0, device=dev)
+    s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    nat.check(nat.lib.lz_episode_starts(n, K, p(done), p(last_in), p(starts), p(last_out), 0, s))
+    ref = torch.empty((K, n), device=dev)
+    ref[0] = last_in
+    if K > 1:
+        ref[1:] = (done[:-1] != 0).to(torch.float32)
+    assert torch.equal(starts, ref)
+    assert torch.equal(last_out, (done[-1] != 0).to(torch.float32))
+
+
+def test_episode_starts_errors(pol):
+    from gym_lorenz import _native as nat
+
+    t = torch.zeros(4, device="cuda:0")
+    d = torch.zeros(4, device="cuda:0", dtype=torch.uint8)
+    p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    assert nat.lib.lz_episode_starts(4, 1, p(d), p(t), p(t), p(t), 0, None) != 0  # alias
+    assert nat.lib.lz_episode_starts(4, 0, p(d), p(t), p(t), None, 0, None) != 0  # K, NULL
+    assert nat.lib.lz_episode_starts(0, 1, p(d), p(t), p(t), p(torch.zeros(1, device="cuda:0")),
+                                     0, None) == 0  # empty batch: nothing to do
