@@ -980,9 +980,10 @@ __global__ __launch_bounds__(256) void k_pol_moments_final(const double* part, i
 // Two schedules, picked by batch size (profiles/r01/policy/gae_ab.json):
 //   DB = true : double-buffered, batch j+1 issued before batch j's arithmetic (U = 4):
 //               a latency-bound small batch (32,768 envs = 512 waves) keeps loads in
-//               flight across batches -- 830 -> 450 us at 32,768 envs x 2048 steps;
-//   DB = false: one batch of U = 8 at a time: with >= 2,048 waves the other waves hide
-//               the gaps, and this schedule runs 5.4 TB/s at 262,144 envs (DB: 4.8).
+//               flight across batches -- 830 -> 450 us at 32,768 envs x 2048 steps,
+//               312 -> 214 us at 131,072 x 512 (gae_threshold.json);
+//   DB = false: one batch of U = 8 at a time: with >= 4,096 waves the other waves hide
+//               the gaps, and this schedule runs 5.4 TB/s at 262,144 envs (DB: 4.9).
 // Same expressions, same order: bit-identical to the straightforward loop either way.
 constexpr int kGaeBlock = 64;
 template <int U, bool DB>
@@ -1506,8 +1507,8 @@ lz_status lz_gae(int64_t n, int32_t K, const float* rew, const float* values, co
   if (hipSetDevice(device) != hipSuccess) return pfail(LZ_ERR_HIP, "hipSetDevice failed");
   // NumPy: python-float gamma * float32 array -> float32(gamma); gamma * gae_lambda is a
   // python-float product rounded once to float32
-  // below 2,048 one-wave groups the batch is latency-bound: double-buffered loads
-  auto kern = n < 131072 ? lz::k_gae<4, true> : lz::k_gae<8, false>;
+  // below 4,096 one-wave groups the batch is latency-bound: double-buffered loads
+  auto kern = n < 262144 ? lz::k_gae<4, true> : lz::k_gae<8, false>;
   hipLaunchKernelGGL(kern, dim3((unsigned)((n + lz::kGaeBlock - 1) / lz::kGaeBlock)),
                      dim3(lz::kGaeBlock), 0,
                      static_cast<hipStream_t>(stream), n, K, rew, values, done, last_values,

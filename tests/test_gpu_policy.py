@@ -260,10 +260,10 @@ def test_policy_vecnormalize(gl, pol):
     assert rms.count == ref.count
 
 
-# (K, n): both load schedules of k_gae (double-buffered U=4 below 131,072 envs, single
-# batches of U=8 above) with K below one batch, exactly 2 and 3 batches, and ragged tails
+# (K, n): both load schedules of k_gae (double-buffered U=4 below 262,144 envs, single
+# batches of U=8 from there) with K below one batch, exactly 2 and 3 batches, and ragged tails
 @pytest.mark.parametrize("K,n", [(37, 5003), (3, 70), (8, 100), (12, 64), (9, 131075),
-                                 (37, 131072)])
+                                 (37, 131072), (5, 262147)])
 def test_gae_bitexact_vs_sb3_restatement(gl, pol, K, n):
     from oracle.sb3_buffer import compute_returns_and_advantage
 
