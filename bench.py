@@ -87,7 +87,7 @@ def cpu_baseline(seconds):
         dt = time.perf_counter() - t0
     out = {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
            "sample": "oracle/lz_oracle.c orc_l3_step_float (scalar C restatement of "
-                     "dynamic.py:86-115), 65,536 envs x %d steps = %.2e env-steps in %.1f s, "
+                     "dynamic.py:61-90), 65,536 envs x %d steps = %.2e env-steps in %.1f s, "
                      "1 thread, GPU box host CPU" % (steps, n * steps, dt)}
     out["reference_loop"] = reference_loop_baseline(min(4.0, seconds / 3))
     return out

@@ -116,10 +116,10 @@ lz_status lz_config_init(lz_config* cfg, int32_t system) {
   cfg->t_done_step = -1;
   double* p = cfg->params;
   switch (system) {
-    case LZ_SYS_LORENZ3:  // dynamic.py:56-58 (u, i, o), :98-100 (0.01), :36-37 (+-500)
-      p[0] = 10; p[1] = 28; p[2] = 8.0 / 3; p[3] = 0.01; p[4] = 500; p[5] = 10;  // T_end :111
+    case LZ_SYS_LORENZ3:  // dynamic.py:31-33 (u, i, o), :73-75 (0.01), :11-12 (+-500)
+      p[0] = 10; p[1] = 28; p[2] = 8.0 / 3; p[3] = 0.01; p[4] = 500; p[5] = 10;  // T_end :86
       break;
-    case LZ_SYS_LORENZ4:  // lorenz_env_transient.py:270-273, :85-88 (0.001), :13-14, :127
+    case LZ_SYS_LORENZ4:  // lorenz_env_transient.py:270-273, :327-330 (0.001), :255-256, :369
       p[0] = 10; p[1] = 8.0 / 3; p[2] = 28; p[3] = 0.001; p[4] = 2; p[5] = 5;
       break;
     case LZ_SYS_PMSM:  // lorenz_env_try_pmsm.py:12-14, :20-23, :39, :50, :113, :174
@@ -194,8 +194,8 @@ lz_status lz_create(const lz_config* cfg_in, lz_handle** out) {
       h->num_cus <= 0)
     h->num_cus = 256;
 
-  // The reference's float accumulator 't += dt; done = t == T' (dynamic.py:110-111,
-  // lorenz_env_transient.py:122,127): replay it on the host in double, exactly as
+  // The reference's float accumulator 't += dt; done = t == T' (dynamic.py:85-89,
+  // lorenz_env_transient.py:364,369): replay it on the host in double, exactly as
   // Python does, and record the step at which it fires (-1: never -- the case for the
   // reference constants).
   cfg.t_done_step = -1;
@@ -340,6 +340,10 @@ lz_status lz_set_stream(lz_handle* h, void* stream) {
 lz_status lz_set_seed(lz_handle* h, uint64_t seed) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
   h->cfg.seed = seed;
+  // rewind the RNG call counter (both ping-pong slots; stream-ordered after any
+  // launch already queued): seed(s) + reset() is then reproducible
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  HIP_TRY(hipMemsetAsync(h->ticks, 0, 2 * sizeof(uint64_t), h->stream));
   return LZ_OK;
 }
 

@@ -73,7 +73,12 @@ template <class Sys, typename T>
 __global__ __launch_bounds__(kBlock) void k_reset(KArgs a) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t tick = *a.tick_in;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.tick_out = tick + a.tick_adv;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *a.tick_out = tick + a.tick_adv;
+    // the next launch's compact-list cursor (lz_reset flips the parity like a step):
+    // without this a step after step(dones) -> reset would start at the old count
+    *a.counter_next = 0;
+  }
   if (i >= a.n) return;
   if (a.mask && a.mask[i] == 0) return;
   Sys sys;

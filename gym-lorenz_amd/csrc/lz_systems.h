@@ -60,7 +60,7 @@ struct Draw<double> {
 };
 
 // ===========================================================================
-// LORENZ3 -- dynamic.py:5-115, lorenzEnv_transient (3-state Lorenz, Euler)
+// LORENZ3 -- dynamic.py:5-93, lorenzEnv_transient (3-state Lorenz, Euler)
 // params: sigma(self.u)=10, rho(self.i)=28, beta(self.o)=8/3, dt=0.01, clip=500
 // planes: x, y, z [, step]
 // ===========================================================================
@@ -83,42 +83,42 @@ struct SysL3 {
   }
   __device__ void store_reset(const KArgs& a, int64_t i) const { store(a, i); }
   __device__ void store_autoreset_extra(const KArgs&, int64_t) const {}
-  // dynamic.py:64-66 / :95-97 / :102-104
+  // dynamic.py:39-41 (reset) / :70-72 / :77-79 (step)
   __device__ void rhs(T& fx, T& fy, T& fz) const {
     fx = sg * (y - x);
     fy = (rh * x - y) - x * z;
     fz = x * y - be * z;
   }
   __device__ static void draw(const KArgs& a, uint64_t gid, uint64_t tick, T* v) {
-    for (int j = 0; j < 3; ++j) v[j] = Draw<T>::uniform(a.seed, gid, tick, j, (T)-30, (T)30);  // :62
+    for (int j = 0; j < 3; ++j) v[j] = Draw<T>::uniform(a.seed, gid, tick, j, (T)-30, (T)30);  // :37
   }
   __device__ void init(const T* v, const KArgs&) { x = v[0]; y = v[1]; z = v[2]; }
-  // reset(): dynamic.py:60-75 -> state0 - zeros(6)
+  // reset(): dynamic.py:35-50 -> state0 - state2 (zeros(6))
   __device__ void reset_obs(T* o) const {
     T fx, fy, fz;
     rhs(fx, fy, fz);
     o[0] = x - (T)0; o[1] = y - (T)0; o[2] = z - (T)0;
     o[3] = fx - (T)0; o[4] = fy - (T)0; o[5] = fz - (T)0;
   }
-  // step(): dynamic.py:86-115
+  // step(): dynamic.py:61-90
   // act: float32 (SB3 hands np.float32 actions; np.clip keeps f32, then promotes)
   __device__ bool step(const float* act, bool, const double*, T* o, T& rew, const KArgs&) {
     const T u1 = clip((T)act[0], -cl, cl), u2 = clip((T)act[1], -cl, cl),
             u3 = clip((T)act[2], -cl, cl);
     T fx, fy, fz;
-    rhs(fx, fy, fz);                 // :95-97, all from the old state
-    x = (x + fx * dt) + u1;          // :98
-    y = (y + fy * dt) + u2;          // :99
-    z = (z + fz * dt) + u3;          // :100
-    reset_obs(o);                    // :102-108 obs = [s', f(s')]
-    // :109 -sum(abs(x) for x in now[0:3]); python's sum starts from int 0
+    rhs(fx, fy, fz);                 // :70-72, all from the old state
+    x = (x + fx * dt) + u1;          // :73
+    y = (y + fy * dt) + u2;          // :74
+    z = (z + fz * dt) + u3;          // :75
+    reset_obs(o);                    // :77-83 obs = [s', f(s')]
+    // :84 -sum(abs(x) for x in now[0:3]); python's sum starts from int 0
     rew = -((((T)0 + fabs(o[0])) + fabs(o[1])) + fabs(o[2]));
-    return false;                    // :110-114 't == 10' handled by t_done_step
+    return false;                    // :85-89 't == 10' handled by t_done_step
   }
 };
 
 // ===========================================================================
-// LORENZ4 -- lorenz_env_transient.py:247-373 (4-state master/slave, Euler)
+// LORENZ4 -- lorenz_env_transient.py:247-376 (4-state master/slave, Euler)
 // params: a=10, b=8/3, c=28, dt=0.001, clip=2; the action is never used (:316-318)
 // planes: master x1..x4, slave x1..x4 [, step]
 // ===========================================================================
@@ -143,7 +143,7 @@ struct SysL4 {
   }
   __device__ void store_reset(const KArgs& a, int64_t i) const { store(a, i); }
   __device__ void store_autoreset_extra(const KArgs&, int64_t) const {}
-  // :81-84
+  // :323-326 (master) / :344-347 (slave); also :280-283, :333-336, :354-357
   __device__ void rhs(const T* v, T* f) const {
     f[0] = pa * (v[1] - v[0]) + v[3];
     f[1] = (pc * v[0] - v[1]) - v[0] * v[2];
@@ -168,16 +168,16 @@ struct SysL4 {
   // :314-373
   __device__ bool step(const float*, bool, const double*, T* o, T& rew, const KArgs&) {
     T f[4];
-    rhs(m, f);                                              // :81-84
+    rhs(m, f);                                              // :323-326
 #pragma unroll
-    for (int j = 0; j < 4; ++j) m[j] = m[j] + f[j] * dt;    // :85-88
-    rhs(s, f);                                              // :102-105
+    for (int j = 0; j < 4; ++j) m[j] = m[j] + f[j] * dt;    // :327-330
+    rhs(s, f);                                              // :344-347
 #pragma unroll
-    for (int j = 0; j < 4; ++j) s[j] = s[j] + f[j] * dt;    // :106-109
-    reset_obs(o);                                           // :91-94, :112-120
-    const T r = -(((((T)0 + fabs(o[0])) + fabs(o[1])) + fabs(o[2])) + fabs(o[3]));  // :121
+    for (int j = 0; j < 4; ++j) s[j] = s[j] + f[j] * dt;    // :348-351
+    reset_obs(o);                                           // :333-339, :354-362
+    const T r = -(((((T)0 + fabs(o[0])) + fabs(o[1])) + fabs(o[2])) + fabs(o[3]));  // :363
     rew = r;
-    return r < (T)-1e6;                                     // :127 (t == 5 never fires)
+    return r < (T)-1e6;                                     // :369 (t == 5 never fires)
   }
 };
 

@@ -202,7 +202,30 @@ if not os.path.exists(LIB_PATH):
         "`make -C gym-lorenz_amd` (or __graft_entry__.build()); there is no CPU fallback"
         % LIB_PATH)
 
+
+def hip_runtimes():
+    """Real paths of the libamdhip64 files mapped into this process."""
+    paths = set()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) >= 6 and os.path.basename(parts[5]).startswith("libamdhip64"):
+                paths.add(os.path.realpath(parts[5]))
+    return sorted(paths)
+
+
 lib = ctypes.CDLL(LIB_PATH)
+# One HIP runtime per process: the library resolves libamdhip64.so.7 to whichever copy
+# is loaded first (torch's, since torch is imported above).  If something loaded
+# /opt/rocm's copy before torch, torch runs on its own runtime and this library on the
+# other: the hipStream_t / device pointers torch hands over (lz_set_stream, every
+# buffer) would belong to a different runtime.  Refuse that loudly.
+HIP_RUNTIME = hip_runtimes()
+if len(HIP_RUNTIME) != 1:
+    raise ImportError(
+        "gym_lorenz: %d HIP runtimes are mapped in this process (%s); torch and "
+        "libgym_lorenz_amd.so must share one.  Import torch (or gym_lorenz) before "
+        "anything that loads a libamdhip64 directly." % (len(HIP_RUNTIME), ", ".join(HIP_RUNTIME)))
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
     _f.restype = _res

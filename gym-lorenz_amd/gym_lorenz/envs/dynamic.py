@@ -1,4 +1,4 @@
-"""Drop-in for dynamic.py:5-118 `lorenzEnv_transient` (3-state Lorenz, Euler dt=0.01,
+"""Drop-in for dynamic.py:5-93 `lorenzEnv_transient` (3-state Lorenz, Euler dt=0.01,
 additive action, 6-D observation, classic gym 4-tuple API).
 
 Same constructor signature, spaces, attributes and RNG consumption as the reference
@@ -44,7 +44,7 @@ class lorenzEnv_transient(GymEnv):  # noqa: N801 (reference name)
         self._core = SingleEnvCore(nat.LORENZ3, dtype, device)
 
     def reset(self):
-        """dynamic.py:60-72"""
+        """dynamic.py:35-47"""
         state1 = np.random.uniform(low=-30, high=30, size=(3,))
         obs = self._core.reset(state1)
         self.state1 = obs[:3].copy()
@@ -67,7 +67,7 @@ class lorenzEnv_transient(GymEnv):  # noqa: N801 (reference name)
         return [self.state1[2], self.state2[2]]
 
     def step(self, action):
-        """dynamic.py:86-115 (kernel: lz_step on LORENZ3)."""
+        """dynamic.py:61-90 (kernel: lz_step on LORENZ3)."""
         self.u1 = np.clip(action[0], self.input_min, self.input_max)
         self.u2 = np.clip(action[1], self.input_min, self.input_max)
         self.u3 = np.clip(action[2], self.input_min, self.input_max)

@@ -1,4 +1,4 @@
-"""Drop-in for lorenz_env_transient.py:247-379 `lorenzEnv_transient` (4-state
+"""Drop-in for lorenz_env_transient.py:247-376 `lorenzEnv_transient` (4-state
 master/slave Lorenz-like system, Euler dt=0.001, 8-D observation, classic gym API)
 -- the env behind the historical id `lorenz_transient-v0` used by code/gym_run.py.
 

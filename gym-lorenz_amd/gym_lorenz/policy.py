@@ -551,6 +551,13 @@ class FusedRolloutCollector:
         r.obs_moments = _p(mom)
         r.done_idx, r.terminal_obs, r.cap, r.n_done = _p(didx), _p(tobs), self.capture_terminal, _p(ndone)
         stack_out = None
+        # the rollout runs on the env handle's stream; the caller's current stream (where
+        # the buffers above were allocated and blob / last_obs written, and where the
+        # follow-up kernels below run) is ordered around it both ways
+        caller = torch.cuda.current_stream(dev)
+        es = self.env.stream
+        if es != caller:
+            es.wait_stream(caller)
         if self.attention_ln:
             stack_out = torch.empty((n, SO), dtype=f32, device=dev)
             nat.check(nat.lib.lz_rollout_policy_attn_stack(self.env._h, ctypes.byref(r),
@@ -559,11 +566,13 @@ class FusedRolloutCollector:
         else:
             launch = nat.lib.lz_rollout_policy_attn if self.attention else nat.lib.lz_rollout_policy
             nat.check(launch(self.env._h, ctypes.byref(r)))
+        if es != caller:
+            caller.wait_stream(es)
         starts = torch.empty((K, n), dtype=f32, device=dev)
         carry = torch.empty((n,), dtype=f32, device=dev)
         nat.check(nat.lib.lz_episode_starts(n, K, _p(done), _p(self.last_episode_starts),
                                             _p(starts), _p(carry), dev.index,
-                                            ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+                                            ctypes.c_void_p(caller.cuda_stream)))
         self.last_episode_starts = carry
         self._keep = (self.blob, self.last_obs, self.last_stack)  # alive until consumed
         self.last_obs = obs_last

@@ -148,8 +148,8 @@ typedef struct lz_config {
   uint32_t flags;            /* LZ_FLAG_* */
   float alpha;               /* PMSM fractional-reward exponent (ctor kwarg alpha) */
   /* System constants, filled with the reference values by lz_config_init:
-   *  LORENZ3: sigma, rho, beta, dt, action clip            (dynamic.py:56-58,73-75,88-90)
-   *  LORENZ4: a, b, c, dt, action clip, T_end              (lorenz_env_transient.py:270-273)
+   *  LORENZ3: sigma, rho, beta, dt, action clip            (dynamic.py:31-33,73-75,63-65)
+   *  LORENZ4: a, b, c, dt, action clip, T_end              (lorenz_env_transient.py:270-273,327-330)
    *  PMSM:    sigma, gamma, dt, f_max, lambda_lr, beta1, beta2, eps, err_threshold,
    *           max_steps, term_threshold                    (lorenz_env_try_pmsm.py:12-50)
    *  HR:      a, b, c, d, r, s, I_bias, x_rest, dt, scale, master_scale,
@@ -193,7 +193,9 @@ lz_status lz_get_info(const lz_handle* h, lz_info* info);
 lz_status lz_get_config(const lz_handle* h, lz_config* cfg);
 
 /* Change the Philox key used by subsequent on-device resets / noise draws
- * (SB3 VecEnv.seed()). */
+ * (SB3 VecEnv.seed()) and rewind the device call counter to 0 (stream-ordered), so
+ * that seed(s) followed by reset() draws the same initial states whatever calls came
+ * before -- SB3 / gymnasium seed-then-reset reproducibility. */
 lz_status lz_set_seed(lz_handle* h, uint64_t seed);
 
 /* Bind the handle to a HIP stream (hipStream_t passed as void*; NULL = default). */

@@ -54,17 +54,17 @@ static inline float cube_ddf(float x) {
 }
 
 /* =========================================================================
- * LORENZ3 -- dynamic.py:5-115 lorenzEnv_transient (3-state, Euler, dt=0.01)
+ * LORENZ3 -- dynamic.py:5-93 lorenzEnv_transient (3-state, Euler, dt=0.01)
  * p = {sigma(self.u)=10, rho(self.i)=28, beta(self.o)=8/3, dt=0.01, clip=500}
  * ========================================================================= */
 #define L3_BODY(T, CLIP)                                                             \
-  /* dynamic.py:64-66 / :95-97 */                                                    \
+  /* dynamic.py:39-41 / :70-72 / :77-79 */                                          \
   static inline void l3_rhs_##T(const T* s, T* f, const T* p) {                     \
     f[0] = p[0] * (s[1] - s[0]);                                                     \
     f[1] = (p[1] * s[0] - s[1]) - s[0] * s[2];                                       \
     f[2] = s[0] * s[1] - p[2] * s[2];                                                \
   }                                                                                  \
-  /* reset obs: dynamic.py:60-75 (state0 - zeros) */                                 \
+  /* reset obs: dynamic.py:35-50 (state0 - zeros) */                                 \
   void orc_l3_reset_obs_##T(int64_t n, const T* st, T* obs, const double* pd) {      \
     T p[5]; for (int j = 0; j < 5; ++j) p[j] = (T)pd[j];                             \
     for (int64_t i = 0; i < n; ++i) {                                                \
@@ -73,19 +73,19 @@ static inline float cube_ddf(float x) {
                                     obs[6 * i + 3 + j] = f[j] - (T)0; }              \
     }                                                                                \
   }                                                                                  \
-  /* step: dynamic.py:86-115 */                                                      \
+  /* step: dynamic.py:61-90 */                                                       \
   void orc_l3_step_##T(int64_t n, T* st, const T* act, T* obs, T* rew,               \
                        const double* pd) {                                           \
     T p[5]; for (int j = 0; j < 5; ++j) p[j] = (T)pd[j];                             \
     for (int64_t i = 0; i < n; ++i) {                                                \
       T* s = st + 3 * i; T u[3], f[3];                                               \
-      for (int j = 0; j < 3; ++j) u[j] = CLIP(act[3 * i + j], -p[4], p[4]); /*:88-90*/\
-      l3_rhs_##T(s, f, p);                                          /* :95-97 */     \
-      for (int j = 0; j < 3; ++j) s[j] = (s[j] + f[j] * p[3]) + u[j]; /* :98-100 */  \
-      l3_rhs_##T(s, f, p);                                          /* :102-104 */   \
+      for (int j = 0; j < 3; ++j) u[j] = CLIP(act[3 * i + j], -p[4], p[4]); /*:63-65*/\
+      l3_rhs_##T(s, f, p);                                          /* :70-72 */     \
+      for (int j = 0; j < 3; ++j) s[j] = (s[j] + f[j] * p[3]) + u[j]; /* :73-75 */   \
+      l3_rhs_##T(s, f, p);                                          /* :77-79 */     \
       T* o = obs + 6 * i;                                                            \
       for (int j = 0; j < 3; ++j) { o[j] = s[j] - (T)0; o[3 + j] = f[j] - (T)0; }    \
-      /* :109  -sum(abs(x) for x in now[0:3]) : python sum starts from int 0 */      \
+      /* :84  -sum(abs(x) for x in now[0:3]) : python sum starts from int 0 */       \
       rew[i] = -((((T)0 + (T)fabs(o[0])) + (T)fabs(o[1])) + (T)fabs(o[2]));          \
     }                                                                                \
   }
@@ -93,11 +93,11 @@ L3_BODY(double, clipd)
 L3_BODY(float, clipf)
 
 /* =========================================================================
- * LORENZ4 -- lorenz_env_transient.py:247-373 (4-state master/slave, dt=0.001)
+ * LORENZ4 -- lorenz_env_transient.py:247-376 (4-state master/slave, dt=0.001)
  * p = {a=10, b=8/3, c=28, dt=0.001, clip=2}; the action is clipped but never used
  * ========================================================================= */
 #define L4_BODY(T)                                                                   \
-  /* :81-84 */                                                                       \
+  /* :323-326 (master), :344-347 (slave) */                                          \
   static inline void l4_rhs_##T(const T* s, T* f, const T* p) {                     \
     f[0] = p[0] * (s[1] - s[0]) + s[3];                                              \
     f[1] = (p[2] * s[0] - s[1]) - s[0] * s[2];                                       \
@@ -120,12 +120,12 @@ L3_BODY(float, clipf)
     T p[5]; for (int j = 0; j < 5; ++j) p[j] = (T)pd[j];                             \
     for (int64_t i = 0; i < n; ++i) {                                                \
       T* m = st + 8 * i; T* s = m + 4; T f[4];                                       \
-      l4_rhs_##T(m, f, p);                                          /* :81-84 */     \
-      for (int j = 0; j < 4; ++j) m[j] = m[j] + f[j] * p[3];        /* :85-88 */     \
-      T fm[4]; l4_rhs_##T(m, fm, p);                                /* :91-94 */     \
-      l4_rhs_##T(s, f, p);                                          /* :102-105 */   \
-      for (int j = 0; j < 4; ++j) s[j] = s[j] + f[j] * p[3];        /* :106-109 */   \
-      T fs[4]; l4_rhs_##T(s, fs, p);                                /* :112-115 */   \
+      l4_rhs_##T(m, f, p);                                          /* :323-326 */   \
+      for (int j = 0; j < 4; ++j) m[j] = m[j] + f[j] * p[3];        /* :327-330 */   \
+      T fm[4]; l4_rhs_##T(m, fm, p);                                /* :333-336 */   \
+      l4_rhs_##T(s, f, p);                                          /* :344-347 */   \
+      for (int j = 0; j < 4; ++j) s[j] = s[j] + f[j] * p[3];        /* :348-351 */   \
+      T fs[4]; l4_rhs_##T(s, fs, p);                                /* :354-357 */   \
       T* o = obs + 8 * i;                                                            \
       for (int j = 0; j < 4; ++j) { o[j] = m[j] - s[j]; o[4 + j] = fm[j] - fs[j]; }  \
       T r = -(((((T)0 + (T)fabs(o[0])) + (T)fabs(o[1])) + (T)fabs(o[2])) +           \
@@ -355,14 +355,13 @@ static inline double u01d(uint32_t a, uint32_t b) {
 /* The on-device reset draws (purpose 1), per system / dtype:
  * init rows as lz_reset's `init` layout.  f32: value j = lo + (hi-lo)*u24(word j);
  * f64 (and PMSM, which the reference draws in f64 then casts): words (2j, 2j+1). */
-void orc_reset_draw(int32_t system, int32_t f64, int64_t n, int64_t gid0, uint64_t seed,
-                    uint64_t tick, int32_t hr_flags, void* out) {
+static void draw_row(int32_t system, int32_t f64, int64_t i, uint64_t g, uint64_t seed,
+                     uint64_t tick, int32_t hr_flags, void* out) {
   const uint32_t RESET = 1;
-  for (int64_t i = 0; i < n; ++i) {
-    uint64_t g = (uint64_t)(gid0 + i);
+  {
     int nv; double lo, hi;
     switch (system) {
-      case 0: nv = 3; lo = -30; hi = 30; break;  /* dynamic.py:62 */
+      case 0: nv = 3; lo = -30; hi = 30; break;  /* dynamic.py:37 */
       case 1: nv = 8; lo = 0; hi = 5; break;     /* lorenz_env_transient.py:277-278 */
       case 2: nv = 6; lo = -30; hi = 30; break;  /* lorenz_env_try_pmsm.py:64-65 */
       case 3: nv = 7; lo = -10; hi = 20; break;  /* lorenz_env_try.py:55-57 (+sigma) */
@@ -375,7 +374,7 @@ void orc_reset_draw(int32_t system, int32_t f64, int64_t n, int64_t gid0, uint64
           if (f64) ((double*)out)[i * 3 + j] = x0[j];
           else ((float*)out)[i * 3 + j] = (float)x0[j];
         }
-        continue;
+        return;
       }
     }
     for (int j = 0; j < nv; ++j) {
@@ -400,8 +399,20 @@ void orc_reset_draw(int32_t system, int32_t f64, int64_t n, int64_t gid0, uint64
   }
 }
 
-/* the reference's float accumulator done test 't == T' (dynamic.py:110-111,
- * lorenz_env_transient.py:122,127): first step k at which it fires, or -1 */
+void orc_reset_draw(int32_t system, int32_t f64, int64_t n, int64_t gid0, uint64_t seed,
+                    uint64_t tick, int32_t hr_flags, void* out) {
+  for (int64_t i = 0; i < n; ++i) draw_row(system, f64, i, (uint64_t)(gid0 + i), seed, tick, hr_flags, out);
+}
+
+/* the same draws for a list of global ids (row r of out = env gids[r]): the auto-reset
+ * draws of a step touch only the envs that finished in it */
+void orc_reset_draw_idx(int32_t system, int32_t f64, int64_t m, const int64_t* gids, uint64_t seed,
+                        uint64_t tick, int32_t hr_flags, void* out) {
+  for (int64_t r = 0; r < m; ++r) draw_row(system, f64, r, (uint64_t)gids[r], seed, tick, hr_flags, out);
+}
+
+/* the reference's float accumulator done test 't == T' (dynamic.py:85-89,
+ * lorenz_env_transient.py:364,369): first step k at which it fires, or -1 */
 int32_t orc_t_done_step(double dt, double t_end, int32_t max_k) {
   double t = 0.0;
   for (int32_t k = 1; k <= max_k; ++k) {

@@ -134,3 +134,42 @@ def test_product_never_imports_the_oracle():
                 src = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in src and "liblz_oracle" not in src, f
                 assert "from oracle" not in src, f
+
+
+def _fresh(code):
+    import subprocess
+    import sys
+
+    from conftest import PKG
+
+    return subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, %r)\n" % PKG + code],
+                          capture_output=True, text=True, timeout=600)
+
+
+def test_one_hip_runtime_when_gym_lorenz_is_imported_first():
+    """`import gym_lorenz` before `import torch`: exactly one libamdhip64 is mapped,
+    torch's (the library's libamdhip64.so.7 binds to it)."""
+    r = _fresh("import gym_lorenz, torch, os\n"
+               "from gym_lorenz import _native as nat\n"
+               "rt = nat.hip_runtimes()\n"
+               "assert len(rt) == 1 and rt == nat.HIP_RUNTIME, rt\n"
+               "assert os.path.dirname(rt[0]) == os.path.realpath(os.path.join("
+               "os.path.dirname(torch.__file__), 'lib')), rt\n"
+               "print('ok')\n")
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_two_hip_runtimes_fail_loudly():
+    """/opt/rocm's libamdhip64 loaded before torch: torch brings its own copy, so the
+    process would hold two runtimes; importing gym_lorenz raises ImportError naming them
+    instead of running on torch's streams from the other runtime."""
+    import glob
+
+    rocm = sorted(glob.glob("/opt/rocm/lib/libamdhip64.so.*"))
+    if not rocm:
+        pytest.skip("no /opt/rocm libamdhip64")
+    r = _fresh("import ctypes\nctypes.CDLL(%r)\n"
+               "try:\n    import gym_lorenz\nexcept ImportError as e:\n"
+               "    print('refused:', e)\nelse:\n    print('imported')\n" % rocm[0])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "refused:" in r.stdout and "2 HIP runtimes" in r.stdout, r.stdout

@@ -244,6 +244,46 @@ def test_autoreset_compaction_truncation(gl, orc):
     assert not _np(d).any()
 
 
+def test_done_cursor_zeroed_by_reset(gl, orc):
+    """step (every env done) -> lz_reset -> step: the reset launch zeroes the compact
+    list cursor the next step reads, so n_done / done_list() report only that step's
+    done envs (the cursor used to start at the previous step's count)."""
+    n, L = 2000, 3
+    be = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=9, max_episode_steps=L)
+    be.reset()
+    a = torch.zeros((n, 3))
+    for _ in range(L):
+        o, r, d = be.step(a)
+    assert (_np(d) == 2).all() and int(be.n_done_dev.item()) == n
+    be.reset()
+    be.set_state(gl._native.L3_STEP, torch.from_numpy(np.where(np.arange(n) % 7 == 0, L - 1, 0)
+                                                       .astype(np.int32)))
+    o, r, d = be.step(a)
+    want = np.nonzero(np.arange(n) % 7 == 0)[0]
+    assert int(be.n_done_dev.item()) == want.size
+    idx, _ = be.done_list()
+    assert np.array_equal(_np(idx), want)
+    assert np.array_equal(np.nonzero(_np(d))[0], want)
+
+
+def test_seed_then_reset_reproducible(gl, orc):
+    """VecEnv.seed(s) + reset() draws the same initial states whatever calls came
+    before (lz_set_seed rewinds the device call counter)."""
+    n = 1000
+    be = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=1)
+    be.reset()
+    for _ in range(5):
+        be.step(torch.zeros((n, 3)))
+    be.set_seed(42)
+    o1 = _np(be.reset()).copy()
+    be.step(torch.zeros((n, 3)))
+    be.reset()
+    be.set_seed(42)
+    o2 = _np(be.reset()).copy()
+    assert bits_equal(o1, o2)
+    assert bits_equal(o1, orc.l3_reset_obs(orc.reset_draw("l3", np.float32, n, 0, 42, 0)))
+
+
 def test_autoreset_termination_pmsm(gl, orc):
     """PMSM error_sum > 1000 termination with auto-reset; Adam state persists."""
     n = 512

@@ -263,7 +263,7 @@ def test_policy_vecnormalize(gl, pol):
 # (K, n): both load schedules of k_gae (double-buffered U=4 below 262,144 envs, single
 # batches of U=8 from there) with K below one batch, exactly 2 and 3 batches, and ragged tails
 @pytest.mark.parametrize("K,n", [(37, 5003), (3, 70), (8, 100), (12, 64), (9, 131075),
-                                 (37, 131072), (5, 262147)])
+                                 (37, 131072), (5, 262147), (37, 262147)])
 def test_gae_bitexact_vs_sb3_restatement(gl, pol, K, n):
     from oracle.sb3_buffer import compute_returns_and_advantage
 
@@ -353,3 +353,26 @@ def test_policy_narrow_net_optuna_setting(gl, pol):
     np.testing.assert_allclose(_np(b.actions).reshape(-1, 2), _np(mean_ref), atol=TOL_A, rtol=TOL_R)
     np.testing.assert_allclose(_np(b.values).reshape(-1), _np(val_ref), atol=TOL_A, rtol=TOL_R)
     assert np.median(np.abs(_np(b.values).reshape(-1) - _np(val_ref))) < 2e-3
+
+
+def test_collect_from_a_side_stream(gl, pol):
+    """collect() + GAE called under a current stream other than the env handle's: the
+    follow-up kernels (episode starts, GAE, obs_rms update) see the rollout's outputs
+     -- results equal a same-stream collect bit for bit."""
+    n, K = 20000, 16
+    _, sd = _random_policy(pol, 6, 2, seed=3, scale=0.2)
+    out = []
+    for side in (False, True):
+        env = gl.BatchedEnv("pmsm", n, seed=12, add_noise=True)
+        col = pol.FusedRolloutCollector(env, sd)
+        col.reset()
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream(device=env.device) if side else torch.cuda.current_stream(env.device)
+        with torch.cuda.stream(s):
+            b = col.collect(K)
+            adv, ret = col.compute_returns_and_advantage(b)
+            res = [t.clone() for t in (b.rewards, b.dones, b.episode_starts, adv, ret)]
+        s.synchronize()
+        out.append([_np(t) for t in res])
+    for x, y in zip(*out):
+        assert np.array_equal(x, y)

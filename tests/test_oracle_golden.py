@@ -10,7 +10,7 @@ from conftest import bits_equal, golden
 
 
 def test_l3_golden_bitexact(orc):
-    """dynamic.py:35-115 in fp64: obs, reward, done, 1000 steps, incl. +-500 clip and
+    """dynamic.py:35-90 in fp64: obs, reward, done, 1000 steps, incl. +-500 clip and
     two trajectories that overflow to inf/NaN."""
     g = golden("l3")
     st = g["x0"].copy()
@@ -20,7 +20,7 @@ def test_l3_golden_bitexact(orc):
             o, r = orc.l3_step(st, g["actions"][:, k].astype(np.float64))
             assert bits_equal(o, g["obs"][:, k]), k
             assert bits_equal(r, g["reward"][:, k]), k
-    assert not g["done"].any()  # dynamic.py:110 never fires (t == 10 on a float sum)
+    assert not g["done"].any()  # dynamic.py:86 never fires (t == 10 on a float sum)
     assert not np.isfinite(g["obs"][-2:, -1]).all()  # the divergent seeds did diverge
 
 
@@ -31,7 +31,7 @@ def test_l3_done_accumulator(orc):
     t = g["t_hist"]
     assert not (t == 10.0).any()
     assert orc.t_done_step(0.01, 10.0) == -1
-    assert orc.t_done_step(0.001, 5.0) == -1  # lorenz_env_transient.py:122,127
+    assert orc.t_done_step(0.001, 5.0) == -1  # lorenz_env_transient.py:364,369
     assert orc.t_done_step(0.25, 1.0) == 4  # an accumulator that does hit T exactly
 
 
