@@ -30,6 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "gym-lorenz_amd"))
 METRIC = "env-steps/sec at 1M parallel Lorenz envs, 1/2/4/8 MI355X; fp32 drift vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+MFMA_F32_PEAK_TFLOPS = 157.3  # dense f32-input MFMA (= the f32 vector peak), MI355X_MICROARCH.md
 
 
 def parse():
@@ -54,6 +55,9 @@ def parse():
                         "vecnorm = VecNormalize(VecEnv).step fused (lz_step_vecnorm + "
                         "lz_vecnorm_apply), 1 GPU")
     p.add_argument("--K", type=int, default=2048, help="rollout length (--mode rollout)")
+    p.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                   help="--mode policy --policy mlp: fp32 = SB3's float32 forward "
+                        "(lz_rollout_policy_f32), bf16 = the bf16-MFMA kernel")
     p.add_argument("--policy", choices=["mlp", "attn", "attn_ln"], default="mlp",
                    help="--mode policy: mlp = SB3 MlpPolicy behind VecNormalize (the PMSM A2C "
                         "learner, code/lorenz_pmsm/train.py); attn = code/train.py's PPO policy "
@@ -323,8 +327,10 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
     net = (ActorCriticAttn(stack * O, A, seed=0, layer_norm=ln) if attn
            else ActorCriticMlp(O, A, seed=0))
     rms = None if attn else DeviceRunningMeanStd(O, device)
+    f32 = not attn and args.precision == "fp32"
     col = FusedRolloutCollector(env, net.state_dict(), gamma=0.99, gae_lambda=0.95, obs_rms=rms,
-                                clip_obs=10.0, training=True, bootstrap=True, frame_stack=stack)
+                                clip_obs=10.0, training=True, bootstrap=True, frame_stack=stack,
+                                precision="fp32" if f32 else "bf16")
     stream = torch.cuda.Stream(device)
     with torch.cuda.stream(stream):
         nat.check(nat.lib.lz_set_stream(env._h, ctypes.c_void_p(stream.cuda_stream)))
@@ -368,6 +374,7 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         elapsed, launch_s = float(t[0]), float(t[1])
     fl = attn_policy_flops(stack * O, A) if attn else policy_flops(O, A)
     achieved = fl * n * K / launch_s / 1e12
+    peak = MFMA_F32_PEAK_TFLOPS if f32 else MFMA_BF16_PEAK_TFLOPS
     mangled = {"pmsm": "7SysPMSME", "lorenz3": "5SysL3IfEE", "lorenz4": "5SysL4IfEE",
                "hr": "5SysHRIfEE"}[args.system]
     return {
@@ -381,7 +388,7 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "bf16 MFMA (fp32 accumulate), f32 env",
+        "dtype": "f32 MFMA (f32 accumulate), f32 env" if f32 else "bf16 MFMA (fp32 accumulate), f32 env",
         "data": "synthetic: on-device Philox initial states and Gaussian action samples; "
                 "SB3-initialised (orthogonal) random policy weights",
         "config": {
@@ -397,22 +404,26 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
                          "+ env step + truncation bootstrap), GAE (lz_gae); %d envs total, %d per "
                          "GPU" if attn else
                          "%s with the SB3 A2C/PPO MlpPolicy (pi/vf [128,128] Tanh) in the loop: "
-                         "%d-step fused rollout (lz_rollout_policy: policy forward + DiagGaussian "
+                         "%d-step fused rollout (lz_rollout_policy" + ("_f32, float32 as SB3" if f32 else
+                                                                     ", bf16 MFMA")
+                         + ": policy forward + DiagGaussian "
                          "sample + clip + env step + truncation bootstrap + VecNormalize obs), "
                          "obs_rms update, GAE (lz_gae); %d envs total, %d per GPU")
                         % (SYSTEM_INFO[args.system][0], K, total, n),
             "system": args.system, "envs_total": total, "envs_per_gpu": n, "mode": "policy",
-            "policy": args.policy,
+            "policy": args.policy, "precision": "fp32" if f32 else "bf16",
             "K": K, "parallelism": "env shard x%d (no collective on step; obs_rms moments "
                                    "all-reduced once per rollout when N>1)" % world,
         },
         "roofline": {
-            "bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS, "traffic": None,
+            "bound": "mfma", "achieved": achieved, "peak": peak,
+            "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
             "kernel": ("_ZN2lz16k_rollout_policyINS_%sLi4ELi32ELi4ELi4EEEvNS_5KArgsENS_5PArgsE"
                        if ln else
                        "_ZN2lz16k_rollout_policyINS_%sLi4ELi32ELi3EEEvNS_5KArgsENS_5PArgsE"
-                       if attn else "_ZN2lz16k_rollout_policyINS_%sLi8EEEvNS_5KArgsENS_5PArgsE")
+                       if attn else
+                       "_ZN2lz16k_rollout_policyINS_%sLi8ELi32ELi5ELi1EEEvNS_5KArgsENS_5PArgsE"
+                       if f32 else "_ZN2lz16k_rollout_policyINS_%sLi8EEEvNS_5KArgsENS_5PArgsE")
                       % mangled,
             "avg_launch_us": launch_s * 1e6, "flop_per_env_step": fl,
             "note": ("achieved = useful FLOP of the attention actor-critic as SB3 computes it "

@@ -608,13 +608,13 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
   return LZ_OK;
 }
 
-// arch: 0 = MlpPolicy, 1 = attention extractor, 2 = residual + LayerNorm attention on
-// VecFrameStack(n_stack) observations
+// arch: 0 = MlpPolicy (bf16), 1 = attention extractor, 2 = residual + LayerNorm attention
+// on VecFrameStack(n_stack) observations, 3 = MlpPolicy in float32
 static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, int arch,
                                 int n_stack = 1, const float* stack_in = nullptr,
                                 float* stack_out = nullptr) {
   if (!h || !r) return fail(LZ_ERR_INVALID, "handle/args is NULL");
-  const bool attn = arch != 0;
+  const bool attn = arch == 1 || arch == 2;
   if (arch == 2) {
     if (n_stack != 1 && n_stack != 4) return fail(LZ_ERR_UNSUPPORTED, "n_stack must be 1 or 4");
     if (!stack_in || !stack_out) return fail(LZ_ERR_INVALID, "stack_in / stack_out must be non-NULL");
@@ -637,8 +637,9 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
   if (!(r->act_low <= r->act_high)) return fail(LZ_ERR_INVALID, "act_low > act_high");
   HIP_TRY(hipSetDevice(h->cfg.device));
   const int64_t n = h->cfg.num_envs;
-  const lz::PolShape sh = attn ? lz::attn_policy_shape(n, h->num_cus)
-                              : lz::policy_shape(n, h->cfg.reserved[0], h->num_cus);
+  const lz::PolShape sh = attn        ? lz::attn_policy_shape(n, h->num_cus)
+                         : arch == 3 ? lz::f32_policy_shape(n, h->num_cus)
+                                     : lz::policy_shape(n, h->cfg.reserved[0], h->num_cus);
   const int W = sh.waves, grid = sh.grid;
   const int O = h->desc.obs_dim;
   const int64_t need = (int64_t)grid * W * 2 * O;
@@ -680,8 +681,9 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
   p.stack_in = stack_in;
   p.stack_out = stack_out;
   int e = arch == 2 ? lz::launch_rollout_policy_attn_ln(h->cfg.system, n_stack, a, p, sh, h->stream)
-          : attn    ? lz::launch_rollout_policy_attn(h->cfg.system, a, p, sh, h->stream)
-                    : lz::launch_rollout_policy(h->cfg.system, a, p, sh, h->stream);
+          : arch == 1 ? lz::launch_rollout_policy_attn(h->cfg.system, a, p, sh, h->stream)
+          : arch == 3 ? lz::launch_rollout_policy_f32(h->cfg.system, a, p, sh, h->stream)
+                      : lz::launch_rollout_policy(h->cfg.system, a, p, sh, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "policy rollout launch: %s", hipGetErrorString((hipError_t)e));
   if (r->obs_moments) {
     e = lz::launch_policy_moments_final(h->pol_part, grid * W, 2 * O, (double)r->K * (double)n,
@@ -696,6 +698,10 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
 
 lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r) {
   return rollout_policy(h, r, 0);
+}
+
+lz_status lz_rollout_policy_f32(lz_handle* h, const lz_policy_rollout_args* r) {
+  return rollout_policy(h, r, 3);
 }
 
 lz_status lz_rollout_policy_attn(lz_handle* h, const lz_policy_rollout_args* r) {

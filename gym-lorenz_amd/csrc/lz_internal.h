@@ -149,6 +149,27 @@ constexpr int kLnPi = kLnExt, kLnVf = kLnExt + kAttNet;
 constexpr int kLnLogStd = kLnExt + 2 * kAttNet;
 constexpr int kLnBlobBytes = kLnLogStd + 64;       // 145984 B (resident in LDS)
 
+// The MlpPolicy again at the precision SB3 runs it (float32 operands, float32
+// accumulation): f32-input MFMA (v_mfma_f32_32x32x2_f32, bit-for-bit a k-ordered fmaf
+// chain) for the two hidden layers, the heads as per-lane fmaf chains, tanh from IEEE
+// basic operations -- every result is a fixed sequence of correctly rounded
+// operations the C oracle restates exactly.  Blob (lz_policy_pack_f32), per net:
+//   W1 [4 out tiles][64 lanes][4 k-steps] f32 (lane (r, h), k-step s: W1[32t + r][2s + h]),
+//   W2 [4 out tiles][16 quads][64 lanes][4] f32 (k-step q = 4 quad + e: input unit
+//      32 (q >> 4) + row(q & 15, h)), b1 / b2 [4][2 halves][16] f32 as accumulator
+//   initialisers, head rows [4][2 halves][64] f32 (element 16t + g: unit 32t + row(g, h)),
+//   head bias [4] f32; net 0 = pi (action_net head), net 1 = vf (value_net head);
+//   log_std / Normal constants float[16] after both nets.
+constexpr int kF32W1 = 0;
+constexpr int kF32W2 = kF32W1 + 4 * 64 * 4 * 4;
+constexpr int kF32B1 = kF32W2 + 4 * 16 * 64 * 4 * 4;
+constexpr int kF32B2 = kF32B1 + 4 * 2 * 16 * 4;
+constexpr int kF32H = kF32B2 + 4 * 2 * 16 * 4;
+constexpr int kF32HB = kF32H + 4 * 2 * 64 * 4;
+constexpr int kF32Net = kF32HB + 64;                 // 72768 B
+constexpr int kF32LogStd = 2 * kF32Net;
+constexpr int kF32BlobBytes = kF32LogStd + 64;      // 145600 B (resident in LDS)
+
 struct PArgs {
   const uint8_t* blob;     // device copy of the packed policy
   const float* obs_in;     // [N, O] raw observation at rollout start
@@ -228,6 +249,12 @@ inline PolShape policy_shape(int64_t n, int variant, int num_cus) {
 }
 int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, const PolShape& sh,
                           void* stream);
+// the float32 MlpPolicy (kF32* blob): 32 envs per wave, 8 waves (two per SIMD; the
+// 146 KB blob leaves room for one workgroup per CU, the obs moments live in registers),
+// 4 waves below 8 tiles per CU
+PolShape f32_policy_shape(int64_t n, int num_cus);
+int launch_rollout_policy_f32(int system, const KArgs& a, const PArgs& p, const PolShape& sh,
+                              void* stream);
 // the attention-extractor policy (kAtt* blob): one shape, 32 envs per wave, 4 waves
 // (one per SIMD: the 137 KB blob leaves room for one workgroup per CU)
 PolShape attn_policy_shape(int64_t n, int num_cus);

@@ -671,11 +671,138 @@ __device__ __forceinline__ void net_fwd(const uint8_t* net, const float* x, bool
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The MlpPolicy at SB3's precision (kMlpF32, kF32* blob).  Float32 operands end to end;
+// every output is a fixed sequence of correctly rounded IEEE operations, so the C
+// oracle (oracle/lz_oracle.c orc_mlp_f32) reproduces it bit for bit:
+//   * hidden layers on v_mfma_f32_32x32x2_f32 (gfx950: bit-for-bit the k-ordered fmaf
+//     chain D = fma(a_k1, b_k1, fma(a_k0, b_k0, C)), k0 = lane half 0's operand).  Same
+//     dataflow as the bf16 kernel: weights = A (32 units x 2 inputs), activations = B
+//     (2 inputs x 32 envs); layer 1's accumulator register g of lane half h (unit
+//     row(g, h) of its tile, env on the lane) is exactly layer 2's B operand for
+//     k-step 16 ti + g, so layer 2 sums its 128 inputs in the order
+//     ti = 0..3, g = 0..15, h = 0, 1 -- the packer permutes W2's columns to match;
+//   * the heads (2-4 rows: a 32-row MFMA tile would waste 90% of it) as one fmaf chain
+//     per lane half over that half's 64 units (t, g ascending), the halves' partial
+//     sums added once (__shfl_xor 32), then the bias;
+//   * tanh from basic operations only (tanh_ieee): expm1 by Cody-Waite reduction + a
+//     degree-8 Taylor polynomial in fmaf, 2^n assembled in the exponent bits, one
+//     correctly rounded division -- no v_exp_f32 / v_rcp_f32, whose bits no CPU
+//     reproduces.  Max error vs tanh in float64: 2.2 ulp (tests/test_policy_f32_host.py).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float tanh_ieee(float x) {
+  const float ax = fabsf(x);
+  const float axc = ax < 9.0f ? ax : 9.0f;  // NaN -> 9: the selects below fix the result
+  const float y = -2.0f * axc;              // exact; tanh(|x|) = -expm1(y) / (2 + expm1(y))
+  const float n = __builtin_rintf(y * 1.44269502f);
+  float r = fmaf(n, -0.693145751953125f, y);  // ln2 high part: n * it is exact
+  r = fmaf(n, -1.42860677e-06f, r);
+  float q = 2.48015873e-05f;                  // 1/8!
+  q = fmaf(q, r, 1.98412698e-04f);
+  q = fmaf(q, r, 1.38888889e-03f);
+  q = fmaf(q, r, 8.33333333e-03f);
+  q = fmaf(q, r, 4.16666667e-02f);
+  q = fmaf(q, r, 1.66666667e-01f);
+  q = fmaf(q, r, 0.5f);
+  const float p = fmaf(r * r, q, r);          // expm1(r), |r| <= ln2 / 2
+  const float s = __uint_as_float((uint32_t)((int)n + 127) << 23);  // 2^n, n in [-26, 0]
+  // |x| < 0.45: -expm1 / (2 + expm1) (no cancellation near 0); else with E = e^-2|x|
+  // < 0.41: (1 - E) / (1 + E) (E's error not amplified near tanh = 1)
+  const bool lo = ax < 0.45f;
+  const float em1 = fmaf(s, p, s - 1.0f);     // 2^n (1 + p) - 1
+  const float e = fmaf(s, p, s);              // 2^n (1 + p)
+  float t = (lo ? -em1 : 1.0f - e) / (lo ? 2.0f + em1 : 1.0f + e);
+  t = ax < 9.0f ? t : 1.0f;                   // 1 - tanh(9) < 2^-25: rounds to 1
+  t = ax < 2.44140625e-04f ? ax : t;          // |x| < 2^-12: tanh(x) = x in float32
+  t = x != x ? x : t;
+  return __builtin_copysignf(t, x);
+}
+
+// One net on the wave's 32-env tile.  xs[s] = this lane's layer-1 input for k-step s
+// (obs[2s + h] of env lane & 31).  Returns the NH head rows in head[] on every lane
+// (both halves hold the same values).
+template <int KS1, int NH>
+__device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int lane, float* head) {
+  asm volatile("" ::: "memory");
+  const int h = lane >> 5;
+  const f32x4* w1 = reinterpret_cast<const f32x4*>(net + kF32W1) + lane;
+  const f32x4* w2 = reinterpret_cast<const f32x4*>(net + kF32W2) + lane;
+  const f32x16* b1 = reinterpret_cast<const f32x16*>(net + kF32B1) + h;
+  const f32x16* b2 = reinterpret_cast<const f32x16*>(net + kF32B2) + h;
+  const float* wh = reinterpret_cast<const float*>(net + kF32H) + h * 64;
+  const float* bh = reinterpret_cast<const float*>(net + kF32HB);
+  f32x16 a1[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f32x4 w = w1[t * 64];
+    f32x16 c = b1[2 * t];
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) c = mfma_f32(w[s], xs[s], c);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      c[g] = tanh_ieee(c[g]);
+    }
+    a1[t] = c;
+  }
+  float acc[NH];
+#pragma unroll
+  for (int j = 0; j < NH; ++j) acc[j] = 0.0f;  // first step fmaf(w, v, +0)
+  // one output tile at a time (not unrolled: four tiles' tanh chains in flight at once
+  // would spill)
+#pragma unroll 1
+  for (int t = 0; t < 4; ++t) {
+    f32x16 c = b2[2 * t];
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti) {
+      // the tile's 16 k-steps of weights in four 16-B loads, issued together
+      asm volatile("" ::: "memory");
+      f32x4 wq[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wq[e] = w2[((t * 16) + ti * 4 + e) * 64];
+#pragma unroll
+      for (int g = 0; g < 16; ++g) c = mfma_f32(wq[g >> 2][g & 3], a1[ti][g], c);
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const float v = tanh_ieee(c[g]);
+#pragma unroll
+      for (int j = 0; j < NH; ++j) {
+        const float w = wh[j * 128 + t * 16 + g];
+        acc[j] = fmaf(w, v, acc[j]);
+      }
+      if ((g & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NH; ++j) {
+    const float o = __shfl_xor(acc[j], 32, 64);
+    head[j] = (acc[j] + o) + bh[j];  // IEEE add commutes: both halves get the same bits
+  }
+}
+
+// this lane's layer-1 inputs from the env-owning lane (half 0) of its env
+template <int O, int KS1>
+__device__ __forceinline__ void f32_inputs(const float* x, int lane, float* xs) {
+  const int src = lane & 31;
+#pragma unroll
+  for (int s = 0; s < KS1; ++s) {
+    const float lo = __shfl(x[2 * s], src, 64);
+    const float hi = __shfl(2 * s + 1 < O ? x[2 * s + 1 < O ? 2 * s + 1 : 0] : 0.0f, src, 64);
+    xs[s] = lane < 32 ? lo : hi;
+  }
+}
+
 // The kernel variants (template parameter kPair of k_rollout_policy): the MlpPolicy
 // nets one after the other / interleaved / interleaved with pipelined weight loads,
 // code/train.py's attention actor-critic, code/lorenz_filter/train.py's residual +
 // LayerNorm attention actor-critic on VecFrameStack observations.
-constexpr int kMlpSerial = 0, kMlpPair = 1, kMlpPairPipe = 2, kAttn = 3, kAttnLn = 4;
+constexpr int kMlpSerial = 0, kMlpPair = 1, kMlpPairPipe = 2, kAttn = 3, kAttnLn = 4,
+              kMlpF32 = 5;
 
 // V(x) alone (truncation bootstrap, last values): the value net, after the shared
 // attention extractor for kPair == kAttn
@@ -686,6 +813,10 @@ __device__ __forceinline__ void value_fwd(const uint8_t* blob, const uint8_t* vf
     bf16x8 f[4];
     attn_extract(blob, obs_frag<O>(x, use), lane, f);
     out[0] = attn_net(blob + kAttVf, f, lane)[0];
+  } else if constexpr (kPair == kMlpF32) {
+    float xs[(O + 1) / 2];
+    f32_inputs<O, (O + 1) / 2>(x, lane, xs);
+    mlp_f32<(O + 1) / 2, 1>(vf_net, xs, lane, out);
   } else {
     net_fwd<E, O, 1>(vf_net, x, use, lane, out);
   }
@@ -694,12 +825,15 @@ __device__ __forceinline__ void value_fwd(const uint8_t* blob, const uint8_t* vf
 // kPair (see kMlpSerial ...): kMlpPair = mlp_pair, kMlpPairPipe = mlp_pair_pipe,
 // kAttn = attn_extract + attn_nets_pair (kAtt* blob), kAttnLn = attn_ln_extract +
 // attn_nets_pair (kLn* blob) with the S-frame stack in the registers of both lane
-// halves of the env
+// halves of the env, kMlpF32 = mlp_f32 twice (kF32* blob; the obs moments accumulate
+// in registers: the blob leaves too little LDS for them)
 template <class Sys, int W, int E, int kPair, int S = 1>
 __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   static_assert(kPair == kMlpSerial || E == 32, "the paired / attention kernels run 32-env tiles");
-  constexpr int kBlob =
-      kPair == kAttnLn ? kLnBlobBytes : kPair == kAttn ? kAttBlobBytes : kPolBlobBytes;
+  constexpr int kBlob = kPair == kAttnLn ? kLnBlobBytes
+                        : kPair == kAttn ? kAttBlobBytes
+                        : kPair == kMlpF32 ? kF32BlobBytes : kPolBlobBytes;
+  constexpr bool kRegMom = kPair == kMlpF32;  // obs moments in registers, not LDS
   constexpr int O = Sys::O, A = Sys::A;
   constexpr int SO = S * O, KS = (SO + 15) / 16;  // kAttnLn: stacked dims, fc1 k-steps
   static_assert(kPair == kAttnLn || S == 1, "frame stacking is the kAttnLn path");
@@ -708,7 +842,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   static_assert(E == 32 || E == 64, "envs per wave");
   __shared__ __attribute__((aligned(64))) uint8_t s_blob[kBlob];
   __shared__ double s_norm[2 * kPolMaxObs];
-  __shared__ double s_mom[kPair == kAttnLn ? 1 : W * E * 2 * O];  // kAttnLn: no obs moments
+  __shared__ double s_mom[(kPair == kAttnLn || kRegMom) ? 1 : W * E * 2 * O];  // kAttnLn: none
   const int tid = (int)threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int slot = E == 64 ? lane : (lane & 31);  // this lane's env within the tile
@@ -729,12 +863,15 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   }
   __syncthreads();
   const uint8_t* pi_net = s_blob + (kPair == kAttnLn ? kLnPi : kPair == kAttn ? kAttPi : 0);
-  const uint8_t* vf_net = s_blob + (kPair == kAttnLn ? kLnVf : kPair == kAttn ? kAttVf : kPolNet);
+  const uint8_t* vf_net =
+      s_blob + (kPair == kAttnLn ? kLnVf : kPair == kAttn ? kAttVf : kPair == kMlpF32 ? kF32Net : kPolNet);
   // torch.distributions.Normal constants, computed by the packer: scale = exp(log_std),
   // 2 * scale**2, log(scale) (LDS, wave-uniform broadcast reads)
   const float* g_scale =
       reinterpret_cast<const float*>(
-          s_blob + (kPair == kAttnLn ? kLnLogStd : kPair == kAttn ? kAttLogStd : kPolLogStd)) + 4;
+          s_blob + (kPair == kAttnLn   ? kLnLogStd
+                    : kPair == kAttn   ? kAttLogStd
+                    : kPair == kMlpF32 ? kF32LogStd : kPolLogStd)) + 4;
   const float* g_var2 = g_scale + 4;
   const float* g_lscale = g_scale + 8;
   const bool norm = p.norm != nullptr;
@@ -743,9 +880,14 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   const bool det = (p.pflags & LZ_POLICY_DETERMINISTIC) != 0;
   const bool boot = (p.pflags & LZ_POLICY_BOOTSTRAP) != 0;
   const float gamma = p.gamma;
-  // per-lane float64 obs-moment accumulators of the env-owning lanes, in LDS
-  double* mom = s_mom + (kPair == kAttnLn ? 0 : (wave * E + slot) * (2 * O));
-  if constexpr (kPair != kAttnLn) {
+  // per-lane float64 obs-moment accumulators of the env-owning lanes, in LDS; kRegMom:
+  // in registers, split over the env's two lanes (half 0 the sums, half 1 the squares)
+  double mom_r[kRegMom ? O : 1];
+  double* mom = kRegMom ? mom_r : s_mom + (kPair == kAttnLn ? 0 : (wave * E + slot) * (2 * O));
+  if constexpr (kRegMom) {
+#pragma unroll
+    for (int j = 0; j < O; ++j) mom_r[j] = 0.0;
+  } else if constexpr (kPair != kAttnLn) {
     if (owner) {
 #pragma unroll
       for (int j = 0; j < 2 * O; ++j) mom[j] = 0.0;
@@ -814,6 +956,12 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
 #pragma unroll
         for (int j = 0; j < A; ++j) mean[j] = hp[j];
         val[0] = hv[0];
+      } else if constexpr (kPair == kMlpF32) {
+        float xs[(O + 1) / 2];
+        f32_inputs<O, (O + 1) / 2>(x, lane, xs);
+        mlp_f32<(O + 1) / 2, A>(pi_net, xs, lane, mean);
+        __builtin_amdgcn_sched_barrier(0);  // the two nets one after the other
+        mlp_f32<(O + 1) / 2, 1>(vf_net, xs, lane, val);
       } else if constexpr (kPair == kMlpPair || kPair == kMlpPairPipe) {
         f32x16 hp, hv;
         if constexpr (kPair == kMlpPairPipe)
@@ -897,12 +1045,21 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       if (live) {
         rew_buf[off] = rew;
         a.done[off] = df;
-        if (kPair != kAttnLn && p.partials) {
+        if (kPair != kAttnLn && !kRegMom && p.partials) {
 #pragma unroll
           for (int j = 0; j < O; ++j) {
             const double v = (double)on[j];
             mom[j] += v;
             mom[O + j] += v * v;
+          }
+        }
+      }
+      if constexpr (kRegMom) {
+        if (p.partials) {
+#pragma unroll
+          for (int j = 0; j < O; ++j) {
+            const double v = (double)__shfl(on[j], lane & 31, 64);
+            if (i < a.n) mom_r[j] += h ? v * v : v;
           }
         }
       }
@@ -937,7 +1094,9 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
     double* dst = p.partials + ((int64_t)blockIdx.x * W + wave) * (2 * O);
 #pragma unroll
     for (int j = 0; j < 2 * O; ++j) {
-      double v = owner ? mom[j] : 0.0;
+      double v;
+      if constexpr (kRegMom) v = (j < O ? h == 0 : h == 1) ? mom_r[j < O ? j : j - O] : 0.0;
+      else v = owner ? mom[j] : 0.0;
 #pragma unroll
       for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
       if (lane == 0) dst[j] = v;
@@ -1093,6 +1252,43 @@ static int launch_pol(const KArgs& a, const PArgs& p, const PolShape& sh, hipStr
   return (int)hipGetLastError();
 }
 
+template <class Sys>
+static int launch_pol_f32(const KArgs& a, const PArgs& p, const PolShape& sh, hipStream_t s) {
+  if (sh.waves == 4)
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, kMlpF32>), dim3((unsigned)sh.grid), dim3(4 * 64), 0, s,
+                       a, p);
+  else
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 32, kMlpF32>), dim3((unsigned)sh.grid), dim3(8 * 64), 0, s,
+                       a, p);
+  return (int)hipGetLastError();
+}
+
+// 8 waves (two per SIMD) when there are enough 32-env tiles for every CU, else 4 (one
+// per SIMD: cfg5's 32,768 envs are 1,024 tiles = 128 eight-wave groups, half the CUs)
+PolShape f32_policy_shape(int64_t n, int num_cus) {
+  const int64_t tiles = (n + 31) / 32;
+  PolShape s = {32, tiles >= 8 * (int64_t)num_cus ? 8 : 4, 0, 0};
+  const int64_t groups = (tiles + s.waves - 1) / s.waves;
+  s.grid = (int)(groups < num_cus ? groups : num_cus);
+  return s;
+}
+
+int launch_rollout_policy_f32(int system, const KArgs& a, const PArgs& p, const PolShape& grid,
+                              void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (system) {
+    case LZ_SYS_LORENZ3: return launch_pol_f32<SysL3<float>>(a, p, grid, s);
+    case LZ_SYS_LORENZ4: return launch_pol_f32<SysL4<float>>(a, p, grid, s);
+    case LZ_SYS_PMSM: return launch_pol_f32<SysPMSM>(a, p, grid, s);
+    case LZ_SYS_HR: return launch_pol_f32<SysHR<float>>(a, p, grid, s);
+    case LZ_SYS_T1: return launch_pol_f32<SysT1<float>>(a, p, grid, s);
+    case LZ_SYS_T2: return launch_pol_f32<SysT2<float>>(a, p, grid, s);
+    case LZ_SYS_TP: return launch_pol_f32<SysTP<float>>(a, p, grid, s);
+    case LZ_SYS_SC: return launch_pol_f32<SysSC<float>>(a, p, grid, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
 int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, const PolShape& grid,
                           void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1225,6 +1421,39 @@ void pack_net(uint8_t* net, int O, int rows3, const float* w1, const float* b1, 
       }
       c3[h * 16 + g] = row_of(g, h) < rows3 ? b3[row_of(g, h)] : 0.0f;
     }
+}
+
+// float32 MlpPolicy net (kF32* layout, see mlp_f32 / lz_internal.h)
+void pack_net_f32(uint8_t* net, int O, int rows3, const float* w1, const float* b1, const float* w2,
+                  const float* b2, const float* w3, const float* b3) {
+  using lz::kPolHidden;
+  float* f1 = reinterpret_cast<float*>(net + lz::kF32W1);
+  float* f2 = reinterpret_cast<float*>(net + lz::kF32W2);
+  float* c1 = reinterpret_cast<float*>(net + lz::kF32B1);
+  float* c2 = reinterpret_cast<float*>(net + lz::kF32B2);
+  float* hw = reinterpret_cast<float*>(net + lz::kF32H);
+  float* hb = reinterpret_cast<float*>(net + lz::kF32HB);
+  for (int lane = 0; lane < 64; ++lane) {
+    const int r = lane & 31, h = lane >> 5;
+    for (int t = 0; t < 4; ++t) {
+      for (int s = 0; s < 4; ++s) {  // layer 1: A[row r][k = h] of k-step s = input 2s + h
+        const int k = 2 * s + h;
+        f1[(t * 64 + lane) * 4 + s] = k < O ? w1[(32 * t + r) * O + k] : 0.0f;
+      }
+      for (int q = 0; q < 64; ++q)  // layer 2: k-step q = input unit 32 (q >> 4) + row(q & 15, h)
+        f2[((t * 16 + q / 4) * 64 + lane) * 4 + q % 4] =
+            w2[(32 * t + r) * kPolHidden + 32 * (q >> 4) + row_of(q & 15, h)];
+    }
+  }
+  for (int h = 0; h < 2; ++h)
+    for (int g = 0; g < 16; ++g)
+      for (int t = 0; t < 4; ++t) {
+        c1[(2 * t + h) * 16 + g] = b1[32 * t + row_of(g, h)];
+        c2[(2 * t + h) * 16 + g] = b2[32 * t + row_of(g, h)];
+        for (int j = 0; j < rows3; ++j)
+          hw[(j * 2 + h) * 64 + t * 16 + g] = w3[j * kPolHidden + 32 * t + row_of(g, h)];
+      }
+  for (int j = 0; j < rows3; ++j) hb[j] = b3[j];
 }
 
 // Attention-extractor actor-critic (kAtt* layout, see lz_internal.h / attn_extract).
@@ -1454,6 +1683,49 @@ lz_status lz_policy_pack_hidden(const lz_mlp_policy* p, int32_t hidden, void* ho
   w.act_w = pad(p->act_w, A, hidden, A, H);
   w.val_w = pad(p->val_w, 1, hidden, 1, H);
   return lz_policy_pack(&w, host_blob, cap);
+}
+
+int64_t lz_policy_f32_blob_bytes(void) { return lz::kF32BlobBytes; }
+
+lz_status lz_policy_pack_f32(const lz_mlp_policy* p, int32_t hidden, void* host_blob, int64_t cap) {
+  if (!p || !host_blob) return pfail(LZ_ERR_INVALID, "policy/blob is NULL");
+  if (cap < lz::kF32BlobBytes) return pfail(LZ_ERR_INVALID, "blob capacity too small");
+  if (hidden < 1 || hidden > lz::kPolHidden) return pfail(LZ_ERR_UNSUPPORTED, "hidden width must be 1..128");
+  if (p->obs_dim < 1 || p->obs_dim > lz::kPolMaxObs || p->act_dim < 1 || p->act_dim > lz::kPolMaxAct)
+    return pfail(LZ_ERR_UNSUPPORTED, "policy supports obs_dim 1..8 and act_dim 1..4");
+  const float* req[] = {p->pi_w1, p->pi_b1, p->pi_w2, p->pi_b2, p->vf_w1, p->vf_b1, p->vf_w2,
+                        p->vf_b2, p->act_w, p->act_b, p->val_w, p->val_b, p->log_std};
+  for (const float* q : req)
+    if (!q) return pfail(LZ_ERR_INVALID, "a policy weight pointer is NULL");
+  // zero-pad a [hidden, hidden] net to the kernel's 128 units (as lz_policy_pack_hidden):
+  // a padded unit is tanh(0) = 0 with zero weights, each of its chain steps fma(0, w, acc)
+  // returns acc unchanged
+  const int H = lz::kPolHidden, O = p->obs_dim, A = p->act_dim;
+  std::vector<float> buf((size_t)2 * (H * O + H + H * H + H) + (size_t)(A + 1) * H, 0.0f);
+  float* q = buf.data();
+  auto pad = [&](const float* src, int rows, int cols, int prow, int pcol) {
+    float* dst = q;
+    for (int r = 0; r < rows; ++r)
+      for (int c = 0; c < cols; ++c) dst[r * pcol + c] = src[r * cols + c];
+    q += (size_t)prow * pcol;
+    return dst;
+  };
+  const float* pw1 = pad(p->pi_w1, hidden, O, H, O);
+  const float* pb1 = pad(p->pi_b1, 1, hidden, 1, H);
+  const float* pw2 = pad(p->pi_w2, hidden, hidden, H, H);
+  const float* pb2 = pad(p->pi_b2, 1, hidden, 1, H);
+  const float* vw1 = pad(p->vf_w1, hidden, O, H, O);
+  const float* vb1 = pad(p->vf_b1, 1, hidden, 1, H);
+  const float* vw2 = pad(p->vf_w2, hidden, hidden, H, H);
+  const float* vb2 = pad(p->vf_b2, 1, hidden, 1, H);
+  const float* aw = pad(p->act_w, A, hidden, A, H);
+  const float* uw = pad(p->val_w, 1, hidden, 1, H);
+  uint8_t* b = static_cast<uint8_t*>(host_blob);
+  std::memset(b, 0, lz::kF32BlobBytes);
+  pack_net_f32(b, O, A, pw1, pb1, pw2, pb2, aw, p->act_b);
+  pack_net_f32(b + lz::kF32Net, O, 1, vw1, vb1, vw2, vb2, uw, p->val_b);
+  pack_gauss(reinterpret_cast<float*>(b + lz::kF32LogStd), A, p->log_std);
+  return LZ_OK;
 }
 
 int64_t lz_attn_policy_blob_bytes(void) { return lz::kAttBlobBytes; }

@@ -179,6 +179,10 @@ _SIGS = {
     "lz_policy_pack_hidden": (ctypes.c_int, [ctypes.POINTER(LzMlpPolicy), ctypes.c_int32, VP,
                                              ctypes.c_int64]),
     "lz_rollout_policy": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
+    "lz_policy_f32_blob_bytes": (ctypes.c_int64, []),
+    "lz_policy_pack_f32": (ctypes.c_int, [ctypes.POINTER(LzMlpPolicy), ctypes.c_int32, VP,
+                                          ctypes.c_int64]),
+    "lz_rollout_policy_f32": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
     "lz_attn_policy_blob_bytes": (ctypes.c_int64, []),
     "lz_attn_policy_pack": (ctypes.c_int, [ctypes.POINTER(LzAttnPolicy), VP, ctypes.c_int64]),
     "lz_rollout_policy_attn": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),

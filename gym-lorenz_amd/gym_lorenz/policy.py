@@ -10,8 +10,11 @@ the host, one ``DummyVecEnv.step`` over the envs one at a time, a RolloutBuffer 
 and finally ``RolloutBuffer.compute_returns_and_advantage``.
 
 ``FusedRolloutCollector.collect(K)`` does all K steps in ONE kernel launch
-(``lz_rollout_policy``): the two 6->128->128 MLPs on bf16 MFMA with fp32
-accumulation, the Gaussian sample (Philox), the action-space clip, the env step with
+(``lz_rollout_policy_f32``): the two 6->128->128 MLPs at SB3's own precision
+(float32 operands and accumulation on f32-input MFMA, a deterministic operation order
+the C oracle reproduces bit for bit; ``precision="bf16"`` selects the faster bf16-MFMA
+kernel ``lz_rollout_policy``, the attention policies run bf16 only), the Gaussian
+sample (Philox), the action-space clip, the env step with
 auto-reset, SB3's truncation bootstrap, and VecNormalize's observation normalisation
 (statistics frozen for the K steps and updated once from the K steps' moments).
 ``compute_returns_and_advantage`` is ``lz_gae``.  The buffers come back as
@@ -342,9 +345,7 @@ def _np(v):
     return np.asarray(v, np.float32)
 
 
-def pack_policy(state_dict, obs_dim, act_dim):
-    """lz_policy_pack / lz_policy_pack_hidden: SB3 state_dict (net_arch pi=[H,H]
-    vf=[H,H], H <= 128) -> uint8 numpy blob (host; needs no GPU)."""
+def _mlp_policy_struct(state_dict, obs_dim, act_dim):
     arrs = []
     for key in KEYS:
         if key not in state_dict:
@@ -361,6 +362,22 @@ def pack_policy(state_dict, obs_dim, act_dim):
     p.obs_dim, p.act_dim = int(obs_dim), int(act_dim)
     for f, a in zip(_FIELDS, arrs):
         setattr(p, f, a.ctypes.data)
+    return p, H, arrs  # arrs keep the weights alive while p points at them
+
+
+def pack_policy_f32(state_dict, obs_dim, act_dim):
+    """lz_policy_pack_f32: SB3 state_dict (net_arch pi=[H,H] vf=[H,H], H <= 128) ->
+    uint8 numpy blob of the float32 kernel (host; needs no GPU)."""
+    p, H, _keep = _mlp_policy_struct(state_dict, obs_dim, act_dim)
+    blob = np.zeros(int(nat.lib.lz_policy_f32_blob_bytes()), np.uint8)
+    nat.check(nat.lib.lz_policy_pack_f32(ctypes.byref(p), H, blob.ctypes.data, blob.size))
+    return blob
+
+
+def pack_policy(state_dict, obs_dim, act_dim):
+    """lz_policy_pack / lz_policy_pack_hidden: SB3 state_dict (net_arch pi=[H,H]
+    vf=[H,H], H <= 128) -> uint8 numpy blob of the bf16 kernel (host; needs no GPU)."""
+    p, H, _keep = _mlp_policy_struct(state_dict, obs_dim, act_dim)
     blob = np.zeros(int(nat.lib.lz_policy_blob_bytes()), np.uint8)
     nat.check(nat.lib.lz_policy_pack_hidden(ctypes.byref(p), H, blob.ctypes.data, blob.size))
     return blob
@@ -452,11 +469,17 @@ class FusedRolloutCollector:
     state_dict:    SB3 ActorCriticPolicy / ActorCriticMlp state_dict
     obs_rms:       gym_lorenz.vec_normalize.DeviceRunningMeanStd or None
     training:      update obs_rms after each rollout (VecNormalize.training)
+    precision:     MlpPolicy arithmetic: "fp32" (default; SB3's float32 forward,
+                   lz_rollout_policy_f32) or "bf16" (bf16 MFMA operands, fp32
+                   accumulation, lz_rollout_policy: ~2.5x faster, ~1e-2 off SB3).  The
+                   attention actor-critics (code/train.py, code/lorenz_filter/train.py)
+                   run bf16 whatever this says (None = default for the policy kind).
     """
 
     def __init__(self, backend, state_dict=None, gamma=0.99, gae_lambda=0.95, obs_rms=None,
                  clip_obs=10.0, norm_eps=1e-8, training=True, bootstrap=True,
-                 deterministic=False, capture_terminal=0, group=None, frame_stack=1):
+                 deterministic=False, capture_terminal=0, group=None, frame_stack=1,
+                 precision=None):
         if backend.tdtype != torch.float32:
             raise ValueError("the fused policy rollout runs float32 env handles")
         self.env = backend
@@ -468,6 +491,10 @@ class FusedRolloutCollector:
         self.capture_terminal = int(capture_terminal)
         self.group = group
         self.act_low, self.act_high = action_bounds(backend.system_name)
+        if precision not in (None, "fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
+        self.precision = precision
+        self.f32 = False
         self.blob = None
         self.attention = False
         self.attention_ln = False
@@ -497,9 +524,13 @@ class FusedRolloutCollector:
             if self.obs_rms is not None:
                 raise ValueError("the LayerNorm attention rollout takes raw observations")
             blob = pack_attn_ln_policy(state_dict, self.frame_stack * self.O, self.A)
+        elif self.attention:
+            blob = pack_attn_policy(state_dict, self.O, self.A)
         else:
-            pack = pack_attn_policy if self.attention else pack_policy
-            blob = pack(state_dict, self.O, self.A)
+            self.f32 = self.precision != "bf16"
+            blob = (pack_policy_f32 if self.f32 else pack_policy)(state_dict, self.O, self.A)
+        if (self.attention or self.attention_ln) and self.precision == "fp32":
+            raise ValueError("the attention actor-critics run bf16 only (precision='bf16')")
         self.blob = torch.from_numpy(blob).to(self.device)
 
     def reset(self):
@@ -564,7 +595,8 @@ class FusedRolloutCollector:
                                                            self.frame_stack, _p(self.last_stack),
                                                            _p(stack_out)))
         else:
-            launch = nat.lib.lz_rollout_policy_attn if self.attention else nat.lib.lz_rollout_policy
+            launch = (nat.lib.lz_rollout_policy_attn if self.attention else
+                      nat.lib.lz_rollout_policy_f32 if self.f32 else nat.lib.lz_rollout_policy)
             nat.check(launch(self.env._h, ctypes.byref(r)))
         if es != caller:
             caller.wait_stream(es)

@@ -297,6 +297,14 @@ lz_status lz_policy_pack(const lz_mlp_policy* p, void* host_blob, int64_t cap);
 lz_status lz_policy_pack_hidden(const lz_mlp_policy* p, int32_t hidden, void* host_blob,
                                 int64_t cap);
 
+/* The same policy packed for SB3's own precision (float32 operands, float32
+ * accumulation; stable-baselines3 runs these nets in torch float32, code/lorenz_pmsm/
+ * train.py:173-178): f32-input MFMA hidden layers (bit-for-bit k-ordered fmaf chains),
+ * fmaf-chain heads, tanh from IEEE basic operations -- deterministic and reproduced bit
+ * for bit by the C oracle.  hidden 1..128 as lz_policy_pack_hidden.  Host-only. */
+int64_t lz_policy_f32_blob_bytes(void);
+lz_status lz_policy_pack_f32(const lz_mlp_policy* p, int32_t hidden, void* host_blob, int64_t cap);
+
 typedef struct lz_policy_rollout_args {
   int32_t K;                /* steps (SB3 n_steps) */
   uint32_t flags;           /* LZ_POLICY_* */
@@ -331,6 +339,10 @@ typedef struct lz_policy_rollout_args {
  * global env id, call counter + k), purpose 3.  The first call on a handle allocates
  * a small scratch buffer for obs_moments (do not capture that first call). */
 lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r);
+/* lz_rollout_policy with an lz_policy_pack_f32 blob: the float32 MlpPolicy (replaces
+ * SB3's ActorCriticPolicy.forward / predict in the same collect_rollouts loop and in
+ * code/lorenz_pmsm/test_evaluate.py:117-120's deterministic closed loop). */
+lz_status lz_rollout_policy_f32(lz_handle* h, const lz_policy_rollout_args* r);
 
 /* The actor-critic of the reference's flagship PPO script, code/train.py:52-112:
  * policy_kwargs = dict(features_extractor_class=AttentionFeaturesExtractor,

@@ -549,3 +549,108 @@ int32_t orc_t_done_step(double dt, double t_end, int32_t max_k) {
   }
 LEGACY_BODY(double)
 LEGACY_BODY(float)
+
+/* =========================================================================
+ * f3 / f2: the float32 MlpPolicy -- stable-baselines3 2.7.1 ActorCriticPolicy
+ * ("MlpPolicy", net_arch pi=[H,H] vf=[H,H], activation Tanh; code/lorenz_pmsm/
+ * train.py:150-176, code/gym_try.py:106-116), whose forward SB3 runs in torch
+ * float32:  latent = tanh(W2 tanh(W1 x + b1) + b2);  mean = action_net(latent_pi);
+ * value = value_net(latent_vf).  Restated in the operation order of the fused
+ * kernel's float32 variant (gym-lorenz_amd/csrc/lz_policy.hip mlp_f32 -- this is the
+ * DEV-mode restatement the GPU is checked against bit for bit; its agreement with the
+ * torch forward SB3 computes is checked separately, tests/test_policy_f32_host.py):
+ *   hidden unit u: acc = b[u]; acc = fmaf(w[u][k], x[k], acc) over the inputs k in the
+ *     order (k-step s, lane half h): layer 1 k = 2s + h, layer 2 k = 32 ti +
+ *     row(g, h) for ti = 0..3, g = 0..15, h = 0, 1; then tanh_ieee(acc);
+ *   head row r: per half h an fmaf chain from +0 over k = 32 t + row(g, h), t = 0..3,
+ *     g = 0..15; out = (part0 + part1) + b[r].
+ * Nets narrower than 128 are zero-padded (exactly what the packer does).
+ * ========================================================================= */
+float orc_tanh_ieee(float x) {
+  /* lz_policy.hip tanh_ieee: -expm1(-2|x|) / (2 + expm1(-2|x|)), expm1 by Cody-Waite
+   * reduction + degree-8 Taylor polynomial, 2^n in the exponent bits */
+  const float ax = fabsf(x);
+  const float axc = ax < 9.0f ? ax : 9.0f;
+  const float y = -2.0f * axc;
+  const float n = rintf(y * 1.44269502f);
+  float r = fmaf(n, -0.693145751953125f, y);
+  r = fmaf(n, -1.42860677e-06f, r);
+  float q = 2.48015873e-05f;
+  q = fmaf(q, r, 1.98412698e-04f);
+  q = fmaf(q, r, 1.38888889e-03f);
+  q = fmaf(q, r, 8.33333333e-03f);
+  q = fmaf(q, r, 4.16666667e-02f);
+  q = fmaf(q, r, 1.66666667e-01f);
+  q = fmaf(q, r, 0.5f);
+  const float p = fmaf(r * r, q, r);
+  uint32_t sb = (uint32_t)((int)n + 127) << 23;
+  float s;
+  memcpy(&s, &sb, 4);
+  /* |x| < 0.45: -expm1 / (2 + expm1) (no cancellation near 0); else with E = e^-2|x|
+   * < 0.41: (1 - E) / (1 + E) (no amplification of E's error near 1) */
+  const int lo = ax < 0.45f;
+  const float em1 = fmaf(s, p, s - 1.0f);
+  const float e = fmaf(s, p, s);
+  float t = (lo ? -em1 : 1.0f - e) / (lo ? 2.0f + em1 : 1.0f + e);
+  t = ax < 9.0f ? t : 1.0f;
+  t = ax < 2.44140625e-04f ? ax : t;
+  t = x != x ? x : t;
+  return copysignf(t, x);
+}
+
+static inline int pol_row(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
+
+static void mlp_f32_one(int O, int H, int R, const float* x, const float* w1, const float* b1,
+                        const float* w2, const float* b2, const float* w3, const float* b3,
+                        float* out) {
+  float a1[128], a2[128];
+  for (int u = 0; u < 128; ++u) {
+    float acc = u < H ? b1[u] : 0.0f;
+    for (int s = 0; s < (O + 1) / 2; ++s)
+      for (int h = 0; h < 2; ++h) {
+        const int k = 2 * s + h;
+        const float w = (u < H && k < O) ? w1[u * O + k] : 0.0f;
+        acc = fmaf(w, k < O ? x[k] : 0.0f, acc);
+      }
+    a1[u] = orc_tanh_ieee(acc);
+  }
+  for (int u = 0; u < 128; ++u) {
+    float acc = u < H ? b2[u] : 0.0f;
+    for (int ti = 0; ti < 4; ++ti)
+      for (int g = 0; g < 16; ++g)
+        for (int h = 0; h < 2; ++h) {
+          const int k = 32 * ti + pol_row(g, h);
+          acc = fmaf((u < H && k < H) ? w2[u * H + k] : 0.0f, a1[k], acc);
+        }
+    a2[u] = orc_tanh_ieee(acc);
+  }
+  for (int r = 0; r < R; ++r) {
+    float part[2];
+    for (int h = 0; h < 2; ++h) {
+      float acc = 0.0f;
+      for (int t = 0; t < 4; ++t)
+        for (int g = 0; g < 16; ++g) {
+          const int k = 32 * t + pol_row(g, h);
+          acc = fmaf(k < H ? w3[r * H + k] : 0.0f, a2[k], acc);
+        }
+      part[h] = acc;
+    }
+    out[r] = (part[0] + part[1]) + b3[r];
+  }
+}
+
+/* x [n, O] (the normalised observation the policy sees) -> mean [n, A], value [n] */
+void orc_mlp_f32(int64_t n, int O, int A, int H, const float* x, const float* pi_w1,
+                 const float* pi_b1, const float* pi_w2, const float* pi_b2, const float* vf_w1,
+                 const float* vf_b1, const float* vf_w2, const float* vf_b2, const float* act_w,
+                 const float* act_b, const float* val_w, const float* val_b, float* mean,
+                 float* value) {
+  for (int64_t i = 0; i < n; ++i) {
+    mlp_f32_one(O, H, A, x + i * O, pi_w1, pi_b1, pi_w2, pi_b2, act_w, act_b, mean + i * A);
+    mlp_f32_one(O, H, 1, x + i * O, vf_w1, vf_b1, vf_w2, vf_b2, val_w, val_b, value + i);
+  }
+}
+
+void orc_tanh_ieee_v(int64_t n, const float* x, float* out) {
+  for (int64_t i = 0; i < n; ++i) out[i] = orc_tanh_ieee(x[i]);
+}

@@ -43,6 +43,13 @@ def pol():
     return policy
 
 
+def _col(pol, *args, **kw):
+    """The bf16-MFMA kernel (this file's restatements are bf16); the float32 kernel has
+    its own tests (test_gpu_policy_f32.py)."""
+    kw.setdefault("precision", "bf16")
+    return pol.FusedRolloutCollector(*args, **kw)
+
+
 def _np(t):
     return t.detach().cpu().numpy()
 
@@ -67,6 +74,7 @@ def _clip_actions(pol, system, act):
     return torch.clamp(act, lo, hi)
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
 @pytest.mark.parametrize("system,n,K,kw", [
     ("pmsm", 1000, 24, dict(add_noise=True, max_episode_steps=7)),
     ("lorenz3", 2051, 12, dict(max_episode_steps=5)),
@@ -76,11 +84,11 @@ def _clip_actions(pol, system, act):
     ("transient_pmsm", 500, 8, dict(max_episode_steps=3)),
     ("singlecontrol", 300, 6, dict(max_episode_steps=4)),
 ])
-def test_policy_rollout_env_part_bitexact(gl, pol, system, n, K, kw):
+def test_policy_rollout_env_part_bitexact(gl, pol, system, n, K, kw, precision):
     envp, envr = _twins(gl, system, n, seed=11, **kw)
     O, A = envp.obs_dim, envp.action_dim
     _, sd = _random_policy(pol, O, A, seed=3)
-    col = pol.FusedRolloutCollector(envp, sd, bootstrap=False, capture_terminal=K * n)
+    col = _col(pol, envp, sd, bootstrap=False, capture_terminal=K * n, precision=precision)
     obs0 = _np(col.reset())
     obs0r = _np(envr.reset())
     assert np.array_equal(obs0, obs0r)
@@ -115,7 +123,7 @@ def test_policy_forward_vs_torch(gl, pol, system):
     env = gl.BatchedEnv(system, n, seed=5, add_noise=(system == "pmsm"))
     O, A = env.obs_dim, env.action_dim
     net, sd = _random_policy(pol, O, A, seed=7)
-    col = pol.FusedRolloutCollector(env, sd, bootstrap=False, deterministic=True)
+    col = _col(pol, env, sd, bootstrap=False, deterministic=True)
     col.reset()
     b = col.collect(K)
     obs = b.observations.reshape(-1, O).cpu()
@@ -153,7 +161,7 @@ def test_policy_bf16_vs_fp32_sb3_init(gl, pol, system):
     net = pol.ActorCriticMlp(O, A, seed=3)
     # as the reference trains PMSM: VecNormalize(norm_obs=True, clip_obs=10) in front
     rms = DeviceRunningMeanStd(O, env.device)
-    col = pol.FusedRolloutCollector(env, net.state_dict(), bootstrap=False, deterministic=True,
+    col = _col(pol, env, net.state_dict(), bootstrap=False, deterministic=True,
                                     obs_rms=rms, training=True)
     col.reset()
     col.collect(K)  # statistics warm-up
@@ -179,7 +187,7 @@ def test_policy_sampling_and_log_prob(gl, pol):
     env = gl.BatchedEnv("pmsm", n, seed=9)
     _, sd = _random_policy(pol, 6, 2, seed=2)
     sd["log_std"] = torch.tensor([-0.5, 0.25])
-    col = pol.FusedRolloutCollector(env, sd, bootstrap=False)
+    col = _col(pol, env, sd, bootstrap=False)
     col.reset()
     b = col.collect(K)
     obs = b.observations.reshape(-1, 6).cpu()
@@ -193,7 +201,7 @@ def test_policy_sampling_and_log_prob(gl, pol):
     np.testing.assert_allclose(_np(b.log_probs).reshape(-1), lp_ref.numpy(), atol=5e-2, rtol=2e-2)
     # a different call counter gives different samples; the same seed reproduces them
     env2 = gl.BatchedEnv("pmsm", n, seed=9)
-    col2 = pol.FusedRolloutCollector(env2, sd, bootstrap=False)
+    col2 = _col(pol, env2, sd, bootstrap=False)
     col2.reset()
     b2 = col2.collect(K)
     assert torch.equal(b.actions, b2.actions)
@@ -204,8 +212,8 @@ def test_policy_truncation_bootstrap(gl, pol):
     n, K, gamma = 2000, 13, 0.97
     ea, eb = _twins(gl, "pmsm", n, seed=21, max_episode_steps=5)
     _, sd = _random_policy(pol, 6, 2, seed=4)
-    ca = pol.FusedRolloutCollector(ea, sd, gamma=gamma, bootstrap=True, capture_terminal=K * n)
-    cb = pol.FusedRolloutCollector(eb, sd, gamma=gamma, bootstrap=False)
+    ca = _col(pol, ea, sd, gamma=gamma, bootstrap=True, capture_terminal=K * n)
+    cb = _col(pol, eb, sd, gamma=gamma, bootstrap=False)
     ca.reset()
     cb.reset()
     ba, bb = ca.collect(K), cb.collect(K)
@@ -238,7 +246,7 @@ def test_policy_vecnormalize(gl, pol):
     rms.set_state(rng.normal(0, 2, 6), rng.uniform(0.5, 30, 6), 1234.0)
     ref = DeviceRunningMeanStd(6, envp.device)
     ref.set_state(rms.mean, rms.var, rms.count)
-    col = pol.FusedRolloutCollector(envp, sd, obs_rms=rms, clip_obs=3.0, bootstrap=False,
+    col = _col(pol, envp, sd, obs_rms=rms, clip_obs=3.0, bootstrap=False,
                                     training=True)
     obs0 = col.last_obs = envp.reset().clone()
     b = col.collect(K)
@@ -276,7 +284,7 @@ def test_gae_bitexact_vs_sb3_restatement(gl, pol, K, n):
     starts[0] = 1.0
     starts[1:] = (done[:-1] != 0)
     env = gl.BatchedEnv("pmsm", 8)
-    col = pol.FusedRolloutCollector(env, gamma=0.99, gae_lambda=0.95)
+    col = _col(pol, env, gamma=0.99, gae_lambda=0.95)
     dev = env.device
     b = pol.RolloutBatch(None, None, None, torch.from_numpy(val).to(dev),
                          torch.from_numpy(rew).to(dev), torch.from_numpy(done).to(dev), None,
@@ -293,7 +301,7 @@ def test_policy_rollout_large_batch(gl, pol):
     n, K = 262144, 16
     envp, envr = _twins(gl, "pmsm", n, seed=41, add_noise=True)
     _, sd = _random_policy(pol, 6, 2, seed=8, scale=0.2)
-    col = pol.FusedRolloutCollector(envp, sd)
+    col = _col(pol, envp, sd)
     col.reset()
     envr.reset()
     b = col.collect(K)
@@ -319,7 +327,7 @@ def test_policy_launch_shapes_agree_bitwise(gl, pol, n):
         _, sd = _random_policy(pol, 6, 2, seed=12, scale=0.2)
         rms = DeviceRunningMeanStd(6, env.device)
         rms.set_state(np.zeros(6), np.full(6, 40.0), 10.0)
-        col = pol.FusedRolloutCollector(env, sd, obs_rms=rms, training=True)
+        col = _col(pol, env, sd, obs_rms=rms, training=True)
         col.last_obs = env.reset().clone()
         b = col.collect(K)
         outs.append(b)
@@ -344,7 +352,7 @@ def test_policy_narrow_net_optuna_setting(gl, pol):
             p.copy_(torch.randn(p.shape, generator=g) * (0.4 if p.dim() > 1 else 0.3))
     sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
     rms = DeviceRunningMeanStd(6, env.device)
-    col = pol.FusedRolloutCollector(env, sd, bootstrap=False, deterministic=True, obs_rms=rms)
+    col = _col(pol, env, sd, bootstrap=False, deterministic=True, obs_rms=rms)
     col.reset()
     col.collect(K)
     b = col.collect(K)
@@ -364,7 +372,7 @@ def test_collect_from_a_side_stream(gl, pol):
     out = []
     for side in (False, True):
         env = gl.BatchedEnv("pmsm", n, seed=12, add_noise=True)
-        col = pol.FusedRolloutCollector(env, sd)
+        col = _col(pol, env, sd)
         col.reset()
         torch.cuda.synchronize()
         s = torch.cuda.Stream(device=env.device) if side else torch.cuda.current_stream(env.device)

@@ -16,24 +16,38 @@ def pol():
     return policy
 
 
+def _col(pol, *args, **kw):
+    """The bf16-MFMA kernel (this file's restatements are bf16); the float32 kernel has
+    its own tests (test_gpu_policy_f32.py)."""
+    kw.setdefault("precision", "bf16")
+    return pol.FusedRolloutCollector(*args, **kw)
+
+
 def _sd(pol, O, A):
     net = pol.ActorCriticMlp(O, A, seed=1)
     return {k: v.detach().clone() for k, v in net.state_dict().items()}
 
 
-@pytest.mark.parametrize("n,K", [(1, 1), (31, 3), (33, 2), (64, 1), (65, 4)])
-def test_tiny_and_ragged_batches(pol, n, K):
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+@pytest.mark.parametrize("n,K", [(1, 1), (31, 3), (33, 2), (64, 1), (65, 4), (257, 3)])
+def test_tiny_and_ragged_batches(pol, n, K, precision):
     import gym_lorenz as gl
 
     envp = gl.BatchedEnv("pmsm", n, seed=3, add_noise=True, max_episode_steps=2)
     envr = gl.BatchedEnv("pmsm", n, seed=3, add_noise=True, max_episode_steps=2)
-    col = pol.FusedRolloutCollector(envp, _sd(pol, 6, 2), bootstrap=False)
+    col = _col(pol, envp, _sd(pol, 6, 2), bootstrap=False, precision=precision)
     col.reset()
     envr.reset()
     b = col.collect(K)
     obs_r, rew_r, done_r = envr.rollout(torch.clamp(b.actions, -1, 1).contiguous())
     assert torch.equal(b.observations[1:], obs_r[:-1]) and torch.equal(b.last_obs, obs_r[-1])
     assert torch.equal(b.rewards, rew_r) and torch.equal(b.dones, done_r)
+    if precision == "fp32":  # the float32 kernel is the oracle's operation order, bit for bit
+        import oracle
+
+        _, val = oracle.mlp_f32(_sd(pol, 6, 2), b.observations.reshape(-1, 6).cpu().numpy())
+        assert np.array_equal(b.values.reshape(-1).cpu().numpy(), val)
+        return
     _, val = pol.reference_forward_bf16(_sd(pol, 6, 2), b.observations.reshape(-1, 6).cpu())
     np.testing.assert_allclose(b.values.reshape(-1).cpu().numpy(), val.numpy(), atol=2e-2,
                                rtol=2e-2)
@@ -46,7 +60,7 @@ def test_terminal_list_capacity(pol):
 
     n, K, cap = 500, 6, 37
     env = gl.BatchedEnv("pmsm", n, seed=4, max_episode_steps=2)
-    col = pol.FusedRolloutCollector(env, _sd(pol, 6, 2), capture_terminal=cap)
+    col = _col(pol, env, _sd(pol, 6, 2), capture_terminal=cap)
     col.reset()
     b = col.collect(K)
     total = int((b.dones != 0).sum().item())
@@ -63,7 +77,7 @@ def test_deterministic_with_bootstrap(pol):
     n, K = 300, 7
     env = gl.BatchedEnv("lorenz3", n, seed=5, max_episode_steps=3)
     sd = _sd(pol, 6, 3)
-    col = pol.FusedRolloutCollector(env, sd, deterministic=True, bootstrap=True, gamma=0.9,
+    col = _col(pol, env, sd, deterministic=True, bootstrap=True, gamma=0.9,
                                     capture_terminal=n * K)
     col.reset()
     b = col.collect(K)
@@ -79,9 +93,9 @@ def test_errors(pol):
 
     env = gl.BatchedEnv("lorenz3", 64, dtype="float64")
     with pytest.raises(ValueError):
-        pol.FusedRolloutCollector(env, _sd(pol, 6, 3))  # float64 handle
+        _col(pol, env, _sd(pol, 6, 3))  # float64 handle
     env32 = gl.BatchedEnv("lorenz3", 64)
-    c = pol.FusedRolloutCollector(env32, _sd(pol, 6, 3))
+    c = _col(pol, env32, _sd(pol, 6, 3))
     r = nat.LzPolicyRolloutArgs()
     r.K = 4
     assert nat.lib.lz_rollout_policy(env32._h, ctypes.byref(r)) == nat.LZ_ERR_STATE  # no reset
