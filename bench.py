@@ -18,6 +18,7 @@ config); --scaling strong splits a fixed global env count instead.
 Rank 0 prints one JSON line.
 """
 import argparse
+import math
 import ctypes
 import json
 import os
@@ -46,6 +47,8 @@ def parse():
     p.add_argument("--ring", type=int, default=16, help="rollout-ring slots for actions/obs")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-drift", action="store_true")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the extra lines of the headline run (fp64 reference precision)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--system", choices=["lorenz3", "lorenz4", "pmsm", "hr"], default="lorenz3",
                    help="lorenz3 = the BASELINE headline (dynamic.py env); pmsm = cfg4")
@@ -69,61 +72,89 @@ def parse():
     return p.parse_args()
 
 
+def _cpu_worker(kind, seconds):
+    """One host core's share of the CPU baseline (run in a spawned process): returns
+    (env-steps, seconds) of `kind` = "ref" (oracle/ref_loop.py, the reference's own per-env
+    NumPy step in a DummyVecEnv loop) or "port" (the oracle's scalar C step)."""
+    import numpy as np
+
+    sys.path.insert(0, ROOT)
+    if kind == "ref":
+        from oracle.ref_loop import LorenzRefEnv, dummy_vec_step
+
+        n = 1024
+        envs = [LorenzRefEnv(x) for x in np.random.default_rng(0).uniform(-30, 30, (n, 3))]
+        acts = np.random.default_rng(1).uniform(-1, 1, (n, 3)).astype(np.float32)
+        bo, br = np.zeros((n, 6), np.float32), np.zeros(n, np.float32)
+        step = lambda k: dummy_vec_step(envs, acts, bo, br)  # noqa: E731
+    else:
+        import oracle
+
+        n = 65536
+        st = oracle.reset_draw("l3", np.float32, n, 0, 0, 0).copy()
+        acts = np.random.default_rng(0).uniform(-1, 1, (8, n, 3)).astype(np.float32)
+        step = lambda k: oracle.l3_step(st, acts[k % 8])  # noqa: E731
+    with np.errstate(all="ignore"):
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < seconds:
+            step(k)
+            k += 1
+        dt = time.perf_counter() - t0
+    return n * k, dt
+
+
+def _cpu_run(kind, seconds, cores):
+    if cores == 1:
+        steps, dt = _cpu_worker(kind, seconds)
+        return steps / dt, steps, dt
+    import multiprocessing as mp
+
+    with mp.get_context("spawn").Pool(cores) as pool:
+        res = pool.starmap(_cpu_worker, [(kind, seconds)] * cores)
+    steps = sum(r[0] for r in res)
+    dt = max(r[1] for r in res)
+    return steps / dt, steps, dt
+
+
+def host_cores():
+    """Host cores of this process's share: the affinity mask, at most 16 (a one-GPU box's
+    CPU share; os.cpu_count() there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
 def cpu_baseline(seconds):
-    """The oracle's scalar C port of dynamic.py's step (fp32, 1 thread) on a bounded
-    sample: 65,536 envs x S steps, S calibrated to ~`seconds` of CPU work."""
-    import numpy as np
-
-    import oracle
-
-    n = 65536
-    st = oracle.reset_draw("l3", np.float32, n, 0, 0, 0).copy()
-    acts = np.random.default_rng(0).uniform(-1, 1, (8, n, 3)).astype(np.float32)
-    with np.errstate(all="ignore"):
-        t0 = time.perf_counter()
-        for k in range(4):
-            oracle.l3_step(st, acts[k % 8])
-        per = (time.perf_counter() - t0) / 4
-        steps = max(8, int(seconds / max(per, 1e-9)))
-        t0 = time.perf_counter()
-        for k in range(steps):
-            oracle.l3_step(st, acts[k % 8])
-        dt = time.perf_counter() - t0
-    out = {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-           "sample": "oracle/lz_oracle.c orc_l3_step_float (scalar C restatement of "
-                     "dynamic.py:61-90), 65,536 envs x %d steps = %.2e env-steps in %.1f s, "
-                     "1 thread, GPU box host CPU" % (steps, n * steps, dt)}
-    out["reference_loop"] = reference_loop_baseline(min(4.0, seconds / 3))
-    return out
-
-
-def reference_loop_baseline(seconds):
-    """The reference's own cost model on the same host core: dynamic.py's step() per env
-    object, driven by a DummyVecEnv-style Python loop (oracle/ref_loop.py restates it;
-    the reference itself does not travel to the GPU box)."""
-    import numpy as np
-
-    from oracle.ref_loop import LorenzRefEnv, dummy_vec_step
-
-    n = 1024
-    x0 = np.random.default_rng(0).uniform(-30, 30, (n, 3))
-    envs = [LorenzRefEnv(x) for x in x0]
-    acts = np.random.default_rng(1).uniform(-1, 1, (n, 3)).astype(np.float32)
-    bo, br = np.zeros((n, 6), np.float32), np.zeros(n, np.float32)
-    with np.errstate(all="ignore"):
-        t0 = time.perf_counter()
-        dummy_vec_step(envs, acts, bo, br)
-        per = time.perf_counter() - t0
-        steps = max(2, int(seconds / max(per, 1e-9)))
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            dummy_vec_step(envs, acts, bo, br)
-        dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1,
-            "kind": "reference-semantics Python loop",
-            "sample": "oracle/ref_loop.py: dynamic.py:61-90 step() per env object in a "
-                      "DummyVecEnv-style loop, %d envs x %d steps in %.1f s, 1 thread, GPU box "
-                      "host CPU" % (n, steps, dt)}
+    """The reference's own cost model on the host: dynamic.py's step() per env object in
+    a DummyVecEnv-style loop (oracle/ref_loop.py, pinned bit-exact to the reference's
+    outputs; the reference itself does not travel to the GPU box), one process per host
+    core (spawned before the GPU is initialised) and on one core; beside it the oracle's
+    scalar C port.  Bounded samples: ~`seconds` / 4 of wall time per measurement."""
+    cores = host_cores()
+    w = max(1.0, seconds / 4)
+    ref_all, ref_steps, ref_dt = _cpu_run("ref", w, cores)
+    ref_one, one_steps, one_dt = _cpu_run("ref", w, 1)
+    port_all, port_steps, port_dt = _cpu_run("port", w, cores)
+    port_one, p1_steps, p1_dt = _cpu_run("port", w, 1)
+    return {
+        "value": ref_all, "unit": "env-steps/s", "cores": cores, "kind": "port",
+        "sample": "oracle/ref_loop.py (dynamic.py:61-90 step() with the reference's per-call "
+                  "NumPy work: 3 np.clip, 4 list - int64 array observations, generator-sum "
+                  "reward; bit-exact vs the reference fixture) driving 1024 envs per process "
+                  "in a DummyVecEnv-style loop, %d processes (one per host core) for %.1f s: "
+                  "%.2e env-steps; GPU box host CPU" % (cores, ref_dt, ref_steps),
+        "one_core": {"value": ref_one, "cores": 1,
+                     "sample": "the same loop, 1 process, %.2e env-steps in %.1f s"
+                               % (one_steps, one_dt)},
+        "c_port": {"value": port_all, "cores": cores, "one_core": port_one, "kind": "port",
+                   "sample": "oracle/lz_oracle.c orc_l3_step_float (scalar C restatement of "
+                             "dynamic.py:61-90, fp32), 65,536 envs per process, %d processes "
+                             "%.2e env-steps in %.1f s; 1 process %.2e env-steps in %.1f s"
+                             % (cores, port_steps, port_dt, p1_steps, p1_dt)},
+    }
 
 
 def fp32_drift(gl, torch, device):
@@ -180,9 +211,11 @@ SYSTEM_INFO = {  # system -> (reference env, mangled k_step / k_rollout names, a
 }
 
 
-def kernel_name(system, mode, n):
+def kernel_name(system, mode, n, f64=False):
     """Mangled name of the dominant kernel (lz_kernels.hip launch_all / launch_rollout_d)."""
     tag = SYSTEM_INFO[system][1]
+    if f64:
+        tag = tag.replace("IfEEf", "IdEEd")
     sysname = ("7" if system == "pmsm" else "5") + tag
     if mode != "rollout":
         return "_ZN2lz6k_stepINS_%sLi0EEEvNS_5KArgsE" % sysname
@@ -436,6 +469,158 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
     }
 
 
+def fp64_line(args, gl, nat, torch, dist, device, n):
+    """The same step benchmark at the reference's precision: float64 LORENZ3, the kernel
+    that is bit-identical to dynamic.py (tests/test_gpu_parity.py::
+    test_l3_f64_golden_bitexact), 1M envs, HIP events on the launch stream."""
+    env = gl.BatchedEnv("lorenz3", n, dtype="float64", seed=0, autoreset=True, device=device.index)
+    tm = measure_steps(args, torch, dist, nat, env, device, 1, 0, False)
+    bytes_step = env.info.bytes_per_env_step
+    launch_s = tm["ev_ms"] / 1e3 / tm["launches"]
+    achieved = bytes_step * n / launch_s / 1e9
+    env.close()
+    return {
+        "metric": METRIC + " (fp64: the reference's arithmetic, bit-exact)",
+        "value": n * tm["steps"] * tm["windows"] / tm["elapsed"], "unit": "env-steps/s",
+        "steps": tm["steps"], "ms_per_step": tm["elapsed"] * 1e3 / (tm["steps"] * tm["windows"]),
+        "dtype": "f64",
+        "config": {"workload": "dynamic.py 3-state Lorenz env step (lz_step, float64, "
+                               "bit-identical to the reference), %d envs on 1 GPU" % n,
+                   "launch": "hipGraph of %d lz_step launches" % tm["graph_len"]},
+        "timing": tm["timing"],
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": kernel_name("lorenz3", "step", n, f64=True),
+                     "avg_launch_us": launch_s * 1e6, "bytes_per_env_step": bytes_step},
+    }
+
+
+def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min_window_s=0.2):
+    """Time EXACTLY K env steps (K = --steps; rollout mode: --steps rounded down to whole
+    --K launches), each timed window bracketed by a barrier + torch.cuda.synchronize()
+    on both sides.  When one window is shorter than `min_window_s` (e.g. the driver's
+    --steps 20 is 0.24 ms at 1M envs), back-to-back windows of the same K steps are timed
+    until their sum reaches it; value = windows x K x envs / summed window time (the
+    MAX over ranks).  Step mode replays a hipGraph of L lz_step launches and launches
+    the K mod L remainder eagerly; an odd remainder is followed by one untimed step so
+    the captured graph's ping-pong parity stays valid."""
+    A, O = env.action_dim, env.obs_dim
+    arange = SYSTEM_INFO[args.system][2]
+    R = args.ring if not rollout else 1
+    T = args.K if rollout else 1
+    tdt = env.tdtype
+    g = torch.Generator(device=device).manual_seed(1000 + rank)
+    acts = (torch.rand((R, T, env.num_envs, A), generator=g, device=device) * 2 - 1) * arange
+    obs = torch.empty((R, T, env.num_envs, O), device=device, dtype=tdt)
+    rew = torch.empty((R, T, env.num_envs), device=device, dtype=tdt)
+    done = torch.empty((R, T, env.num_envs), dtype=torch.uint8, device=device)
+    env.reset()
+    h = env._h
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    slots = [(P(acts[r]), P(obs[r]), P(rew[r]), P(done[r])) for r in range(R)]
+    didx, tobs = P(env.done_idx), P(env.term_obs)
+    lz_step, lz_rollout = nat.lib.lz_step, nat.lib.lz_rollout
+    counter = [0]
+
+    def one():
+        a, o, r_, d = slots[counter[0] % R]
+        counter[0] += 1
+        if rollout:
+            st = lz_rollout(h, T, a, o, r_, d, None, None, 0, None)
+        else:
+            st = lz_step(h, a, None, o, r_, d, didx, tobs, None)
+        if st:
+            nat.check(st)
+
+    stream = torch.cuda.Stream(device)
+    graph = None
+    L = max(2, args.graph_len - args.graph_len % 2)  # even: keeps the ping-pong parity
+    if R > 1 and L % R and R % L:
+        L = R
+    launches = args.steps if not rollout else max(1, args.steps // T)
+    warm = args.warmup if not rollout else 2
+    if rollout:
+        L = 1
+    with torch.cuda.stream(stream):
+        nat.check(nat.lib.lz_set_stream(h, ctypes.c_void_p(stream.cuda_stream)))
+        for _ in range(max(warm, 2)):
+            one()
+        if args.launch == "graph" and not rollout:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                for _ in range(L):
+                    one()
+        torch.cuda.synchronize(device)
+
+        def run(nlaunch):  # exactly nlaunch launches
+            if graph is None:
+                for _ in range(nlaunch):
+                    one()
+                return
+            for _ in range(nlaunch // L):
+                graph.replay()
+            for _ in range(nlaunch % L):
+                one()
+
+        def fix_parity(nlaunch):  # untimed: an odd eager remainder flipped the parity
+            if graph is not None and (nlaunch % L) % 2:
+                one()
+
+        if graph is not None:
+            run(max(warm, L))  # warm the graph path too
+            fix_parity(max(warm, L))
+        torch.cuda.synchronize(device)
+
+        def window():
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(device)
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            ev0.record(stream)
+            run(launches)
+            ev1.record(stream)
+            torch.cuda.synchronize(device)
+            if world > 1:
+                dist.barrier()
+            t1 = time.perf_counter()
+            fix_parity(launches)
+            return t1 - t0, ev0.elapsed_time(ev1)
+
+        first = window()
+        # windows needed for min_window_s in total (all ranks agree: MAX over ranks)
+        need = math.ceil(min_window_s / max(first[0], 1e-9))
+        need = max(1, min(need, 5000))
+        if world > 1:
+            t = torch.tensor([need], device=device, dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            need = int(t.item())
+        wins = [window() for _ in range(need)]
+    elapsed = sum(w[0] for w in wins)
+    ev_ms = sum(w[1] for w in wins)
+    if world > 1:
+        t = torch.tensor([elapsed, ev_ms], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, ev_ms = float(t[0]), float(t[1])
+    wms = sorted(w[0] * 1e3 for w in wins)
+    K = launches * T
+    return {
+        "steps": K, "T": T, "ring": R, "graph_len": L, "graph": graph is not None,
+        "warmup": warm, "launches": launches * need, "windows": need,
+        "elapsed": elapsed, "ev_ms": ev_ms,
+        "timing": {
+            "requested_steps": args.steps, "steps_per_window": K, "windows": need,
+            "timed_steps_total": K * need, "timed_seconds": elapsed,
+            "window_ms_min": wms[0], "window_ms_median": wms[len(wms) // 2],
+            "method": "each window = exactly `steps` env steps of every env, bracketed by "
+                      "barrier + torch.cuda.synchronize() on both sides; windows repeated "
+                      "until >= %.0f ms are timed; value = windows x steps x envs / summed "
+                      "window time (MAX over ranks)" % (min_window_s * 1e3),
+        },
+    }
+
+
 def main():
     args = parse()
     import torch
@@ -447,6 +632,11 @@ def main():
     if world == 1 and args.gpus > 1:
         raise SystemExit("--gpus %d needs torch.distributed.run with %d processes"
                          % (args.gpus, args.gpus))
+    headline = args.system == "lorenz3" and args.mode == "step"
+    cpu = None
+    if rank == 0 and world == 1 and headline and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)  # first: its worker processes start before
+        #                                       anything initialises the GPU
     # LZ_BENCH_BACKEND=gloo + ranks sharing a GPU: rehearsal of the multi-rank path on a
     # 1-GPU box (the driver's 8-GPU runs use the default: RCCL, one GPU per rank)
     backend = os.environ.get("LZ_BENCH_BACKEND", "nccl")
@@ -492,86 +682,13 @@ def main():
         if rank == 0:
             print(json.dumps(out), flush=True)
         return
-    A, O = env.action_dim, env.obs_dim
-    arange = SYSTEM_INFO[args.system][2]
     rollout = args.mode == "rollout"
-    R = args.ring if not rollout else 1
-    T = args.K if rollout else 1
-    g = torch.Generator(device=device).manual_seed(1000 + rank)
-    acts = (torch.rand((R, T, n, A), generator=g, device=device) * 2 - 1) * arange
-    obs = torch.empty((R, T, n, O), device=device)
-    rew = torch.empty((R, T, n), device=device)
-    done = torch.empty((R, T, n), dtype=torch.uint8, device=device)
-    env.reset()
-
-    h = env._h
-    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    slots = [(P(acts[r]), P(obs[r]), P(rew[r]), P(done[r])) for r in range(R)]
-    didx, tobs = P(env.done_idx), P(env.term_obs)
-    lz_step, lz_rollout = nat.lib.lz_step, nat.lib.lz_rollout
-
-    def one(k):
-        a, o, r_, d = slots[k % R]
-        if rollout:
-            st = lz_rollout(h, T, a, o, r_, d, None, None, 0, None)
-        else:
-            st = lz_step(h, a, None, o, r_, d, didx, tobs, None)
-        if st:
-            nat.check(st)
-
-    stream = torch.cuda.Stream(device)
-    graph = None
-    L = max(2, args.graph_len - args.graph_len % 2)  # even: keeps the ping-pong parity
-    if R > 1 and L % R and R % L:
-        L = R
-    launches = args.steps if not rollout else max(2, args.steps // T)
-    warm = args.warmup if not rollout else 2
-    if rollout:
-        L = 2
-    with torch.cuda.stream(stream):
-        nat.check(nat.lib.lz_set_stream(h, ctypes.c_void_p(stream.cuda_stream)))
-        for k in range(max(warm, 2)):
-            one(k)
-        if args.launch == "graph" and not rollout:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=stream):
-                for k in range(L):
-                    one(k)
-        torch.cuda.synchronize(device)
-
-        def run(nlaunch):
-            if graph is None:
-                for k in range(nlaunch):
-                    one(k)
-                return nlaunch
-            reps = max(1, nlaunch // L)
-            for _ in range(reps):
-                graph.replay()
-            return reps * L
-
-        if not rollout:
-            run(max(warm, L))  # warm the graph path too
-        torch.cuda.synchronize(device)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(device)
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        nl = run(launches)
-        ev1.record(stream)
-        torch.cuda.synchronize(device)
-        if world > 1:
-            dist.barrier()
-        t1 = time.perf_counter()
-    K = nl * T  # env steps per env in the timed region
-    elapsed = t1 - t0
-    ev_ms = ev0.elapsed_time(ev1)
-    if world > 1:
-        t = torch.tensor([elapsed, ev_ms], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, ev_ms = float(t[0]), float(t[1])
+    tm = measure_steps(args, torch, dist, nat, env, device, world, rank, rollout)
+    K, L, R, T = tm["steps"], tm["graph_len"], tm["ring"], tm["T"]
+    elapsed, ev_ms, nl = tm["elapsed"], tm["ev_ms"], tm["launches"]
+    warm = tm["warmup"]
+    graph = tm["graph"]
+    arange = SYSTEM_INFO[args.system][2]
 
     info = env.info
     if rollout:  # state planes once per launch, per-step I/O every step
@@ -590,12 +707,12 @@ def main():
                     "done in a %d-slot on-device rollout ring" % (ref_env, total, n, R))
     out = {
         "metric": METRIC,
-        "value": total * K / elapsed,
+        "value": total * K * tm["windows"] / elapsed,
         "unit": "env-steps/s",
         "n_gpus": world,
         "steps": K,
         "warmup": warm,
-        "ms_per_step": elapsed * 1e3 / K,
+        "ms_per_step": elapsed * 1e3 / (K * tm["windows"]),
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
@@ -607,9 +724,10 @@ def main():
             "workload": workload, "system": args.system, "envs_total": total,
             "envs_per_gpu": n, "mode": args.mode,
             "parallelism": "env shard x%d (contiguous global ids, no collective on step)" % world,
-            "launch": ("hipGraph of %d lz_step launches" % L) if graph is not None else
+            "launch": ("hipGraph of %d lz_step launches" % L) if graph else
                       ("%d-step lz_rollout launches" % T if rollout else "eager"),
         },
+        "timing": tm["timing"],
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -626,8 +744,10 @@ def main():
     headline = args.system == "lorenz3" and not rollout
     if rank == 0 and world == 1 and headline and not args.no_drift:
         out["fp32_drift"] = fp32_drift(gl, torch, device)
-    if rank == 0 and world == 1 and headline and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0 and world == 1 and headline and not args.no_extras:
+        out["extra_lines"] = [fp64_line(args, gl, nat, torch, dist, device, n)]
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     env.close()
     if world > 1:
         dist.barrier()

@@ -18,27 +18,40 @@ def gl():
     return gym_lorenz
 
 
-def test_frame_stack_kernel_vs_sb3(gl):
+@pytest.mark.parametrize("n,S,O,misalign", [
+    (3001, 4, 6, False),   # LDS tiles, 16-B vectors, a ragged last tile, obs tail scalar
+    (512, 4, 8, False),    # whole tiles, all-vector
+    (3001, 4, 6, True),    # obs not 16-B aligned: scalar tile path
+    (300, 3, 5, False),    # S*O = 15: scalar tile path
+    (1, 2, 3, False),
+    (100, 20, 6, False),   # S*O + O > 64: the per-row kernel
+])
+def test_frame_stack_kernel_vs_sb3(gl, n, S, O, misalign):
     from gym_lorenz import _native as nat
     from oracle.sb3_framestack import StackedObservations
 
     rng = np.random.default_rng(0)
-    n, S, O = 3001, 4, 6
     ref = StackedObservations(n, S, O)
     st = torch.zeros((n, S * O), dtype=torch.float32, device="cuda")
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def dev(a):  # optionally 4 B past a 16-B boundary
+        t = torch.zeros(a.size + 1, dtype=torch.float32, device="cuda")
+        v = t[1:] if misalign else t[:-1]
+        v.copy_(torch.from_numpy(a.reshape(-1)))
+        return v
+
     obs = rng.normal(size=(n, O)).astype(np.float32)
     ref.reset(obs)
-    nat.check(nat.lib.lz_frame_stack(P(st), P(torch.from_numpy(obs).cuda()), None, n, S, O, 1, 0, sp))
+    nat.check(nat.lib.lz_frame_stack(P(st), P(dev(obs)), None, n, S, O, 1, 0, sp))
     assert np.array_equal(st.cpu().numpy(), ref.stacked_obs)
     for _ in range(12):
         obs = rng.normal(size=(n, O)).astype(np.float32)
         done = rng.random(n) < 0.1
         ref.update(obs, done, [{} for _ in range(n)])
         d = torch.from_numpy(done.astype(np.uint8)).cuda()
-        nat.check(nat.lib.lz_frame_stack(P(st), P(torch.from_numpy(obs).cuda()), P(d), n, S, O, 0, 0,
-                                         sp))
+        nat.check(nat.lib.lz_frame_stack(P(st), P(dev(obs)), P(d), n, S, O, 0, 0, sp))
         assert np.array_equal(st.cpu().numpy(), ref.stacked_obs)
 
 
