@@ -60,13 +60,24 @@ __device__ __forceinline__ void make_noise(const Sys& sys, const KArgs& a, int64
 // (post-reset if reset); with kKeepTerm, o_term[] receives the pre-reset observation.
 // lead = false: a lane that computes a copy of another lane's env (the split-lane
 // rollout) -- same arithmetic, but it takes no slot in the compact done list.
-template <class Sys, typename T, bool kRollout, bool kKeepTerm = false>
+// kNoDone: the launch can produce no done at all (a never-terminating system and no
+// step counter, see no_done()): the step alone, no done bookkeeping.
+template <class Sys, typename T, bool kRollout, bool kKeepTerm = false, bool kNoDone = false>
 __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KArgs& a, int64_t i,
                                              bool live, const float* act, uint64_t tick, int k,
                                              T* o, T& rew, bool& did_reset,
                                              T* o_term = nullptr, bool lead = true) {
   uint8_t dflag = 0;
   did_reset = false;
+  if constexpr (kNoDone) {
+    static_assert(never_terminates<Sys>::value && !Sys::kNoise && !kKeepTerm,
+                  "kNoDone: a never-terminating, noise-free system");
+    if (live) {
+      double nz[3] = {0.0, 0.0, 0.0};
+      (void)sys.step(act, false, nz, o, rew, a);
+    }
+    return 0;
+  }
   if (live) {
     double nz[3] = {0.0, 0.0, 0.0};
     bool use_nz = false;
@@ -115,6 +126,13 @@ __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KAr
     did_reset = true;
   }
   return dflag;
+}
+
+// The launch-wide condition for step_body's kNoDone (host side): no step counter and a
+// system whose step never terminates
+template <class Sys>
+inline bool no_done(const KArgs& a) {
+  return never_terminates<Sys>::value && !a.count_steps;
 }
 
 }  // namespace lz

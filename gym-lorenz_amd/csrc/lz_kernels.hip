@@ -349,6 +349,28 @@ __device__ __forceinline__ void dma4_nt(const float* g, uint32_t m0) {
                : "v"(g), "s"(m0)
                : "memory");
 }
+// 16-B LDS-DMA (global_load_lds_dwordx4); the s_nop separates the M0 write from the
+// DMA that reads it.
+__device__ __forceinline__ void dma16_nt(const float* g, uint32_t m0) {
+  uint32_t saved;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(saved)
+               : "v"(g), "s"(m0)
+               : "memory");
+}
+// Row DMA of the fused rollout: ONE 16-B LDS-DMA per wave and step moves the wave's
+// contiguous [envs, A] action slice (envs = 64, or 32 in the split-lane kernel) into the
+// wave's own 1-KiB LDS region, row-major: lane l loads 16-B chunk l mod C of the slice
+// (C = envs * A / 4 chunks; the remaining lanes repeat chunks, so no lane reads past
+// the slice), landing at region + 16 l.  Needs the slice 16-B aligned (the launch's
+// vec_ok: actions 16-B aligned, N a multiple of 4) and envs * A a multiple of 4.
+template <int A, int E>
+constexpr bool row_dma() { return (A == 2 || A == 3) && (E * A) % 4 == 0; }
+constexpr int kRowRegionF = 256;  // floats per wave region and slot (64 lanes x 16 B)
+// LDS floats of the DMA ring per slot for a B-lane workgroup
+template <int A, int B>
+constexpr int act_slot_floats() { return row_dma<A, 64>() ? (B / 64) * kRowRegionF : B * A; }
 // LDS reads of the DMA'd slot, also from asm (with their own lgkmcnt wait), so that
 // no compiler-visible LDS access depends on the hidden DMA.
 template <int A>
@@ -394,7 +416,7 @@ __device__ __forceinline__ void ladder_wait(int k) {
   }
 }
 
-template <class Sys, typename T, int B, bool FULL, int D>
+template <class Sys, typename T, int B, bool FULL, int D, bool kNoDone>
 __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any_reset,
                                              const KArgs& a, int64_t base, int tid, int nb,
                                              uint64_t tick, float* s_act, T* s_obs) {
@@ -414,7 +436,10 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   // row, which hipcc may merge into ceil(row/16) stores.  A LOWER bound is safe.
   constexpr int kRowB = Sys::O * (int)sizeof(T);
   constexpr int kSt = 2 + (kDirect ? (kRowB + 15) / 16 : CO::N);
-  constexpr int kA = Sys::A;  // DMA instructions per step
+  constexpr bool kRow = row_dma<Sys::A, 64>();
+  constexpr int kA = kRow ? 1 : Sys::A;  // DMA instructions per step
+  constexpr int kSlotF = act_slot_floats<Sys::A, B>();
+  const int lane = tid & 63;
   // steady-state wait: step k's DMA has one step's stores plus D-1 steps' (DMA +
   // stores) issued after it (lower bounds, see kSt)
   constexpr int kSteady = kSt + (D - 1) * (kA + kSt);
@@ -426,14 +451,21 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   // M0 = LDS byte address of this wave's 64 destination floats: computed once,
   // wave-uniform, then constant offsets per slot / component (no per-DMA address-space
   // cast or readfirstlane)
-  const uint32_t m0_wave = __builtin_amdgcn_readfirstlane(lds_off(s_act) + (uint32_t)wave * 256u);
+  const uint32_t m0_wave = __builtin_amdgcn_readfirstlane(
+      lds_off(s_act) + (uint32_t)wave * (kRow ? kRowRegionF * 4u : 256u));
   auto issue = [&](const float* src, int slot) __attribute__((always_inline)) {
+    if constexpr (kRow) {
+      dma16_nt(src, m0_wave + (uint32_t)(slot * kSlotF) * 4u);
+    } else {
 #pragma unroll
-    for (int j = 0; j < Sys::A; ++j)
-      dma4_nt(src + (kDirect ? j : j * B), m0_wave + (uint32_t)((slot * Sys::A + j) * B) * 4u);
+      for (int j = 0; j < Sys::A; ++j)
+        dma4_nt(src + (kDirect ? j : j * B), m0_wave + (uint32_t)((slot * Sys::A + j) * B) * 4u);
+    }
   };
   // this lane's DMA source pointer for step kk, and the per-step advance
-  const int64_t lane0 = kDirect ? (base + tid) * Sys::A : base * Sys::A + tid;
+  const int64_t wave_row0 = (base + 64 * (int64_t)wave) * Sys::A;  // the wave's slice
+  const int64_t lane0 = kRow ? wave_row0 + 4 * (lane % (64 * Sys::A / 4))
+                             : kDirect ? (base + tid) * Sys::A : base * Sys::A + tid;
   const int64_t dstride = a.n * Sys::A;
   auto dma_src = [&](int kk) __attribute__((always_inline)) {
     return gact + ((int64_t)kk * dstride + lane0);
@@ -458,10 +490,19 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
       if constexpr (FULL) {
         if constexpr (decltype(ladder)::value) ladder_wait<D, kA, kSt>(k);
         else wait_vmcnt<kSteady>();
-        if constexpr (!kDirect) wg_barrier<false>();  // every wave's DMA has landed
-        const float* slot = s_act + (k % kDmaSlots) * (B * Sys::A);
-        if constexpr (kDirect) lds_read_act<Sys::A>(act, slot + tid, B);
-        else lds_read_act<Sys::A>(act, slot + tid * Sys::A, 1);
+        // staged path: every wave is past the previous step's reads of s_obs (and, without
+        // row DMA, every wave's DMA of this slot has landed)
+        if constexpr (!kDirect) wg_barrier<false>();
+        const float* slot = s_act + (k % kDmaSlots) * kSlotF;
+        if constexpr (kRow) {  // ordinary LDS loads: ordered after the wait by its clobber
+#pragma unroll
+          for (int j = 0; j < Sys::A; ++j)
+            act[j] = slot[wave * kRowRegionF + lane * Sys::A + j];
+        } else if constexpr (kDirect) {
+          lds_read_act<Sys::A>(act, slot + tid, B);
+        } else {
+          lds_read_act<Sys::A>(act, slot + tid * Sys::A, 1);
+        }
         // prefetch step k+D into the slot step k-1 used (every reader is past this
         // point); near the end re-read step K-1: no branch, same op count
         issue(dsrc, (k + D) % kDmaSlots);
@@ -478,8 +519,9 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
     T o[Sys::O];
     T rew = (T)0;
     bool did_reset;
-    const uint8_t dflag = step_body<Sys, T, true>(sys, steps, a, i, live, act, tick + (uint64_t)k,
-                                                  k, o, rew, did_reset);
+    const uint8_t dflag = step_body<Sys, T, true, false, kNoDone>(sys, steps, a, i, live, act,
+                                                                  tick + (uint64_t)k, k, o, rew,
+                                                                  did_reset);
     any_reset = any_reset || did_reset;
     T* gobs = static_cast<T*>(a.obs) + (off + base) * Sys::O;
     if constexpr (kDirect) {
@@ -514,9 +556,9 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   for (; k < a.K; ++k) run_step(k, std::false_type{});
 }
 
-template <class Sys, typename T, int B, int D>
+template <class Sys, typename T, int B, int D, bool kNoDone = false>
 __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
-  __shared__ __attribute__((aligned(16))) float s_act[dma_slots<D>() * B * Sys::A];  // DMA ring
+  __shared__ __attribute__((aligned(16))) float s_act[dma_slots<D>() * act_slot_floats<Sys::A, B>()];  // DMA ring
   __shared__ __attribute__((aligned(16))) T s_obs[B * Sys::O];
   const int tid = (int)threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * B;
@@ -537,9 +579,9 @@ __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
     if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
   }
   if (nb == B && a.vec_ok)
-    rollout_loop<Sys, T, B, true, D>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
+    rollout_loop<Sys, T, B, true, D, kNoDone>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
   else
-    rollout_loop<Sys, T, B, false, D>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
+    rollout_loop<Sys, T, B, false, D, kNoDone>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
   if (live) {
     sys.store(a, i);
     if (any_reset) sys.store_autoreset_extra(a, i);
@@ -576,12 +618,25 @@ __device__ __forceinline__ void store_half(T* p, const T* v) {
   }
 }
 
-template <class Sys, typename T, int R, bool FULL, int D>
+// kNoDone: no done can occur in this launch (never-terminating system, no step
+// counter; LORENZ3 with the reference's constants): step_body's done bookkeeping --
+// compact list, auto-reset, step counter -- is compiled out (~25 of ~130 instructions
+// per step), and the done byte stored is a constant 0.
+// Actions (A = 2, 3): ONE 16-B row DMA per step (row_dma) moves the wave's 32 action
+// rows into a row-major LDS slot (the launch needs vec_ok; otherwise every workgroup
+// takes the gload path); the step reads its row with ordinary LDS loads after the
+// vmcnt wait (the wait asm's
+// memory clobber orders them after it, and the slot's address escapes into the DMA
+// asm, so the compiler assumes the DMA writes it) -- the compiler then places the
+// lgkmcnt wait where the action is first used, and the state-only part of the step
+// (the RHS of the old state) overlaps the LDS latency.
+template <class Sys, typename T, int R, bool FULL, int D, bool kNoDone>
 __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_reset,
                                            const KArgs& a, int64_t base, int tid, int nb,
                                            uint64_t tick, float* s_act) {
   static_assert(R == 2 && Sys::O % 2 == 0, "split-lane rollout: two lanes per env");
   constexpr int H = Sys::O / R;  // obs elements stored per lane
+  constexpr bool kRow = row_dma<Sys::A, 32>();  // one 16-B DMA per step (else 4-B per component)
   const int el = tid / R, q = tid % R;
   const bool lead = q == 0;
   const int64_t i = base + el;
@@ -590,19 +645,24 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
   // vector-memory ops every step issues after its DMA (lower bound): reward or done
   // (two exec-masked stores) + at least one obs store
   constexpr int kSt = 3;
-  constexpr int kA = Sys::A;
+  constexpr int kA = kRow ? 1 : Sys::A;
   constexpr int kSteady = kSt + (D - 1) * (kA + kSt);
   static_assert(D >= 1 && kSteady <= 63, "vmcnt immediate (6 bits on gfx9)");
   constexpr int kDmaSlots = dma_slots<D>();
+  constexpr int kSlotF = kRow ? kRowRegionF : 64 * Sys::A;  // floats per slot
   const uint32_t m0_wave = __builtin_amdgcn_readfirstlane(lds_off(s_act));
-  // component-major slot [A][64]: lane tid reads its env's action at slot[j*64 + tid]
-  // (both lanes of a pair load the same source float; the coalescer merges them)
   auto issue = [&](const float* src, int slot) __attribute__((always_inline)) {
+    if constexpr (kRow) {
+      dma16_nt(src, m0_wave + (uint32_t)(slot * kSlotF) * 4u);
+    } else {
 #pragma unroll
-    for (int j = 0; j < Sys::A; ++j) dma4_nt(src + j, m0_wave + (uint32_t)((slot * Sys::A + j) * 64) * 4u);
+      for (int j = 0; j < Sys::A; ++j) dma4_nt(src + j, m0_wave + (uint32_t)((slot * Sys::A + j) * 64) * 4u);
+    }
   };
   const int64_t dstride = a.n * Sys::A;
-  const float* dsrc = gact + i * Sys::A;
+  // kRow: lane tid loads chunk tid mod C of the wave's 32-env slice; else: lane tid
+  // loads its own env's components
+  const float* dsrc = kRow ? gact + base * Sys::A + 4 * (tid % (32 * Sys::A / 4)) : gact + i * Sys::A;
   if constexpr (FULL) __builtin_amdgcn_s_waitcnt(0x0F70);
   if constexpr (FULL && Sys::kUsesAction) {
 #pragma unroll
@@ -616,7 +676,13 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
       if constexpr (FULL) {
         if constexpr (decltype(ladder)::value) ladder_wait<D, kA, kSt>(k);
         else wait_vmcnt<kSteady>();
-        lds_read_act<Sys::A>(act, s_act + (k % kDmaSlots) * (64 * Sys::A) + tid, 64);
+        const float* slot = s_act + (k % kDmaSlots) * kSlotF;
+        if constexpr (kRow) {
+#pragma unroll
+          for (int j = 0; j < Sys::A; ++j) act[j] = slot[el * Sys::A + j];
+        } else {
+          lds_read_act<Sys::A>(act, slot + tid, 64);
+        }
         issue(dsrc, (k + D) % kDmaSlots);
         if (k + D + 1 < a.K) dsrc += dstride;
       } else if (live) {
@@ -627,12 +693,13 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
     T o[Sys::O];
     T rew = (T)0;
     bool did_reset;
-    const uint8_t dflag = step_body<Sys, T, true>(sys, steps, a, i, live, act, tick + (uint64_t)k,
-                                                  k, o, rew, did_reset, nullptr, lead);
+    const uint8_t dflag = step_body<Sys, T, true, false, kNoDone>(sys, steps, a, i, live, act,
+                                                                  tick + (uint64_t)k, k, o, rew,
+                                                                  did_reset, nullptr, lead);
     any_reset = any_reset || did_reset;
     if (!live) return;
     if (lead) gstore<true>(static_cast<T*>(a.rew) + off + i, rew);
-    else gstore<true>(a.done + off + i, dflag);
+    else gstore<true>(a.done + off + i, kNoDone ? (uint8_t)0 : dflag);
     // this lane's half row: elements [q*H, q*H + H) of env i = elements tid*H of the
     // block's contiguous obs slice
     T* p = static_cast<T*>(a.obs) + (off + base) * Sys::O + (int64_t)tid * H;
@@ -649,10 +716,10 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
   for (; k < a.K; ++k) run_step(k, std::false_type{});
 }
 
-template <class Sys, typename T, int R, int D>
+template <class Sys, typename T, int R, int D, bool kNoDone = false>
 __global__ __launch_bounds__(64) void k_rollout_split(KArgs a) {
   constexpr int E = 64 / R;  // envs per one-wave workgroup
-  __shared__ __attribute__((aligned(16))) float s_act[dma_slots<D>() * 64 * Sys::A];
+  __shared__ __attribute__((aligned(16))) float s_act[dma_slots<D>() * (row_dma<Sys::A, 32>() ? kRowRegionF : 64 * Sys::A)];
   const int tid = (int)threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * E;
   const int el = tid / R;
@@ -673,10 +740,10 @@ __global__ __launch_bounds__(64) void k_rollout_split(KArgs a) {
     sys.load(a, i);
     if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
   }
-  if (nb == E)
-    split_loop<Sys, T, R, true, D>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
+  if (nb == E && a.vec_ok)
+    split_loop<Sys, T, R, true, D, kNoDone>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
   else
-    split_loop<Sys, T, R, false, D>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
+    split_loop<Sys, T, R, false, D, kNoDone>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
   if (live && lead) {
     sys.store(a, i);
     if (any_reset) sys.store_autoreset_extra(a, i);
@@ -704,13 +771,27 @@ static inline bool rollout_split(const KArgs& a) {
 template <class Sys, typename T, int D>
 static void launch_rollout_d(const KArgs& a, hipStream_t s) {
   if (a.n < 2 * 256 * kBlock) {  // < 2 full workgroups per CU: one-wave groups
-    if (rollout_split<Sys>(a))
-      hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, D>), dim3((unsigned)((a.n + 31) / 32)),
-                         dim3(64), 0, s, a);
-    else
+    if (rollout_split<Sys>(a)) {
+      const dim3 g((unsigned)((a.n + 31) / 32));
+      if constexpr (never_terminates<Sys>::value && !Sys::kNoise) {
+        if (no_done<Sys>(a) && !(a.variant & 2048)) {  // variant bit 2048: keep the done path (A/B)
+          hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, D, true>), g, dim3(64), 0, s, a);
+          return;
+        }
+      }
+      hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, D>), g, dim3(64), 0, s, a);
+    } else {
       hipLaunchKernelGGL((k_rollout<Sys, T, 64, D>), dim3((unsigned)((a.n + 63) / 64)), dim3(64),
                          0, s, a);
+    }
   } else {
+    if constexpr (never_terminates<Sys>::value && !Sys::kNoise) {
+      if (no_done<Sys>(a) && !(a.variant & 2048)) {
+        hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D, true>), dim3((unsigned)grid_for(a.n)),
+                           dim3(kBlock), 0, s, a);
+        return;
+      }
+    }
     hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D>), dim3((unsigned)grid_for(a.n)), dim3(kBlock),
                        0, s, a);
   }

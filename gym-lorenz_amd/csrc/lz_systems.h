@@ -64,10 +64,20 @@ struct Draw<double> {
 // params: sigma(self.u)=10, rho(self.i)=28, beta(self.o)=8/3, dt=0.01, clip=500
 // planes: x, y, z [, step]
 // ===========================================================================
+// A system whose step() can never report termination (done then only comes from the
+// step counter: truncation or the reference's 't == T')
+template <class S, class = void>
+struct never_terminates { static constexpr bool value = false; };
+template <class S>
+struct never_terminates<S, decltype((void)S::kNeverTerminates)> {
+  static constexpr bool value = S::kNeverTerminates;
+};
+
 template <typename T>
 struct SysL3 {
   static constexpr int A = 3, O = 6, NI = 3;
   static constexpr bool kUsesAction = true, kNoise = false;
+  static constexpr bool kNeverTerminates = true;  // step() returns false: :85-89
   static constexpr int kStepPlane = LZ_L3_STEP;
   T x, y, z;
   T sg, rh, be, dt, cl;

@@ -133,3 +133,40 @@ def test_cfg5_pmsm_rollout_k2048_bitexact(gl, orc):
     from ragged starts, actions U(-1.2, 1.2) (exercising the [-1, 1] clip), Adam dual
     carried across the auto-resets."""
     _run(gl, orc, "pmsm", 32768, L=2000, seed=32, lo=-1.2, hi=1.2)
+
+
+@pytest.mark.parametrize("n", [32768, 40001, 262144])
+def test_cfg5_l3_rollout_no_timelimit_bitexact(gl, orc, n):
+    """The bench's cfg5 workload as dynamic.py runs it: no TimeLimit, and the
+    reference's own done (t == 10) never fires -- the launch takes the kernel without
+    done bookkeeping (kNoDone).  K = 2048 oracle steps bit for bit, every done byte 0,
+    the final state; and the same bits as the general kernel (variant bit 2048).
+    n = 40,001 adds a ragged last workgroup (the non-DMA path of the same kernel);
+    262,144 is the 256-lane k_rollout path."""
+    seed = 41
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(seed)
+    A = torch.rand((K, n, 3), generator=gen, device="cuda") * 3 - 1.5
+    res = []
+    for var in (0, 2048):
+        be = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=seed, variant=var)
+        be.reset()
+        obs, rew, done = be.rollout(A)
+        torch.cuda.synchronize()
+        res.append((obs, rew, done, np.stack([be.get_state(j).cpu().numpy() for j in range(3)], 1)))
+        be.close()
+    (o0, r0, d0, s0), (o1, r1, d1, s1) = res
+    assert torch.equal(d0, d1) and int(d0.count_nonzero()) == 0
+    assert _nan_eq(s0, s1)
+    st = orc.reset_draw("l3", np.float32, n, 0, seed, 0).copy()
+    bad = []
+    with np.errstate(all="ignore"):
+        for k in range(K):
+            oo, rr = orc.l3_step(st, A[k].cpu().numpy())
+            for tag, got, other, want in (("obs", o0[k], o1[k], oo), ("reward", r0[k], r1[k], rr)):
+                g = got.cpu().numpy()
+                if not (_nan_eq(g, want) and _nan_eq(other.cpu().numpy(), g)):
+                    bad.append((k, tag))
+            assert len(bad) < 5, bad
+    assert not bad, bad
+    assert _nan_eq(s0, st)

@@ -332,7 +332,9 @@ def test_shard_invariance(gl):
 @pytest.mark.parametrize("system,dtype,n", [("lorenz3", "float32", 1000), ("pmsm", "float32", 1000),
                                             ("hr", "float64", 1000), ("lorenz4", "float32", 1000),
                                             ("lorenz3", "float32", 40001),
-                                            ("lorenz3", "float32", 140000)])
+                                            ("lorenz3", "float32", 140000),
+                                            ("pmsm", "float32", 140000),
+                                            ("hr", "float32", 140000)])
 def test_rollout_equals_steps(gl, system, dtype, n):
     """Fused rollout (one-wave workgroups below 131,072 envs -- two lanes per env for
     LORENZ3 f32 from 32,768 -- 256-lane above) == K steps."""
