@@ -211,8 +211,10 @@ SYSTEM_INFO = {  # system -> (reference env, mangled k_step / k_rollout names, a
 }
 
 
-def kernel_name(system, mode, n, f64=False):
-    """Mangled name of the dominant kernel (lz_kernels.hip launch_all / launch_rollout_d)."""
+def kernel_name(system, mode, n, f64=False, no_done=False):
+    """Mangled name of the dominant kernel (lz_kernels.hip launch_all / launch_rollout_d).
+    no_done: a rollout launch that cannot produce a done (LORENZ3 without a TimeLimit)
+    runs the done-free instantiation (kNoDone = true)."""
     tag = SYSTEM_INFO[system][1]
     if f64:
         tag = tag.replace("IfEEf", "IdEEd")
@@ -220,11 +222,12 @@ def kernel_name(system, mode, n, f64=False):
     if mode != "rollout":
         return "_ZN2lz6k_stepINS_%sLi0EEEvNS_5KArgsE" % sysname
     D = 7  # kDmaDist
+    b = "Lb%dE" % int(no_done and system == "lorenz3")
     if n < 2 * 256 * 256:  # one-wave workgroups; two lanes per env for LORENZ3 f32 >= 32,768
         if system == "lorenz3" and n >= 32768:
-            return "_ZN2lz15k_rollout_splitINS_%sLi2ELi%dEEEvNS_5KArgsE" % (sysname, D)
-        return "_ZN2lz9k_rolloutINS_%sLi64ELi%dEEEvNS_5KArgsE" % (sysname, D)
-    return "_ZN2lz9k_rolloutINS_%sLi256ELi%dEEEvNS_5KArgsE" % (sysname, D)
+            return "_ZN2lz15k_rollout_splitINS_%sLi2ELi%dE%sEEvNS_5KArgsE" % (sysname, D, b)
+        return "_ZN2lz9k_rolloutINS_%sLi64ELi%dE%sEEvNS_5KArgsE" % (sysname, D, b)
+    return "_ZN2lz9k_rolloutINS_%sLi256ELi%dE%sEEvNS_5KArgsE" % (sysname, D, b)
 
 
 def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
@@ -731,7 +734,8 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": kernel_name(args.system, args.mode, n), "avg_launch_us": launch_s * 1e6,
+            "kernel": kernel_name(args.system, args.mode, n, no_done=args.max_episode_steps == 0),
+            "avg_launch_us": launch_s * 1e6,
             "bytes_per_env_step": bytes_step,
             "note": "achieved = algorithmic bytes per launch (bytes_per_env_step x envs_per_gpu"
                     " x steps per launch) / HIP-event average launch time on the launch stream",
