@@ -37,7 +37,8 @@
  *   lz_get_state / lz_set_state
  *       -> attribute access env.state1 / state2 / state_master / state_slave /
  *          lambda_coef ... used by code/lorenz_pmsm/test_evaluate.py:99-111
- *   lz_policy_pack[_hidden] / lz_rollout_policy / lz_gae / lz_episode_starts
+ *   lz_policy_pack_f32 / lz_rollout_policy_f32 / lz_policy_pack[_hidden] /
+ *   lz_rollout_policy / lz_gae / lz_episode_starts
  *       -> SB3 OnPolicyAlgorithm.collect_rollouts + RolloutBuffer.compute_returns_and_
  *          advantage for the MlpPolicy learners (code/lorenz_pmsm/train.py:155-178,
  *          optimize.py:36-60 ([64,64] / [128,128]), code/gym_run.py:83 (PPO default
