@@ -151,15 +151,16 @@ constexpr int kLnBlobBytes = kLnLogStd + 64;       // 145984 B (resident in LDS)
 
 // The MlpPolicy again at the precision SB3 runs it (float32 operands, float32
 // accumulation): f32-input MFMA (v_mfma_f32_32x32x2_f32, bit-for-bit a k-ordered fmaf
-// chain) for the two hidden layers, the heads as per-lane fmaf chains, tanh from IEEE
-// basic operations -- every result is a fixed sequence of correctly rounded
+// chain) for the two hidden layers, the heads as per-lane fmaf chains, tanh as a
+// piecewise polynomial in fmaf -- every result is a fixed sequence of correctly rounded
 // operations the C oracle restates exactly.  Blob (lz_policy_pack_f32), per net:
 //   W1 [4 out tiles][64 lanes][4 k-steps] f32 (lane (r, h), k-step s: W1[32t + r][2s + h]),
 //   W2 [4 out tiles][16 quads][64 lanes][4] f32 (k-step q = 4 quad + e: input unit
 //      32 (q >> 4) + row(q & 15, h)), b1 / b2 [4][2 halves][16] f32 as accumulator
 //   initialisers, head rows [4][2 halves][64] f32 (element 16t + g: unit 32t + row(g, h)),
 //   head bias [4] f32; net 0 = pi (action_net head), net 1 = vf (value_net head);
-//   log_std / Normal constants float[16] after both nets.
+//   log_std / Normal constants float[16] after both nets, then the tanh coefficient
+//   table (lz_policy.hip tanh_tab).
 constexpr int kF32W1 = 0;
 constexpr int kF32W2 = kF32W1 + 4 * 64 * 4 * 4;
 constexpr int kF32B1 = kF32W2 + 4 * 16 * 64 * 4 * 4;
@@ -168,7 +169,8 @@ constexpr int kF32H = kF32B2 + 4 * 2 * 16 * 4;
 constexpr int kF32HB = kF32H + 4 * 2 * 64 * 4;
 constexpr int kF32Net = kF32HB + 64;                 // 72768 B
 constexpr int kF32LogStd = 2 * kF32Net;
-constexpr int kF32BlobBytes = kF32LogStd + 64;      // 145600 B (resident in LDS)
+constexpr int kF32Tanh = kF32LogStd + 64;           // tanh table: 36 segments x 8 floats
+constexpr int kF32BlobBytes = kF32Tanh + 36 * 32;   // 146752 B (resident in LDS)
 
 struct PArgs {
   const uint8_t* blob;     // device copy of the packed policy

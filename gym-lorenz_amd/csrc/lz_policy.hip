@@ -685,49 +685,44 @@ __device__ __forceinline__ void net_fwd(const uint8_t* net, const float* x, bool
 //   * the heads (2-4 rows: a 32-row MFMA tile would waste 90% of it) as one fmaf chain
 //     per lane half over that half's 64 units (t, g ascending), the halves' partial
 //     sums added once (__shfl_xor 32), then the bias;
-//   * tanh from basic operations only (tanh_ieee): expm1 by Cody-Waite reduction + a
-//     degree-8 Taylor polynomial in fmaf, 2^n assembled in the exponent bits, one
-//     correctly rounded division -- no v_exp_f32 / v_rcp_f32, whose bits no CPU
-//     reproduces.  Max error vs tanh in float64: 2.2 ulp (tests/test_policy_f32_host.py).
+//   * tanh as a piecewise polynomial (tanh_tab: 36 segments of width 1/4, degree 6,
+//     Horner in fmaf; coefficients from tools/tanh_table.py in the blob) -- no
+//     v_exp_f32 / v_rcp_f32, whose bits no CPU reproduces, and no division.  Max error
+//     vs tanh in float64: 1.11 ulp (tests/test_policy_f32_host.py).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float tanh_ieee(float x) {
+// tanh(x) = sign(x) p_k(|x| - k/4), k = floor(4|x|) < 36, p_k a degree-6 polynomial
+// (tools/tanh_table.py; segment 0 is t q(t): full relative accuracy near 0) evaluated by
+// Horner in fmaf; 1 for |x| >= 9 (1 - tanh(9) < 2^-25).  ~20 instructions, two of them
+// LDS reads of the segment's coefficients (the table sits in the blob, tab = LDS).
+__device__ __forceinline__ float tanh_tab(float x, const float* tab) {
   const float ax = fabsf(x);
-  const float axc = ax < 9.0f ? ax : 9.0f;  // NaN -> 9: the selects below fix the result
-  const float y = -2.0f * axc;              // exact; tanh(|x|) = -expm1(y) / (2 + expm1(y))
-  const float n = __builtin_rintf(y * 1.44269502f);
-  float r = fmaf(n, -0.693145751953125f, y);  // ln2 high part: n * it is exact
-  r = fmaf(n, -1.42860677e-06f, r);
-  float q = 2.48015873e-05f;                  // 1/8!
-  q = fmaf(q, r, 1.98412698e-04f);
-  q = fmaf(q, r, 1.38888889e-03f);
-  q = fmaf(q, r, 8.33333333e-03f);
-  q = fmaf(q, r, 4.16666667e-02f);
-  q = fmaf(q, r, 1.66666667e-01f);
-  q = fmaf(q, r, 0.5f);
-  const float p = fmaf(r * r, q, r);          // expm1(r), |r| <= ln2 / 2
-  const float s = __uint_as_float((uint32_t)((int)n + 127) << 23);  // 2^n, n in [-26, 0]
-  // |x| < 0.45: -expm1 / (2 + expm1) (no cancellation near 0); else with E = e^-2|x|
-  // < 0.41: (1 - E) / (1 + E) (E's error not amplified near tanh = 1)
-  const bool lo = ax < 0.45f;
-  const float em1 = fmaf(s, p, s - 1.0f);     // 2^n (1 + p) - 1
-  const float e = fmaf(s, p, s);              // 2^n (1 + p)
-  float t = (lo ? -em1 : 1.0f - e) / (lo ? 2.0f + em1 : 1.0f + e);
-  t = ax < 9.0f ? t : 1.0f;                   // 1 - tanh(9) < 2^-25: rounds to 1
-  t = ax < 2.44140625e-04f ? ax : t;          // |x| < 2^-12: tanh(x) = x in float32
-  t = x != x ? x : t;
-  return __builtin_copysignf(t, x);
+  int k = (int)(ax * 4.0f);                 // exact product; NaN -> 0, inf -> INT_MAX
+  k = k < 35 ? k : 35;
+  const f32x4 lo = reinterpret_cast<const f32x4*>(tab)[2 * k];
+  const f32x4 hi = reinterpret_cast<const f32x4*>(tab)[2 * k + 1];
+  const float t = fmaf((float)k, -0.25f, ax);  // |x| - k/4, exact
+  float y = fmaf(hi[2], t, hi[1]);
+  y = fmaf(y, t, hi[0]);
+  y = fmaf(y, t, lo[3]);
+  y = fmaf(y, t, lo[2]);
+  y = fmaf(y, t, lo[1]);
+  y = fmaf(y, t, lo[0]);
+  y = ax < 9.0f ? y : 1.0f;
+  y = x != x ? x : y;
+  return __builtin_copysignf(y, x);
 }
 
 // One net on the wave's 32-env tile.  xs[s] = this lane's layer-1 input for k-step s
 // (obs[2s + h] of env lane & 31).  Returns the NH head rows in head[] on every lane
 // (both halves hold the same values).
 template <int KS1, int NH>
-__device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int lane, float* head) {
+__device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int lane, float* head,
+                                        const float* ttab) {
   asm volatile("" ::: "memory");
   const int h = lane >> 5;
   const f32x4* w1 = reinterpret_cast<const f32x4*>(net + kF32W1) + lane;
@@ -745,7 +740,7 @@ __device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int
     for (int s = 0; s < KS1; ++s) c = mfma_f32(w[s], xs[s], c);
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
-      c[g] = tanh_ieee(c[g]);
+      c[g] = tanh_tab(c[g], ttab);
     }
     a1[t] = c;
   }
@@ -769,7 +764,7 @@ __device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int
     }
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
-      const float v = tanh_ieee(c[g]);
+      const float v = tanh_tab(c[g], ttab);
 #pragma unroll
       for (int j = 0; j < NH; ++j) {
         const float w = wh[j * 128 + t * 16 + g];
@@ -816,7 +811,8 @@ __device__ __forceinline__ void value_fwd(const uint8_t* blob, const uint8_t* vf
   } else if constexpr (kPair == kMlpF32) {
     float xs[(O + 1) / 2];
     f32_inputs<O, (O + 1) / 2>(x, lane, xs);
-    mlp_f32<(O + 1) / 2, 1>(vf_net, xs, lane, out);
+    mlp_f32<(O + 1) / 2, 1>(vf_net, xs, lane, out,
+                            reinterpret_cast<const float*>(blob + kF32Tanh));
   } else {
     net_fwd<E, O, 1>(vf_net, x, use, lane, out);
   }
@@ -959,9 +955,10 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
       } else if constexpr (kPair == kMlpF32) {
         float xs[(O + 1) / 2];
         f32_inputs<O, (O + 1) / 2>(x, lane, xs);
-        mlp_f32<(O + 1) / 2, A>(pi_net, xs, lane, mean);
+        const float* ttab = reinterpret_cast<const float*>(s_blob + kF32Tanh);
+        mlp_f32<(O + 1) / 2, A>(pi_net, xs, lane, mean, ttab);
         __builtin_amdgcn_sched_barrier(0);  // the two nets one after the other
-        mlp_f32<(O + 1) / 2, 1>(vf_net, xs, lane, val);
+        mlp_f32<(O + 1) / 2, 1>(vf_net, xs, lane, val, ttab);
       } else if constexpr (kPair == kMlpPair || kPair == kMlpPairPipe) {
         f32x16 hp, hv;
         if constexpr (kPair == kMlpPairPipe)
@@ -1423,6 +1420,46 @@ void pack_net(uint8_t* net, int O, int rows3, const float* w1, const float* b1, 
     }
 }
 
+// tanh_tab's coefficients (kF32Tanh in the blob)
+const float kTanhTab[36 * 8] = {
+    0.0f, 0x1.0000000000000p+0f, -0x1.a6f07c0000000p-20f, -0x1.5541d60000000p-2f, -0x1.51fdca0000000p-10f, 0x1.25eb3e0000000p-3f, -0x1.341fb80000000p-5f, 0.0f,
+    0x1.f597ea0000000p-3f, 0x1.e149a00000000p-1f, -0x1.d780900000000p-3f, -0x1.0727420000000p-2f, 0x1.1ec2f20000000p-3f, 0x1.2261f80000000p-4f, -0x1.1b659e0000000p-4f, 0.0f,
+    0x1.d9353e0000000p-2f, 0x1.92a9440000000p-1f, -0x1.7425ea0000000p-2f, -0x1.825e100000000p-4f, 0x1.5449660000000p-3f, -0x1.2783dc0000000p-5f, -0x1.8ef0980000000p-6f, 0.0f,
+    0x1.45323e0000000p-1f, 0x1.3173b00000000p-1f, -0x1.8403420000000p-2f, 0x1.560dd80000000p-5f, 0x1.9b48860000000p-4f, -0x1.1769ea0000000p-4f, 0x1.a6713e0000000p-7f, 0.0f,
+    0x1.85efac0000000p-1f, 0x1.ae0dc20000000p-2f, -0x1.4786dc0000000p-2f, 0x1.a866540000000p-4f, 0x1.c491be0000000p-6f, -0x1.77ff4a0000000p-5f, 0x1.2ec4800000000p-6f, 0.0f,
+    0x1.b2523c0000000p-1f, 0x1.1f25140000000p-2f, -0x1.e7298e0000000p-3f, 0x1.bbba5c0000000p-4f, -0x1.a47efa0000000p-7f, -0x1.22d1140000000p-6f, 0x1.67d68c0000000p-7f, 0.0f,
+    0x1.cf6f980000000p-1f, 0x1.7216540000000p-3f, -0x1.4efc240000000p-3f, 0x1.67c0400000000p-4f, -0x1.9ba00c0000000p-6f, -0x1.bcba0c0000000p-10f, 0x1.0e231a0000000p-8f, 0.0f,
+    0x1.e1fbfa0000000p-1f, 0x1.d22ca20000000p-4f, -0x1.b6d8980000000p-4f, 0x1.01c00a0000000p-4f, -0x1.8273cc0000000p-6f, 0x1.0d86d80000000p-8f, 0x1.555f3a0000000p-11f, 0.0f,
+    0x1.ed95060000000p-1f, 0x1.2162c20000000p-4f, -0x1.16f9e40000000p-4f, 0x1.58f8500000000p-5f, -0x1.2570440000000p-6f, 0x1.412f980000000p-8f, -0x1.257fee0000000p-11f, 0.0f,
+    0x1.f4bfd60000000p-1f, 0x1.64108a0000000p-5f, -0x1.5c3d900000000p-5f, 0x1.bbccc00000000p-6f, -0x1.93c6980000000p-7f, 0x1.058f1c0000000p-8f, -0x1.9070c40000000p-11f, 0.0f,
+    0x1.f925820000000p-1f, 0x1.b3afe20000000p-6f, -0x1.addad20000000p-6f, 0x1.16dd620000000p-6f, -0x1.078aa60000000p-7f, 0x1.72a9220000000p-9f, -0x1.4e321a0000000p-11f, 0.0f,
+    0x1.fbd50a0000000p-1f, 0x1.09a7a60000000p-6f, -0x1.077df80000000p-6f, 0x1.5993b20000000p-7f, -0x1.4de50a0000000p-8f, 0x1.eae9760000000p-10f, -0x1.dd197e0000000p-12f, 0.0f,
+    0x1.fd77d20000000p-1f, 0x1.434a520000000p-7f, -0x1.41b0ec0000000p-7f, 0x1.a8a6ee0000000p-8f, -0x1.9fb5500000000p-9f, 0x1.3966ca0000000p-10f, -0x1.3ccca80000000p-12f, 0.0f,
+    0x1.fe767a0000000p-1f, 0x1.88ef660000000p-8f, -0x1.87c13a0000000p-8f, 0x1.0395e20000000p-8f, -0x1.001dfc0000000p-9f, 0x1.87e6320000000p-11f, -0x1.94f38c0000000p-13f, 0.0f,
+    0x1.ff112c0000000p-1f, 0x1.dd37d00000000p-9f, -0x1.dc59020000000p-9f, 0x1.3c634e0000000p-9f, -0x1.39a2900000000p-10f, 0x1.e41e880000000p-12f, -0x1.faa5220000000p-14f, 0.0f,
+    0x1.ff6f180000000p-1f, 0x1.21a7ae0000000p-9f, -0x1.2155920000000p-9f, 0x1.80e6b80000000p-10f, -0x1.7ea3800000000p-11f, 0x1.28dce60000000p-12f, -0x1.3903a60000000p-14f, 0.0f,
+    0x1.ffa8180000000p-1f, 0x1.5f85ac0000000p-10f, -0x1.5f49280000000p-10f, 0x1.d3b8e20000000p-11f, -0x1.d1c5e00000000p-12f, 0x1.6a7fda0000000p-13f, -0x1.7ff0380000000p-15f, 0.0f,
+    0x1.ffcaac0000000p-1f, 0x1.aa87ce0000000p-11f, -0x1.aa5b2e0000000p-11f, 0x1.1bfcc80000000p-11f, -0x1.1b192c0000000p-12f, 0x1.b97e0e0000000p-14f, -0x1.d4dade0000000p-16f, 0.0f,
+    0x1.ffdfa80000000p-1f, 0x1.02bec80000000p-11f, -0x1.02ae500000000p-11f, 0x1.58b6fa0000000p-12f, -0x1.57da400000000p-13f, 0x1.0c6dd40000000p-14f, -0x1.1d895e0000000p-16f, 0.0f,
+    0x1.ffec620000000p-1f, 0x1.39e7820000000p-12f, -0x1.39db540000000p-12f, 0x1.a2528c0000000p-13f, -0x1.a16f780000000p-14f, 0x1.4618b60000000p-15f, -0x1.5b362e0000000p-17f, 0.0f,
+    0x1.fff41a0000000p-1f, 0x1.7ccec00000000p-13f, -0x1.7cc5b80000000p-13f, 0x1.fb91fe0000000p-14f, -0x1.fa9c820000000p-15f, 0x1.8bed2e0000000p-16f, -0x1.a5d0140000000p-18f, 0.0f,
+    0x1.fff8c80000000p-1f, 0x1.cdf5a20000000p-14f, -0x1.cdeee60000000p-14f, 0x1.33e69c0000000p-14f, -0x1.335c760000000p-15f, 0x1.e085f60000000p-17f, -0x1.0004dc0000000p-18f, 0.0f,
+    0x1.fffba00000000p-1f, 0x1.1832dc0000000p-14f, -0x1.1830540000000p-14f, 0x1.7588f40000000p-15f, -0x1.74e9940000000p-16f, 0x1.238cdc0000000p-17f, -0x1.36c0a20000000p-19f, 0.0f,
+    0x1.fffd580000000p-1f, 0x1.53e7140000000p-15f, -0x1.53e5260000000p-15f, 0x1.c524fe0000000p-16f, -0x1.c469360000000p-17f, 0x1.61b9aa0000000p-18f, -0x1.7903ba0000000p-20f, 0.0f,
+    0x1.fffe640000000p-1f, 0x1.9c53760000000p-16f, -0x1.9c51f80000000p-16f, 0x1.12dadc0000000p-16f, -0x1.126bbe0000000p-17f, 0x1.ad2ec00000000p-19f, -0x1.c9aebc0000000p-21f, 0.0f,
+    0x1.ffff060000000p-1f, 0x1.f42dde0000000p-17f, -0x1.f42cae0000000p-17f, 0x1.4d6c300000000p-17f, -0x1.4ce84a0000000p-18f, 0x1.045fc00000000p-19f, -0x1.15e2d80000000p-21f, 0.0f,
+    0x1.ffff680000000p-1f, 0x1.2f5ffa0000000p-17f, -0x1.2f5f7a0000000p-17f, 0x1.9477420000000p-18f, -0x1.93d3dc0000000p-19f, 0x1.3bb4400000000p-20f, -0x1.5024c80000000p-22f, 0.0f,
+    0x1.ffffa40000000p-1f, 0x1.7003540000000p-18f, -0x1.7002e60000000p-18f, 0x1.eaa5a20000000p-19f, -0x1.e9e7700000000p-20f, 0x1.7f371a0000000p-21f, -0x1.992cde0000000p-23f, 0.0f,
+    0x1.ffffc80000000p-1f, 0x1.be6c3e0000000p-19f, -0x1.be6bd20000000p-19f, 0x1.29977a0000000p-19f, -0x1.291c300000000p-20f, 0x1.d0577a0000000p-22f, -0x1.ed543e0000000p-24f, 0.0f,
+    0x1.ffffde0000000p-1f, 0x1.0ec4f20000000p-19f, -0x1.0ec4ba0000000p-19f, 0x1.68ff460000000p-20f, -0x1.6866240000000p-21f, 0x1.19808a0000000p-22f, -0x1.2a59200000000p-24f, 0.0f,
+    0x1.ffffec0000000p-1f, 0x1.4875bc0000000p-20f, -0x1.4875940000000p-20f, 0x1.b5ec720000000p-21f, -0x1.b561300000000p-22f, 0x1.56fa300000000p-23f, -0x1.7293ba0000000p-25f, 0.0f,
+    0x1.fffff40000000p-1f, 0x1.8e712e0000000p-21f, -0x1.8e710c0000000p-21f, 0x1.099da80000000p-21f, -0x1.094dba0000000p-22f, 0x1.a04dc60000000p-24f, -0x1.c2dc0c0000000p-26f, 0.0f,
+    0x1.fffff80000000p-1f, 0x1.e355b40000000p-22f, -0x1.e355980000000p-22f, 0x1.4236320000000p-22f, -0x1.41e41c0000000p-23f, 0x1.fa028c0000000p-25f, -0x1.14787e0000000p-26f, 0.0f,
+    0x1.fffffc0000000p-1f, 0x1.25284c0000000p-22f, -0x1.25284e0000000p-22f, 0x1.86dff60000000p-23f, -0x1.86b3020000000p-24f, 0x1.34c63a0000000p-25f, -0x1.5aa20a0000000p-27f, 0.0f,
+    0x1.fffffe0000000p-1f, 0x1.639e300000000p-23f, -0x1.639e640000000p-23f, 0x1.da2e6a0000000p-24f, -0x1.da604a0000000p-25f, 0x1.79e8e40000000p-26f, -0x1.b7d2120000000p-28f, 0.0f,
+    0x1.fffffe0000000p-1f, 0x1.af62e60000000p-24f, -0x1.af62c60000000p-24f, 0x1.1f95fc0000000p-24f, -0x1.1f781e0000000p-25f, 0x1.c729ba0000000p-27f, -0x1.0279980000000p-28f, 0.0f,
+};
+
 // float32 MlpPolicy net (kF32* layout, see mlp_f32 / lz_internal.h)
 void pack_net_f32(uint8_t* net, int O, int rows3, const float* w1, const float* b1, const float* w2,
                   const float* b2, const float* w3, const float* b3) {
@@ -1725,6 +1762,7 @@ lz_status lz_policy_pack_f32(const lz_mlp_policy* p, int32_t hidden, void* host_
   pack_net_f32(b, O, A, pw1, pb1, pw2, pb2, aw, p->act_b);
   pack_net_f32(b + lz::kF32Net, O, 1, vw1, vb1, vw2, vb2, uw, p->val_b);
   pack_gauss(reinterpret_cast<float*>(b + lz::kF32LogStd), A, p->log_std);
+  std::memcpy(b + lz::kF32Tanh, kTanhTab, sizeof kTanhTab);
   return LZ_OK;
 }
 

@@ -561,41 +561,68 @@ LEGACY_BODY(float)
  * torch forward SB3 computes is checked separately, tests/test_policy_f32_host.py):
  *   hidden unit u: acc = b[u]; acc = fmaf(w[u][k], x[k], acc) over the inputs k in the
  *     order (k-step s, lane half h): layer 1 k = 2s + h, layer 2 k = 32 ti +
- *     row(g, h) for ti = 0..3, g = 0..15, h = 0, 1; then tanh_ieee(acc);
+ *     row(g, h) for ti = 0..3, g = 0..15, h = 0, 1; then orc_tanh_tab(acc);
  *   head row r: per half h an fmaf chain from +0 over k = 32 t + row(g, h), t = 0..3,
  *     g = 0..15; out = (part0 + part1) + b[r].
  * Nets narrower than 128 are zero-padded (exactly what the packer does).
  * ========================================================================= */
-float orc_tanh_ieee(float x) {
-  /* lz_policy.hip tanh_ieee: -expm1(-2|x|) / (2 + expm1(-2|x|)), expm1 by Cody-Waite
-   * reduction + degree-8 Taylor polynomial, 2^n in the exponent bits */
+/* lz_policy.hip tanh_tab: sign(x) p_k(|x| - k/4), k = floor(4|x|) (segments of width
+ * 1/4 over [0, 9)), p_k of degree 6 by Horner in fmaf; 1 for |x| >= 9.  The coefficients
+ * (tools/tanh_table.py) are the same 36 x 8 floats the packer puts into the blob. */
+static const float orc_tanh_coef[36 * 8] = {
+    0.0f, 0x1.0000000000000p+0f, -0x1.a6f07c0000000p-20f, -0x1.5541d60000000p-2f, -0x1.51fdca0000000p-10f, 0x1.25eb3e0000000p-3f, -0x1.341fb80000000p-5f, 0.0f,
+    0x1.f597ea0000000p-3f, 0x1.e149a00000000p-1f, -0x1.d780900000000p-3f, -0x1.0727420000000p-2f, 0x1.1ec2f20000000p-3f, 0x1.2261f80000000p-4f, -0x1.1b659e0000000p-4f, 0.0f,
+    0x1.d9353e0000000p-2f, 0x1.92a9440000000p-1f, -0x1.7425ea0000000p-2f, -0x1.825e100000000p-4f, 0x1.5449660000000p-3f, -0x1.2783dc0000000p-5f, -0x1.8ef0980000000p-6f, 0.0f,
+    0x1.45323e0000000p-1f, 0x1.3173b00000000p-1f, -0x1.8403420000000p-2f, 0x1.560dd80000000p-5f, 0x1.9b48860000000p-4f, -0x1.1769ea0000000p-4f, 0x1.a6713e0000000p-7f, 0.0f,
+    0x1.85efac0000000p-1f, 0x1.ae0dc20000000p-2f, -0x1.4786dc0000000p-2f, 0x1.a866540000000p-4f, 0x1.c491be0000000p-6f, -0x1.77ff4a0000000p-5f, 0x1.2ec4800000000p-6f, 0.0f,
+    0x1.b2523c0000000p-1f, 0x1.1f25140000000p-2f, -0x1.e7298e0000000p-3f, 0x1.bbba5c0000000p-4f, -0x1.a47efa0000000p-7f, -0x1.22d1140000000p-6f, 0x1.67d68c0000000p-7f, 0.0f,
+    0x1.cf6f980000000p-1f, 0x1.7216540000000p-3f, -0x1.4efc240000000p-3f, 0x1.67c0400000000p-4f, -0x1.9ba00c0000000p-6f, -0x1.bcba0c0000000p-10f, 0x1.0e231a0000000p-8f, 0.0f,
+    0x1.e1fbfa0000000p-1f, 0x1.d22ca20000000p-4f, -0x1.b6d8980000000p-4f, 0x1.01c00a0000000p-4f, -0x1.8273cc0000000p-6f, 0x1.0d86d80000000p-8f, 0x1.555f3a0000000p-11f, 0.0f,
+    0x1.ed95060000000p-1f, 0x1.2162c20000000p-4f, -0x1.16f9e40000000p-4f, 0x1.58f8500000000p-5f, -0x1.2570440000000p-6f, 0x1.412f980000000p-8f, -0x1.257fee0000000p-11f, 0.0f,
+    0x1.f4bfd60000000p-1f, 0x1.64108a0000000p-5f, -0x1.5c3d900000000p-5f, 0x1.bbccc00000000p-6f, -0x1.93c6980000000p-7f, 0x1.058f1c0000000p-8f, -0x1.9070c40000000p-11f, 0.0f,
+    0x1.f925820000000p-1f, 0x1.b3afe20000000p-6f, -0x1.addad20000000p-6f, 0x1.16dd620000000p-6f, -0x1.078aa60000000p-7f, 0x1.72a9220000000p-9f, -0x1.4e321a0000000p-11f, 0.0f,
+    0x1.fbd50a0000000p-1f, 0x1.09a7a60000000p-6f, -0x1.077df80000000p-6f, 0x1.5993b20000000p-7f, -0x1.4de50a0000000p-8f, 0x1.eae9760000000p-10f, -0x1.dd197e0000000p-12f, 0.0f,
+    0x1.fd77d20000000p-1f, 0x1.434a520000000p-7f, -0x1.41b0ec0000000p-7f, 0x1.a8a6ee0000000p-8f, -0x1.9fb5500000000p-9f, 0x1.3966ca0000000p-10f, -0x1.3ccca80000000p-12f, 0.0f,
+    0x1.fe767a0000000p-1f, 0x1.88ef660000000p-8f, -0x1.87c13a0000000p-8f, 0x1.0395e20000000p-8f, -0x1.001dfc0000000p-9f, 0x1.87e6320000000p-11f, -0x1.94f38c0000000p-13f, 0.0f,
+    0x1.ff112c0000000p-1f, 0x1.dd37d00000000p-9f, -0x1.dc59020000000p-9f, 0x1.3c634e0000000p-9f, -0x1.39a2900000000p-10f, 0x1.e41e880000000p-12f, -0x1.faa5220000000p-14f, 0.0f,
+    0x1.ff6f180000000p-1f, 0x1.21a7ae0000000p-9f, -0x1.2155920000000p-9f, 0x1.80e6b80000000p-10f, -0x1.7ea3800000000p-11f, 0x1.28dce60000000p-12f, -0x1.3903a60000000p-14f, 0.0f,
+    0x1.ffa8180000000p-1f, 0x1.5f85ac0000000p-10f, -0x1.5f49280000000p-10f, 0x1.d3b8e20000000p-11f, -0x1.d1c5e00000000p-12f, 0x1.6a7fda0000000p-13f, -0x1.7ff0380000000p-15f, 0.0f,
+    0x1.ffcaac0000000p-1f, 0x1.aa87ce0000000p-11f, -0x1.aa5b2e0000000p-11f, 0x1.1bfcc80000000p-11f, -0x1.1b192c0000000p-12f, 0x1.b97e0e0000000p-14f, -0x1.d4dade0000000p-16f, 0.0f,
+    0x1.ffdfa80000000p-1f, 0x1.02bec80000000p-11f, -0x1.02ae500000000p-11f, 0x1.58b6fa0000000p-12f, -0x1.57da400000000p-13f, 0x1.0c6dd40000000p-14f, -0x1.1d895e0000000p-16f, 0.0f,
+    0x1.ffec620000000p-1f, 0x1.39e7820000000p-12f, -0x1.39db540000000p-12f, 0x1.a2528c0000000p-13f, -0x1.a16f780000000p-14f, 0x1.4618b60000000p-15f, -0x1.5b362e0000000p-17f, 0.0f,
+    0x1.fff41a0000000p-1f, 0x1.7ccec00000000p-13f, -0x1.7cc5b80000000p-13f, 0x1.fb91fe0000000p-14f, -0x1.fa9c820000000p-15f, 0x1.8bed2e0000000p-16f, -0x1.a5d0140000000p-18f, 0.0f,
+    0x1.fff8c80000000p-1f, 0x1.cdf5a20000000p-14f, -0x1.cdeee60000000p-14f, 0x1.33e69c0000000p-14f, -0x1.335c760000000p-15f, 0x1.e085f60000000p-17f, -0x1.0004dc0000000p-18f, 0.0f,
+    0x1.fffba00000000p-1f, 0x1.1832dc0000000p-14f, -0x1.1830540000000p-14f, 0x1.7588f40000000p-15f, -0x1.74e9940000000p-16f, 0x1.238cdc0000000p-17f, -0x1.36c0a20000000p-19f, 0.0f,
+    0x1.fffd580000000p-1f, 0x1.53e7140000000p-15f, -0x1.53e5260000000p-15f, 0x1.c524fe0000000p-16f, -0x1.c469360000000p-17f, 0x1.61b9aa0000000p-18f, -0x1.7903ba0000000p-20f, 0.0f,
+    0x1.fffe640000000p-1f, 0x1.9c53760000000p-16f, -0x1.9c51f80000000p-16f, 0x1.12dadc0000000p-16f, -0x1.126bbe0000000p-17f, 0x1.ad2ec00000000p-19f, -0x1.c9aebc0000000p-21f, 0.0f,
+    0x1.ffff060000000p-1f, 0x1.f42dde0000000p-17f, -0x1.f42cae0000000p-17f, 0x1.4d6c300000000p-17f, -0x1.4ce84a0000000p-18f, 0x1.045fc00000000p-19f, -0x1.15e2d80000000p-21f, 0.0f,
+    0x1.ffff680000000p-1f, 0x1.2f5ffa0000000p-17f, -0x1.2f5f7a0000000p-17f, 0x1.9477420000000p-18f, -0x1.93d3dc0000000p-19f, 0x1.3bb4400000000p-20f, -0x1.5024c80000000p-22f, 0.0f,
+    0x1.ffffa40000000p-1f, 0x1.7003540000000p-18f, -0x1.7002e60000000p-18f, 0x1.eaa5a20000000p-19f, -0x1.e9e7700000000p-20f, 0x1.7f371a0000000p-21f, -0x1.992cde0000000p-23f, 0.0f,
+    0x1.ffffc80000000p-1f, 0x1.be6c3e0000000p-19f, -0x1.be6bd20000000p-19f, 0x1.29977a0000000p-19f, -0x1.291c300000000p-20f, 0x1.d0577a0000000p-22f, -0x1.ed543e0000000p-24f, 0.0f,
+    0x1.ffffde0000000p-1f, 0x1.0ec4f20000000p-19f, -0x1.0ec4ba0000000p-19f, 0x1.68ff460000000p-20f, -0x1.6866240000000p-21f, 0x1.19808a0000000p-22f, -0x1.2a59200000000p-24f, 0.0f,
+    0x1.ffffec0000000p-1f, 0x1.4875bc0000000p-20f, -0x1.4875940000000p-20f, 0x1.b5ec720000000p-21f, -0x1.b561300000000p-22f, 0x1.56fa300000000p-23f, -0x1.7293ba0000000p-25f, 0.0f,
+    0x1.fffff40000000p-1f, 0x1.8e712e0000000p-21f, -0x1.8e710c0000000p-21f, 0x1.099da80000000p-21f, -0x1.094dba0000000p-22f, 0x1.a04dc60000000p-24f, -0x1.c2dc0c0000000p-26f, 0.0f,
+    0x1.fffff80000000p-1f, 0x1.e355b40000000p-22f, -0x1.e355980000000p-22f, 0x1.4236320000000p-22f, -0x1.41e41c0000000p-23f, 0x1.fa028c0000000p-25f, -0x1.14787e0000000p-26f, 0.0f,
+    0x1.fffffc0000000p-1f, 0x1.25284c0000000p-22f, -0x1.25284e0000000p-22f, 0x1.86dff60000000p-23f, -0x1.86b3020000000p-24f, 0x1.34c63a0000000p-25f, -0x1.5aa20a0000000p-27f, 0.0f,
+    0x1.fffffe0000000p-1f, 0x1.639e300000000p-23f, -0x1.639e640000000p-23f, 0x1.da2e6a0000000p-24f, -0x1.da604a0000000p-25f, 0x1.79e8e40000000p-26f, -0x1.b7d2120000000p-28f, 0.0f,
+    0x1.fffffe0000000p-1f, 0x1.af62e60000000p-24f, -0x1.af62c60000000p-24f, 0x1.1f95fc0000000p-24f, -0x1.1f781e0000000p-25f, 0x1.c729ba0000000p-27f, -0x1.0279980000000p-28f, 0.0f,
+};
+
+float orc_tanh_tab(float x) {
   const float ax = fabsf(x);
-  const float axc = ax < 9.0f ? ax : 9.0f;
-  const float y = -2.0f * axc;
-  const float n = rintf(y * 1.44269502f);
-  float r = fmaf(n, -0.693145751953125f, y);
-  r = fmaf(n, -1.42860677e-06f, r);
-  float q = 2.48015873e-05f;
-  q = fmaf(q, r, 1.98412698e-04f);
-  q = fmaf(q, r, 1.38888889e-03f);
-  q = fmaf(q, r, 8.33333333e-03f);
-  q = fmaf(q, r, 4.16666667e-02f);
-  q = fmaf(q, r, 1.66666667e-01f);
-  q = fmaf(q, r, 0.5f);
-  const float p = fmaf(r * r, q, r);
-  uint32_t sb = (uint32_t)((int)n + 127) << 23;
-  float s;
-  memcpy(&s, &sb, 4);
-  /* |x| < 0.45: -expm1 / (2 + expm1) (no cancellation near 0); else with E = e^-2|x|
-   * < 0.41: (1 - E) / (1 + E) (no amplification of E's error near 1) */
-  const int lo = ax < 0.45f;
-  const float em1 = fmaf(s, p, s - 1.0f);
-  const float e = fmaf(s, p, s);
-  float t = (lo ? -em1 : 1.0f - e) / (lo ? 2.0f + em1 : 1.0f + e);
-  t = ax < 9.0f ? t : 1.0f;
-  t = ax < 2.44140625e-04f ? ax : t;
-  t = x != x ? x : t;
-  return copysignf(t, x);
+  int k = ax < 9.0f ? (int)(ax * 4.0f) : 35;  /* NaN / inf / >= 9: any segment, overridden */
+  if (k > 35) k = 35;
+  const float* c = orc_tanh_coef + 8 * k;
+  const float t = fmaf((float)k, -0.25f, ax);
+  float y = fmaf(c[6], t, c[5]);
+  y = fmaf(y, t, c[4]);
+  y = fmaf(y, t, c[3]);
+  y = fmaf(y, t, c[2]);
+  y = fmaf(y, t, c[1]);
+  y = fmaf(y, t, c[0]);
+  y = ax < 9.0f ? y : 1.0f;
+  y = x != x ? x : y;
+  return copysignf(y, x);
 }
 
 static inline int pol_row(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
@@ -612,7 +639,7 @@ static void mlp_f32_one(int O, int H, int R, const float* x, const float* w1, co
         const float w = (u < H && k < O) ? w1[u * O + k] : 0.0f;
         acc = fmaf(w, k < O ? x[k] : 0.0f, acc);
       }
-    a1[u] = orc_tanh_ieee(acc);
+    a1[u] = orc_tanh_tab(acc);
   }
   for (int u = 0; u < 128; ++u) {
     float acc = u < H ? b2[u] : 0.0f;
@@ -622,7 +649,7 @@ static void mlp_f32_one(int O, int H, int R, const float* x, const float* w1, co
           const int k = 32 * ti + pol_row(g, h);
           acc = fmaf((u < H && k < H) ? w2[u * H + k] : 0.0f, a1[k], acc);
         }
-    a2[u] = orc_tanh_ieee(acc);
+    a2[u] = orc_tanh_tab(acc);
   }
   for (int r = 0; r < R; ++r) {
     float part[2];
@@ -651,6 +678,6 @@ void orc_mlp_f32(int64_t n, int O, int A, int H, const float* x, const float* pi
   }
 }
 
-void orc_tanh_ieee_v(int64_t n, const float* x, float* out) {
-  for (int64_t i = 0; i < n; ++i) out[i] = orc_tanh_ieee(x[i]);
+void orc_tanh_tab_v(int64_t n, const float* x, float* out) {
+  for (int64_t i = 0; i < n; ++i) out[i] = orc_tanh_tab(x[i]);
 }
