@@ -232,8 +232,8 @@ def kernel_name(system, mode, n, f64=False, no_done=False):
 
 def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
     """--mode vecnorm: one SB3 VecNormalize(norm_obs, norm_reward, clip_obs=10) step per
-    step (code/lorenz_pmsm/train.py:170), fused: lz_step_vecnorm (step + float64 moments
-    + fixed-order reduction) and lz_vecnorm_apply (RunningMeanStd updates + normalised
+    step (code/lorenz_pmsm/train.py:170), fused: lz_step_vecnorm (step + float64 moment
+    partials) and lz_vecnorm_apply (fixed-order reduction, RunningMeanStd updates + normalised
     obs / reward / terminal rows, bool dones); actions / outputs in a 16-slot ring, a
     hipGraph of 64 steps.  Per-rank statistics (the all-reduce of the multi-GPU path,
     LZ_VN_DEFER, is not captured here)."""
@@ -313,7 +313,7 @@ def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
                 "pre-generated on device" % (arange, arange),
         "config": {
             "workload": "VecNormalize(norm_obs, norm_reward, clip_obs=10) over %s, fused step "
-                        "(lz_step_vecnorm + lz_vecnorm_apply: 3 kernels, no host sync), %d envs"
+                        "(lz_step_vecnorm + lz_vecnorm_apply: 2 kernels, no host sync), %d envs"
                         % (SYSTEM_INFO[args.system][0], n),
             "system": args.system, "envs_total": total, "envs_per_gpu": n, "mode": "vecnorm",
             "parallelism": "env shard x%d (per-rank statistics)" % world,
@@ -321,7 +321,7 @@ def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": "k_step_vn + k_vn_colsum + k_vn_apply (one fused VecNormalize step)",
+            "kernel": "k_step_vn + k_vn_apply (one fused VecNormalize step)",
             "avg_launch_us": step_s * 1e6, "bytes_per_env_step": bytes_step,
             "note": "achieved = algorithmic bytes of the whole fused step (lz_step's + 16 B of "
                     "float64 returns + the normalise pass: raw obs/reward/done read, normalised "

@@ -96,6 +96,8 @@ struct lz_handle {
   int64_t pol_part_n;  // doubles allocated
   uint8_t* vn_ws;      // lz_step_vecnorm moment partials (lazily allocated)
   int vn_pending;      // lz_step_vecnorm left totals for lz_vecnorm_apply's updates
+  int32_t* vn_nd_out;  // lz_step_vecnorm's n_done_out, published by lz_vecnorm_apply
+  int32_t* vn_counter; // ... from this done cursor (the step's)
   uint8_t* hs_pin;     // lz_step_host: mapped host staging (actions | noise || obs | rew | done)
   uint8_t* hs_dev;     // lz_step_host: its device address
   size_t hs_in, hs_out;  // bytes of the input / output parts
@@ -495,10 +497,11 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
     return fail(LZ_ERR_INVALID, "actions/obs/rew/done/done_idx/terminal_obs/n_done must be non-NULL");
   HIP_TRY(hipSetDevice(h->cfg.device));
   const int64_t n = h->cfg.num_envs;
-  const int64_t n_wg = (n + lz::kBlock - 1) / lz::kBlock;
+  const int64_t n_wg = (n + lz::vn_block() - 1) / lz::vn_block();
   if (!h->vn_ws) {  // column-major per-workgroup partials, W = 2 (kVnMaxObs + 1) at most,
-                    // then the W column totals and the statistics snapshot
-    const size_t bytes = (size_t)(n_wg + 2) * 2 * (lz::kVnMaxObs + 1) * sizeof(double);
+                    // then the statistics snapshot (sized for the smallest workgroups)
+    const int64_t max_wg = (n + lz::kBlock - 1) / lz::kBlock;
+    const size_t bytes = (size_t)(max_wg + 2) * 2 * (lz::kVnMaxObs + 1) * sizeof(double);
     if (hipMalloc(reinterpret_cast<void**>(&h->vn_ws), bytes) != hipSuccess)
       return fail(LZ_ERR_OOM, "vecnorm workspace (%zu B)", bytes);
   }
@@ -515,8 +518,7 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
   std::memset(&v, 0, sizeof v);
   v.returns = vn->returns;
   v.part = reinterpret_cast<double*>(h->vn_ws);
-  v.tot = v.part + (size_t)n_wg * 2 * (lz::kVnMaxObs + 1);
-  v.old = v.tot + 2 * (lz::kVnMaxObs + 1);
+  v.old = v.part + (size_t)n_wg * 2 * (lz::kVnMaxObs + 1);
   v.n_done_out = n_done_out;
   v.obs_state = lz::rms_state(vn->obs_rms);
   v.ret_state = lz::rms_state(vn->ret_rms);
@@ -528,6 +530,9 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
   if (e != 0) return fail(LZ_ERR_HIP, "step launch: %s", hipGetErrorString((hipError_t)e));
   h->parity ^= 1;
   h->vn_pending = (vn->flags & LZ_VN_TRAINING) && !(vn->flags & LZ_VN_DEFER);
+  // without LZ_VN_DEFER the done count is published by the paired lz_vecnorm_apply
+  h->vn_nd_out = (vn->flags & LZ_VN_DEFER) ? nullptr : n_done_out;
+  h->vn_counter = a.counter;
   return LZ_OK;
 }
 
@@ -557,20 +562,23 @@ lz_status lz_vecnorm_apply(lz_handle* h, const lz_vecnorm* vn, const void* obs_r
   // deferred) are applied by this normalise pass
   lz::VnUpdate upd{};
   if (h->vn_pending && (vn->flags & LZ_VN_TRAINING) && !(vn->flags & LZ_VN_DEFER)) {
-    const int64_t n_wg = (h->cfg.num_envs + lz::kBlock - 1) / lz::kBlock;
-    const double* tot = reinterpret_cast<const double*>(h->vn_ws) + (size_t)n_wg * 2 * (lz::kVnMaxObs + 1);
-    upd.tot = tot;
-    upd.old = tot + 2 * (lz::kVnMaxObs + 1);
+    const int64_t n_wg = (h->cfg.num_envs + lz::vn_block() - 1) / lz::vn_block();
+    upd.part = reinterpret_cast<const double*>(h->vn_ws);
+    upd.n_wg = (int)n_wg;
+    upd.old = upd.part + (size_t)n_wg * 2 * (lz::kVnMaxObs + 1);
     upd.batch = (double)h->cfg.num_envs;
     upd.upd_obs = (vn->flags & LZ_VN_NORM_OBS) != 0;
   }
   h->vn_pending = 0;
+  int32_t* nd_out = h->vn_nd_out;
+  const int32_t* counter = nd_out ? h->vn_counter : nullptr;
+  h->vn_nd_out = nullptr;
   const int e = lz::launch_vn_apply(
       h->f64, O, h->cfg.num_envs, obs_raw, rew_raw, done, term ? terminal_obs_raw : nullptr,
       term ? n_done : nullptr, lz::rms_state(vn->obs_rms), lz::rms_state(vn->ret_rms),
       (vn->flags & LZ_VN_NORM_OBS) != 0, (vn->flags & LZ_VN_NORM_REWARD) != 0, vn->epsilon,
       vn->clip_obs, vn->clip_reward, obs_norm, rew_norm, dones_out, term ? term_norm : nullptr,
-      upd, h->stream);
+      upd, counter, nd_out, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "normalise launch: %s", hipGetErrorString((hipError_t)e));
   return LZ_OK;
 }

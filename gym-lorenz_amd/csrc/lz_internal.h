@@ -52,14 +52,18 @@ struct KArgs {
 // VecNormalize epilogue of the step kernel (lz_step_vecnorm).  Per-workgroup float64
 // partials of the batch moments, column-major [W][n_wg] with W = 2 (O + 1) columns:
 // sums of obs column 0..O-1, of the returns, then the sums of squares likewise;
-// k_vn_colsum (the next launch) reduces them; the normalise pass of lz_vecnorm_apply
-// applies the statistics updates.
+// every workgroup of the normalise pass of lz_vecnorm_apply reduces them (the same
+// fixed order, lz_rms_math.h vn_col_totals) and applies the statistics updates; with
+// LZ_VN_DEFER k_vn_colsum (the step's only other launch) reduces them into the moments.
+// kVnBlock envs per step workgroup: 1024, so that a 262,144-env step leaves 256
+// partials per column for every normalise workgroup to read.
 constexpr int kVnMaxObs = 8;
+constexpr int kVnBlock = 1024;
+int vn_block();  // the step workgroup size in use (kVnBlock; LZ_VN_BLOCK=256 for A/B)
 struct VArgs {
   double* returns;     // [N] VecNormalize.returns
   double* part;        // [W][n_wg]
-  double* tot;         // [W] column totals (k_vn_colsum -> the normalise pass)
-  double* old;         // [2O+1 obs][3 returns] statistics snapshot taken by k_vn_colsum
+  double* old;         // [2O+1 obs][3 returns] statistics snapshot (step block 0)
   double* obs_state;   // obs_rms mean[O], var[O], count
   double* ret_state;   // ret_rms mean, var, count
   double* moments;     // LZ_VN_DEFER: [2O+1 obs][3 returns] batch moments out
@@ -197,10 +201,11 @@ double* rms_state(lz_rms* r);  // mean[dim], var[dim], count
 // RunningMeanStd.update_from_moments on `stream` (moments: count, sums, sums of squares)
 int launch_rms_update(lz_rms* r, const double* moments, void* stream);
 // The RunningMeanStd updates folded into the normalise pass (training, not deferred):
-// every workgroup derives the new statistics from the snapshot + column totals the
-// step's k_vn_colsum left, workgroup 0 writes them back.
+// every workgroup reduces the step's moment partials and derives the new statistics
+// from them and the snapshot the step's block 0 took; workgroup 0 writes them back.
 struct VnUpdate {
-  const double* tot;   // [2 (O + 1)] column totals (nullptr: no update in this pass)
+  const double* part;  // [2 (O + 1)][n_wg] partials (nullptr: no update in this pass)
+  int n_wg;
   const double* old;   // [2O+1 obs][3 returns] snapshot of the statistics
   double batch;        // batch count n
   int upd_obs;         // obs_rms.update (TRAINING and NORM_OBS)
@@ -211,7 +216,8 @@ int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
                     const uint8_t* done, const void* term, const int32_t* n_done,
                     double* obs_state, double* ret_state, int norm_obs, int norm_rew,
                     double eps, double clip_obs, double clip_rew, float* obs_n, float* rew_n,
-                    uint8_t* dones, float* term_n, const VnUpdate& upd, void* stream);
+                    uint8_t* dones, float* term_n, const VnUpdate& upd, const int32_t* counter,
+                    int32_t* n_done_out, void* stream);
 
 // record the thread-local message lz_last_error() returns; returns s
 lz_status set_error(lz_status s, const char* msg);

@@ -14,6 +14,7 @@
 // See lz_systems.h for the per-system arithmetic and its reference citations.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "lz_body.h"
@@ -114,90 +115,92 @@ constexpr int step_block() {  // bits 3-4 of V: workgroup size
 
 // ------------------------------------------------------------------ VecNormalize epilogue
 // (lz_step_vecnorm, lz_internal.h VArgs).  Per-workgroup float64 moments of the obs
-// columns (read back from the LDS obs tile) and of the updated returns: each column
-// summed by 32 lanes over strided rows, then a fixed xor tree; one plain store per
-// column into the column-major partials.  k_vn_colsum, the next launch on the stream,
-// sums them in a fixed order (no cross-workgroup synchronisation inside the step: an
-// in-kernel last-arriver reduction needs every workgroup to wait for its stores'
-// acknowledgements before taking a ticket, which measured 4x the step time at 1M envs).
-template <int O, typename T>
+// columns (read back from the LDS obs tile as the float32 values SB3 sees) and of the
+// updated returns: Q groups of 32 lanes per column (Q = 1 for 256-env, 4 for 1024-env
+// workgroups), lane j of group q summing rows j + 32 k of the q-th row quarter in order,
+// then the lane sums in a fixed order; one plain store per column into the column-major
+// partials.  Every normalise workgroup of lz_vecnorm_apply reduces them in one fixed
+// order (no cross-workgroup synchronisation inside the step: an in-kernel last-arriver
+// reduction needs every workgroup to wait for its stores' acknowledgements before
+// taking a ticket, which measured 4x the step time at 1M envs).
+template <int O, int SB, typename T>
 __device__ __forceinline__ void vn_epilogue(const T* s_obs, const double* s_ret, int nb, int tid,
                                             const VArgs& v) {
   constexpr int C = O + 1;
-  __shared__ double red[2 * C][33];  // [column sums | sums of squares][lane], padded
+  constexpr int G = SB / 32;                   // 32-lane groups
+  constexpr int CP = C <= 8 ? 8 : 16;          // column slots
+  constexpr int Q = G / CP >= 1 ? G / CP : 1;  // groups per column
+  constexpr int KR = SB / 32 / Q;              // rows per lane
+  __shared__ double red[2 * C][Q * 32 + 1];    // [column sums | sums of squares][lane]
   const int j = tid & 31;
-  for (int c = tid >> 5; c < C; c += kBlock / 32) {
-    double s = 0.0, q = 0.0;
+  for (int it = tid >> 5; it < C * Q; it += G) {
+    const int c = it / Q, q = it % Q;
+    double s = 0.0, sq = 0.0;
 #pragma unroll
-    for (int k = 0; k < kBlock / 32; ++k) {  // rows j, j+32, ..., in order
-      const int r = j + 32 * k;
+    for (int k = 0; k < KR; ++k) {  // rows j + 32 (q KR + k), in order
+      const int r = j + 32 * (q * KR + k);
       if (r < nb) {
         const double x = c < O ? (double)(float)s_obs[r * O + c] : s_ret[r];
         s += x;
-        q += x * x;
+        sq += x * x;
       }
     }
-    red[c][j] = s;
-    red[C + c][j] = q;
+    red[c][q * 32 + j] = s;
+    red[C + c][q * 32 + j] = sq;
   }
   __syncthreads();
-  if (tid < 2 * C) {
-    double t = 0.0;
+  if constexpr (Q == 1) {
+    if (tid < 2 * C) {
+      double t = 0.0;
 #pragma unroll
-    for (int k = 0; k < 32; ++k) t += red[tid][k];
-    v.part[(int64_t)tid * v.n_wg + blockIdx.x] = t;
+      for (int k = 0; k < 32; ++k) t += red[tid][k];
+      v.part[(int64_t)tid * v.n_wg + blockIdx.x] = t;
+    }
+  } else {
+    __shared__ double red2[2 * C][Q];
+    if (tid < 2 * C * Q) {
+      const int c = tid / Q, q = tid % Q;
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) t += red[c][q * 32 + k];
+      red2[c][q] = t;
+    }
+    __syncthreads();
+    if (tid < 2 * C) {
+      double t = red2[tid][0];
+#pragma unroll
+      for (int q = 1; q < Q; ++q) t += red2[tid][q];
+      v.part[(int64_t)tid * v.n_wg + blockIdx.x] = t;
+    }
   }
 }
 
-// The batch moments from the n_wg per-workgroup partials: one workgroup per partial
-// column (2 (O + 1) of them) sums it in a fixed order -- lane t adds rows t, t + 1024,
-// ... into accumulator u of rows t + 256 u (mod 1024), the 4 accumulators in order,
-// then a fixed LDS tree -- and stores the column total.  (A single workgroup for all
-// columns measured 11.5 us per 1M-env step; a column per workgroup spreads the 458 KB
-// of partials over 14 CUs.)  With LZ_VN_DEFER each total goes to its slot of the
-// moments vector for the caller's all-reduce; otherwise workgroup 0 snapshots the
-// statistics, and lz_vecnorm_apply's normalise pass applies the RunningMeanStd updates
-// (no separate update launch).  Block 0 also publishes the step's done count.
+// LZ_VN_DEFER: the step's second launch.  Block 0 publishes the step's done count and,
+// in training, reduces the partial columns (vn_col_totals, the order the normalise pass
+// uses) into the moments vector for the caller's all-reduce; lz_vecnorm_apply updates
+// the statistics from the moments.  (Without LZ_VN_DEFER there is no second launch: the
+// step kernel's block 0 snapshots the statistics and the normalise pass reduces the
+// partials and publishes the done count.)
 constexpr int kVnColBlock = 256;
 template <int O>
 __global__ __launch_bounds__(kVnColBlock) void k_vn_colsum(VArgs v, int64_t n,
                                                           const int32_t* counter,
                                                           int32_t* n_done_out) {
   constexpr int C = O + 1;
-  __shared__ double red[kVnColBlock];
-  const int tid = (int)threadIdx.x, c = (int)blockIdx.x;
-  if (c == 0 && tid == 0) *n_done_out = *counter;
+  const int tid = (int)threadIdx.x;
+  if (tid == 0) *n_done_out = *counter;
   if (!(v.flags & LZ_VN_TRAINING)) return;
-  const bool defer = (v.flags & LZ_VN_DEFER) != 0;
-  if (c == 0 && !defer) {  // statistics as they were before this step
-    if (tid < 2 * O + 1) v.old[tid] = v.obs_state[tid];
-    if (tid < 3) v.old[2 * O + 1 + tid] = v.ret_state[tid];
-  }
-  const double* col = v.part + (int64_t)c * v.n_wg;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int r = tid; r < v.n_wg; r += 4 * kVnColBlock) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int ru = r + u * kVnColBlock;
-      if (ru < v.n_wg) acc[u] += col[ru];
-    }
-  }
-  red[tid] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-  __syncthreads();
-#pragma unroll
-  for (int half = kVnColBlock / 2; half > 0; half >>= 1) {  // fixed pairing tree
-    if (tid < half) red[tid] += red[tid + half];
-    __syncthreads();
-  }
-  if (tid != 0) return;
-  v.tot[c] = red[0];
-  if (defer) {  // (count, sums[O], sumsq[O]) for obs, then (count, sum, sumsq) for returns
-    const int slot = c < O ? 1 + c : c == O ? 2 * O + 2 : c < C + O ? 1 + O + (c - C) : 2 * O + 3;
-    v.moments[slot] = red[0];
-    if (c == 0) {
-      v.moments[0] = (double)n;
-      v.moments[2 * O + 1] = (double)n;
-    }
+  __shared__ double red[LZ_VN_RED(2 * C)];
+  __shared__ double tot[2 * C];
+  vn_col_totals<2 * C>(v.part, v.n_wg, red, tot);
+  if (tid >= 2 * C) return;
+  // (count, sums[O], sumsq[O]) for obs, then (count, sum, sumsq) for returns
+  const int slot =
+      tid < O ? 1 + tid : tid == O ? 2 * O + 2 : tid < C + O ? 1 + O + (tid - C) : 2 * O + 3;
+  v.moments[slot] = tot[tid];
+  if (tid == 0) {
+    v.moments[0] = (double)n;
+    v.moments[2 * O + 1] = (double)n;
   }
 }
 
@@ -220,6 +223,12 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
   if (blockIdx.x == 0 && tid == 0) {
     *a.counter_next = 0;
     *a.tick_out = tick + a.tick_adv;
+  }
+  if constexpr (kVN) {  // the statistics before this step, for the normalise pass
+    if (blockIdx.x == 0 && (v.flags & LZ_VN_TRAINING) && !(v.flags & LZ_VN_DEFER)) {
+      if (tid < 2 * Sys::O + 1) v.old[tid] = v.obs_state[tid];
+      if (tid < 3) v.old[2 * Sys::O + 1 + tid] = v.ret_state[tid];
+    }
   }
   Sys sys;
   sys.setup(a);
@@ -248,12 +257,11 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
   T o[Sys::O];
   T rew = (T)0;
   bool did_reset;
-  double* s_ret_p = nullptr;
+  double rn = 0.0;  // kVN: the updated VecNormalize.returns[i] (before the done reset)
   const uint8_t dflag =
       step_body<Sys, T, false>(sys, steps, a, i, live, act, tick, 0, o, rew, did_reset);
+  __shared__ double s_ret[kVN ? SB : 1];
   if constexpr (kVN) {  // VecNormalize.returns: r*gamma + reward, moments, then [done] = 0
-    __shared__ double s_ret[SB];
-    double rn = 0.0;
     if (live) {
       double r0 = ret_in;
       if (v.flags & LZ_VN_TRAINING) r0 = r0 * v.gamma + (double)(float)rew;
@@ -261,7 +269,6 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
       v.returns[i] = dflag ? 0.0 : r0;
     }
     s_ret[tid] = rn;
-    s_ret_p = s_ret;
   }
   if (live) {
     sys.store(a, i);
@@ -282,8 +289,8 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
     stage_out<NT, T, Sys::O, SB>(static_cast<T*>(a.obs) + base * Sys::O, s_obs, nb, tid, vec);
   }
   if constexpr (kVN) {
-    static_assert(kLds && SB == kBlock, "the VecNormalize epilogue reads the LDS obs tile");
-    if (v.flags & LZ_VN_TRAINING) vn_epilogue<Sys::O, T>(s_obs, s_ret_p, nb, tid, v);
+    static_assert(kLds, "the VecNormalize epilogue reads the LDS obs tile");
+    if (v.flags & LZ_VN_TRAINING) vn_epilogue<Sys::O, SB, T>(s_obs, s_ret, nb, tid, v);
   }
 }
 
@@ -305,9 +312,10 @@ __attribute__((amdgpu_waves_per_eu(step_waves<Sys>::value))) void k_step(KArgs a
   step_tile<Sys, T, V, false>(a, VArgs{});
 }
 
-template <class Sys, typename T>
-__global__ __launch_bounds__(kBlock) void k_step_vn(KArgs a, VArgs v) {
-  step_tile<Sys, T, 0, true>(a, v);
+// VB: the step variant carrying the workgroup size (0: 256, 24: 1024 envs)
+template <class Sys, typename T, int VB>
+__global__ __launch_bounds__(step_block<VB>()) void k_step_vn(KArgs a, VArgs v) {
+  step_tile<Sys, T, VB, true>(a, v);
 }
 
 
@@ -858,12 +866,27 @@ static int dispatch(int which, int system, int f64, const KArgs& a, void* stream
   return (int)hipErrorInvalidValue;
 }
 
+// lz_step_vecnorm's envs per workgroup: kVnBlock, or LZ_VN_BLOCK=256 (A/B knob)
+int vn_block() {
+  static const int b = [] {
+    const char* e = std::getenv("LZ_VN_BLOCK");
+    return e && std::atoi(e) == 256 ? 256 : kVnBlock;
+  }();
+  return b;
+}
+
 template <class Sys, typename T>
 static int launch_vn(const KArgs& a, const VArgs& v, hipStream_t s) {
   static_assert(Sys::O <= kVnMaxObs, "obs too wide for the VecNormalize epilogue");
-  hipLaunchKernelGGL((k_step_vn<Sys, T>), dim3((unsigned)grid_for(a.n)), dim3(kBlock), 0, s, a, v);
-  hipLaunchKernelGGL((k_vn_colsum<Sys::O>), dim3(2 * (Sys::O + 1)), dim3(kVnColBlock), 0, s, v,
-                     a.n, a.counter, v.n_done_out);
+  const int vb = vn_block();
+  const unsigned grid = (unsigned)((a.n + vb - 1) / vb);
+  if (vb == 1024)
+    hipLaunchKernelGGL((k_step_vn<Sys, T, 24>), dim3(grid), dim3(1024), 0, s, a, v);
+  else
+    hipLaunchKernelGGL((k_step_vn<Sys, T, 0>), dim3(grid), dim3(256), 0, s, a, v);
+  if (v.flags & LZ_VN_DEFER)
+    hipLaunchKernelGGL((k_vn_colsum<Sys::O>), dim3(1), dim3(kVnColBlock), 0, s, v, a.n, a.counter,
+                       v.n_done_out);
   return (int)hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -140,13 +141,16 @@ __global__ void k_returns(double* ret, const void* rew, const uint8_t* done, int
   else if (done[i]) ret[i] = 0.0;
 }
 
-// lz_vecnorm_apply: the normalised outputs of one VecNormalize.step_wait.  Threads of
-// the first row_blocks workgroups own R consecutive env rows each (R * O a multiple of
-// 4, so the obs columns of each element are compile-time constants and the rows move
-// as 16-B vectors when aligned): obs rows, rewards and the done flags as 0/1 bytes
-// (SB3's bool dones); the remaining workgroups grid-stride over the n_done terminal
-// rows.  Inputs are rounded to float32 first: SB3's VecNormalize sees DummyVecEnv's
-// float32 buffers.
+// lz_vecnorm_apply: the normalised outputs of one VecNormalize.step_wait.  The first
+// row_blocks workgroups grid-stride over the row tiles (256 threads owning R
+// consecutive env rows each, R * O a multiple of 4, so the obs columns of each element
+// are compile-time constants and the rows move as 16-B vectors when aligned): obs rows,
+// rewards and the done flags as 0/1 bytes (SB3's bool dones); the remaining workgroups
+// grid-stride over the n_done terminal rows.  Inputs are rounded to float32 first:
+// SB3's VecNormalize sees DummyVecEnv's float32 buffers.  In training every workgroup
+// first reduces the step's moment partials (vn_col_totals: one fixed order, the same
+// bits in every workgroup and in the LZ_VN_DEFER reduction) -- the first tile's loads
+// are issued before that, so the reduction runs while they are in flight.
 struct VnApplyArgs {
   int64_t n;
   const void* obs;
@@ -154,14 +158,17 @@ struct VnApplyArgs {
   const void* term;
   const uint8_t* done;
   const int32_t* n_done;
+  const int32_t* counter;  // the step's done cursor (nullptr: read n_done)
+  int32_t* n_done_out;     // published from *counter by block 0 (nullable)
   double* os;        // obs_rms mean[O], var[O], count
   double* rs;        // ret_rms mean, var, count
-  lz::VnUpdate upd;  // statistics updates folded into this pass (upd.tot != nullptr)
+  lz::VnUpdate upd;  // statistics updates folded into this pass (upd.part != nullptr)
   double eps, clip_obs, clip_rew;
   float* obs_n;
   float* rew_n;
   float* term_n;
   uint8_t* dones;
+  int64_t row_tiles;
   int norm_obs, norm_rew, vec, row_blocks;
 };
 
@@ -171,19 +178,48 @@ template <typename T, int O>
 __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
   constexpr int R = (O % 4 == 0) ? 1 : (O % 2 == 0 ? 2 : 4);
   constexpr int E = R * O;
+  constexpr int W = 2 * (O + 1);
+  constexpr bool kF32 = std::is_same<T, float>::value;
+  const int t = (int)threadIdx.x;
+  const bool rows = (int)blockIdx.x < p.row_blocks;
+  const T* obs = static_cast<const T*>(p.obs);
+  const T* rew = static_cast<const T*>(p.rew);
+  auto tile_full = [&](int64_t tl) { return (tl + 1) * 256 * R <= p.n; };  // uniform
+  // the first tile's raw obs (16-B vectors, read once: non-temporal), rewards, dones
+  f4a q[E / 4];
+  float rw[R];
+  uint8_t dn[R];
+  auto load_tile = [&](int64_t tl) {
+    const f4a* src = reinterpret_cast<const f4a*>(obs + tl * 256 * E);
+#pragma unroll
+    for (int k = 0; k < E / 4; ++k) q[k] = __builtin_nontemporal_load(src + t + 256 * k);
+    const int64_t r0 = (tl * 256 + t) * R;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      rw[k] = (float)rew[r0 + k];
+      dn[k] = p.dones ? p.done[r0 + k] : 0;
+    }
+  };
+  if (p.n_done_out && blockIdx.x == 0 && t == 0) *p.n_done_out = *p.counter;
+  int64_t tile = blockIdx.x;
+  const bool pre = kF32 && rows && p.vec && tile < p.row_tiles && tile_full(tile);
+  if (pre) load_tile(tile);
+
   double mean[O], sd[O], rsd;
-  if (p.upd.tot) {
+  if (p.upd.part) {
     // RunningMeanStd.update_from_moments for every obs column (lanes 0..O-1) and the
-    // returns (lane 64), from the pre-step snapshot -- so no workgroup reads statistics
-    // that workgroup 0 is rewriting -- then broadcast through LDS
+    // returns (lane 64), from the step's column totals and the pre-step snapshot, then
+    // broadcast through LDS
+    __shared__ double s_red[LZ_VN_RED(W)];
+    __shared__ double s_tot[W];
     __shared__ double s_st[2 * O + 1];
-    const int t = (int)threadIdx.x;
+    lz::vn_col_totals<W>(p.upd.part, p.upd.n_wg, s_red, s_tot);
     const double* old = p.upd.old;
     const double bc = p.upd.batch;
     if (t < O) {
       double nm = old[t], nv = old[O + t];
       if (p.upd.upd_obs)
-        lz::rms_new(old[t], old[O + t], old[2 * O], bc, p.upd.tot[t], p.upd.tot[O + 1 + t], nm, nv);
+        lz::rms_new(old[t], old[O + t], old[2 * O], bc, s_tot[t], s_tot[O + 1 + t], nm, nv);
       s_st[t] = nm;
       s_st[O + t] = sqrt(nv + p.eps);
       if (blockIdx.x == 0 && p.upd.upd_obs) {
@@ -195,7 +231,7 @@ __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
     if (t == 64) {
       const double* r = old + 2 * O + 1;
       double nm, nv;
-      lz::rms_new(r[0], r[1], r[2], bc, p.upd.tot[O], p.upd.tot[2 * O + 1], nm, nv);
+      lz::rms_new(r[0], r[1], r[2], bc, s_tot[O], s_tot[2 * O + 1], nm, nv);
       s_st[2 * O] = sqrt(nv + p.eps);
       if (blockIdx.x == 0) {
         p.rs[0] = nm;
@@ -218,64 +254,70 @@ __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
     }
     rsd = sqrt(p.rs[1] + p.eps);
   }
-  const T* obs = static_cast<const T*>(p.obs);
-  if ((int)blockIdx.x < p.row_blocks) {
-    const int64_t r0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * R;
-    if (r0 >= p.n) return;  // only in the last (partial, barrier-free) tile
-    const bool tile_full = ((int64_t)blockIdx.x + 1) * 256 * R <= p.n;  // uniform
-    float x[E], y[E];
-    if (std::is_same<T, float>::value && p.vec && tile_full) {
-      // the workgroup's [256 R, O] slice moves as contiguous float4s through LDS
-      __shared__ f4a tile[256 * E / 4];
-      const f4a* src = reinterpret_cast<const f4a*>(obs + (int64_t)blockIdx.x * 256 * E);
+  if (rows) {
+    __shared__ f4a lds[256 * E / 4];
+    for (; tile < p.row_tiles; tile += p.row_blocks) {
+      const int64_t r0 = (tile * 256 + t) * R;
+      float x[E], y[E];
+      if (kF32 && p.vec && tile_full(tile)) {
+        // the workgroup's [256 R, O] slice moves as contiguous float4s through LDS
+        if (tile != (int64_t)blockIdx.x || !pre) load_tile(tile);
+        __syncthreads();  // the previous tile's stores have read lds
 #pragma unroll
-      for (int k = 0; k < E / 4; ++k)  // raw obs: read once (non-temporal)
-        tile[threadIdx.x + 256 * k] = __builtin_nontemporal_load(src + threadIdx.x + 256 * k);
-      __syncthreads();
+        for (int k = 0; k < E / 4; ++k) lds[t + 256 * k] = q[k];
+        __syncthreads();
 #pragma unroll
-      for (int k = 0; k < E / 4; ++k) {
-        const f4a q = tile[threadIdx.x * (E / 4) + k];
-        x[4 * k] = q[0]; x[4 * k + 1] = q[1]; x[4 * k + 2] = q[2]; x[4 * k + 3] = q[3];
+        for (int k = 0; k < E / 4; ++k) {
+          const f4a v = lds[t * (E / 4) + k];
+          x[4 * k] = v[0]; x[4 * k + 1] = v[1]; x[4 * k + 2] = v[2]; x[4 * k + 3] = v[3];
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          y[e] = p.norm_obs ? lz::rms_norm_sd((double)x[e], mean[e % O], sd[e % O], true, p.clip_obs)
+                            : x[e];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < E / 4; ++k)
+          lds[t * (E / 4) + k] = (f4a){y[4 * k], y[4 * k + 1], y[4 * k + 2], y[4 * k + 3]};
+        __syncthreads();
+        f4a* dst = reinterpret_cast<f4a*>(p.obs_n + tile * 256 * E);
+#pragma unroll
+        for (int k = 0; k < E / 4; ++k)  // normalised obs: written once (non-temporal)
+          __builtin_nontemporal_store(lds[t + 256 * k], dst + t + 256 * k);
+      } else {  // the last, partial tile (or unaligned / float64 inputs): no barriers
+        if (r0 >= p.n) continue;
+#pragma unroll
+        for (int e = 0; e < E; ++e) x[e] = (r0 + e / O < p.n) ? (float)obs[r0 * O + e] : 0.0f;
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          y[e] = p.norm_obs ? lz::rms_norm_sd((double)x[e], mean[e % O], sd[e % O], true, p.clip_obs)
+                            : x[e];
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (r0 + e / O < p.n) p.obs_n[r0 * O + e] = y[e];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          if (r0 + k < p.n) {
+            rw[k] = (float)rew[r0 + k];
+            dn[k] = p.dones ? p.done[r0 + k] : 0;
+          }
+        }
       }
 #pragma unroll
-      for (int e = 0; e < E; ++e)
-        y[e] = p.norm_obs ? lz::rms_norm_sd((double)x[e], mean[e % O], sd[e % O], true, p.clip_obs)
-                          : x[e];
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < E / 4; ++k)
-        tile[threadIdx.x * (E / 4) + k] = (f4a){y[4 * k], y[4 * k + 1], y[4 * k + 2], y[4 * k + 3]};
-      __syncthreads();
-      f4a* dst = reinterpret_cast<f4a*>(p.obs_n + (int64_t)blockIdx.x * 256 * E);
-#pragma unroll
-      for (int k = 0; k < E / 4; ++k)  // normalised obs: written once (non-temporal)
-        __builtin_nontemporal_store(tile[threadIdx.x + 256 * k], dst + threadIdx.x + 256 * k);
-    } else {
-#pragma unroll
-      for (int e = 0; e < E; ++e) x[e] = (r0 + e / O < p.n) ? (float)obs[r0 * O + e] : 0.0f;
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-        y[e] = p.norm_obs ? lz::rms_norm_sd((double)x[e], mean[e % O], sd[e % O], true, p.clip_obs)
-                          : x[e];
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-        if (r0 + e / O < p.n) p.obs_n[r0 * O + e] = y[e];
-    }
-    const T* rew = static_cast<const T*>(p.rew);
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      if (r0 + k >= p.n) break;
-      const float r = (float)rew[r0 + k];
-      p.rew_n[r0 + k] = p.norm_rew ? lz::rms_norm_sd((double)r, 0.0, rsd, false, p.clip_rew) : r;
-      if (p.dones) p.dones[r0 + k] = p.done[r0 + k] != 0;
+      for (int k = 0; k < R; ++k) {
+        if (r0 + k >= p.n) break;
+        p.rew_n[r0 + k] =
+            p.norm_rew ? lz::rms_norm_sd((double)rw[k], 0.0, rsd, false, p.clip_rew) : rw[k];
+        if (p.dones) p.dones[r0 + k] = dn[k] != 0;
+      }
     }
     return;
   }
   if (p.term == nullptr) return;
   const T* term = static_cast<const T*>(p.term);
-  const int64_t m = *p.n_done;
+  const int64_t m = p.counter ? *p.counter : *p.n_done;
   const int64_t stride = (int64_t)(gridDim.x - p.row_blocks) * 256;
-  for (int64_t j = (int64_t)(blockIdx.x - p.row_blocks) * 256 + threadIdx.x; j < m; j += stride) {
+  for (int64_t j = (int64_t)(blockIdx.x - p.row_blocks) * 256 + t; j < m; j += stride) {
 #pragma unroll
     for (int d = 0; d < O; ++d) {
       const float x = (float)term[j * O + d];
@@ -314,11 +356,22 @@ int launch_rms_update(lz_rms* r, const double* moments, void* stream) {
   return (int)hipGetLastError();
 }
 
+// row workgroups of the normalise pass: 512 (two per CU), LZ_VN_APPLY_BLOCKS for A/B
+static int vn_apply_blocks() {
+  static const int b = [] {
+    const char* e = std::getenv("LZ_VN_APPLY_BLOCKS");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 512;
+  }();
+  return b;
+}
+
 int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
                     const uint8_t* done, const void* term, const int32_t* n_done,
                     double* obs_state, double* ret_state, int norm_obs, int norm_rew,
                     double eps, double clip_obs, double clip_rew, float* obs_n, float* rew_n,
-                    uint8_t* dones, float* term_n, const VnUpdate& upd, void* stream) {
+                    uint8_t* dones, float* term_n, const VnUpdate& upd, const int32_t* counter,
+                    int32_t* n_done_out, void* stream) {
   if (n == 0) return 0;
   const int R = (O % 4 == 0) ? 1 : (O % 2 == 0 ? 2 : 4);
   VnApplyArgs p;
@@ -328,6 +381,8 @@ int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
   p.term = term;
   p.done = done;
   p.n_done = n_done;
+  p.counter = counter;
+  p.n_done_out = n_done_out;
   p.os = obs_state;
   p.rs = ret_state;
   p.upd = upd;
@@ -341,7 +396,10 @@ int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
   p.norm_obs = norm_obs;
   p.norm_rew = norm_rew;
   p.vec = !f64 && ((uintptr_t)obs % 16 == 0) && ((uintptr_t)obs_n % 16 == 0);
-  p.row_blocks = (int)((n + 256 * R - 1) / (256 * R));
+  p.row_tiles = (n + 256 * R - 1) / (256 * R);
+  // at most vn_apply_blocks() row workgroups (each reduces the partials once)
+  const int64_t cap = vn_apply_blocks();
+  p.row_blocks = (int)(p.row_tiles < cap ? p.row_tiles : cap);
   const int tb = term ? (p.row_blocks < 64 ? p.row_blocks : 64) : 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)(p.row_blocks + tb)), block(256);

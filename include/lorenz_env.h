@@ -479,15 +479,16 @@ lz_status lz_returns_update(double* returns, const void* rew, int32_t dtype, con
  *   obs_out  = NORM_OBS    ? clip((obs - mean)/sqrt(var + eps), +-clip_obs)  : obs
  *   rew_out  = NORM_REWARD ? clip(reward/sqrt(ret_var + eps), +-clip_reward) : reward
  *   terminal observations normalised like obs; returns[done] = 0
- * lz_step_vecnorm runs the env step (its kernel also writes float64 per-workgroup
- * moment partials of the obs and of the updated returns) and a column-per-workgroup
- * reduction in a fixed order (deterministic, no float atomics) -- two launches;
- * lz_vecnorm_apply (one launch) applies the two RunningMeanStd updates (every
- * workgroup derives them from the step's totals; workgroup 0 writes them back) and
- * writes the normalised outputs: the statistics are updated once lz_vecnorm_apply has
- * run, so call the two as a pair.  With LZ_VN_DEFER the reduction leaves the batch moments (obs:
- * count, sums[O], sumsq[O]; then returns: count, sum, sumsq) in moments for a
- * multi-GPU all-reduce and lz_vecnorm_apply performs the updates first.  Every
+ * lz_step_vecnorm runs the env step (one launch: its kernel also writes float64
+ * per-workgroup moment partials of the obs and of the updated returns);
+ * lz_vecnorm_apply (one launch) reduces them in a fixed order (deterministic, no float
+ * atomics; every workgroup derives the same totals), applies the two RunningMeanStd
+ * updates (workgroup 0 writes them back) and writes the normalised outputs.  Call the
+ * two as a pair, apply right after step on the same stream: the statistics are updated,
+ * and the step's *n_done_out is written, by the lz_vecnorm_apply launch.  With
+ * LZ_VN_DEFER the step adds a second launch that publishes *n_done_out and leaves the
+ * batch moments (obs: count, sums[O], sumsq[O]; then returns: count, sum, sumsq) in
+ * moments for a multi-GPU all-reduce, and lz_vecnorm_apply performs the updates first.  Every
  * pointer is device memory; the statistics are those of the two lz_rms objects (dims
  * O and 1).
  * ------------------------------------------------------------------------------ */
@@ -513,7 +514,8 @@ typedef struct lz_vecnorm {
 
 /* lz_step's contract for the raw outputs (obs_out/rew_out/done/compact list) plus the
  * VecNormalize bookkeeping above.  n_done_out (device int32) is required: the compact
- * list is how lz_vecnorm_apply finds the terminal rows to normalise. */
+ * list is how lz_vecnorm_apply finds the terminal rows to normalise; it is written by
+ * the paired lz_vecnorm_apply launch (LZ_VN_DEFER: by this call's second launch). */
 lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* actions,
                           void* obs_out, void* rew_out, uint8_t* done_out, int32_t* done_idx_out,
                           void* terminal_obs_out, int32_t* n_done_out);
@@ -521,7 +523,8 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
  * dones_out are non-NULL, dones_out[i] = (done[i] != 0) (uint8 0/1, SB3's bool
  * dones); if terminal_obs_raw and term_norm are non-NULL, term_norm float32
  * [n_done, O] from terminal_obs_raw [n_done, O], n_done read on the device from
- * n_done (the lz_step_vecnorm output). */
+ * n_done (the lz_step_vecnorm output; right after lz_step_vecnorm the count comes
+ * from the step itself and this launch writes it to the step's n_done_out). */
 lz_status lz_vecnorm_apply(lz_handle* h, const lz_vecnorm* vn, const void* obs_raw,
                            const void* rew_raw, const uint8_t* done, float* obs_norm,
                            float* rew_norm, uint8_t* dones_out, const void* terminal_obs_raw,
