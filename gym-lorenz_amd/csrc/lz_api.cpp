@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <new>
@@ -101,9 +102,32 @@ struct lz_handle {
   uint8_t* hs_pin;     // lz_step_host: mapped host staging (actions | noise || obs | rew | done)
   uint8_t* hs_dev;     // lz_step_host: its device address
   size_t hs_in, hs_out;  // bytes of the input / output parts
+  // lz_resident_step: mailbox in mapped coherent host memory (cmd | resp | act | noise
+  // || obs | rew | done), its device address, the server's own stream
+  uint8_t* rs_pin;
+  uint8_t* rs_dev;
+  hipStream_t rs_stream;
+  hipEvent_t rs_ev;
+  bool rs_active;       // a k_resident launch may be running
+  int rs_use_noise;     // ... serving injected noise
+  int64_t rs_seq;       // number of the last request posted
+  uint64_t rs_idle;     // idle exit, wall-clock ticks
 };
 
+// Stop the resident step server (if any) and wait for it: every other call on the
+// handle starts with this, so the server's register-held state is back in the planes
+// and the handle's stream ordering is the plain one again.
+#define RESIDENT_QUIESCE(h)                           \
+  do {                                                \
+    if ((h)->rs_active) {                             \
+      const lz_status q_ = resident_stop(h);          \
+      if (q_ != LZ_OK) return q_;                     \
+    }                                                 \
+  } while (0)
+
 extern "C" {
+
+static lz_status resident_stop(lz_handle* h);
 
 int32_t lz_abi_version(void) { return LZ_ABI_VERSION; }
 
@@ -278,6 +302,10 @@ lz_status lz_create(const lz_config* cfg_in, lz_handle** out) {
 lz_status lz_destroy(lz_handle* h) {
   if (!h) return LZ_OK;
   (void)hipSetDevice(h->cfg.device);
+  if (h->rs_active) (void)resident_stop(h);
+  if (h->rs_stream) (void)hipStreamDestroy(h->rs_stream);
+  if (h->rs_ev) (void)hipEventDestroy(h->rs_ev);
+  if (h->rs_pin) (void)hipHostFree(h->rs_pin);
   for (int p = 0; p < lz::kMaxPlanes; ++p)
     if (h->planes[p]) (void)hipFree(h->planes[p]);
   if (h->counters) (void)hipFree(h->counters);
@@ -335,12 +363,14 @@ lz_status lz_get_config(const lz_handle* h, lz_config* cfg) {
 
 lz_status lz_set_stream(lz_handle* h, void* stream) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  RESIDENT_QUIESCE(h);
   h->stream = static_cast<hipStream_t>(stream);
   return LZ_OK;
 }
 
 lz_status lz_set_seed(lz_handle* h, uint64_t seed) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  RESIDENT_QUIESCE(h);
   h->cfg.seed = seed;
   // rewind the RNG call counter (both ping-pong slots; stream-ordered after any
   // launch already queued): seed(s) + reset() is then reproducible
@@ -351,6 +381,7 @@ lz_status lz_set_seed(lz_handle* h, uint64_t seed) {
 
 lz_status lz_sync(lz_handle* h) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  RESIDENT_QUIESCE(h);
   HIP_TRY(hipSetDevice(h->cfg.device));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return LZ_OK;
@@ -382,6 +413,7 @@ static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 lz_status lz_reset(lz_handle* h, const uint8_t* mask, const void* init, void* obs_out) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  RESIDENT_QUIESCE(h);
   HIP_TRY(hipSetDevice(h->cfg.device));
   KArgs a;
   fill_common(h, a);
@@ -399,6 +431,7 @@ lz_status lz_step(lz_handle* h, const void* actions, const double* noise, void* 
                   void* rew_out, uint8_t* done_out, int32_t* done_idx_out, void* terminal_obs_out,
                   int32_t* n_done_out) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  RESIDENT_QUIESCE(h);
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_step before the first lz_reset");
   // LORENZ4 ignores its action, SC takes none
   const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4 && h->cfg.system != LZ_SYS_SC;
@@ -432,6 +465,7 @@ static size_t align16(size_t b) { return (b + 15) & ~(size_t)15; }
 lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, void* obs_out,
                        void* rew_out, uint8_t* done_out) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  RESIDENT_QUIESCE(h);
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_step_host before the first lz_reset");
   const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4 && h->cfg.system != LZ_SYS_SC;
   if ((needs_act && !actions) || !obs_out || !rew_out || !done_out)
@@ -470,6 +504,141 @@ lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, 
   return LZ_OK;
 }
 
+// ---- resident step server (lz_resident_step)
+// mailbox layout (bytes): cmd int64 @0, resp int64 @128 (own cache lines), actions
+// float32 [n, A] @256, noise double [n, 3] @kRsNoise, then obs | reward | done @kRsOut
+constexpr size_t kRsCmd = 0, kRsResp = 128, kRsAct = 256;
+constexpr size_t kRsNoise = kRsAct + 64 * 4 * 4, kRsOut = kRsNoise + 64 * 3 * 8;
+constexpr int kRsMaxEnvs = 64;
+
+static size_t rs_rew_off(const lz_handle* h) {
+  return kRsOut + align16((size_t)h->cfg.num_envs * h->desc.obs_dim * (h->f64 ? 8 : 4));
+}
+static size_t rs_done_off(const lz_handle* h) {
+  return rs_rew_off(h) + align16((size_t)h->cfg.num_envs * (h->f64 ? 8 : 4));
+}
+
+static volatile int64_t* rs_word(const lz_handle* h, size_t off) {
+  return reinterpret_cast<volatile int64_t*>(h->rs_pin + off);
+}
+
+static lz_status resident_launch(lz_handle* h, int64_t next, int use_noise) {
+  KArgs a;
+  fill_common(h, a);
+  lz::ResBox box;
+  box.cmd = reinterpret_cast<const int64_t*>(h->rs_dev + kRsCmd);
+  box.resp = reinterpret_cast<int64_t*>(h->rs_dev + kRsResp);
+  box.act = reinterpret_cast<const float*>(h->rs_dev + kRsAct);
+  box.noise = reinterpret_cast<const double*>(h->rs_dev + kRsNoise);
+  box.obs = h->rs_dev + kRsOut;
+  box.rew = h->rs_dev + rs_rew_off(h);
+  box.done = h->rs_dev + rs_done_off(h);
+  box.next = next;
+  box.idle_ticks = h->rs_idle;
+  box.use_noise = use_noise;
+  // after everything already queued on the handle's stream (reset, set_state, ...)
+  HIP_TRY(hipEventRecord(h->rs_ev, h->stream));
+  HIP_TRY(hipStreamWaitEvent(h->rs_stream, h->rs_ev, 0));
+  const int e = lz::launch_resident(h->cfg.system, h->f64, a, box, h->rs_stream);
+  if (e != 0) return fail(LZ_ERR_HIP, "resident launch: %s", hipGetErrorString((hipError_t)e));
+  h->rs_active = true;
+  h->rs_use_noise = use_noise;
+  return LZ_OK;
+}
+
+// the launch has ended (stop command or idle exit): its state is in the planes and its
+// tick in the other ping-pong slot
+static void resident_ended(lz_handle* h) {
+  h->rs_active = false;
+  h->parity ^= 1;
+}
+
+static lz_status resident_stop(lz_handle* h) {
+  __atomic_store_n(const_cast<int64_t*>(rs_word(h, kRsCmd)), (int64_t)-1, __ATOMIC_RELEASE);
+  const hipError_t e = hipStreamSynchronize(h->rs_stream);
+  resident_ended(h);
+  if (e != hipSuccess) return fail(LZ_ERR_HIP, "resident stop: %s", hipGetErrorString(e));
+  return LZ_OK;
+}
+
+lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noise, void* obs_out,
+                           void* rew_out, uint8_t* done_out) {
+  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_resident_step before the first lz_reset");
+  const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4 && h->cfg.system != LZ_SYS_SC;
+  if ((needs_act && !actions) || !obs_out || !rew_out || !done_out)
+    return fail(LZ_ERR_INVALID, "actions/obs_out/rew_out/done_out must be non-NULL");
+  const int64_t n = h->cfg.num_envs;
+  if (n > kRsMaxEnvs) return fail(LZ_ERR_UNSUPPORTED, "lz_resident_step: at most %d envs", kRsMaxEnvs);
+  if (h->cfg.flags & LZ_FLAG_AUTORESET)
+    return fail(LZ_ERR_UNSUPPORTED, "lz_resident_step: handles without LZ_FLAG_AUTORESET only");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  const size_t es = h->f64 ? 8 : 4;
+  if (!h->rs_pin) {
+    const size_t bytes = rs_done_off(h) + align16((size_t)n);
+    if (hipHostMalloc(reinterpret_cast<void**>(&h->rs_pin), bytes,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return fail(LZ_ERR_OOM, "lz_resident_step: mailbox (%zu B)", bytes);
+    std::memset(h->rs_pin, 0, bytes);
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, h->rs_pin, 0) != hipSuccess || !dp)
+      return fail(LZ_ERR_HIP, "lz_resident_step: no device address for the mailbox");
+    h->rs_dev = static_cast<uint8_t*>(dp);
+    HIP_TRY(hipStreamCreateWithFlags(&h->rs_stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&h->rs_ev, hipEventDisableTiming));
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->cfg.device) != hipSuccess ||
+        khz <= 0)
+      khz = 100000;
+    const char* ev = std::getenv("LZ_RESIDENT_IDLE_US");
+    // short: a device-wide synchronize (torch.cuda.synchronize()) waits for the idle
+    // exit, and a caller that leaves > 1 ms between steps pays one relaunch (~20 us)
+    const double idle_us = ev ? std::atof(ev) : 1000.0;
+    h->rs_idle = (uint64_t)(idle_us * khz / 1000.0);
+    h->rs_seq = 0;
+  }
+  const int use_noise = noise != nullptr;
+  if (h->rs_active && use_noise != h->rs_use_noise) {
+    const lz_status q = resident_stop(h);
+    if (q != LZ_OK) return q;
+  }
+  const int64_t seq = h->rs_seq + 1;
+  if (needs_act) std::memcpy(h->rs_pin + kRsAct, actions, (size_t)n * h->desc.action_dim * 4);
+  if (noise) std::memcpy(h->rs_pin + kRsNoise, noise, (size_t)n * 3 * 8);
+  __atomic_store_n(const_cast<int64_t*>(rs_word(h, kRsCmd)), seq, __ATOMIC_RELEASE);
+  h->rs_seq = seq;
+  if (!h->rs_active) {
+    const lz_status q = resident_launch(h, seq, use_noise);
+    if (q != LZ_OK) return q;
+  }
+  volatile int64_t* resp = rs_word(h, kRsResp);
+  for (uint32_t spin = 1;; ++spin) {
+    if (__atomic_load_n(const_cast<int64_t*>(resp), __ATOMIC_ACQUIRE) == seq) break;
+    if ((spin & 4095u) == 0) {
+      // the server may have exited (idle) before it saw this request
+      const hipError_t q = hipStreamQuery(h->rs_stream);
+      if (q == hipErrorNotReady) continue;
+      if (__atomic_load_n(const_cast<int64_t*>(resp), __ATOMIC_ACQUIRE) == seq) break;
+      resident_ended(h);
+      if (q != hipSuccess) return fail(LZ_ERR_HIP, "resident server: %s", hipGetErrorString(q));
+      const lz_status r = resident_launch(h, seq, use_noise);
+      if (r != LZ_OK) return r;
+    }
+    __builtin_ia32_pause();
+  }
+  std::memcpy(obs_out, h->rs_pin + kRsOut, (size_t)n * h->desc.obs_dim * es);
+  std::memcpy(rew_out, h->rs_pin + rs_rew_off(h), (size_t)n * es);
+  std::memcpy(done_out, h->rs_pin + rs_done_off(h), (size_t)n);
+  return LZ_OK;
+}
+
+lz_status lz_resident_stop(lz_handle* h) {
+  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  RESIDENT_QUIESCE(h);
+  return LZ_OK;
+}
+
 static lz_status check_vecnorm(const lz_handle* h, const lz_vecnorm* vn) {
   if (!vn || !vn->obs_rms || !vn->ret_rms || !vn->returns)
     return fail(LZ_ERR_INVALID, "vecnorm: obs_rms/ret_rms/returns must be non-NULL");
@@ -488,6 +657,7 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
                           void* rew_out, uint8_t* done_out, int32_t* done_idx_out,
                           void* terminal_obs_out, int32_t* n_done_out) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  RESIDENT_QUIESCE(h);
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_step_vecnorm before the first lz_reset");
   const lz_status c = check_vecnorm(h, vn);
   if (c != LZ_OK) return c;
@@ -541,6 +711,7 @@ lz_status lz_vecnorm_apply(lz_handle* h, const lz_vecnorm* vn, const void* obs_r
                            float* rew_norm, uint8_t* dones_out, const void* terminal_obs_raw,
                            const int32_t* n_done, float* term_norm) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  RESIDENT_QUIESCE(h);
   const lz_status c = check_vecnorm(h, vn);
   if (c != LZ_OK) return c;
   if (!obs_raw || !rew_raw || !obs_norm || !rew_norm)
@@ -587,6 +758,7 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
                      uint8_t* done_out, int64_t* done_idx_out, void* terminal_obs_out, int64_t cap,
                      int32_t* n_done_out) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
+  RESIDENT_QUIESCE(h);
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_rollout before the first lz_reset");
   if (K <= 0) return fail(LZ_ERR_INVALID, "K must be >= 1");
   const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4 && h->cfg.system != LZ_SYS_SC;
@@ -622,6 +794,7 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
                                 int n_stack = 1, const float* stack_in = nullptr,
                                 float* stack_out = nullptr) {
   if (!h || !r) return fail(LZ_ERR_INVALID, "handle/args is NULL");
+  RESIDENT_QUIESCE(h);
   const bool attn = arch == 1 || arch == 2;
   if (arch == 2) {
     if (n_stack != 1 && n_stack != 4) return fail(LZ_ERR_UNSUPPORTED, "n_stack must be 1 or 4");
@@ -728,6 +901,7 @@ int32_t lz_plane_elem_size(const lz_handle* h, int32_t plane) {
 
 lz_status lz_get_state(lz_handle* h, int32_t plane, void* dst) {
   if (!h || !dst) return fail(LZ_ERR_INVALID, "handle/dst is NULL");
+  RESIDENT_QUIESCE(h);
   const int es = plane_elem(h->cfg.system, h->f64, plane);
   if (!es) return fail(LZ_ERR_INVALID, "invalid plane %d", plane);
   HIP_TRY(hipSetDevice(h->cfg.device));
@@ -738,6 +912,7 @@ lz_status lz_get_state(lz_handle* h, int32_t plane, void* dst) {
 
 lz_status lz_set_state(lz_handle* h, int32_t plane, const void* src) {
   if (!h || !src) return fail(LZ_ERR_INVALID, "handle/src is NULL");
+  RESIDENT_QUIESCE(h);
   const int es = plane_elem(h->cfg.system, h->f64, plane);
   if (!es) return fail(LZ_ERR_INVALID, "invalid plane %d", plane);
   HIP_TRY(hipSetDevice(h->cfg.device));

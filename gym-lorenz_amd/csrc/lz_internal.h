@@ -225,6 +225,28 @@ lz_status set_error(lz_status s, const char* msg);
 // host-side launchers (lz_kernels.hip)
 int launch_reset(int system, int f64, const KArgs& a, void* stream);
 int launch_step(int system, int f64, const KArgs& a, void* stream);
+
+// Resident step server of a small handle (lz_resident_step, n <= 64 envs, one wave):
+// the device addresses of its mailbox in mapped, coherent host memory.  The kernel
+// holds the state in registers, polls *cmd (system-scope loads), serves request
+// `next`, `next + 1`, ... each exactly as one k_step launch would (step_body), writes
+// obs | reward | done into the mailbox and then *resp = the request's number (release,
+// system scope).  It stores the state back and exits on cmd == -1 or after idle_ticks
+// wall-clock ticks without a request; the host relaunches it when a request finds it
+// gone.
+struct ResBox {
+  const int64_t* cmd;   // host -> device: request number, -1 = stop
+  int64_t* resp;        // device -> host: number of the last request served
+  const float* act;     // [n, A]
+  const double* noise;  // [n, 3] (with use_noise)
+  void* obs;            // T [n, O]
+  void* rew;            // T [n]
+  uint8_t* done;        // [n]
+  int64_t next;         // first request this launch serves
+  uint64_t idle_ticks;  // wall_clock64() ticks
+  int32_t use_noise;
+};
+int launch_resident(int system, int f64, const KArgs& a, const ResBox& box, void* stream);
 int launch_rollout(int system, int f64, const KArgs& a, void* stream);
 int launch_step_vecnorm(int system, int f64, const KArgs& a, const VArgs& v, void* stream);
 // Launch shape of the policy rollout (one workgroup per CU: the weights fill LDS).

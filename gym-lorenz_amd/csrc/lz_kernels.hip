@@ -866,11 +866,120 @@ static int dispatch(int which, int system, int f64, const KArgs& a, void* stream
   return (int)hipErrorInvalidValue;
 }
 
-// lz_step_vecnorm's envs per workgroup: kVnBlock, or LZ_VN_BLOCK=256 (A/B knob)
+// ------------------------------------------------------------------ resident step server
+// lz_resident_step (lz_internal.h ResBox): the per-env drop-in classes step ONE env per
+// env.step() call, and a launch + stream synchronisation per call costs 20-27 us
+// (profiles/r01/dropin).  This kernel stays on the GPU between calls: lane 0 polls the
+// host's command word over PCIe, the wave serves the request with the same step_body
+// as k_step (state in registers, tick += 1 per request, injected noise staged through
+// LDS), and the reply goes straight into host memory.  Bounded: it exits on the stop
+// command or after idle_ticks without one.
+template <class Sys, typename T>
+__global__ __launch_bounds__(64) void k_resident(KArgs a, ResBox box) {
+  const int lane = (int)threadIdx.x;
+  const bool live = lane < a.n;
+  __shared__ double s_nz[64 * 3];
+  Sys sys;
+  sys.setup(a);
+  int32_t steps = 0;
+  if (live) {
+    sys.load(a, lane);
+    if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[lane];
+  }
+  uint64_t tick = *a.tick_in;
+  if (lane == 0) *a.counter_next = 0;  // as k_step leaves it for the launch that follows
+  KArgs b = a;
+  b.noise = box.use_noise ? s_nz : nullptr;
+  b.term_obs = nullptr;
+  int64_t next = box.next;
+  uint64_t t_last = wall_clock64();
+  for (;;) {
+    int64_t c = 0;
+    if (lane == 0) {
+      for (;;) {
+        c = __hip_atomic_load(box.cmd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (c == next || c < 0) break;
+        if (wall_clock64() - t_last > box.idle_ticks) {
+          c = -2;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    c = __shfl(c, 0, 64);
+    if (c < 0) break;
+    float act[Sys::A > 0 ? Sys::A : 1];
+    if (live) {
+#pragma unroll
+      for (int j = 0; j < Sys::A; ++j)
+        act[j] = __hip_atomic_load(box.act + lane * Sys::A + j, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+      if (box.use_noise) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          s_nz[lane * 3 + j] = __hip_atomic_load(box.noise + lane * 3 + j, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    T o[Sys::O];
+    T rew = (T)0;
+    bool did_reset;
+    const uint8_t d = step_body<Sys, T, false>(sys, steps, b, lane, live, act, tick, 0, o, rew,
+                                               did_reset);
+    if (live) {
+#pragma unroll
+      for (int j = 0; j < Sys::O; ++j) static_cast<T*>(box.obs)[lane * Sys::O + j] = o[j];
+      static_cast<T*>(box.rew)[lane] = rew;
+      box.done[lane] = d;
+    }
+    tick += 1;
+    // the outputs of the whole wave reach host memory before the reply (release)
+    if (lane == 0) __hip_atomic_store(box.resp, next, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    ++next;
+    t_last = wall_clock64();
+  }
+  if (live) {
+    sys.store(a, lane);
+    if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[lane] = steps;
+  }
+  if (lane == 0) *a.tick_out = tick;
+}
+
+template <class Sys, typename T>
+static int launch_res(const KArgs& a, const ResBox& box, hipStream_t s) {
+  hipLaunchKernelGGL((k_resident<Sys, T>), dim3(1), dim3(64), 0, s, a, box);
+  return (int)hipGetLastError();
+}
+
+int launch_resident(int system, int f64, const KArgs& a, const ResBox& box, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (system) {
+    case LZ_SYS_LORENZ3:
+      return f64 ? launch_res<SysL3<double>, double>(a, box, s) : launch_res<SysL3<float>, float>(a, box, s);
+    case LZ_SYS_LORENZ4:
+      return f64 ? launch_res<SysL4<double>, double>(a, box, s) : launch_res<SysL4<float>, float>(a, box, s);
+    case LZ_SYS_PMSM:
+      return launch_res<SysPMSM, float>(a, box, s);
+    case LZ_SYS_HR:
+      return f64 ? launch_res<SysHR<double>, double>(a, box, s) : launch_res<SysHR<float>, float>(a, box, s);
+    case LZ_SYS_T1:
+      return f64 ? launch_res<SysT1<double>, double>(a, box, s) : launch_res<SysT1<float>, float>(a, box, s);
+    case LZ_SYS_T2:
+      return f64 ? launch_res<SysT2<double>, double>(a, box, s) : launch_res<SysT2<float>, float>(a, box, s);
+    case LZ_SYS_TP:
+      return f64 ? launch_res<SysTP<double>, double>(a, box, s) : launch_res<SysTP<float>, float>(a, box, s);
+    case LZ_SYS_SC:
+      return f64 ? launch_res<SysSC<double>, double>(a, box, s) : launch_res<SysSC<float>, float>(a, box, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// lz_step_vecnorm's envs per workgroup: kVnBlock, or LZ_VN_BLOCK=256 / 512 (A/B knob)
 int vn_block() {
   static const int b = [] {
     const char* e = std::getenv("LZ_VN_BLOCK");
-    return e && std::atoi(e) == 256 ? 256 : kVnBlock;
+    const int b = e ? std::atoi(e) : 0;
+    return b == 256 || b == 512 ? b : kVnBlock;
   }();
   return b;
 }
@@ -882,6 +991,8 @@ static int launch_vn(const KArgs& a, const VArgs& v, hipStream_t s) {
   const unsigned grid = (unsigned)((a.n + vb - 1) / vb);
   if (vb == 1024)
     hipLaunchKernelGGL((k_step_vn<Sys, T, 24>), dim3(grid), dim3(1024), 0, s, a, v);
+  else if (vb == 512)
+    hipLaunchKernelGGL((k_step_vn<Sys, T, 8>), dim3(grid), dim3(512), 0, s, a, v);
   else
     hipLaunchKernelGGL((k_step_vn<Sys, T, 0>), dim3(grid), dim3(256), 0, s, a, v);
   if (v.flags & LZ_VN_DEFER)

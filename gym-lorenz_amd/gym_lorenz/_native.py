@@ -156,6 +156,8 @@ _SIGS = {
     "lz_step": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, VP, VP, VP]),
     "lz_rollout": (ctypes.c_int, [VP, ctypes.c_int32, VP, VP, VP, VP, VP, VP, ctypes.c_int64, VP]),
     "lz_step_host": (ctypes.c_int, [VP, VP, VP, VP, VP, VP]),
+    "lz_resident_step": (ctypes.c_int, [VP, VP, VP, VP, VP, VP]),
+    "lz_resident_stop": (ctypes.c_int, [VP]),
     "lz_get_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
     "lz_set_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
     "lz_plane_elem_size": (ctypes.c_int32, [VP, ctypes.c_int32]),

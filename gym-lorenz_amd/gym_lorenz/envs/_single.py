@@ -7,6 +7,8 @@ the same host draws in the same order, so a caller's RNG streams evolve as with 
 reference, and inject the values into the kernel (lz_reset init / lz_step noise);
 every dynamics, observation, reward and done computation runs in the HIP kernel.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -31,6 +33,13 @@ class SingleEnvCore:
         es = np.dtype(self._np_dtype).itemsize
         self._o_end = o * es
         self._r_end = (o + 1) * es
+        # lz_resident_step (a resident one-wave step server polling a host mailbox: no
+        # launch or stream sync per step); LZ_RESIDENT=0 selects lz_step_host
+        self._step_fn = (nat.lib.lz_step_host if os.environ.get("LZ_RESIDENT", "1") == "0"
+                         else nat.lib.lz_resident_step)
+        # the host buffers' addresses, looked up once (ndarray.ctypes costs ~0.5 us a call)
+        self._p = (self._act_h.ctypes.data, self._noise_h.ctypes.data, self._obs_h.ctypes.data,
+                   self._rew_h.ctypes.data, self._done_h.ctypes.data)
 
     def _unpack(self):
         raw = self.be.packed.cpu().numpy()  # one D2H copy: obs | rew | done
@@ -45,16 +54,20 @@ class SingleEnvCore:
         return self._unpack()[0]
 
     def step(self, action, noise=None):
-        # lz_step_host: actions (+ injected noise) in, obs | reward | done out, host
-        # memory, one synchronous library call (pinned staging inside the library)
-        self._act_h[...] = np.asarray(action, dtype=np.float32).reshape(1, -1)
+        # lz_resident_step / lz_step_host: actions (+ injected noise) in, obs | reward |
+        # done out, host memory, one synchronous library call
+        try:
+            self._act_h[0] = action  # float32 cast
+        except ValueError:  # e.g. a [1, A] action
+            self._act_h[...] = np.asarray(action, dtype=np.float32).reshape(1, -1)
         nz = None
+        p = self._p
         if noise is not None:
             self._noise_h[...] = np.asarray(noise, dtype=np.float64).reshape(1, 3)
-            nz = self._noise_h.ctypes.data
-        nat.check(nat.lib.lz_step_host(self.be._h, self._act_h.ctypes.data, nz,
-                                       self._obs_h.ctypes.data, self._rew_h.ctypes.data,
-                                       self._done_h.ctypes.data))
+            nz = p[1]
+        st = self._step_fn(self.be._h, p[0], nz, p[2], p[3], p[4])
+        if st:
+            nat.check(st)
         return self._obs_h[0].copy(), self._rew_h[0], int(self._done_h[0])
 
     def plane(self, p):

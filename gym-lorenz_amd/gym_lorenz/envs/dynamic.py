@@ -67,16 +67,49 @@ class lorenzEnv_transient(GymEnv):  # noqa: N801 (reference name)
         return [self.state1[2], self.state2[2]]
 
     def step(self, action):
-        """dynamic.py:61-90 (kernel: lz_step on LORENZ3)."""
-        self.u1 = np.clip(action[0], self.input_min, self.input_max)
-        self.u2 = np.clip(action[1], self.input_min, self.input_max)
-        self.u3 = np.clip(action[2], self.input_min, self.input_max)
+        """dynamic.py:61-90 (kernel: lz_step on LORENZ3).  The reference's per-step
+        attribute bookkeeping -- u1..u3 = np.clip(action[j]) (:63-65), state1 / state0 /
+        state (:80-82) -- is kept with the same values and types, but materialised on
+        first access (_lazy): three np.clip calls and the list conversion were ~40% of a
+        resident-kernel step."""
+        self._act = np.array(action, copy=True)
         obs, reward, done = self._core.step(action)
-        self.state1 = obs[:3].copy()
-        self.state0 = list(obs)
-        self.state = obs
+        self._obs = obs
+        self._lz = {}
         self.t = self.t + 0.01
         return obs, reward, bool(done & nat.DONE_TERMINATED), {}
+
+    # ---- lazily materialised step attributes (see step)
+    def _lazy(self, name):
+        lz = self.__dict__.get("_lz")
+        if lz is None or self.__dict__.get("_obs") is None:
+            return self.__dict__.get("_" + name + "_v")
+        if name not in lz:
+            a, o = self._act, self._obs
+            if name in ("u1", "u2", "u3"):
+                lz[name] = np.clip(a[int(name[1]) - 1], self.input_min, self.input_max)
+            elif name == "state1":
+                lz[name] = o[:3].copy()
+            elif name == "state0":
+                lz[name] = list(o)
+            else:  # state
+                lz[name] = o
+        return lz[name]
+
+    def _set_lazy(self, name, v):
+        lz = self.__dict__.get("_lz")
+        if lz is not None and self.__dict__.get("_obs") is not None:
+            for k in ("u1", "u2", "u3", "state1", "state0", "state"):  # freeze the others
+                self.__dict__["_" + k + "_v"] = self._lazy(k)
+            self.__dict__["_lz"] = None
+        self.__dict__["_" + name + "_v"] = v
+
+    u1 = property(lambda s: s._lazy("u1"), lambda s, v: s._set_lazy("u1", v))
+    u2 = property(lambda s: s._lazy("u2"), lambda s, v: s._set_lazy("u2", v))
+    u3 = property(lambda s: s._lazy("u3"), lambda s, v: s._set_lazy("u3", v))
+    state1 = property(lambda s: s._lazy("state1"), lambda s, v: s._set_lazy("state1", v))
+    state0 = property(lambda s: s._lazy("state0"), lambda s, v: s._set_lazy("state0", v))
+    state = property(lambda s: s._lazy("state"), lambda s, v: s._set_lazy("state", v))
 
     def set_state(self, state1):
         """Inject a 3-state (the reference's `env.state1 = ...`)."""

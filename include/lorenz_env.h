@@ -239,6 +239,22 @@ lz_status lz_step(lz_handle* h, const void* actions, const double* noise, void* 
 lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, void* obs_out,
                        void* rew_out, uint8_t* done_out);
 
+/* lz_step_host's contract (same arguments, same results bit for bit -- the same step
+ * body, tick for tick) served by a RESIDENT kernel: the first call launches a one-wave
+ * server on a stream of its own that keeps the state in registers and polls a mailbox
+ * in mapped host memory; each call posts its request there and spins until the reply
+ * lands in host memory -- no launch, no stream synchronisation per step (the
+ * reference's per-env callers step one env per env.step(), code/train.py:98-100,
+ * gym_run.py).  Handles of at most 64 envs without LZ_FLAG_AUTORESET
+ * (LZ_ERR_UNSUPPORTED otherwise).  The server exits by itself after
+ * LZ_RESIDENT_IDLE_US (default 1000) microseconds without a request and is
+ * relaunched by the next call (a device-wide synchronize waits for that exit); every
+ * other call on the handle stops it first (its state goes back to the planes), as
+ * does lz_resident_stop. */
+lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noise,
+                           void* obs_out, void* rew_out, uint8_t* done_out);
+lz_status lz_resident_stop(lz_handle* h);
+
 /* K fused steps in ONE launch, state held in registers.  Time-major buffers:
  *   actions T [K, N, action_dim]; obs_out T [K, N, obs_dim]; rew_out T [K, N];
  *   done_out uint8 [K, N]; done_idx_out int64 [cap] (k * N + env) and

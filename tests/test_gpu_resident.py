@@ -1,0 +1,196 @@
+"""GPU: lz_resident_step (the resident one-wave step server behind the per-env
+drop-in classes) against lz_step_host -- the same step body tick for tick, so the
+results must be bit-identical -- including the server's idle exit + relaunch, state
+access in between (which stops it), injected noise, 64-env handles, the unsupported
+cases, and that it does not hold up torch work on other streams while it waits.
+
+The drop-in class tests in test_gpu_parity.py (test_dropin_*) run through the resident
+path too (it is the default) against the reference's golden fixtures."""
+import os
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import bits_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gl():
+    import gym_lorenz
+
+    return gym_lorenz
+
+
+def _pair(system, n, dtype, **kw):
+    from gym_lorenz.core import BatchedEnv
+
+    envs = []
+    for _ in range(2):
+        be = BatchedEnv(system, n, dtype=dtype, seed=7, autoreset=False, compact=False,
+                        max_episode_steps=0, **kw)
+        be.reset()
+        envs.append(be)
+    return envs
+
+
+def _bufs(be):
+    npd = np.float64 if be.tdtype == torch.float64 else np.float32
+    return (np.zeros((be.num_envs, be.obs_dim), npd), np.zeros((be.num_envs,), npd),
+            np.zeros((be.num_envs,), np.uint8))
+
+
+def _step(fn, be, act, noise, bufs):
+    import gym_lorenz._native as nat
+
+    o, r, d = bufs
+    nat.check(fn(be._h, act.ctypes.data, None if noise is None else noise.ctypes.data,
+                 o.ctypes.data, r.ctypes.data, d.ctypes.data))
+    return o.copy(), r.copy(), d.copy()
+
+
+@pytest.mark.parametrize("system,n,dtype,kw,noise", [
+    ("lorenz3", 1, "float64", {}, False),
+    ("lorenz3", 64, "float32", {}, False),
+    ("pmsm", 1, "float32", {"add_noise": True}, True),
+    ("pmsm", 3, "float32", {"add_noise": True}, False),
+    ("hr", 1, "float64", {"add_noise": True}, True),
+    ("hr", 17, "float32", {"add_noise": True, "add_filter": True}, False),
+    ("lorenz4", 1, "float64", {}, False),
+])
+def test_resident_equals_step_host(gl, system, n, dtype, kw, noise):
+    import gym_lorenz._native as nat
+
+    a, b = _pair(system, n, dtype, **kw)
+    ba, bb = _bufs(a), _bufs(b)
+    rng = np.random.default_rng(3)
+    A = max(a.action_dim, 1)
+    for k in range(400):
+        act = rng.uniform(-1, 1, (n, A)).astype(np.float32)
+        nz = rng.standard_normal((n, 3)) if noise else None
+        x = _step(nat.lib.lz_step_host, a, act, nz, ba)
+        y = _step(nat.lib.lz_resident_step, b, act, nz, bb)
+        for p, q in zip(x, y):
+            assert bits_equal(p, q), (system, k)
+        if k == 150:  # state access in between stops the server; the next step relaunches it
+            for pl in range(2):
+                assert bits_equal(a.get_state(pl).cpu().numpy(), b.get_state(pl).cpu().numpy())
+    # the server's register-held state goes back to the planes
+    nat.check(nat.lib.lz_resident_stop(b._h))
+    for pl in range(2):
+        assert bits_equal(a.get_state(pl).cpu().numpy(), b.get_state(pl).cpu().numpy())
+    a.close(), b.close()
+
+
+def test_resident_idle_exit_and_relaunch(gl, monkeypatch):
+    """With a 300 us idle limit the server exits between spaced-out requests and is
+    relaunched by the next one; the trajectory (and the RNG tick) is unchanged."""
+    import gym_lorenz._native as nat
+
+    monkeypatch.setenv("LZ_RESIDENT_IDLE_US", "300")
+    a, b = _pair("pmsm", 2, "float32", add_noise=True)  # device-drawn noise: tick matters
+    ba, bb = _bufs(a), _bufs(b)
+    rng = np.random.default_rng(5)
+    for k in range(60):
+        act = rng.uniform(-1, 1, (2, 2)).astype(np.float32)
+        x = _step(nat.lib.lz_step_host, a, act, None, ba)
+        y = _step(nat.lib.lz_resident_step, b, act, None, bb)
+        for p, q in zip(x, y):
+            assert bits_equal(p, q), k
+        if k % 7 == 3:
+            time.sleep(0.003)  # > the idle limit: the server has exited
+    a.close(), b.close()
+
+
+def test_resident_then_plain_calls(gl):
+    """lz_step / lz_reset after resident steps see the state and tick the server left."""
+    import gym_lorenz._native as nat
+
+    a, b = _pair("hr", 4, "float64", add_noise=True)
+    ba, bb = _bufs(a), _bufs(b)
+    rng = np.random.default_rng(9)
+    for k in range(30):
+        act = rng.uniform(-1, 1, (4, 2)).astype(np.float32)
+        _step(nat.lib.lz_step_host, a, act, None, ba)
+        _step(nat.lib.lz_resident_step, b, act, None, bb)
+    act = torch.as_tensor(rng.uniform(-1, 1, (4, 2)).astype(np.float32), device=a.device)
+    oa, ra, da = a.step(act)
+    ob, rb, db = b.step(act)
+    torch.cuda.synchronize()
+    assert bits_equal(oa.cpu().numpy(), ob.cpu().numpy())
+    a.reset(), b.reset()
+    for k in range(5):
+        act = rng.uniform(-1, 1, (4, 2)).astype(np.float32)
+        x = _step(nat.lib.lz_step_host, a, act, None, ba)
+        y = _step(nat.lib.lz_resident_step, b, act, None, bb)
+        for p, q in zip(x, y):
+            assert bits_equal(p, q)
+    a.close(), b.close()
+
+
+def test_resident_unsupported(gl):
+    import gym_lorenz._native as nat
+    from gym_lorenz.core import BatchedEnv
+
+    be = BatchedEnv("lorenz3", 65, autoreset=False, compact=False)
+    be.reset()
+    o, r, d = _bufs(be)
+    act = np.zeros((65, 3), np.float32)
+    st = nat.lib.lz_resident_step(be._h, act.ctypes.data, None, o.ctypes.data, r.ctypes.data,
+                                  d.ctypes.data)
+    assert st == nat.LZ_ERR_UNSUPPORTED
+    be.close()
+    be = BatchedEnv("lorenz3", 4, autoreset=True, compact=False)
+    be.reset()
+    o, r, d = _bufs(be)
+    st = nat.lib.lz_resident_step(be._h, act.ctypes.data, None, o.ctypes.data, r.ctypes.data,
+                                  d.ctypes.data)
+    assert st == nat.LZ_ERR_UNSUPPORTED
+    be.close()
+
+
+def test_resident_does_not_block_torch(gl):
+    """While the server waits for its next request, torch work on torch's stream
+    completes without waiting for it (own non-blocking stream, own hardware queue);
+    a device-wide synchronize waits at most for its idle exit."""
+    x = torch.ones(1024, device="cuda")
+    for _ in range(3):  # load the kernels first
+        x = x + 1
+    torch.cuda.synchronize()
+    env = gl.LorenzDynamicEnv()
+    env.reset()
+    env.step(np.zeros(3, np.float32))  # the server is now resident and polling
+    s = torch.cuda.current_stream()
+    t0 = time.perf_counter()
+    for _ in range(20):
+        x = x + 1
+    s.synchronize()
+    dt = time.perf_counter() - t0
+    assert dt < 0.002, dt  # not serialised behind the server
+    assert float(x[0]) == 24.0
+    t0 = time.perf_counter()
+    torch.cuda.synchronize()  # device-wide: includes the server's idle exit (1 ms)
+    assert time.perf_counter() - t0 < 0.05
+    env.step(np.zeros(3, np.float32))  # relaunched
+    env.close()
+
+
+def test_dropin_resident_matches_step_host(gl, monkeypatch):
+    """The drop-in class with LZ_RESIDENT=0 (lz_step_host) and the default (resident)."""
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("LZ_RESIDENT", flag)
+        env = gl.make("lorenz_pmsm-v0", alpha=0.5, add_noise=True)
+        o, _ = env.reset(seed=11)
+        rng = np.random.default_rng(2)
+        traj = [o]
+        for k in range(200):
+            o, r, te, tr, _ = env.step(rng.uniform(-1, 1, 2).astype(np.float32))
+            traj.append(np.concatenate([o, [r, te, tr]]).astype(np.float64))
+        env.close()
+        outs.append(traj)
+    for p, q in zip(*outs):
+        assert bits_equal(np.asarray(p), np.asarray(q))

@@ -26,16 +26,41 @@ def timed(env, act, steps):
 
 def main():
     out = {}
-    np.random.seed(0)
-    e = gl.make("lorenz_dynamic-v0")
-    e.reset()
-    out["lorenz_dynamic-v0 (fp64)"] = timed(e, np.zeros(3, np.float32), 2000)
-    e = gl.make("lorenz_try-v0")
-    e.reset(seed=0)
-    out["lorenz_try-v0 HR (fp64)"] = timed(e, np.zeros(2, np.float32), 2000)
-    e = gl.make("lorenz_pmsm-v0")
-    e.reset(seed=0)
-    out["lorenz_pmsm-v0 (fp32)"] = timed(e, np.zeros(2, np.float32), 2000)
+    for flag, label in (("0", "lz_step_host"), ("1", "lz_resident_step")):
+        os.environ["LZ_RESIDENT"] = flag
+        res = {}
+        np.random.seed(0)
+        e = gl.make("lorenz_dynamic-v0")
+        e.reset()
+        res["lorenz_dynamic-v0 (fp64)"] = timed(e, np.zeros(3, np.float32), 5000)
+        e.close()
+        e = gl.make("lorenz_try-v0")
+        e.reset(seed=0)
+        res["lorenz_try-v0 HR (fp64)"] = timed(e, np.zeros(2, np.float32), 5000)
+        e.close()
+        e = gl.make("lorenz_pmsm-v0")
+        e.reset(seed=0)
+        res["lorenz_pmsm-v0 (fp32)"] = timed(e, np.zeros(2, np.float32), 5000)
+        e.close()
+        out[label] = res
+    # the C call alone (no gymnasium / class overhead): lorenz3 fp64, 1 env
+    import gym_lorenz._native as nat
+    from gym_lorenz.core import BatchedEnv
+    for fn in ("lz_step_host", "lz_resident_step"):
+        be = BatchedEnv("lorenz3", 1, dtype="float64", autoreset=False, compact=False)
+        be.reset()
+        a = np.zeros((1, 3), np.float32)
+        o, r, d = np.zeros((1, 6)), np.zeros(1), np.zeros(1, np.uint8)
+        f = getattr(nat.lib, fn)
+        args = (be._h, a.ctypes.data, None, o.ctypes.data, r.ctypes.data, d.ctypes.data)
+        for _ in range(100):
+            f(*args)
+        t0 = time.perf_counter()
+        for _ in range(20000):
+            f(*args)
+        out.setdefault("C call only, lorenz3 fp64 1 env", {})[fn] = (
+            (time.perf_counter() - t0) / 20000 * 1e6)
+        be.close()
     from oracle.ref_loop import LorenzRefEnv
     r = LorenzRefEnv(np.array([1.0, 2.0, 3.0]))
     a = np.zeros(3, np.float32)
