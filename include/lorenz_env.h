@@ -25,6 +25,10 @@
  *          lorenz_env_try_pmsm.py:76-184, lorenz_env_try.py:80-179, batched over
  *          the env axis with SB3 DummyVecEnv.step_wait auto-reset semantics
  *          (terminal observation kept, post-reset observation returned)
+ *   lz_step_host / lz_resident_step
+ *       -> ONE env's step(action) from host memory, the per-env classes'
+ *          DummyVecEnv([lambda: gymnasium.make(id)]) path (code/train.py:98-100);
+ *          lz_resident_step serves it from a resident kernel (no launch per step)
  *   lz_rollout
  *       -> K consecutive step() calls fused in one launch (state kept in VGPRs)
  *   (legacy, unregistered: lorenz_env_transient1.py:18-104,
