@@ -1,12 +1,14 @@
 // C-ABI of libgym_lorenz_amd.so: handle lifetime, validation, device buffers and
 // launch plumbing around the kernels in lz_kernels.hip.  See include/lorenz_env.h.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <mutex>
 #include <cstring>
 #include <new>
 #include <string>
@@ -522,6 +524,18 @@ static volatile int64_t* rs_word(const lz_handle* h, size_t off) {
   return reinterpret_cast<volatile int64_t*>(h->rs_pin + off);
 }
 
+// handles whose server may be running, so that unloading the library (process exit
+// without lz_destroy) can post their stop commands first
+static std::mutex g_rs_mu;
+static std::vector<lz_handle*> g_rs_live;
+
+__attribute__((destructor)) static void resident_unload() {
+  std::lock_guard<std::mutex> lk(g_rs_mu);
+  for (lz_handle* h : g_rs_live)
+    __atomic_store_n(const_cast<int64_t*>(rs_word(h, kRsCmd)), (int64_t)-1, __ATOMIC_RELEASE);
+  if (!g_rs_live.empty()) usleep(2000);  // a poll period is ~2 us; they exit on sight
+}
+
 static lz_status resident_launch(lz_handle* h, int64_t next, int use_noise) {
   KArgs a;
   fill_common(h, a);
@@ -543,6 +557,8 @@ static lz_status resident_launch(lz_handle* h, int64_t next, int use_noise) {
   if (e != 0) return fail(LZ_ERR_HIP, "resident launch: %s", hipGetErrorString((hipError_t)e));
   h->rs_active = true;
   h->rs_use_noise = use_noise;
+  std::lock_guard<std::mutex> lk(g_rs_mu);
+  if (std::find(g_rs_live.begin(), g_rs_live.end(), h) == g_rs_live.end()) g_rs_live.push_back(h);
   return LZ_OK;
 }
 
@@ -551,6 +567,8 @@ static lz_status resident_launch(lz_handle* h, int64_t next, int use_noise) {
 static void resident_ended(lz_handle* h) {
   h->rs_active = false;
   h->parity ^= 1;
+  std::lock_guard<std::mutex> lk(g_rs_mu);
+  g_rs_live.erase(std::remove(g_rs_live.begin(), g_rs_live.end(), h), g_rs_live.end());
 }
 
 static lz_status resident_stop(lz_handle* h) {
