@@ -524,16 +524,34 @@ static volatile int64_t* rs_word(const lz_handle* h, size_t off) {
   return reinterpret_cast<volatile int64_t*>(h->rs_pin + off);
 }
 
-// handles whose server may be running, so that unloading the library (process exit
-// without lz_destroy) can post their stop commands first
-static std::mutex g_rs_mu;
-static std::vector<lz_handle*> g_rs_live;
+// handles whose server may be running, so that process exit without lz_destroy posts
+// their stop commands first (an atexit handler registered at the first launch: it runs
+// before the HIP runtime's own exit-time teardown, which was registered earlier).
+constexpr int kRsLiveMax = 1024;
+static std::mutex g_rs_mu;  // trivially destructible
+static lz_handle* g_rs_live[kRsLiveMax];
+static int g_rs_n;
 
-__attribute__((destructor)) static void resident_unload() {
+static void rs_live_add(lz_handle* h) {
   std::lock_guard<std::mutex> lk(g_rs_mu);
-  for (lz_handle* h : g_rs_live)
-    __atomic_store_n(const_cast<int64_t*>(rs_word(h, kRsCmd)), (int64_t)-1, __ATOMIC_RELEASE);
-  if (!g_rs_live.empty()) usleep(2000);  // a poll period is ~2 us; they exit on sight
+  for (int i = 0; i < g_rs_n; ++i)
+    if (g_rs_live[i] == h) return;
+  if (g_rs_n < kRsLiveMax) g_rs_live[g_rs_n++] = h;
+}
+static void rs_live_remove(lz_handle* h) {
+  std::lock_guard<std::mutex> lk(g_rs_mu);
+  for (int i = 0; i < g_rs_n; ++i)
+    if (g_rs_live[i] == h) {
+      g_rs_live[i] = g_rs_live[--g_rs_n];
+      return;
+    }
+}
+
+static void resident_unload() {
+  for (int i = 0; i < g_rs_n; ++i)
+    __atomic_store_n(const_cast<int64_t*>(rs_word(g_rs_live[i], kRsCmd)), (int64_t)-1,
+                     __ATOMIC_RELEASE);
+  if (g_rs_n > 0) usleep(2000);  // a poll period is ~2 us; they exit on sight
 }
 
 static lz_status resident_launch(lz_handle* h, int64_t next, int use_noise) {
@@ -557,8 +575,9 @@ static lz_status resident_launch(lz_handle* h, int64_t next, int use_noise) {
   if (e != 0) return fail(LZ_ERR_HIP, "resident launch: %s", hipGetErrorString((hipError_t)e));
   h->rs_active = true;
   h->rs_use_noise = use_noise;
-  std::lock_guard<std::mutex> lk(g_rs_mu);
-  if (std::find(g_rs_live.begin(), g_rs_live.end(), h) == g_rs_live.end()) g_rs_live.push_back(h);
+  rs_live_add(h);
+  static const int registered = std::atexit(resident_unload);
+  (void)registered;
   return LZ_OK;
 }
 
@@ -567,8 +586,7 @@ static lz_status resident_launch(lz_handle* h, int64_t next, int use_noise) {
 static void resident_ended(lz_handle* h) {
   h->rs_active = false;
   h->parity ^= 1;
-  std::lock_guard<std::mutex> lk(g_rs_mu);
-  g_rs_live.erase(std::remove(g_rs_live.begin(), g_rs_live.end(), h), g_rs_live.end());
+  rs_live_remove(h);
 }
 
 static lz_status resident_stop(lz_handle* h) {

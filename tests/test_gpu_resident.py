@@ -194,3 +194,22 @@ def test_dropin_resident_matches_step_host(gl, monkeypatch):
         outs.append(traj)
     for p, q in zip(*outs):
         assert bits_equal(np.asarray(p), np.asarray(q))
+
+
+@pytest.mark.parametrize("close", [False, True])
+def test_process_exit_with_live_server(close):
+    """A script that exits while the server is resident (no close(): the atexit hook
+    posts the stop command) or after close() ends cleanly."""
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import numpy as np, gym_lorenz as gl\n"
+            "e = gl.make('lorenz_pmsm-v0'); e.reset(seed=1)\n"
+            "for _ in range(100): e.step(np.zeros(2, np.float32))\n"
+            "%s\n"
+            "print('ok')\n" % (ROOT + "/gym-lorenz_amd", "e.close()" if close else "pass"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
