@@ -697,7 +697,7 @@ __device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
 
 // tanh(x) = sign(x) p_k(|x| - k/4), k = floor(4|x|) < 36, p_k a degree-6 polynomial
 // (tools/tanh_table.py; segment 0 is t q(t): full relative accuracy near 0) evaluated by
-// Horner in fmaf; 1 for |x| >= 9 (1 - tanh(9) < 2^-25).  ~20 instructions, two of them
+// Horner in fmaf; 1 for |x| >= 9 (1 - tanh(9) < 2^-25).  ~18 instructions, two of them
 // LDS reads of the segment's coefficients (the table sits in the blob, tab = LDS).
 __device__ __forceinline__ float tanh_tab(float x, const float* tab) {
   const float ax = fabsf(x);
@@ -712,8 +712,7 @@ __device__ __forceinline__ float tanh_tab(float x, const float* tab) {
   y = fmaf(y, t, lo[2]);
   y = fmaf(y, t, lo[1]);
   y = fmaf(y, t, lo[0]);
-  y = ax < 9.0f ? y : 1.0f;
-  y = x != x ? x : y;
+  y = ax >= 9.0f ? 1.0f : y;  // NaN: the compare is false and t (so y) is already NaN
   return __builtin_copysignf(y, x);
 }
 

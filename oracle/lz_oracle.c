@@ -620,8 +620,7 @@ float orc_tanh_tab(float x) {
   y = fmaf(y, t, c[2]);
   y = fmaf(y, t, c[1]);
   y = fmaf(y, t, c[0]);
-  y = ax < 9.0f ? y : 1.0f;
-  y = x != x ? x : y;
+  y = ax >= 9.0f ? 1.0f : y;  /* NaN: ax >= 9 is false and t (so y) is already NaN */
   return copysignf(y, x);
 }
 
