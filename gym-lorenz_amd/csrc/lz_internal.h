@@ -173,8 +173,8 @@ constexpr int kF32H = kF32B2 + 4 * 2 * 16 * 4;
 constexpr int kF32HB = kF32H + 4 * 2 * 64 * 4;
 constexpr int kF32Net = kF32HB + 64;                 // 72768 B
 constexpr int kF32LogStd = 2 * kF32Net;
-constexpr int kF32Tanh = kF32LogStd + 64;           // tanh table: 36 segments x 8 floats
-constexpr int kF32BlobBytes = kF32Tanh + 36 * 32;   // 146752 B (resident in LDS)
+constexpr int kF32Tanh = kF32LogStd + 64;           // tanh table: 72 segments x 8 floats
+constexpr int kF32BlobBytes = kF32Tanh + 72 * 32;   // 147904 B (resident in LDS)
 
 struct PArgs {
   const uint8_t* blob;     // device copy of the packed policy

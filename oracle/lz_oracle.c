@@ -566,56 +566,92 @@ LEGACY_BODY(float)
  *     g = 0..15; out = (part0 + part1) + b[r].
  * Nets narrower than 128 are zero-padded (exactly what the packer does).
  * ========================================================================= */
-/* lz_policy.hip tanh_tab: sign(x) p_k(|x| - k/4), k = floor(4|x|) (segments of width
- * 1/4 over [0, 9)), p_k of degree 6 by Horner in fmaf; 1 for |x| >= 9.  The coefficients
- * (tools/tanh_table.py) are the same 36 x 8 floats the packer puts into the blob. */
-static const float orc_tanh_coef[36 * 8] = {
-    0.0f, 0x1.0000000000000p+0f, -0x1.a6f07c0000000p-20f, -0x1.5541d60000000p-2f, -0x1.51fdca0000000p-10f, 0x1.25eb3e0000000p-3f, -0x1.341fb80000000p-5f, 0.0f,
-    0x1.f597ea0000000p-3f, 0x1.e149a00000000p-1f, -0x1.d780900000000p-3f, -0x1.0727420000000p-2f, 0x1.1ec2f20000000p-3f, 0x1.2261f80000000p-4f, -0x1.1b659e0000000p-4f, 0.0f,
-    0x1.d9353e0000000p-2f, 0x1.92a9440000000p-1f, -0x1.7425ea0000000p-2f, -0x1.825e100000000p-4f, 0x1.5449660000000p-3f, -0x1.2783dc0000000p-5f, -0x1.8ef0980000000p-6f, 0.0f,
-    0x1.45323e0000000p-1f, 0x1.3173b00000000p-1f, -0x1.8403420000000p-2f, 0x1.560dd80000000p-5f, 0x1.9b48860000000p-4f, -0x1.1769ea0000000p-4f, 0x1.a6713e0000000p-7f, 0.0f,
-    0x1.85efac0000000p-1f, 0x1.ae0dc20000000p-2f, -0x1.4786dc0000000p-2f, 0x1.a866540000000p-4f, 0x1.c491be0000000p-6f, -0x1.77ff4a0000000p-5f, 0x1.2ec4800000000p-6f, 0.0f,
-    0x1.b2523c0000000p-1f, 0x1.1f25140000000p-2f, -0x1.e7298e0000000p-3f, 0x1.bbba5c0000000p-4f, -0x1.a47efa0000000p-7f, -0x1.22d1140000000p-6f, 0x1.67d68c0000000p-7f, 0.0f,
-    0x1.cf6f980000000p-1f, 0x1.7216540000000p-3f, -0x1.4efc240000000p-3f, 0x1.67c0400000000p-4f, -0x1.9ba00c0000000p-6f, -0x1.bcba0c0000000p-10f, 0x1.0e231a0000000p-8f, 0.0f,
-    0x1.e1fbfa0000000p-1f, 0x1.d22ca20000000p-4f, -0x1.b6d8980000000p-4f, 0x1.01c00a0000000p-4f, -0x1.8273cc0000000p-6f, 0x1.0d86d80000000p-8f, 0x1.555f3a0000000p-11f, 0.0f,
-    0x1.ed95060000000p-1f, 0x1.2162c20000000p-4f, -0x1.16f9e40000000p-4f, 0x1.58f8500000000p-5f, -0x1.2570440000000p-6f, 0x1.412f980000000p-8f, -0x1.257fee0000000p-11f, 0.0f,
-    0x1.f4bfd60000000p-1f, 0x1.64108a0000000p-5f, -0x1.5c3d900000000p-5f, 0x1.bbccc00000000p-6f, -0x1.93c6980000000p-7f, 0x1.058f1c0000000p-8f, -0x1.9070c40000000p-11f, 0.0f,
-    0x1.f925820000000p-1f, 0x1.b3afe20000000p-6f, -0x1.addad20000000p-6f, 0x1.16dd620000000p-6f, -0x1.078aa60000000p-7f, 0x1.72a9220000000p-9f, -0x1.4e321a0000000p-11f, 0.0f,
-    0x1.fbd50a0000000p-1f, 0x1.09a7a60000000p-6f, -0x1.077df80000000p-6f, 0x1.5993b20000000p-7f, -0x1.4de50a0000000p-8f, 0x1.eae9760000000p-10f, -0x1.dd197e0000000p-12f, 0.0f,
-    0x1.fd77d20000000p-1f, 0x1.434a520000000p-7f, -0x1.41b0ec0000000p-7f, 0x1.a8a6ee0000000p-8f, -0x1.9fb5500000000p-9f, 0x1.3966ca0000000p-10f, -0x1.3ccca80000000p-12f, 0.0f,
-    0x1.fe767a0000000p-1f, 0x1.88ef660000000p-8f, -0x1.87c13a0000000p-8f, 0x1.0395e20000000p-8f, -0x1.001dfc0000000p-9f, 0x1.87e6320000000p-11f, -0x1.94f38c0000000p-13f, 0.0f,
-    0x1.ff112c0000000p-1f, 0x1.dd37d00000000p-9f, -0x1.dc59020000000p-9f, 0x1.3c634e0000000p-9f, -0x1.39a2900000000p-10f, 0x1.e41e880000000p-12f, -0x1.faa5220000000p-14f, 0.0f,
-    0x1.ff6f180000000p-1f, 0x1.21a7ae0000000p-9f, -0x1.2155920000000p-9f, 0x1.80e6b80000000p-10f, -0x1.7ea3800000000p-11f, 0x1.28dce60000000p-12f, -0x1.3903a60000000p-14f, 0.0f,
-    0x1.ffa8180000000p-1f, 0x1.5f85ac0000000p-10f, -0x1.5f49280000000p-10f, 0x1.d3b8e20000000p-11f, -0x1.d1c5e00000000p-12f, 0x1.6a7fda0000000p-13f, -0x1.7ff0380000000p-15f, 0.0f,
-    0x1.ffcaac0000000p-1f, 0x1.aa87ce0000000p-11f, -0x1.aa5b2e0000000p-11f, 0x1.1bfcc80000000p-11f, -0x1.1b192c0000000p-12f, 0x1.b97e0e0000000p-14f, -0x1.d4dade0000000p-16f, 0.0f,
-    0x1.ffdfa80000000p-1f, 0x1.02bec80000000p-11f, -0x1.02ae500000000p-11f, 0x1.58b6fa0000000p-12f, -0x1.57da400000000p-13f, 0x1.0c6dd40000000p-14f, -0x1.1d895e0000000p-16f, 0.0f,
-    0x1.ffec620000000p-1f, 0x1.39e7820000000p-12f, -0x1.39db540000000p-12f, 0x1.a2528c0000000p-13f, -0x1.a16f780000000p-14f, 0x1.4618b60000000p-15f, -0x1.5b362e0000000p-17f, 0.0f,
-    0x1.fff41a0000000p-1f, 0x1.7ccec00000000p-13f, -0x1.7cc5b80000000p-13f, 0x1.fb91fe0000000p-14f, -0x1.fa9c820000000p-15f, 0x1.8bed2e0000000p-16f, -0x1.a5d0140000000p-18f, 0.0f,
-    0x1.fff8c80000000p-1f, 0x1.cdf5a20000000p-14f, -0x1.cdeee60000000p-14f, 0x1.33e69c0000000p-14f, -0x1.335c760000000p-15f, 0x1.e085f60000000p-17f, -0x1.0004dc0000000p-18f, 0.0f,
-    0x1.fffba00000000p-1f, 0x1.1832dc0000000p-14f, -0x1.1830540000000p-14f, 0x1.7588f40000000p-15f, -0x1.74e9940000000p-16f, 0x1.238cdc0000000p-17f, -0x1.36c0a20000000p-19f, 0.0f,
-    0x1.fffd580000000p-1f, 0x1.53e7140000000p-15f, -0x1.53e5260000000p-15f, 0x1.c524fe0000000p-16f, -0x1.c469360000000p-17f, 0x1.61b9aa0000000p-18f, -0x1.7903ba0000000p-20f, 0.0f,
-    0x1.fffe640000000p-1f, 0x1.9c53760000000p-16f, -0x1.9c51f80000000p-16f, 0x1.12dadc0000000p-16f, -0x1.126bbe0000000p-17f, 0x1.ad2ec00000000p-19f, -0x1.c9aebc0000000p-21f, 0.0f,
-    0x1.ffff060000000p-1f, 0x1.f42dde0000000p-17f, -0x1.f42cae0000000p-17f, 0x1.4d6c300000000p-17f, -0x1.4ce84a0000000p-18f, 0x1.045fc00000000p-19f, -0x1.15e2d80000000p-21f, 0.0f,
-    0x1.ffff680000000p-1f, 0x1.2f5ffa0000000p-17f, -0x1.2f5f7a0000000p-17f, 0x1.9477420000000p-18f, -0x1.93d3dc0000000p-19f, 0x1.3bb4400000000p-20f, -0x1.5024c80000000p-22f, 0.0f,
-    0x1.ffffa40000000p-1f, 0x1.7003540000000p-18f, -0x1.7002e60000000p-18f, 0x1.eaa5a20000000p-19f, -0x1.e9e7700000000p-20f, 0x1.7f371a0000000p-21f, -0x1.992cde0000000p-23f, 0.0f,
-    0x1.ffffc80000000p-1f, 0x1.be6c3e0000000p-19f, -0x1.be6bd20000000p-19f, 0x1.29977a0000000p-19f, -0x1.291c300000000p-20f, 0x1.d0577a0000000p-22f, -0x1.ed543e0000000p-24f, 0.0f,
-    0x1.ffffde0000000p-1f, 0x1.0ec4f20000000p-19f, -0x1.0ec4ba0000000p-19f, 0x1.68ff460000000p-20f, -0x1.6866240000000p-21f, 0x1.19808a0000000p-22f, -0x1.2a59200000000p-24f, 0.0f,
-    0x1.ffffec0000000p-1f, 0x1.4875bc0000000p-20f, -0x1.4875940000000p-20f, 0x1.b5ec720000000p-21f, -0x1.b561300000000p-22f, 0x1.56fa300000000p-23f, -0x1.7293ba0000000p-25f, 0.0f,
-    0x1.fffff40000000p-1f, 0x1.8e712e0000000p-21f, -0x1.8e710c0000000p-21f, 0x1.099da80000000p-21f, -0x1.094dba0000000p-22f, 0x1.a04dc60000000p-24f, -0x1.c2dc0c0000000p-26f, 0.0f,
-    0x1.fffff80000000p-1f, 0x1.e355b40000000p-22f, -0x1.e355980000000p-22f, 0x1.4236320000000p-22f, -0x1.41e41c0000000p-23f, 0x1.fa028c0000000p-25f, -0x1.14787e0000000p-26f, 0.0f,
-    0x1.fffffc0000000p-1f, 0x1.25284c0000000p-22f, -0x1.25284e0000000p-22f, 0x1.86dff60000000p-23f, -0x1.86b3020000000p-24f, 0x1.34c63a0000000p-25f, -0x1.5aa20a0000000p-27f, 0.0f,
-    0x1.fffffe0000000p-1f, 0x1.639e300000000p-23f, -0x1.639e640000000p-23f, 0x1.da2e6a0000000p-24f, -0x1.da604a0000000p-25f, 0x1.79e8e40000000p-26f, -0x1.b7d2120000000p-28f, 0.0f,
-    0x1.fffffe0000000p-1f, 0x1.af62e60000000p-24f, -0x1.af62c60000000p-24f, 0x1.1f95fc0000000p-24f, -0x1.1f781e0000000p-25f, 0x1.c729ba0000000p-27f, -0x1.0279980000000p-28f, 0.0f,
+/* lz_policy.hip tanh_tab: sign(x) p_k(|x| - k/8), k = floor(8|x|) (segments of width
+ * 1/8 over [0, 9)), p_k of degree 5 by Horner in fmaf; 1 for |x| >= 9.  The coefficients
+ * (tools/tanh_table.py) are the 72 x 8 floats the packer puts into the blob, scaled by
+ * 8^-j there (the kernel's Horner runs in u = 8 t: the same bits, see lz_policy.hip). */
+static const float orc_tanh_coef[72 * 8] = {
+    0.0f, 0x1.0000000000000p+0f, 0x1.c0e2b20000000p-22f, -0x1.555bea0000000p-2f, 0x1.06810a0000000p-11f, 0x1.0a051c0000000p-3f, 0.0f, 0.0f,
+    0x1.fd59920000000p-4f, 0x1.f815240000000p-1f, -0x1.f574200000000p-4f, -0x1.40a4860000000p-2f, 0x1.51c1e40000000p-4f, 0x1.8de4da0000000p-4f, 0.0f, 0.0f,
+    0x1.f597ea0000000p-3f, 0x1.e1499e0000000p-1f, -0x1.d77de40000000p-3f, -0x1.075b220000000p-2f, 0x1.258ef60000000p-3f, 0x1.784c640000000p-5f, 0.0f, 0.0f,
+    0x1.6ef53e0000000p-2f, 0x1.be3fb80000000p-1f, -0x1.3fd3c00000000p-2f, -0x1.6e322a0000000p-3f, 0x1.5f12440000000p-3f, -0x1.76ae540000000p-8f, 0.0f, 0.0f,
+    0x1.d9353e0000000p-2f, 0x1.92a9460000000p-1f, -0x1.7426460000000p-2f, -0x1.8264340000000p-4f, 0x1.559cc60000000p-3f, -0x1.634c080000000p-5f, 0.0f, 0.0f,
+    0x1.1bf47e0000000p-1f, 0x1.6284c20000000p-1f, -0x1.893b040000000p-2f, -0x1.24e9760000000p-6f, 0x1.1c00ce0000000p-3f, -0x1.f82a900000000p-5f, 0.0f, 0.0f,
+    0x1.45323e0000000p-1f, 0x1.3173b20000000p-1f, -0x1.8403fc0000000p-2f, 0x1.56a9400000000p-5f, 0x1.977e660000000p-4f, -0x1.00bcee0000000p-4f, 0.0f, 0.0f,
+    0x1.6866500000000p-1f, 0x1.02500a0000000p-1f, -0x1.6ba8380000000p-2f, 0x1.4f4f300000000p-4f, 0x1.eb1db60000000p-5f, -0x1.b2d63e0000000p-5f, 0.0f, 0.0f,
+    0x1.85efac0000000p-1f, 0x1.ae0dc20000000p-2f, -0x1.4787420000000p-2f, 0x1.a8a1900000000p-4f, 0x1.b57c4e0000000p-6f, -0x1.407aea0000000p-5f, 0.0f, 0.0f,
+    0x1.9e5cb60000000p-1f, 0x1.6150040000000p-2f, -0x1.1df01e0000000p-2f, 0x1.c6cada0000000p-4f, 0x1.336ae80000000p-9f, -0x1.9e7f2e0000000p-6f, 0.0f, 0.0f,
+    0x1.b2523c0000000p-1f, 0x1.1f25140000000p-2f, -0x1.e729ca0000000p-3f, 0x1.bbd41a0000000p-4f, -0x1.b407840000000p-7f, -0x1.c879220000000p-7f, 0.0f, 0.0f,
+    0x1.c278a60000000p-1f, 0x1.cea7460000000p-3f, -0x1.970e820000000p-3f, 0x1.97f8360000000p-4f, -0x1.6603360000000p-6f, -0x1.7519460000000p-8f, 0.0f, 0.0f,
+    0x1.cf6f980000000p-1f, 0x1.7216540000000p-3f, -0x1.4efc260000000p-3f, 0x1.67c6940000000p-4f, -0x1.9e1e4a0000000p-6f, -0x1.603d9c0000000p-12f, 0.0f, 0.0f,
+    0x1.d9c6fa0000000p-1f, 0x1.265e340000000p-3f, -0x1.1064960000000p-3f, 0x1.33e9b00000000p-4f, -0x1.9ff4a80000000p-6f, 0x1.6a701c0000000p-9f, 0.0f, 0.0f,
+    0x1.e1fbfa0000000p-1f, 0x1.d22ca20000000p-4f, -0x1.b6d87e0000000p-4f, 0x1.01bee00000000p-4f, -0x1.8292880000000p-6f, 0x1.1880380000000p-8f, 0.0f, 0.0f,
+    0x1.e8789e0000000p-1f, 0x1.6fcfa60000000p-4f, -0x1.5ee8980000000p-4f, 0x1.a85d6c0000000p-5f, -0x1.56176c0000000p-6f, 0x1.38ecea0000000p-8f, 0.0f, 0.0f,
+    0x1.ed95060000000p-1f, 0x1.2162c20000000p-4f, -0x1.16f9c80000000p-4f, 0x1.58f26e0000000p-5f, -0x1.24d6160000000p-6f, 0x1.3214000000000p-8f, 0.0f, 0.0f,
+    0x1.f1994e0000000p-1f, 0x1.c65b1c0000000p-5f, -0x1.b993580000000p-5f, 0x1.15af780000000p-5f, -0x1.e9aec00000000p-7f, 0x1.16bf740000000p-8f, 0.0f, 0.0f,
+    0x1.f4bfd60000000p-1f, 0x1.64108a0000000p-5f, -0x1.5c3d680000000p-5f, 0x1.bbc1f20000000p-6f, -0x1.9277020000000p-7f, 0x1.e5ac020000000p-9f, 0.0f, 0.0f,
+    0x1.f737760000000p-1f, 0x1.16a7fc0000000p-5f, -0x1.11e0100000000p-5f, 0x1.608ac80000000p-6f, -0x1.46997e0000000p-7f, 0x1.9ab50e0000000p-9f, 0.0f, 0.0f,
+    0x1.f925820000000p-1f, 0x1.b3afe20000000p-6f, -0x1.adda9c0000000p-6f, 0x1.16d5660000000p-6f, -0x1.0683400000000p-7f, 0x1.54263a0000000p-9f, 0.0f, 0.0f,
+    0x1.faa7940000000p-1f, 0x1.5452000000000p-6f, -0x1.50c42c0000000p-6f, 0x1.b78e260000000p-7f, -0x1.a2f4000000000p-8f, 0x1.1581420000000p-9f, 0.0f, 0.0f,
+    0x1.fbd50a0000000p-1f, 0x1.09a7a60000000p-6f, -0x1.077dd60000000p-6f, 0x1.5988ec0000000p-7f, -0x1.4c77120000000p-8f, 0x1.bfccd00000000p-10f, 0.0f, 0.0f,
+    0x1.fcc04c0000000p-1f, 0x1.9e87d00000000p-7f, -0x1.9be6180000000p-7f, 0x1.0f10080000000p-7f, -0x1.06b6a00000000p-8f, 0x1.6650e60000000p-10f, 0.0f, 0.0f,
+    0x1.fd77d20000000p-1f, 0x1.434a500000000p-7f, -0x1.41b0c00000000p-7f, 0x1.a8990a0000000p-8f, -0x1.9dd60e0000000p-9f, 0x1.1cecac0000000p-10f, 0.0f, 0.0f,
+    0x1.fe06ec0000000p-1f, 0x1.f81bd80000000p-8f, -0x1.f62a160000000p-8f, 0x1.4c220c0000000p-8f, -0x1.451fa40000000p-9f, 0x1.c2fa040000000p-11f, 0.0f, 0.0f,
+    0x1.fe767a0000000p-1f, 0x1.88ef660000000p-8f, -0x1.87c1060000000p-8f, 0x1.038d260000000p-8f, -0x1.fddc240000000p-10f, 0x1.639ac00000000p-11f, 0.0f, 0.0f,
+    0x1.fecd6c0000000p-1f, 0x1.3238b60000000p-8f, -0x1.3181100000000p-8f, 0x1.955ae60000000p-9f, -0x1.8f2d7a0000000p-10f, 0x1.179dc40000000p-11f, 0.0f, 0.0f,
+    0x1.ff112c0000000p-1f, 0x1.dd37d00000000p-9f, -0x1.dc58c00000000p-9f, 0x1.3c587c0000000p-9f, -0x1.3828040000000p-10f, 0x1.b6c8d60000000p-12f, 0.0f, 0.0f,
+    0x1.ff45f60000000p-1f, 0x1.73cec00000000p-9f, -0x1.73474a0000000p-9f, 0x1.ed89380000000p-10f, -0x1.e7c4640000000p-11f, 0x1.57b4ac0000000p-12f, 0.0f, 0.0f,
+    0x1.ff6f180000000p-1f, 0x1.21a7ae0000000p-9f, -0x1.21556a0000000p-9f, 0x1.80d9700000000p-10f, -0x1.7cd1160000000p-11f, 0x1.0ce2680000000p-12f, 0.0f, 0.0f,
+    0x1.ff8f220000000p-1f, 0x1.c347040000000p-10f, -0x1.c2e3180000000p-10f, 0x1.2c03a80000000p-10f, -0x1.2927280000000p-11f, 0x1.a4466a0000000p-13f, 0.0f, 0.0f,
+    0x1.ffa8180000000p-1f, 0x1.5f85ac0000000p-10f, -0x1.5f48f80000000p-10f, 0x1.d3a8a20000000p-11f, -0x1.cf8a840000000p-12f, 0x1.4832700000000p-13f, 0.0f, 0.0f,
+    0x1.ffbb880000000p-1f, 0x1.11ce6e0000000p-10f, -0x1.11a98a0000000p-10f, 0x1.6c6dd60000000p-11f, -0x1.696d9a0000000p-12f, 0x1.0023620000000p-13f, 0.0f, 0.0f,
+    0x1.ffcaac0000000p-1f, 0x1.aa87ce0000000p-11f, -0x1.aa5af40000000p-11f, 0x1.1bf2e20000000p-11f, -0x1.19bcb40000000p-12f, 0x1.8f9f0c0000000p-14f, 0.0f, 0.0f,
+    0x1.ffd6780000000p-1f, 0x1.4c36520000000p-11f, -0x1.4c1b0a0000000p-11f, 0x1.ba702e0000000p-12f, -0x1.b725680000000p-13f, 0x1.37a1340000000p-14f, 0.0f, 0.0f,
+    0x1.ffdfa80000000p-1f, 0x1.02bec80000000p-11f, -0x1.02ae2c0000000p-11f, 0x1.58aaf00000000p-12f, -0x1.5632180000000p-13f, 0x1.e5df3a0000000p-15f, 0.0f, 0.0f,
+    0x1.ffe6ce0000000p-1f, 0x1.930b440000000p-12f, -0x1.92f7060000000p-12f, 0x1.0c7c6a0000000p-12f, -0x1.0a9da60000000p-13f, 0x1.7aad8a0000000p-15f, 0.0f, 0.0f,
+    0x1.ffec620000000p-1f, 0x1.39e7820000000p-12f, -0x1.39db2a0000000p-12f, 0x1.a243ee0000000p-13f, -0x1.9f6bf40000000p-14f, 0x1.271a400000000p-15f, 0.0f, 0.0f,
+    0x1.fff0b80000000p-1f, 0x1.e8f43c0000000p-13f, -0x1.e8e5260000000p-13f, 0x1.45c9dc0000000p-13f, -0x1.439da40000000p-14f, 0x1.cbe1040000000p-16f, 0.0f, 0.0f,
+    0x1.fff41a0000000p-1f, 0x1.7ccec00000000p-13f, -0x1.7cc5840000000p-13f, 0x1.fb80320000000p-14f, -0x1.f829880000000p-15f, 0x1.6640d60000000p-16f, 0.0f, 0.0f,
+    0x1.fff6bc0000000p-1f, 0x1.2894480000000p-13f, -0x1.288e9e0000000p-13f, 0x1.8b46180000000p-14f, -0x1.88b4ba0000000p-15f, 0x1.171a0c0000000p-16f, 0.0f, 0.0f,
+    0x1.fff8c80000000p-1f, 0x1.cdf5a20000000p-14f, -0x1.cdeea60000000p-14f, 0x1.33dbd40000000p-14f, -0x1.31e0360000000p-15f, 0x1.b2ce400000000p-17f, 0.0f, 0.0f,
+    0x1.fffa600000000p-1f, 0x1.67c7600000000p-14f, -0x1.67c30e0000000p-14f, 0x1.df8b600000000p-15f, -0x1.dc79c40000000p-16f, 0x1.52aa580000000p-17f, 0.0f, 0.0f,
+    0x1.fffba00000000p-1f, 0x1.1832dc0000000p-14f, -0x1.18302e0000000p-14f, 0x1.757be60000000p-15f, -0x1.731cf80000000p-16f, 0x1.07d4f00000000p-17f, 0.0f, 0.0f,
+    0x1.fffc980000000p-1f, 0x1.b470ec0000000p-15f, -0x1.b46d940000000p-15f, 0x1.22e0e40000000p-15f, -0x1.210ba60000000p-16f, 0x1.9b105c0000000p-18f, 0.0f, 0.0f,
+    0x1.fffd580000000p-1f, 0x1.53e7140000000p-15f, -0x1.53e4f80000000p-15f, 0x1.c5151c0000000p-16f, -0x1.c239000000000p-17f, 0x1.400d220000000p-18f, 0.0f, 0.0f,
+    0x1.fffdee0000000p-1f, 0x1.08b7b60000000p-15f, -0x1.08b6600000000p-15f, 0x1.60de040000000p-16f, -0x1.5ea5540000000p-17f, 0x1.f28c3a0000000p-19f, 0.0f, 0.0f,
+    0x1.fffe640000000p-1f, 0x1.9c53760000000p-16f, -0x1.9c51c00000000p-16f, 0x1.12d13a0000000p-16f, -0x1.1118080000000p-17f, 0x1.8454820000000p-19f, 0.0f, 0.0f,
+    0x1.fffebe0000000p-1f, 0x1.411ee60000000p-16f, -0x1.411dca0000000p-16f, 0x1.ac0f620000000p-17f, -0x1.a95f840000000p-18f, 0x1.2e64980000000p-19f, 0.0f, 0.0f,
+    0x1.ffff060000000p-1f, 0x1.f42dde0000000p-17f, -0x1.f42c680000000p-17f, 0x1.4d60680000000p-17f, -0x1.4b4a280000000p-18f, 0x1.d70dd80000000p-20f, 0.0f, 0.0f,
+    0x1.ffff3e0000000p-1f, 0x1.858a640000000p-17f, -0x1.85896a0000000p-17f, 0x1.03a2b60000000p-17f, -0x1.02031a0000000p-18f, 0x1.6ee1380000000p-20f, 0.0f, 0.0f,
+    0x1.ffff680000000p-1f, 0x1.2f5ffa0000000p-17f, -0x1.2f5f520000000p-17f, 0x1.9469a00000000p-18f, -0x1.91ea5c0000000p-19f, 0x1.1df0ce0000000p-20f, 0.0f, 0.0f,
+    0x1.ffff8a0000000p-1f, 0x1.d889a60000000p-18f, -0x1.d888be0000000p-18f, 0x1.3af4e80000000p-18f, -0x1.38fc400000000p-19f, 0x1.bcf95a0000000p-21f, 0.0f, 0.0f,
+    0x1.ffffa40000000p-1f, 0x1.7003540000000p-18f, -0x1.7002b40000000p-18f, 0x1.ea946c0000000p-19f, -0x1.e789c40000000p-20f, 0x1.5ac44a0000000p-21f, 0.0f, 0.0f,
+    0x1.ffffb80000000p-1f, 0x1.1e9be60000000p-18f, -0x1.1e9b7c0000000p-18f, 0x1.7e11e00000000p-19f, -0x1.7bcc880000000p-20f, 0x1.0ec8be0000000p-21f, 0.0f, 0.0f,
+    0x1.ffffc80000000p-1f, 0x1.be6c3e0000000p-19f, -0x1.be6b9c0000000p-19f, 0x1.298dc20000000p-19f, -0x1.27ba2a0000000p-20f, 0x1.a4eaee0000000p-22f, 0.0f, 0.0f,
+    0x1.ffffd40000000p-1f, 0x1.5bacb00000000p-19f, -0x1.5bac320000000p-19f, 0x1.cf76bc0000000p-20f, -0x1.cc7ce60000000p-21f, 0x1.46e1680000000p-22f, 0.0f, 0.0f,
+    0x1.ffffde0000000p-1f, 0x1.0ec4f20000000p-19f, -0x1.0ec4900000000p-19f, 0x1.68f1bc0000000p-20f, -0x1.6696900000000p-21f, 0x1.fc8a4a0000000p-23f, 0.0f, 0.0f,
+    0x1.ffffe60000000p-1f, 0x1.a5c0340000000p-20f, -0x1.a5bfa80000000p-20f, 0x1.191ab80000000p-20f, -0x1.1742f20000000p-21f, 0x1.8bd10e0000000p-23f, 0.0f, 0.0f,
+    0x1.ffffec0000000p-1f, 0x1.4875bc0000000p-20f, -0x1.48755e0000000p-20f, 0x1.b5dbf00000000p-21f, -0x1.b3351a0000000p-22f, 0x1.35f54e0000000p-23f, 0.0f, 0.0f,
+    0x1.fffff00000000p-1f, 0x1.ff9c180000000p-21f, -0x1.ff9ba20000000p-21f, 0x1.5503ba0000000p-21f, -0x1.531eac0000000p-22f, 0x1.e539840000000p-24f, 0.0f, 0.0f,
+    0x1.fffff40000000p-1f, 0x1.8e712c0000000p-21f, -0x1.8e70b00000000p-21f, 0x1.09921a0000000p-21f, -0x1.07e4e20000000p-22f, 0x1.771bba0000000p-24f, 0.0f, 0.0f,
+    0x1.fffff60000000p-1f, 0x1.364e9a0000000p-21f, -0x1.364e0a0000000p-21f, 0x1.9d9b540000000p-22f, -0x1.99fd1a0000000p-23f, 0x1.1c3ce60000000p-24f, 0.0f, 0.0f,
+    0x1.fffff80000000p-1f, 0x1.e355b40000000p-22f, -0x1.e3555a0000000p-22f, 0x1.422b420000000p-22f, -0x1.4059560000000p-23f, 0x1.c98be20000000p-25f, 0.0f, 0.0f,
+    0x1.fffffa0000000p-1f, 0x1.786be80000000p-22f, -0x1.786bb40000000p-22f, 0x1.f5d4f60000000p-23f, -0x1.f3812a0000000p-24f, 0x1.6887700000000p-25f, 0.0f, 0.0f,
+    0x1.fffffc0000000p-1f, 0x1.25284a0000000p-22f, -0x1.2528040000000p-22f, 0x1.86cd8c0000000p-23f, -0x1.8485200000000p-24f, 0x1.1556120000000p-25f, 0.0f, 0.0f,
+    0x1.fffffc0000000p-1f, 0x1.c89f580000000p-23f, -0x1.c89f6a0000000p-23f, 0x1.306a580000000p-23f, -0x1.2fd5d00000000p-24f, 0x1.c2272c0000000p-26f, 0.0f, 0.0f,
+    0x1.fffffe0000000p-1f, 0x1.639e2c0000000p-23f, -0x1.639d480000000p-23f, 0x1.d9f5440000000p-24f, -0x1.d516000000000p-25f, 0x1.40da540000000p-26f, 0.0f, 0.0f,
+    0x1.fffffe0000000p-1f, 0x1.14f49e0000000p-23f, -0x1.14f4b20000000p-23f, 0x1.7144f40000000p-24f, -0x1.705de60000000p-25f, 0x1.0f59800000000p-26f, 0.0f, 0.0f,
+    0x1.fffffe0000000p-1f, 0x1.af62e00000000p-24f, -0x1.af60b00000000p-24f, 0x1.1f5d940000000p-24f, -0x1.1a7e740000000p-25f, 0x1.69ea620000000p-27f, 0.0f, 0.0f,
+    0x1.fffffe0000000p-1f, 0x1.4ff6c80000000p-24f, -0x1.4ff5fe0000000p-24f, 0x1.bfc5e20000000p-25f, -0x1.bb37d80000000p-26f, 0x1.2ea2320000000p-27f, 0.0f, 0.0f,
 };
 
 float orc_tanh_tab(float x) {
   const float ax = fabsf(x);
-  int k = ax < 9.0f ? (int)(ax * 4.0f) : 35;  /* NaN / inf / >= 9: any segment, overridden */
-  if (k > 35) k = 35;
+  int k = ax < 9.0f ? (int)(ax * 8.0f) : 71;  /* NaN / inf / >= 9: any segment, overridden */
+  if (k > 71) k = 71;
   const float* c = orc_tanh_coef + 8 * k;
-  const float t = fmaf((float)k, -0.25f, ax);
-  float y = fmaf(c[6], t, c[5]);
-  y = fmaf(y, t, c[4]);
+  const float t = fmaf((float)k, -0.125f, ax);
+  float y = fmaf(c[5], t, c[4]);
   y = fmaf(y, t, c[3]);
   y = fmaf(y, t, c[2]);
   y = fmaf(y, t, c[1]);
