@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -1266,7 +1267,12 @@ static int launch_pol_f32(const KArgs& a, const PArgs& p, const PolShape& sh, hi
 // per SIMD: cfg5's 32,768 envs are 1,024 tiles = 128 eight-wave groups, half the CUs)
 PolShape f32_policy_shape(int64_t n, int num_cus) {
   const int64_t tiles = (n + 31) / 32;
-  PolShape s = {32, tiles >= 8 * (int64_t)num_cus ? 8 : 4, 0, 0};
+  static const int forced = [] {  // LZ_POL_F32_WAVES=4|8: A/B knob
+    const char* e = std::getenv("LZ_POL_F32_WAVES");
+    const int w = e ? std::atoi(e) : 0;
+    return w == 4 || w == 8 ? w : 0;
+  }();
+  PolShape s = {32, forced ? forced : tiles >= 8 * (int64_t)num_cus ? 8 : 4, 0, 0};
   const int64_t groups = (tiles + s.waves - 1) / s.waves;
   s.grid = (int)(groups < num_cus ? groups : num_cus);
   return s;
