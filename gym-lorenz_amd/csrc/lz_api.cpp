@@ -703,11 +703,11 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
     return fail(LZ_ERR_INVALID, "actions/obs/rew/done/done_idx/terminal_obs/n_done must be non-NULL");
   HIP_TRY(hipSetDevice(h->cfg.device));
   const int64_t n = h->cfg.num_envs;
-  const int64_t n_wg = (n + lz::vn_block() - 1) / lz::vn_block();
+  const int64_t n_wg = (n + lz::vn_block(n) - 1) / lz::vn_block(n);
   if (!h->vn_ws) {  // column-major per-workgroup partials, W = 2 (kVnMaxObs + 1) at most,
                     // then the statistics snapshot (sized for the smallest workgroups)
     const int64_t max_wg = (n + lz::kBlock - 1) / lz::kBlock;
-    const size_t bytes = (size_t)(max_wg + 2) * 2 * (lz::kVnMaxObs + 1) * sizeof(double);
+    const size_t bytes = (size_t)(max_wg + 3) * 2 * (lz::kVnMaxObs + 1) * sizeof(double);
     if (hipMalloc(reinterpret_cast<void**>(&h->vn_ws), bytes) != hipSuccess)
       return fail(LZ_ERR_OOM, "vecnorm workspace (%zu B)", bytes);
   }
@@ -725,6 +725,8 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
   v.returns = vn->returns;
   v.part = reinterpret_cast<double*>(h->vn_ws);
   v.old = v.part + (size_t)n_wg * 2 * (lz::kVnMaxObs + 1);
+  v.tot = v.old + 2 * (lz::kVnMaxObs + 1) + 4;
+  v.fused = lz::vn_fused(n);
   v.n_done_out = n_done_out;
   v.obs_state = lz::rms_state(vn->obs_rms);
   v.ret_state = lz::rms_state(vn->ret_rms);
@@ -736,8 +738,9 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
   if (e != 0) return fail(LZ_ERR_HIP, "step launch: %s", hipGetErrorString((hipError_t)e));
   h->parity ^= 1;
   h->vn_pending = (vn->flags & LZ_VN_TRAINING) && !(vn->flags & LZ_VN_DEFER);
-  // without LZ_VN_DEFER the done count is published by the paired lz_vecnorm_apply
-  h->vn_nd_out = (vn->flags & LZ_VN_DEFER) ? nullptr : n_done_out;
+  // without a second launch the done count is published by the paired lz_vecnorm_apply
+  const bool second = (vn->flags & LZ_VN_DEFER) || ((vn->flags & LZ_VN_TRAINING) && !v.fused);
+  h->vn_nd_out = second ? nullptr : n_done_out;
   h->vn_counter = a.counter;
   return LZ_OK;
 }
@@ -769,10 +772,15 @@ lz_status lz_vecnorm_apply(lz_handle* h, const lz_vecnorm* vn, const void* obs_r
   // deferred) are applied by this normalise pass
   lz::VnUpdate upd{};
   if (h->vn_pending && (vn->flags & LZ_VN_TRAINING) && !(vn->flags & LZ_VN_DEFER)) {
-    const int64_t n_wg = (h->cfg.num_envs + lz::vn_block() - 1) / lz::vn_block();
-    upd.part = reinterpret_cast<const double*>(h->vn_ws);
+    const int64_t n = h->cfg.num_envs;
+    const int64_t n_wg = (n + lz::vn_block(n) - 1) / lz::vn_block(n);
+    const double* part = reinterpret_cast<const double*>(h->vn_ws);
     upd.n_wg = (int)n_wg;
-    upd.old = upd.part + (size_t)n_wg * 2 * (lz::kVnMaxObs + 1);
+    upd.old = part + (size_t)n_wg * 2 * (lz::kVnMaxObs + 1);
+    if (lz::vn_fused(n))
+      upd.part = part;
+    else
+      upd.tot = upd.old + 2 * (lz::kVnMaxObs + 1) + 4;
     upd.batch = (double)h->cfg.num_envs;
     upd.upd_obs = (vn->flags & LZ_VN_NORM_OBS) != 0;
   }

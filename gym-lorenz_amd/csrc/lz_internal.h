@@ -55,15 +55,23 @@ struct KArgs {
 // every workgroup of the normalise pass of lz_vecnorm_apply reduces them (the same
 // fixed order, lz_rms_math.h vn_col_totals) and applies the statistics updates; with
 // LZ_VN_DEFER k_vn_colsum (the step's only other launch) reduces them into the moments.
-// kVnBlock envs per step workgroup: 1024, so that a 262,144-env step leaves 256
-// partials per column for every normalise workgroup to read.
+// kVnBlock envs per step workgroup on the fused path: 1024, so that a 262,144-env step
+// leaves 256 partials per column for every normalise workgroup to read.
 constexpr int kVnMaxObs = 8;
 constexpr int kVnBlock = 1024;
-int vn_block();  // the step workgroup size in use (kVnBlock; LZ_VN_BLOCK=256 for A/B)
+// Fused path (n <= vn_fuse_max_wg() * kVnBlock envs, 262,144 by default): 1024-env step
+// workgroups and the normalise pass reduces the partials itself -- two launches.  Split
+// path (larger n): 256-env step workgroups and k_vn_colsum reduces the partials once,
+// one workgroup per column -- three launches.  Measured same-box against the round-1
+// design (always split): fused +13% at PMSM 262k, but -10% at 393k and 1M.
+int vn_fuse_max_wg();        // LZ_VN_FUSE_MAX_WG
+bool vn_fused(int64_t n);
+int vn_block(int64_t n);     // the step workgroup size for n envs (LZ_VN_BLOCK for A/B)
 struct VArgs {
   double* returns;     // [N] VecNormalize.returns
   double* part;        // [W][n_wg]
   double* old;         // [2O+1 obs][3 returns] statistics snapshot (step block 0)
+  double* tot;         // [W] column totals (split path: k_vn_colsum -> normalise pass)
   double* obs_state;   // obs_rms mean[O], var[O], count
   double* ret_state;   // ret_rms mean, var, count
   double* moments;     // LZ_VN_DEFER: [2O+1 obs][3 returns] batch moments out
@@ -71,6 +79,7 @@ struct VArgs {
   double gamma;
   uint32_t flags;      // LZ_VN_*
   int32_t n_wg;
+  int32_t fused;       // the normalise pass reduces the partials itself (n_wg small)
 };
 
 // Policy-in-the-loop rollout (lz_policy.hip): SB3 ActorCriticPolicy (MlpPolicy,
@@ -204,8 +213,10 @@ int launch_rms_update(lz_rms* r, const double* moments, void* stream);
 // every workgroup reduces the step's moment partials and derives the new statistics
 // from them and the snapshot the step's block 0 took; workgroup 0 writes them back.
 struct VnUpdate {
-  const double* part;  // [2 (O + 1)][n_wg] partials (nullptr: no update in this pass)
+  const double* part;  // [2 (O + 1)][n_wg] partials to reduce here (fused), or nullptr
   int n_wg;
+  const double* tot;   // [2 (O + 1)] totals k_vn_colsum left (split), or nullptr
+                       // (both nullptr: no update in this pass)
   const double* old;   // [2O+1 obs][3 returns] snapshot of the statistics
   double batch;        // batch count n
   int upd_obs;         // obs_rms.update (TRAINING and NORM_OBS)

@@ -175,12 +175,13 @@ __device__ __forceinline__ void vn_epilogue(const T* s_obs, const double* s_ret,
   }
 }
 
-// LZ_VN_DEFER: the step's second launch.  Block 0 publishes the step's done count and,
-// in training, reduces the partial columns (vn_col_totals, the order the normalise pass
-// uses) into the moments vector for the caller's all-reduce; lz_vecnorm_apply updates
-// the statistics from the moments.  (Without LZ_VN_DEFER there is no second launch: the
-// step kernel's block 0 snapshots the statistics and the normalise pass reduces the
-// partials and publishes the done count.)
+// The step's second launch, with LZ_VN_DEFER or when there are too many partials for
+// every normalise workgroup to reduce them (VArgs::fused == 0).  It publishes the
+// step's done count and, in training, reduces the partial columns (vn_col_totals, the
+// order the normalise pass uses) into the moments vector for the caller's all-reduce
+// (DEFER; lz_vecnorm_apply then updates from the moments) or into the totals the
+// normalise pass reads.  (Otherwise there is no second launch: the normalise pass
+// reduces the partials and publishes the done count.)
 constexpr int kVnColBlock = 256;
 template <int O>
 __global__ __launch_bounds__(kVnColBlock) void k_vn_colsum(VArgs v, int64_t n,
@@ -188,20 +189,51 @@ __global__ __launch_bounds__(kVnColBlock) void k_vn_colsum(VArgs v, int64_t n,
                                                           int32_t* n_done_out) {
   constexpr int C = O + 1;
   const int tid = (int)threadIdx.x;
-  if (tid == 0) *n_done_out = *counter;
+  if (blockIdx.x == 0 && tid == 0) *n_done_out = *counter;
   if (!(v.flags & LZ_VN_TRAINING)) return;
-  __shared__ double red[LZ_VN_RED(2 * C)];
-  __shared__ double tot[2 * C];
-  vn_col_totals<2 * C>(v.part, v.n_wg, red, tot);
-  if (tid >= 2 * C) return;
+  const bool defer = (v.flags & LZ_VN_DEFER) != 0;
   // (count, sums[O], sumsq[O]) for obs, then (count, sum, sumsq) for returns
-  const int slot =
-      tid < O ? 1 + tid : tid == O ? 2 * O + 2 : tid < C + O ? 1 + O + (tid - C) : 2 * O + 3;
-  v.moments[slot] = tot[tid];
-  if (tid == 0) {
-    v.moments[0] = (double)n;
-    v.moments[2 * O + 1] = (double)n;
+  auto put = [&](int c, double t) {
+    if (!defer) {
+      v.tot[c] = t;
+      return;
+    }
+    const int slot = c < O ? 1 + c : c == O ? 2 * O + 2 : c < C + O ? 1 + O + (c - C) : 2 * O + 3;
+    v.moments[slot] = t;
+    if (c == 0) {
+      v.moments[0] = (double)n;
+      v.moments[2 * O + 1] = (double)n;
+    }
+  };
+  if (v.fused) {  // one workgroup, the normalise pass's order (DEFER at fused sizes)
+    __shared__ double red[LZ_VN_RED(2 * C)];
+    __shared__ double tot[2 * C];
+    vn_col_totals<2 * C>(v.part, v.n_wg, red, tot);
+    if (tid < 2 * C) put(tid, tot[tid]);
+    return;
   }
+  // many partials: one workgroup per column (2 (O + 1) of them), lane t adds rows t,
+  // t + 1024, ... into accumulator u of rows t + 256 u, the 4 accumulators in order,
+  // then a fixed LDS pairing tree
+  __shared__ double red[kVnColBlock];
+  const int c = (int)blockIdx.x;
+  const double* col = v.part + (int64_t)c * v.n_wg;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int r = tid; r < v.n_wg; r += 4 * kVnColBlock) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ru = r + u * kVnColBlock;
+      if (ru < v.n_wg) acc[u] += col[ru];
+    }
+  }
+  red[tid] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+#pragma unroll
+  for (int half = kVnColBlock / 2; half > 0; half >>= 1) {
+    if (tid < half) red[tid] += red[tid + half];
+    __syncthreads();
+  }
+  if (tid == 0) put(c, red[0]);
 }
 
 // One 256-env tile of lz_step (k_step) or lz_step_vecnorm (k_step_vn, kVN).
@@ -974,20 +1006,32 @@ int launch_resident(int system, int f64, const KArgs& a, const ResBox& box, void
   return (int)hipErrorInvalidValue;
 }
 
-// lz_step_vecnorm's envs per workgroup: kVnBlock, or LZ_VN_BLOCK=256 / 512 (A/B knob)
-int vn_block() {
-  static const int b = [] {
+// lz_step_vecnorm's envs per workgroup: kVnBlock on the fused path, kBlock on the split
+// path (the round-1 shape, faster there), or LZ_VN_BLOCK (A/B knob)
+int vn_fuse_max_wg() {
+  static const int m = [] {
+    const char* e = std::getenv("LZ_VN_FUSE_MAX_WG");
+    return e ? std::atoi(e) : 256;
+  }();
+  return m;
+}
+
+bool vn_fused(int64_t n) { return (n + kVnBlock - 1) / kVnBlock <= vn_fuse_max_wg(); }
+
+int vn_block(int64_t n) {
+  static const int forced = [] {
     const char* e = std::getenv("LZ_VN_BLOCK");
     const int b = e ? std::atoi(e) : 0;
-    return b == 256 || b == 512 ? b : kVnBlock;
+    return b == 256 || b == 512 || b == 1024 ? b : 0;
   }();
-  return b;
+  if (forced) return forced;
+  return vn_fused(n) ? kVnBlock : kBlock;
 }
 
 template <class Sys, typename T>
 static int launch_vn(const KArgs& a, const VArgs& v, hipStream_t s) {
   static_assert(Sys::O <= kVnMaxObs, "obs too wide for the VecNormalize epilogue");
-  const int vb = vn_block();
+  const int vb = vn_block(a.n);
   const unsigned grid = (unsigned)((a.n + vb - 1) / vb);
   if (vb == 1024)
     hipLaunchKernelGGL((k_step_vn<Sys, T, 24>), dim3(grid), dim3(1024), 0, s, a, v);
@@ -995,9 +1039,9 @@ static int launch_vn(const KArgs& a, const VArgs& v, hipStream_t s) {
     hipLaunchKernelGGL((k_step_vn<Sys, T, 8>), dim3(grid), dim3(512), 0, s, a, v);
   else
     hipLaunchKernelGGL((k_step_vn<Sys, T, 0>), dim3(grid), dim3(256), 0, s, a, v);
-  if (v.flags & LZ_VN_DEFER)
-    hipLaunchKernelGGL((k_vn_colsum<Sys::O>), dim3(1), dim3(kVnColBlock), 0, s, v, a.n, a.counter,
-                       v.n_done_out);
+  if ((v.flags & LZ_VN_DEFER) || ((v.flags & LZ_VN_TRAINING) && !v.fused))
+    hipLaunchKernelGGL((k_vn_colsum<Sys::O>), dim3(v.fused ? 1 : 2 * (Sys::O + 1)),
+                       dim3(kVnColBlock), 0, s, v, a.n, a.counter, v.n_done_out);
   return (int)hipGetLastError();
 }
 

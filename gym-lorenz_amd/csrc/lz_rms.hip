@@ -162,7 +162,7 @@ struct VnApplyArgs {
   int32_t* n_done_out;     // published from *counter by block 0 (nullable)
   double* os;        // obs_rms mean[O], var[O], count
   double* rs;        // ret_rms mean, var, count
-  lz::VnUpdate upd;  // statistics updates folded into this pass (upd.part != nullptr)
+  lz::VnUpdate upd;  // statistics updates folded into this pass (upd.part or upd.tot)
   double eps, clip_obs, clip_rew;
   float* obs_n;
   float* rew_n;
@@ -174,7 +174,9 @@ struct VnApplyArgs {
 
 typedef float f4a __attribute__((ext_vector_type(4)));
 
-template <typename T, int O>
+// kRed: this instance reduces the partials (fused path); the others carry no
+// reduction code (its accumulators would raise every instance's VGPR count)
+template <typename T, int O, bool kRed>
 __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
   constexpr int R = (O % 4 == 0) ? 1 : (O % 2 == 0 ? 2 : 4);
   constexpr int E = R * O;
@@ -189,10 +191,12 @@ __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
   f4a q[E / 4];
   float rw[R];
   uint8_t dn[R];
-  auto load_tile = [&](int64_t tl) {
+  auto load_obs = [&](int64_t tl) {
     const f4a* src = reinterpret_cast<const f4a*>(obs + tl * 256 * E);
 #pragma unroll
     for (int k = 0; k < E / 4; ++k) q[k] = __builtin_nontemporal_load(src + t + 256 * k);
+  };
+  auto load_rd = [&](int64_t tl) {  // a full tile's rewards / done bytes
     const int64_t r0 = (tl * 256 + t) * R;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -202,18 +206,27 @@ __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
   };
   if (p.n_done_out && blockIdx.x == 0 && t == 0) *p.n_done_out = *p.counter;
   int64_t tile = blockIdx.x;
-  const bool pre = kF32 && rows && p.vec && tile < p.row_tiles && tile_full(tile);
-  if (pre) load_tile(tile);
+  // (the split path has nothing to overlap: no prefetch, fewer live registers)
+  const bool pre = kRed && kF32 && rows && p.vec && tile < p.row_tiles && tile_full(tile);
+  if (pre) {
+    load_obs(tile);
+    load_rd(tile);
+  }
 
   double mean[O], sd[O], rsd;
-  if (p.upd.part) {
+  if (p.upd.part || p.upd.tot) {
     // RunningMeanStd.update_from_moments for every obs column (lanes 0..O-1) and the
     // returns (lane 64), from the step's column totals and the pre-step snapshot, then
     // broadcast through LDS
-    __shared__ double s_red[LZ_VN_RED(W)];
+    __shared__ double s_red[kRed ? LZ_VN_RED(W) : 1];
     __shared__ double s_tot[W];
     __shared__ double s_st[2 * O + 1];
-    lz::vn_col_totals<W>(p.upd.part, p.upd.n_wg, s_red, s_tot);
+    if constexpr (kRed) {
+      lz::vn_col_totals<W>(p.upd.part, p.upd.n_wg, s_red, s_tot);
+    } else {
+      if (t < W) s_tot[t] = p.upd.tot[t];
+      __syncthreads();
+    }
     const double* old = p.upd.old;
     const double bc = p.upd.batch;
     if (t < O) {
@@ -256,12 +269,16 @@ __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
   }
   if (rows) {
     __shared__ f4a lds[256 * E / 4];
-    for (; tile < p.row_tiles; tile += p.row_blocks) {
+    // split path: one tile per workgroup (the grid covers them), no loop
+    const int64_t tile_end = kRed ? p.row_tiles : (tile < p.row_tiles ? tile + 1 : tile);
+    for (; tile < tile_end; tile += p.row_blocks) {
       const int64_t r0 = (tile * 256 + t) * R;
       float x[E], y[E];
+      const bool pref = pre && tile == (int64_t)blockIdx.x;  // loaded before the statistics
+      bool rd = pref;                                        // rw / dn loaded
       if (kF32 && p.vec && tile_full(tile)) {
         // the workgroup's [256 R, O] slice moves as contiguous float4s through LDS
-        if (tile != (int64_t)blockIdx.x || !pre) load_tile(tile);
+        if (!pref) load_obs(tile);
         __syncthreads();  // the previous tile's stores have read lds
 #pragma unroll
         for (int k = 0; k < E / 4; ++k) lds[t + 256 * k] = q[k];
@@ -302,7 +319,9 @@ __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
             dn[k] = p.dones ? p.done[r0 + k] : 0;
           }
         }
+        rd = true;
       }
+      if (!rd) load_rd(tile);  // after the obs stores, as few registers live as possible
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         if (r0 + k >= p.n) break;
@@ -318,6 +337,128 @@ __global__ __launch_bounds__(256) void k_vn_apply(VnApplyArgs p) {
   const int64_t m = p.counter ? *p.counter : *p.n_done;
   const int64_t stride = (int64_t)(gridDim.x - p.row_blocks) * 256;
   for (int64_t j = (int64_t)(blockIdx.x - p.row_blocks) * 256 + t; j < m; j += stride) {
+#pragma unroll
+    for (int d = 0; d < O; ++d) {
+      const float x = (float)term[j * O + d];
+      p.term_n[j * O + d] =
+          p.norm_obs ? lz::rms_norm_sd((double)x, mean[d], sd[d], true, p.clip_obs) : x;
+    }
+  }
+}
+
+// The split path's normalise pass (n above the fused limit): one row tile per
+// workgroup, the statistics from the totals k_vn_colsum left, no prefetch -- the
+// round-1 kernel, kept as is because its lower register count (56 VGPRs against 76 for
+// the fused kernel's non-reducing instance) fits the whole 1M-env grid in one round.
+template <typename T, int O>
+__global__ __launch_bounds__(256) void k_vn_apply_split(VnApplyArgs p) {
+  constexpr int R = (O % 4 == 0) ? 1 : (O % 2 == 0 ? 2 : 4);
+  constexpr int E = R * O;
+  double mean[O], sd[O], rsd;
+  if (p.upd.tot) {
+    // RunningMeanStd.update_from_moments for every obs column (lanes 0..O-1) and the
+    // returns (lane 64), from the pre-step snapshot -- so no workgroup reads statistics
+    // that workgroup 0 is rewriting -- then broadcast through LDS
+    __shared__ double s_st[2 * O + 1];
+    const int t = (int)threadIdx.x;
+    const double* old = p.upd.old;
+    const double bc = p.upd.batch;
+    if (t < O) {
+      double nm = old[t], nv = old[O + t];
+      if (p.upd.upd_obs)
+        lz::rms_new(old[t], old[O + t], old[2 * O], bc, p.upd.tot[t], p.upd.tot[O + 1 + t], nm, nv);
+      s_st[t] = nm;
+      s_st[O + t] = sqrt(nv + p.eps);
+      if (blockIdx.x == 0 && p.upd.upd_obs) {
+        p.os[t] = nm;
+        p.os[O + t] = nv;
+        if (t == 0) p.os[2 * O] = old[2 * O] + bc;
+      }
+    }
+    if (t == 64) {
+      const double* r = old + 2 * O + 1;
+      double nm, nv;
+      lz::rms_new(r[0], r[1], r[2], bc, p.upd.tot[O], p.upd.tot[2 * O + 1], nm, nv);
+      s_st[2 * O] = sqrt(nv + p.eps);
+      if (blockIdx.x == 0) {
+        p.rs[0] = nm;
+        p.rs[1] = nv;
+        p.rs[2] = r[2] + bc;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < O; ++d) {
+      mean[d] = s_st[d];
+      sd[d] = s_st[O + d];
+    }
+    rsd = s_st[2 * O];
+  } else {
+#pragma unroll
+    for (int d = 0; d < O; ++d) {
+      mean[d] = p.os[d];
+      sd[d] = sqrt(p.os[O + d] + p.eps);
+    }
+    rsd = sqrt(p.rs[1] + p.eps);
+  }
+  const T* obs = static_cast<const T*>(p.obs);
+  if ((int)blockIdx.x < p.row_blocks) {
+    const int64_t r0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * R;
+    if (r0 >= p.n) return;  // only in the last (partial, barrier-free) tile
+    const bool tile_full = ((int64_t)blockIdx.x + 1) * 256 * R <= p.n;  // uniform
+    float x[E], y[E];
+    if (std::is_same<T, float>::value && p.vec && tile_full) {
+      // the workgroup's [256 R, O] slice moves as contiguous float4s through LDS
+      __shared__ f4a tile[256 * E / 4];
+      const f4a* src = reinterpret_cast<const f4a*>(obs + (int64_t)blockIdx.x * 256 * E);
+#pragma unroll
+      for (int k = 0; k < E / 4; ++k)  // raw obs: read once (non-temporal)
+        tile[threadIdx.x + 256 * k] = __builtin_nontemporal_load(src + threadIdx.x + 256 * k);
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < E / 4; ++k) {
+        const f4a q = tile[threadIdx.x * (E / 4) + k];
+        x[4 * k] = q[0]; x[4 * k + 1] = q[1]; x[4 * k + 2] = q[2]; x[4 * k + 3] = q[3];
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        y[e] = p.norm_obs ? lz::rms_norm_sd((double)x[e], mean[e % O], sd[e % O], true, p.clip_obs)
+                          : x[e];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < E / 4; ++k)
+        tile[threadIdx.x * (E / 4) + k] = (f4a){y[4 * k], y[4 * k + 1], y[4 * k + 2], y[4 * k + 3]};
+      __syncthreads();
+      f4a* dst = reinterpret_cast<f4a*>(p.obs_n + (int64_t)blockIdx.x * 256 * E);
+#pragma unroll
+      for (int k = 0; k < E / 4; ++k)  // normalised obs: written once (non-temporal)
+        __builtin_nontemporal_store(tile[threadIdx.x + 256 * k], dst + threadIdx.x + 256 * k);
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) x[e] = (r0 + e / O < p.n) ? (float)obs[r0 * O + e] : 0.0f;
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        y[e] = p.norm_obs ? lz::rms_norm_sd((double)x[e], mean[e % O], sd[e % O], true, p.clip_obs)
+                          : x[e];
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (r0 + e / O < p.n) p.obs_n[r0 * O + e] = y[e];
+    }
+    const T* rew = static_cast<const T*>(p.rew);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if (r0 + k >= p.n) break;
+      const float r = (float)rew[r0 + k];
+      p.rew_n[r0 + k] = p.norm_rew ? lz::rms_norm_sd((double)r, 0.0, rsd, false, p.clip_rew) : r;
+      if (p.dones) p.dones[r0 + k] = p.done[r0 + k] != 0;
+    }
+    return;
+  }
+  if (p.term == nullptr) return;
+  const T* term = static_cast<const T*>(p.term);
+  const int64_t m = *p.n_done;
+  const int64_t stride = (int64_t)(gridDim.x - p.row_blocks) * 256;
+  for (int64_t j = (int64_t)(blockIdx.x - p.row_blocks) * 256 + threadIdx.x; j < m; j += stride) {
 #pragma unroll
     for (int d = 0; d < O; ++d) {
       const float x = (float)term[j * O + d];
@@ -397,19 +538,29 @@ int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
   p.norm_rew = norm_rew;
   p.vec = !f64 && ((uintptr_t)obs % 16 == 0) && ((uintptr_t)obs_n % 16 == 0);
   p.row_tiles = (n + 256 * R - 1) / (256 * R);
-  // at most vn_apply_blocks() row workgroups (each reduces the partials once)
-  const int64_t cap = vn_apply_blocks();
+  // fused: at most vn_apply_blocks() row workgroups (each reduces the partials once);
+  // otherwise one per row tile
+  const int64_t cap = upd.part ? vn_apply_blocks() : p.row_tiles;
   p.row_blocks = (int)(p.row_tiles < cap ? p.row_tiles : cap);
   const int tb = term ? (p.row_blocks < 64 ? p.row_blocks : 64) : 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)(p.row_blocks + tb)), block(256);
+  // 1: reduce the partials here (fused); 0: publish the done count, no reduction (not
+  // training); 2: the split path's round-1 kernel (totals from k_vn_colsum, which also
+  // published the done count)
+  const int kind = upd.part ? 1 : counter ? 0 : 2;
+#define LZ_VN_APPLY(T, O_)                                                                        \
+  if (kind == 1) hipLaunchKernelGGL((k_vn_apply<T, O_, true>), grid, block, 0, s, p);             \
+  else if (kind == 0) hipLaunchKernelGGL((k_vn_apply<T, O_, false>), grid, block, 0, s, p);       \
+  else hipLaunchKernelGGL((k_vn_apply_split<T, O_>), grid, block, 0, s, p);
   switch (O * 2 + (f64 ? 1 : 0)) {
-    case 12: hipLaunchKernelGGL((k_vn_apply<float, 6>), grid, block, 0, s, p); break;
-    case 13: hipLaunchKernelGGL((k_vn_apply<double, 6>), grid, block, 0, s, p); break;
-    case 16: hipLaunchKernelGGL((k_vn_apply<float, 8>), grid, block, 0, s, p); break;
-    case 17: hipLaunchKernelGGL((k_vn_apply<double, 8>), grid, block, 0, s, p); break;
+    case 12: LZ_VN_APPLY(float, 6) break;
+    case 13: LZ_VN_APPLY(double, 6) break;
+    case 16: LZ_VN_APPLY(float, 8) break;
+    case 17: LZ_VN_APPLY(double, 8) break;
     default: return (int)hipErrorInvalidValue;
   }
+#undef LZ_VN_APPLY
   return (int)hipGetLastError();
 }
 

@@ -233,7 +233,14 @@ if len(HIP_RUNTIME) != 1:
         "libgym_lorenz_amd.so must share one.  Import torch (or gym_lorenz) before "
         "anything that loads a libamdhip64 directly." % (len(HIP_RUNTIME), ", ".join(HIP_RUNTIME)))
 for _name, (_res, _args) in _SIGS.items():
-    _f = getattr(lib, _name)
+    try:
+        _f = getattr(lib, _name)
+    except AttributeError:
+        # an older build loaded on purpose by the A/B tooling (tools/ab_lib.py sets
+        # LZ_LIB_AB) may predate an entry point; the product library has them all
+        if os.environ.get("LZ_LIB_AB"):
+            continue
+        raise
     _f.restype = _res
     _f.argtypes = _args
 

@@ -44,6 +44,7 @@ def _vn(gl, n, env_id="lorenz_pmsm-v0", seed=5, mes=37, dtype="float32", **kw):
     ("lorenz_pmsm-v0", 300, "float32", 2, 6, False),          # 2 workgroups, 1 group
     ("lorenz_transient-v0", 5000, "float32", 3, 8, True),     # obs_dim 8
     ("lorenz_dynamic-v0", 4096 + 5, "float64", 3, 6, True),   # fp64 env, float32 VecEnv view
+    ("lorenz_pmsm-v0", 400000 + 13, "float32", 2, 6, True),   # 391 partials: split path
 ])
 def test_fused_vecnormalize_matches_sb3_restatement(gl, env_id, n, dtype, act_dim, obs_dim,
                                                     norm_reward):
@@ -58,17 +59,20 @@ def test_fused_vecnormalize_matches_sb3_restatement(gl, env_id, n, dtype, act_di
     # the same statistics from float64 copies of the float32 obs: SB3's np.mean / np.var
     # run in float32 (rel error ~1e-6 at 20k rows), the device sums in float64
     ref64 = RunningMeanStd(shape=(obs_dim,))
+    # above ~1e5 rows SB3's float32 np.mean / np.var over axis 0 (a row-by-row sum) is
+    # itself off by ~1e-4: feed the restatement float64 copies there
+    cast = (lambda x: x.astype(np.float64)) if n > 100000 else (lambda x: x)
     o_raw = raw.reset()
     ref64.update(o_raw.astype(np.float64))
-    np.testing.assert_allclose(dev.reset(), ref.reset(o_raw), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(dev.reset(), ref.reset(cast(o_raw)), rtol=1e-5, atol=1e-5)
     rng = np.random.default_rng(0)
     lo = 1.0 if env_id != "lorenz_dynamic-v0" else 5.0
     saw_done = 0
     for k in range(25):
         a = rng.uniform(-lo, lo, (n, act_dim)).astype(np.float32)
         o_raw, r_raw, d_raw, i_raw = raw.step(a)
-        term = {i: i_raw[i]["terminal_observation"] for i in np.nonzero(d_raw)[0]}
-        o_ref, r_ref, d_ref, tn_ref = ref.step(o_raw, r_raw, d_raw, term)
+        term = {i: cast(i_raw[i]["terminal_observation"]) for i in np.nonzero(d_raw)[0]}
+        o_ref, r_ref, d_ref, tn_ref = ref.step(cast(o_raw), r_raw, d_raw, term)
         ref64.update(o_raw.astype(np.float64))
         o_dev, r_dev, d_dev, i_dev = dev.step(a)
         assert np.array_equal(d_dev, d_raw)
@@ -120,12 +124,14 @@ def test_fused_matches_unfused_and_is_deterministic(gl):
         assert np.array_equal(x[2], y[2])
 
 
-def test_defer_matches_in_kernel_update(gl):
+@pytest.mark.parametrize("n", [20000, 400000 + 13])  # fused / split reduction
+def test_defer_matches_in_kernel_update(gl, n):
     """The multi-GPU split (moments out, all-reduce, update in lz_vecnorm_apply) with a
-    one-rank 'all-reduce' (identity) is bit-identical to the in-kernel update."""
+    one-rank 'all-reduce' (identity) is bit-identical to the in-kernel update, with the
+    normalise pass reducing the partials itself (20k envs) or k_vn_colsum doing it once
+    (400k envs: more than 384 partials per column)."""
     import gym_lorenz._native as nat
 
-    n = 20000
     va, vb = _vn(gl, n, norm_reward=True), _vn(gl, n, norm_reward=True)
     va.reset(), vb.reset()
     vb.group = object()  # DEFER flag; the all-reduce itself is skipped below
