@@ -14,12 +14,13 @@ vec_normalize.py) but runs it on the GPU over the LorenzVecEnv's device outputs
               terminal observations normalised; returns[dones] = 0
   reset:      returns = 0; obs_rms.update(obs); normalised obs
 
-step_wait over a LorenzVecEnv runs as two launches and no host synchronisation
-(lz_step_vecnorm + lz_vecnorm_apply): the env step kernel also produces float64
-per-workgroup moments of the observations and of the updated returns; every
-workgroup of the second kernel reduces them in one fixed order, applies the two
-RunningMeanStd updates and writes the normalised obs / rewards / terminal
-observations and the bool dones.  infos are materialised lazily (only done envs get
+step_wait over a LorenzVecEnv runs as two launches (three above 262,144 envs) and no
+host synchronisation (lz_step_vecnorm + lz_vecnorm_apply): the env step kernel also
+produces float64 per-workgroup moments of the observations and of the updated
+returns; they are reduced in one fixed order (by every workgroup of the normalise
+kernel, or above 262,144 envs by a column-total launch), and the normalise kernel
+applies the two RunningMeanStd updates and writes the normalised obs / rewards /
+terminal observations and the bool dones.  infos are materialised lazily (only done envs get
 dicts, on first access).
 
 Multi-GPU: pass `group` (a torch.distributed process group): the batch moments

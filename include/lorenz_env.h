@@ -499,14 +499,15 @@ lz_status lz_returns_update(double* returns, const void* rew, int32_t dtype, con
  *   obs_out  = NORM_OBS    ? clip((obs - mean)/sqrt(var + eps), +-clip_obs)  : obs
  *   rew_out  = NORM_REWARD ? clip(reward/sqrt(ret_var + eps), +-clip_reward) : reward
  *   terminal observations normalised like obs; returns[done] = 0
- * lz_step_vecnorm runs the env step (one launch: its kernel also writes float64
- * per-workgroup moment partials of the obs and of the updated returns);
- * lz_vecnorm_apply (one launch) reduces them in a fixed order (deterministic, no float
- * atomics; every workgroup derives the same totals), applies the two RunningMeanStd
- * updates (workgroup 0 writes them back) and writes the normalised outputs.  Call the
- * two as a pair, apply right after step on the same stream: the statistics are updated,
- * and the step's *n_done_out is written, by the lz_vecnorm_apply launch.  With
- * LZ_VN_DEFER the step adds a second launch that publishes *n_done_out and leaves the
+ * lz_step_vecnorm runs the env step (its kernel also writes float64 per-workgroup
+ * moment partials of the obs and of the updated returns); the partials are reduced in
+ * a fixed order (deterministic, no float atomics) -- up to 262,144 envs by every
+ * workgroup of lz_vecnorm_apply, above that by a second launch of lz_step_vecnorm --
+ * and lz_vecnorm_apply (one launch) applies the two RunningMeanStd updates (workgroup 0
+ * writes them back) and writes the normalised outputs.  Call the two as a pair, apply
+ * right after step on the same stream: the statistics are updated, and (without a
+ * second launch) the step's *n_done_out is written, by the lz_vecnorm_apply launch.
+ * With LZ_VN_DEFER the step's second launch publishes *n_done_out and leaves the
  * batch moments (obs: count, sums[O], sumsq[O]; then returns: count, sum, sumsq) in
  * moments for a multi-GPU all-reduce, and lz_vecnorm_apply performs the updates first.  Every
  * pointer is device memory; the statistics are those of the two lz_rms objects (dims
