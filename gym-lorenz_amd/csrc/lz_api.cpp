@@ -609,6 +609,11 @@ lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noi
   if (h->cfg.flags & LZ_FLAG_AUTORESET)
     return fail(LZ_ERR_UNSUPPORTED, "lz_resident_step: handles without LZ_FLAG_AUTORESET only");
   HIP_TRY(hipSetDevice(h->cfg.device));
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (h->stream && hipStreamIsCapturing(h->stream, &cap) == hipSuccess &&
+      cap != hipStreamCaptureStatusNone)
+    return fail(LZ_ERR_STATE, "lz_resident_step: the handle's stream is being captured "
+                              "(a synchronous host round trip cannot be captured)");
   const size_t es = h->f64 ? 8 : 4;
   if (!h->rs_pin) {
     const size_t bytes = rs_done_off(h) + align16((size_t)n);

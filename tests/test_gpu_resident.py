@@ -213,3 +213,29 @@ def test_process_exit_with_live_server(close):
             "print('ok')\n" % (ROOT + "/gym-lorenz_amd", "e.close()" if close else "pass"))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_resident_refused_under_capture(gl):
+    """A resident step is a synchronous host round trip: refused while the handle's
+    stream is being captured into a hipGraph."""
+    import ctypes
+
+    import gym_lorenz._native as nat
+    from gym_lorenz.core import BatchedEnv
+
+    be = BatchedEnv("lorenz3", 1, autoreset=False, compact=False)
+    be.reset()
+    torch.cuda.synchronize()
+    o, r, d = _bufs(be)
+    act = np.zeros((1, 3), np.float32)
+    s = torch.cuda.Stream()
+    nat.check(nat.lib.lz_set_stream(be._h, ctypes.c_void_p(s.cuda_stream)))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        torch.zeros(1, device="cuda")  # keep the capture non-empty
+        st = nat.lib.lz_resident_step(be._h, act.ctypes.data, None, o.ctypes.data,
+                                      r.ctypes.data, d.ctypes.data)
+    assert st == nat.LZ_ERR_STATE
+    nat.check(nat.lib.lz_set_stream(be._h, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    _step(nat.lib.lz_resident_step, be, act, None, (o, r, d))  # fine outside the capture
+    be.close()
