@@ -254,7 +254,8 @@ lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, 
  * LZ_RESIDENT_IDLE_US (default 1000) microseconds without a request and is
  * relaunched by the next call (a device-wide synchronize waits for that exit); every
  * other call on the handle stops it first (its state goes back to the planes), as
- * does lz_resident_stop. */
+ * does lz_resident_stop.  Synchronous: LZ_ERR_STATE while the handle's stream is
+ * being captured into a graph. */
 lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noise,
                            void* obs_out, void* rew_out, uint8_t* done_out);
 lz_status lz_resident_stop(lz_handle* h);
