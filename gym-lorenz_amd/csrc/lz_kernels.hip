@@ -946,11 +946,14 @@ __global__ __launch_bounds__(64) void k_resident(KArgs a, ResBox box) {
       for (int j = 0; j < Sys::A; ++j)
         act[j] = __hip_atomic_load(box.act + lane * Sys::A + j, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
-      if (box.use_noise) {
+      if (box.use_noise) {  // the three loads in flight together, then into LDS
+        double nzv[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          s_nz[lane * 3 + j] = __hip_atomic_load(box.noise + lane * 3 + j, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_SYSTEM);
+          nzv[j] = __hip_atomic_load(box.noise + lane * 3 + j, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) s_nz[lane * 3 + j] = nzv[j];
       }
     }
     T o[Sys::O];
