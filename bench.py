@@ -308,6 +308,12 @@ def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
     achieved = bytes_step * n / step_s / 1e9
     obs_rms.close()
     ret_rms.close()
+    # PMC bytes of the two kernels (tools/pmc_vecnorm.sh summaries), when committed for
+    # this system and size
+    tr = [load_traffic(k, n) for k in (
+        "_ZN2lz9k_step_vnINS_7SysPMSMEfLi24EEEvNS_5KArgsENS_5VArgsE",
+        "_ZN12_GLOBAL__N_110k_vn_applyIfLi6ELb1EEEvNS_11VnApplyArgsE")] if args.system == "pmsm" else [None]
+    traffic = sum(t["bytes_per_launch"] for t in tr) if all(tr) else None
     return {
         "metric": METRIC, "value": total * steps / elapsed, "unit": "env-steps/s",
         "n_gpus": world, "steps": steps, "warmup": args.warmup,
@@ -328,7 +334,8 @@ def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
             "launch": "hipGraph of %d steps" % L},
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_source": [t["source"] for t in tr] if traffic else None,
             "kernel": "k_step_vn + k_vn_apply (one fused VecNormalize step)",
             "avg_launch_us": step_s * 1e6, "bytes_per_env_step": bytes_step,
             "note": "achieved = algorithmic bytes of the whole fused step (lz_step's + 16 B of "
