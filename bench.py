@@ -61,6 +61,11 @@ def parse():
     p.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                    help="--mode policy --policy mlp: fp32 = SB3's float32 forward "
                         "(lz_rollout_policy_f32), bf16 = the bf16-MFMA kernel")
+    p.add_argument("--vecnorm-update", choices=["step", "rollout"], default="step",
+                   help="--mode policy --policy mlp fp32: step = SB3's VecNormalize order (obs_rms "
+                        "updated by every step's batch before it is normalised; one launch per "
+                        "step, lz_rollout_policy_f32_vn); rollout = one K-step launch with the "
+                        "rollout-start statistics and a pooled update (opt-in, not SB3's order)")
     p.add_argument("--policy", choices=["mlp", "attn", "attn_ln"], default="mlp",
                    help="--mode policy: mlp = SB3 MlpPolicy behind VecNormalize (the PMSM A2C "
                         "learner, code/lorenz_pmsm/train.py); attn = code/train.py's PPO policy "
@@ -379,9 +384,12 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
            else ActorCriticMlp(O, A, seed=0))
     rms = None if attn else DeviceRunningMeanStd(O, device)
     f32 = not attn and args.precision == "fp32"
+    per_step = f32 and args.vecnorm_update == "step"
     col = FusedRolloutCollector(env, net.state_dict(), gamma=0.99, gae_lambda=0.95, obs_rms=rms,
                                 clip_obs=10.0, training=True, bootstrap=True, frame_stack=stack,
-                                precision="fp32" if f32 else "bf16")
+                                precision="fp32" if f32 else "bf16",
+                                vecnorm_update=("step" if per_step else "rollout") if f32 else None)
+    assert col.per_step_vecnorm == per_step
     stream = torch.cuda.Stream(device)
     with torch.cuda.stream(stream):
         nat.check(nat.lib.lz_set_stream(env._h, ctypes.c_void_p(stream.cuda_stream)))
@@ -455,14 +463,23 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
                          "+ env step + truncation bootstrap), GAE (lz_gae); %d envs total, %d per "
                          "GPU" if attn else
                          "%s with the SB3 A2C/PPO MlpPolicy (pi/vf [128,128] Tanh) in the loop: "
-                         "%d-step fused rollout (lz_rollout_policy" + ("_f32, float32 as SB3" if f32 else
-                                                                     ", bf16 MFMA")
-                         + ": policy forward + DiagGaussian "
-                         "sample + clip + env step + truncation bootstrap + VecNormalize obs), "
-                         "obs_rms update, GAE (lz_gae); %d envs total, %d per GPU")
+                         + ("%d-step collect in SB3's VecNormalize order (lz_rollout_policy_f32_vn: "
+                            "per step one launch of VecNormalize obs with the statistics updated by "
+                            "the previous step's batch + float32 policy forward + DiagGaussian sample "
+                            "+ clip + env step + float64 tile moments, then the obs_rms update; "
+                            "truncation bootstraps valued with their step's statistics), GAE "
+                            "(lz_gae); %d envs total, %d per GPU" if per_step else
+                            "%d-step fused rollout (lz_rollout_policy" + ("_f32, float32 as SB3" if f32 else
+                                                                          ", bf16 MFMA")
+                            + ": policy forward + DiagGaussian "
+                            "sample + clip + env step + truncation bootstrap + VecNormalize obs with "
+                            "the rollout-start statistics), pooled obs_rms update, GAE (lz_gae); "
+                            "%d envs total, %d per GPU"))
                         % (SYSTEM_INFO[args.system][0], K, total, n),
             "system": args.system, "envs_total": total, "envs_per_gpu": n, "mode": "policy",
             "policy": args.policy, "precision": "fp32" if f32 else "bf16",
+            "vecnorm_update": None if attn else ("step (SB3 order)" if per_step
+                                                 else "rollout (pooled, opt-in)"),
             "K": K, "parallelism": "env shard x%d (no collective on step; obs_rms moments "
                                    "all-reduced once per rollout when N>1)" % world,
         },
@@ -473,6 +490,8 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
                        if ln else
                        "_ZN2lz16k_rollout_policyINS_%sLi4ELi32ELi3EEEvNS_5KArgsENS_5PArgsE"
                        if attn else
+                       "_ZN2lz17k_policy_step_f32INS_%sLi8EEEvNS_5KArgsENS_5PArgsENS_9PStepArgsE"
+                       if per_step else
                        "_ZN2lz16k_rollout_policyINS_%sLi8ELi32ELi5ELi1EEEvNS_5KArgsENS_5PArgsE"
                        if f32 else "_ZN2lz16k_rollout_policyINS_%sLi8EEEvNS_5KArgsENS_5PArgsE")
                       % mangled,
@@ -480,6 +499,9 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
             "note": ("achieved = useful FLOP of the attention actor-critic as SB3 computes it "
                      "(extractor + pi + vf, %d per env-step) x envs x K / HIP-event time of one "
                      "collect() (one policy-rollout launch)" if attn else
+                     "achieved = useful MLP FLOP (pi + vf, %d per env-step) x envs x K / HIP-event "
+                     "time of one collect() (K + 1 policy-step launches + K statistics updates)"
+                     if per_step else
                      "achieved = useful MLP FLOP (pi + vf, %d per env-step) x envs x K / HIP-event "
                      "time of one collect() (policy kernel + a 1-block moments reduction + the "
                      "obs_rms update)") % fl,

@@ -97,6 +97,12 @@ struct lz_handle {
   int num_cus;         // compute units of the device (policy rollout grid)
   double* pol_part;    // policy rollout obs-moment partials (lazily allocated)
   int64_t pol_part_n;  // doubles allocated
+  // lz_policy_step_f32 (SB3-exact VecNormalize): tile moments [2 O][ntiles] + the
+  // statistics snapshot [2 O + 1], the raw terminal-obs carry [N, O], the collect's
+  // compact-list cursor (+ one spare int), all lazily allocated
+  double* ps_tiles;
+  float* ps_term;
+  int32_t* ps_cursor;
   uint8_t* vn_ws;      // lz_step_vecnorm moment partials (lazily allocated)
   int vn_pending;      // lz_step_vecnorm left totals for lz_vecnorm_apply's updates
   int32_t* vn_nd_out;  // lz_step_vecnorm's n_done_out, published by lz_vecnorm_apply
@@ -314,6 +320,9 @@ lz_status lz_destroy(lz_handle* h) {
   if (h->ticks) (void)hipFree(h->ticks);
   if (h->bc) (void)hipFree(h->bc);
   if (h->pol_part) (void)hipFree(h->pol_part);
+  if (h->ps_tiles) (void)hipFree(h->ps_tiles);
+  if (h->ps_term) (void)hipFree(h->ps_term);
+  if (h->ps_cursor) (void)hipFree(h->ps_cursor);
   if (h->vn_ws) (void)hipFree(h->vn_ws);
   if (h->hs_pin) (void)hipHostFree(h->hs_pin);  // hs_dev is its mapped device address
   delete h;
@@ -936,6 +945,109 @@ lz_status lz_rollout_policy_f32(lz_handle* h, const lz_policy_rollout_args* r) {
 
 lz_status lz_rollout_policy_attn(lz_handle* h, const lz_policy_rollout_args* r) {
   return rollout_policy(h, r, 1);
+}
+
+// ---- SB3-exact VecNormalize in the float32 rollout (lz_internal.h PStepArgs)
+lz_status lz_policy_step_f32(lz_handle* h, const lz_policy_rollout_args* r, int32_t k,
+                             double* obs_rms_state, double* moments_out) {
+  if (!h || !r) return fail(LZ_ERR_INVALID, "handle/args is NULL");
+  RESIDENT_QUIESCE(h);
+  if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_policy_step_f32 before the first lz_reset");
+  if (h->f64) return fail(LZ_ERR_UNSUPPORTED, "the policy rollout runs float32 handles only");
+  if (r->K <= 0) return fail(LZ_ERR_INVALID, "K must be >= 1");
+  if (k < 0 || k > r->K) return fail(LZ_ERR_INVALID, "step %d outside [0, K = %d]", k, r->K);
+  if (!obs_rms_state) return fail(LZ_ERR_INVALID, "obs_rms_state must be non-NULL");
+  if (r->obs_norm && r->obs_norm != obs_rms_state)
+    return fail(LZ_ERR_INVALID, "obs_norm must be NULL or obs_rms_state");
+  if (r->obs_moments) return fail(LZ_ERR_INVALID, "obs_moments must be NULL (per-step statistics)");
+  if (!r->blob || !r->obs_in || !r->obs_last || !r->obs_buf || !r->act_buf || !r->logp_buf ||
+      !r->val_buf || !r->rew_buf || !r->done_buf || !r->last_values)
+    return fail(LZ_ERR_INVALID, "blob / obs / rollout buffers must be non-NULL");
+  if ((r->done_idx == nullptr) != (r->terminal_obs == nullptr))
+    return fail(LZ_ERR_INVALID, "done_idx and terminal_obs go together");
+  if ((int64_t)r->K * h->cfg.num_envs > ((int64_t)1 << 40)) return fail(LZ_ERR_INVALID, "K*N too large");
+  if (!(r->act_low <= r->act_high)) return fail(LZ_ERR_INVALID, "act_low > act_high");
+  const int O = h->desc.obs_dim;
+  if (O > lz::kVnMaxObs) return fail(LZ_ERR_UNSUPPORTED, "obs too wide");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  const int64_t n = h->cfg.num_envs;
+  const int64_t ntiles = (n + lz::kVnTile - 1) / lz::kVnTile;
+  if (!h->ps_tiles) {
+    double* t = nullptr;
+    float* term = nullptr;
+    int32_t* cur = nullptr;
+    const size_t bt = (size_t)(2 * O * ntiles + 2 * O + 1) * sizeof(double);
+    if (hipMalloc(reinterpret_cast<void**>(&t), bt) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&term), (size_t)n * O * sizeof(float)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&cur), 2 * sizeof(int32_t)) != hipSuccess) {
+      if (t) (void)hipFree(t);
+      if (term) (void)hipFree(term);
+      return fail(LZ_ERR_OOM, "lz_policy_step_f32 scratch allocation failed");
+    }
+    h->ps_tiles = t;
+    h->ps_term = term;
+    h->ps_cursor = cur;
+  }
+  const bool fin = k == r->K;
+  if (k == 0) HIP_TRY(hipMemsetAsync(h->ps_cursor, 0, 2 * sizeof(int32_t), h->stream));
+  const lz::PolShape sh = lz::f32_policy_shape(n, h->num_cus);
+  KArgs a;
+  fill_common(h, a);
+  a.obs = r->obs_buf;
+  a.rew = r->rew_buf;
+  a.done = r->done_buf;
+  a.done_idx64 = r->done_idx;
+  a.term_obs = r->terminal_obs;
+  a.term_cap = r->cap;
+  a.K = r->K;
+  a.counter = h->ps_cursor;       // one cursor for the whole collect (zeroed at k = 0)
+  a.counter_next = h->ps_cursor + 1;
+  lz::PArgs p;
+  std::memset(&p, 0, sizeof p);
+  p.blob = static_cast<const uint8_t*>(r->blob);
+  p.obs_in = r->obs_in;
+  p.obs_last = r->obs_last;
+  p.norm = obs_rms_state;
+  p.eps = r->norm_eps;
+  p.clip = r->clip_obs;
+  p.gamma = (float)r->gamma;
+  p.act_lo = r->act_low;
+  p.act_hi = r->act_high;
+  p.pflags = r->flags;
+  p.act = r->act_buf;
+  p.logp = r->logp_buf;
+  p.val = r->val_buf;
+  p.last_val = r->last_values;
+  lz::PStepArgs st;
+  std::memset(&st, 0, sizeof st);
+  st.k = k;
+  st.final_ = fin ? 1 : 0;
+  st.ntiles = ntiles;
+  st.tiles = fin ? nullptr : h->ps_tiles;
+  st.snap = fin ? nullptr : h->ps_tiles + 2 * O * ntiles;
+  st.term = h->ps_term;
+  st.obs_src = k == 0 ? r->obs_in : r->obs_last;
+  int e = lz::launch_policy_step_f32(h->cfg.system, a, p, st, sh, h->stream);
+  if (e != 0) return fail(LZ_ERR_HIP, "policy step launch: %s", hipGetErrorString((hipError_t)e));
+  if (!fin) {
+    h->parity ^= 1;  // the launch advanced the RNG tick by one (ping-pong)
+    e = lz::launch_vn_tile_update(st.tiles, ntiles, O, (double)n, st.snap, obs_rms_state, moments_out,
+                                  h->stream);
+    if (e != 0) return fail(LZ_ERR_HIP, "statistics update launch: %s", hipGetErrorString((hipError_t)e));
+  } else if (r->n_done) {
+    HIP_TRY(hipMemcpyAsync(r->n_done, h->ps_cursor, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
+  }
+  return LZ_OK;
+}
+
+lz_status lz_rollout_policy_f32_vn(lz_handle* h, const lz_policy_rollout_args* r,
+                                   double* obs_rms_state) {
+  if (!h || !r) return fail(LZ_ERR_INVALID, "handle/args is NULL");
+  for (int32_t k = 0; k <= r->K; ++k) {
+    const lz_status s = lz_policy_step_f32(h, r, k, obs_rms_state, nullptr);
+    if (s != LZ_OK) return s;
+  }
+  return LZ_OK;
 }
 
 lz_status lz_rollout_policy_attn_stack(lz_handle* h, const lz_policy_rollout_args* r,

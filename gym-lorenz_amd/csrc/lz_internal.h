@@ -203,6 +203,39 @@ struct PArgs {
   float* stack_out;        // kPair 4: [N, n_stack * O] after the K steps
 };
 
+// SB3-exact VecNormalize in the float32 policy rollout (lz_policy_step_f32): one env
+// step per launch, because step k's policy input is normalised with statistics that
+// include step k's whole batch (VecNormalize.step_wait updates obs_rms, then normalises).
+// Launch k < K: deferred truncation bootstrap of step k-1, normalise obs_src with the
+// statistics p.norm holds (S_k), forward, sample, env step, raw obs -> p.obs_last, the
+// float64 tile moments of that raw obs -> tiles; then k_vn_tile_update (lz_rms.hip)
+// turns snap (= S_k) + the tile moments into S_{k+1} in place.  Launch K (final): the
+// bootstrap of step K-1 and the last values only.
+//
+// Moment order (restated by oracle/lz_oracle.c orc_vn_tile_totals): tile t = envs
+// 32t .. 32t+31 (0.0 past n); per tile a 32-lane butterfly v_l += v_{l ^ m}, m = 16, 8,
+// 4, 2, 1 of (double)x (sums) and (double)x * (double)x (squares); per column thread
+// tau < 256 sums tiles tau, tau + 256, ... from 0.0 in order, then the LDS tree
+// s[tau] += s[tau + m], m = 128 .. 1; then RunningMeanStd.update_from_moments
+// (lz_rms_math.h rms_new) with batch count n.
+constexpr int kVnTile = 32;
+struct PStepArgs {
+  int32_t k;            // step of the collect (the tick advances once per step launch)
+  int32_t final_;       // the epilogue launch (k == K)
+  int64_t ntiles;       // ceil(n / kVnTile): column stride of tiles
+  double* tiles;        // [2 O][ntiles] float64 tile moments of the step's raw obs
+  double* snap;         // [2 O + 1] the statistics this launch normalised with (block 0)
+  float* term;          // [N, O] raw terminal obs of the step's done envs (carry)
+  const float* obs_src; // [N, O] raw obs the policy sees this step
+};
+// S_{k+1} from snap + tiles (moments == nullptr), or (moments != nullptr) the batch
+// moments (n, sums[O], sums of squares[O]) for a multi-GPU all-reduce + lz_rms_update
+int launch_vn_tile_update(const double* tiles, int64_t ntiles, int O, double batch,
+                          const double* snap, double* state, double* moments, void* stream);
+// tile moments of x [n, O] float32 in the order above (block 0 snapshots state -> snap)
+int launch_obs_tile_moments(const float* x, int64_t n, int O, double* tiles, const double* state,
+                            double* snap, void* stream);
+
 // lz_rms internals for the fused VecNormalize step (lz_rms.hip)
 int rms_dim(const lz_rms* r);
 int rms_device(const lz_rms* r);
@@ -296,6 +329,9 @@ int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, const PolS
 PolShape f32_policy_shape(int64_t n, int num_cus);
 int launch_rollout_policy_f32(int system, const KArgs& a, const PArgs& p, const PolShape& sh,
                               void* stream);
+// SB3-exact VecNormalize: one step of the float32 policy rollout (PStepArgs above)
+int launch_policy_step_f32(int system, const KArgs& a, const PArgs& p, const PStepArgs& s,
+                           const PolShape& sh, void* stream);
 // the attention-extractor policy (kAtt* blob): one shape, 32 envs per wave, 4 waves
 // (one per SIMD: the 137 KB blob leaves room for one workgroup per CU)
 PolShape attn_policy_shape(int64_t n, int num_cus);

@@ -1104,6 +1104,162 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// SB3-exact VecNormalize in the float32 rollout (lz_policy_step_f32).  SB3 2.7.1's
+// collect_rollouts under VecNormalize(training=True) (code/lorenz_pmsm/train.py:170-181):
+//   step k:   actions, values = policy(_last_obs)            (_last_obs normalised by S_k)
+//             obs, rew, done, infos = venv.step(clip(actions))  -> raw obs_{k+1}
+//             VecNormalize.step_wait: S_{k+1} = obs_rms.update(S_k, raw obs_{k+1} batch);
+//               obs_{k+1} = normalise(raw, S_{k+1}); infos' terminal obs normalised by
+//               S_{k+1} too
+//             truncated: rew += gamma * V(terminal obs)       (needs S_{k+1})
+// Step k's input depends on a reduction over the whole batch of step k's outputs, so
+// the collect runs one launch per step with the statistics update between launches
+// (k_vn_tile_update), and each launch first settles the previous step's truncation
+// bootstraps with the statistics that step produced.  Per launch: the blob to LDS, the
+// env state from / to its planes (no VGPR residency across steps), the raw obs carry.
+// The forward is mlp_f32 (the same bits as k_rollout_policy<kMlpF32>); the obs moments
+// are float64 sums per 32-env tile (lz_internal.h PStepArgs: the order the oracle
+// restates).  32 envs per wave: lane r (h = 0) owns env r, lane r + 32 its second half.
+template <class Sys, int W>
+__global__ __launch_bounds__(W * 64) void k_policy_step_f32(KArgs a, PArgs p, PStepArgs s) {
+  constexpr int O = Sys::O, A = Sys::A, KS1 = (O + 1) / 2;
+  static_assert(O <= kPolMaxObs && A <= kPolMaxAct, "policy tile shape");
+  __shared__ __attribute__((aligned(64))) uint8_t s_blob[kF32BlobBytes];
+  __shared__ double s_norm[2 * kPolMaxObs];
+  const int tid = (int)threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int slot = lane & 31;
+  {
+    const f4v* src = reinterpret_cast<const f4v*>(p.blob);
+    f4v* dst = reinterpret_cast<f4v*>(s_blob);
+    for (int v = tid; v < kF32BlobBytes / 16; v += W * 64) dst[v] = src[v];
+  }
+  if (tid < O) {
+    s_norm[tid] = p.norm[tid];
+    s_norm[kPolMaxObs + tid] = sqrt(p.norm[O + tid] + p.eps);
+  }
+  // S_k for the update after this launch (read-only there: no race with the write-back)
+  if (blockIdx.x == 0 && s.snap && tid < 2 * O + 1) s.snap[tid] = p.norm[tid];
+  const uint64_t tick = *a.tick_in;
+  if (blockIdx.x == 0 && tid == 0 && !s.final_) *a.tick_out = tick + 1;
+  __syncthreads();
+  const uint8_t* pi_net = s_blob;
+  const uint8_t* vf_net = s_blob + kF32Net;
+  const float* ttab = reinterpret_cast<const float*>(s_blob + kF32Tanh);
+  const float* g_scale = reinterpret_cast<const float*>(s_blob + kF32LogStd) + 4;
+  const float* g_var2 = g_scale + 4;
+  const float* g_lscale = g_scale + 8;
+  const double* mu = s_norm;
+  const double* sd = s_norm + kPolMaxObs;
+  const bool det = (p.pflags & LZ_POLICY_DETERMINISTIC) != 0;
+  const bool boot = (p.pflags & LZ_POLICY_BOOTSTRAP) != 0;
+  const int k = s.k;
+  Sys sys;
+  sys.setup(a);
+  float* obs_buf = static_cast<float*>(a.obs);
+  float* rew_buf = static_cast<float*>(a.rew);
+  const int64_t ntiles = (a.n + kVnTile - 1) / kVnTile;
+  for (int64_t tile = (int64_t)blockIdx.x * W + wave; tile < ntiles; tile += (int64_t)gridDim.x * W) {
+    const int64_t i = tile * kVnTile + slot;
+    const bool valid = i < a.n;
+    const bool live = h == 0 && valid;
+    // 1. the truncation bootstraps of step k - 1: V(terminal obs normalised by S_k)
+    if (boot && k > 0) {
+      const int64_t po = (int64_t)(k - 1) * a.n + i;
+      const uint8_t d = live ? a.done[po] : (uint8_t)0;
+      const bool bt = live && (d & LZ_DONE_TRUNCATED) && !(d & LZ_DONE_TERMINATED);
+      if (__ballot(bt) != 0ull) {  // wave-uniform
+        float ot[O], xt[O], vt[1];
+#pragma unroll
+        for (int j = 0; j < O; ++j) ot[j] = bt ? s.term[i * O + j] : 0.0f;
+        normalize<O>(ot, xt, true, mu, sd, p.clip);
+        value_fwd<32, O, kMlpF32>(s_blob, vf_net, xt, bt, lane, vt);
+        if (bt) rew_buf[po] = rew_buf[po] + p.gamma * vt[0];
+      }
+    }
+    // 2. the observation the policy sees: the raw obs normalised by S_k
+    float o[O], x[O];
+#pragma unroll
+    for (int j = 0; j < O; ++j) o[j] = live ? s.obs_src[i * O + j] : 0.0f;
+    normalize<O>(o, x, true, mu, sd, p.clip);
+    if (s.final_) {  // the epilogue: last values (SB3 compute_returns_and_advantage input)
+      float vl[1];
+      value_fwd<32, O, kMlpF32>(s_blob, vf_net, x, live, lane, vl);
+      if (live) p.last_val[i] = vl[0];
+      continue;
+    }
+    int32_t steps = 0;
+    if (live) {
+      sys.load(a, i);
+      if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
+    }
+    const int64_t off = (int64_t)k * a.n + i;
+    if (live) {
+#pragma unroll
+      for (int j = 0; j < O; ++j) obs_buf[off * O + j] = x[j];
+    }
+    float mean[A], val[1];
+    {
+      float xs[KS1];
+      f32_inputs<O, KS1>(x, lane, xs);
+      mlp_f32<KS1, A>(pi_net, xs, lane, mean, ttab);
+      __builtin_amdgcn_sched_barrier(0);
+      mlp_f32<KS1, 1>(vf_net, xs, lane, val, ttab);
+    }
+    float act_c[A];
+    if (live) {
+      float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (!det) {
+        if constexpr (A <= 2) normal2(a.seed, (uint64_t)(a.gid0 + i), tick, z);
+        else normal4(a.seed, (uint64_t)(a.gid0 + i), tick, z);
+      }
+      float lp = 0.0f;
+#pragma unroll
+      for (int j = 0; j < A; ++j) {
+        const float aj = det ? mean[j] : mean[j] + z[j] * g_scale[j];
+        const float dd = aj - mean[j];
+        const float lpj = (-(dd * dd)) / g_var2[j] - g_lscale[j] - 0.91893853320467274f;
+        lp = j == 0 ? lpj : lp + lpj;
+        act_c[j] = clip(aj, p.act_lo, p.act_hi);
+        p.act[off * A + j] = aj;
+      }
+      p.logp[off] = lp;
+      p.val[off] = val[0];
+    }
+    float on[O], ot[O];
+    float rew = 0.0f;
+    bool did_reset;
+    const uint8_t df = step_body<Sys, float, true, true>(sys, steps, a, i, live, act_c, tick, k, on,
+                                                         rew, did_reset, ot);
+    if (live) {
+      rew_buf[off] = rew;
+      a.done[off] = df;
+#pragma unroll
+      for (int j = 0; j < O; ++j) p.obs_last[i * O + j] = on[j];
+      if (df) {
+#pragma unroll
+        for (int j = 0; j < O; ++j) s.term[i * O + j] = ot[j];
+      }
+      sys.store(a, i);
+      if (did_reset) sys.store_autoreset_extra(a, i);
+      if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
+    }
+    // 3. the tile's float64 moments of the raw obs VecNormalize updates obs_rms with:
+    // half 0 sums, half 1 squares, a 32-lane butterfly within each half
+    if (s.tiles) {
+#pragma unroll
+      for (int j = 0; j < O; ++j) {
+        const double v = (double)__shfl(on[j], slot, 64);
+        double m = valid ? (h ? v * v : v) : 0.0;
+#pragma unroll
+        for (int q = 16; q >= 1; q >>= 1) m += __shfl_xor(m, q, 64);
+        if (slot == 0) s.tiles[(int64_t)(h * O + j) * s.ntiles + tile] = m;
+      }
+    }
+  }
+}
+
 // obs moments: out = (count, column sums, column sums of squares) from the per-wave
 // partials, summed in a fixed order.  One workgroup per column (the column loop ran in
 // a single workgroup before: 22.9 us per collect at 262,144 envs, 2.8% of K=16); the
@@ -1290,6 +1446,32 @@ int launch_rollout_policy_f32(int system, const KArgs& a, const PArgs& p, const 
     case LZ_SYS_T2: return launch_pol_f32<SysT2<float>>(a, p, grid, s);
     case LZ_SYS_TP: return launch_pol_f32<SysTP<float>>(a, p, grid, s);
     case LZ_SYS_SC: return launch_pol_f32<SysSC<float>>(a, p, grid, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+template <class Sys>
+static int launch_step_f32(const KArgs& a, const PArgs& p, const PStepArgs& st, const PolShape& sh,
+                           hipStream_t s) {
+  if (sh.waves == 4)
+    hipLaunchKernelGGL((k_policy_step_f32<Sys, 4>), dim3((unsigned)sh.grid), dim3(4 * 64), 0, s, a, p, st);
+  else
+    hipLaunchKernelGGL((k_policy_step_f32<Sys, 8>), dim3((unsigned)sh.grid), dim3(8 * 64), 0, s, a, p, st);
+  return (int)hipGetLastError();
+}
+
+int launch_policy_step_f32(int system, const KArgs& a, const PArgs& p, const PStepArgs& st,
+                           const PolShape& grid, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (system) {
+    case LZ_SYS_LORENZ3: return launch_step_f32<SysL3<float>>(a, p, st, grid, s);
+    case LZ_SYS_LORENZ4: return launch_step_f32<SysL4<float>>(a, p, st, grid, s);
+    case LZ_SYS_PMSM: return launch_step_f32<SysPMSM>(a, p, st, grid, s);
+    case LZ_SYS_HR: return launch_step_f32<SysHR<float>>(a, p, st, grid, s);
+    case LZ_SYS_T1: return launch_step_f32<SysT1<float>>(a, p, st, grid, s);
+    case LZ_SYS_T2: return launch_step_f32<SysT2<float>>(a, p, st, grid, s);
+    case LZ_SYS_TP: return launch_step_f32<SysTP<float>>(a, p, st, grid, s);
+    case LZ_SYS_SC: return launch_step_f32<SysSC<float>>(a, p, st, grid, s);
   }
   return (int)hipErrorInvalidValue;
 }

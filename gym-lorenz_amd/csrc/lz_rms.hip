@@ -468,6 +468,88 @@ __global__ __launch_bounds__(256) void k_vn_apply_split(VnApplyArgs p) {
   }
 }
 
+// SB3-exact VecNormalize (lz_internal.h PStepArgs): the statistics update of one step
+// from the float64 tile moments, one workgroup per obs dim d (sums column d, squares
+// column O + d): thread t sums tiles t, t + 256, ... from 0.0 in order, then the LDS
+// tree s[t] += s[t + m], m = 128 .. 1.  snap holds the statistics the step normalised
+// with (S_k); S_{k+1} goes to state (read-only snap: no race between the workgroups),
+// or with moments != nullptr the batch moments (n, sums, sums of squares) for an
+// all-reduce + k_rms_update instead.
+__global__ __launch_bounds__(256) void k_vn_tile_update(const double* tiles, int64_t ntiles, int O,
+                                                        double batch, const double* snap,
+                                                        double* state, double* moments) {
+  __shared__ double red[2][256];
+  const int d = (int)blockIdx.x, t = (int)threadIdx.x;
+  const double* cs = tiles + (int64_t)d * ntiles;
+  const double* cq = tiles + (int64_t)(O + d) * ntiles;
+  double a = 0.0, b = 0.0;
+  // the same in-order sums, with 8 rows of loads issued before their adds (the plain
+  // loop left one load in flight per add: 12 us at 8,192 tiles)
+  int64_t r = t;
+  for (; r + 7 * 256 < ntiles; r += 8 * 256) {
+    double va[8], vb[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      va[u] = cs[r + u * 256];
+      vb[u] = cq[r + u * 256];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a += va[u];
+      b += vb[u];
+    }
+  }
+  for (; r < ntiles; r += 256) {
+    a += cs[r];
+    b += cq[r];
+  }
+  red[0][t] = a;
+  red[1][t] = b;
+  __syncthreads();
+  for (int m = 128; m >= 1; m >>= 1) {
+    if (t < m) {
+      red[0][t] += red[0][t + m];
+      red[1][t] += red[1][t + m];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (moments) {
+      moments[1 + d] = red[0][0];
+      moments[1 + O + d] = red[1][0];
+      if (d == 0) moments[0] = batch;
+    } else {
+      double nm, nv;
+      lz::rms_new(snap[d], snap[O + d], snap[2 * O], batch, red[0][0], red[1][0], nm, nv);
+      state[d] = nm;
+      state[O + d] = nv;
+      if (d == 0) state[2 * O] = snap[2 * O] + batch;
+    }
+  }
+}
+
+// The tile moments of an obs array x [n, O] float32 in k_policy_step_f32's order (one
+// wave per tile of 32 envs, half 0 sums, half 1 squares, 32-lane butterfly) -- the
+// reset() update of the SB3-exact collect; block 0 snapshots the statistics.
+__global__ __launch_bounds__(256) void k_obs_tile_moments(const float* x, int64_t n, int O,
+                                                          double* tiles, const double* state,
+                                                          double* snap) {
+  const int lane = (int)threadIdx.x & 63, h = lane >> 5, slot = lane & 31;
+  if (blockIdx.x == 0 && (int)threadIdx.x < 2 * O + 1) snap[threadIdx.x] = state[threadIdx.x];
+  const int64_t ntiles = (n + lz::kVnTile - 1) / lz::kVnTile;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); tile < ntiles;
+       tile += (int64_t)gridDim.x * 4) {
+    const int64_t i = tile * lz::kVnTile + slot;
+    for (int j = 0; j < O; ++j) {
+      const double v = i < n ? (double)x[i * O + j] : 0.0;
+      double m = h ? v * v : v;
+#pragma unroll
+      for (int q = 16; q >= 1; q >>= 1) m += __shfl_xor(m, q, 64);
+      if (slot == 0) tiles[(int64_t)(h * O + j) * ntiles + tile] = m;
+    }
+  }
+}
+
 }  // namespace
 
 struct lz_rms {
@@ -476,6 +558,8 @@ struct lz_rms {
   hipStream_t stream;
   double* state;    // mean[dim], var[dim], count
   double* partial;  // [kRmsMaxBlocks][2*dim]
+  double* tiles;    // lz_rms_update_obs: [2*dim][ntiles] tile moments + [2*dim+1] snapshot
+  int64_t tiles_n;  // doubles allocated
 };
 
 #define RMS_HIP(expr)                                                                       \
@@ -564,6 +648,23 @@ int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
   return (int)hipGetLastError();
 }
 
+int launch_vn_tile_update(const double* tiles, int64_t ntiles, int O, double batch,
+                          const double* snap, double* state, double* moments, void* stream) {
+  hipLaunchKernelGGL(k_vn_tile_update, dim3((unsigned)O), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     tiles, ntiles, O, batch, snap, state, moments);
+  return (int)hipGetLastError();
+}
+
+int launch_obs_tile_moments(const float* x, int64_t n, int O, double* tiles, const double* state,
+                            double* snap, void* stream) {
+  const int64_t ntiles = (n + kVnTile - 1) / kVnTile;
+  const int64_t g = (ntiles + 3) / 4;
+  const unsigned grid = (unsigned)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+  hipLaunchKernelGGL(k_obs_tile_moments, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), x,
+                     n, O, tiles, state, snap);
+  return (int)hipGetLastError();
+}
+
 }  // namespace lz
 
 extern "C" {
@@ -584,6 +685,8 @@ lz_status lz_rms_create(int32_t dim, int32_t device, double count_init, lz_rms**
   r->stream = nullptr;
   r->state = nullptr;
   r->partial = nullptr;
+  r->tiles = nullptr;
+  r->tiles_n = 0;
   if (hipMalloc(reinterpret_cast<void**>(&r->state), (2 * dim + 1) * sizeof(double)) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&r->partial),
                 (size_t)kRmsMaxBlocks * 2 * dim * sizeof(double)) != hipSuccess) {
@@ -607,6 +710,7 @@ lz_status lz_rms_destroy(lz_rms* r) {
   (void)hipSetDevice(r->device);
   if (r->state) (void)hipFree(r->state);
   if (r->partial) (void)hipFree(r->partial);
+  if (r->tiles) (void)hipFree(r->tiles);
   delete r;
   return LZ_OK;
 }
@@ -698,6 +802,29 @@ lz_status lz_returns_update(double* returns, const void* rew, int32_t dtype, con
   else
     hipLaunchKernelGGL(k_returns<float>, grid, block, 0, s, returns, rew, done, n, gamma, phase);
   RMS_HIP(hipGetLastError());
+  return LZ_OK;
+}
+
+lz_status lz_rms_update_obs(lz_rms* r, const float* x, int64_t n, double* moments_out) {
+  if (!r || (!x && n > 0)) return rfail(LZ_ERR_INVALID, "NULL argument");
+  if (n <= 0) return rfail(LZ_ERR_INVALID, "n must be >= 1");
+  RMS_HIP(hipSetDevice(r->device));
+  const int D = r->dim;
+  if (D > lz::kVnMaxObs) return rfail(LZ_ERR_UNSUPPORTED, "lz_rms_update_obs: dim > %d", lz::kVnMaxObs);
+  const int64_t ntiles = (n + lz::kVnTile - 1) / lz::kVnTile;
+  const int64_t need = 2 * D * ntiles + 2 * D + 1;
+  if (r->tiles_n < need) {
+    if (r->tiles) RMS_HIP(hipFree(r->tiles));
+    r->tiles = nullptr;
+    r->tiles_n = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&r->tiles), (size_t)need * sizeof(double)) != hipSuccess)
+      return rfail(LZ_ERR_OOM, "lz_rms_update_obs: tile scratch (%lld doubles)", (long long)need);
+    r->tiles_n = need;
+  }
+  double* snap = r->tiles + 2 * D * ntiles;
+  RMS_HIP((hipError_t)lz::launch_obs_tile_moments(x, n, D, r->tiles, r->state, snap, r->stream));
+  RMS_HIP((hipError_t)lz::launch_vn_tile_update(r->tiles, ntiles, D, (double)n, snap, r->state,
+                                                moments_out, r->stream));
   return LZ_OK;
 }
 

@@ -169,6 +169,7 @@ _SIGS = {
                                     ctypes.POINTER(VP)]),
     "lz_rms_moments": (ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int64, VP]),
     "lz_rms_update": (ctypes.c_int, [VP, VP]),
+    "lz_rms_update_obs": (ctypes.c_int, [VP, VP, ctypes.c_int64, VP]),
     "lz_rms_normalize": (ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int64, VP, ctypes.c_int32,
                                         ctypes.c_double, ctypes.c_double]),
     "lz_returns_update": (ctypes.c_int, [VP, VP, ctypes.c_int32, VP, ctypes.c_int64, ctypes.c_double,
@@ -185,6 +186,9 @@ _SIGS = {
     "lz_policy_pack_f32": (ctypes.c_int, [ctypes.POINTER(LzMlpPolicy), ctypes.c_int32, VP,
                                           ctypes.c_int64]),
     "lz_rollout_policy_f32": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
+    "lz_policy_step_f32": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs), ctypes.c_int32, VP,
+                                          VP]),
+    "lz_rollout_policy_f32_vn": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs), VP]),
     "lz_attn_policy_blob_bytes": (ctypes.c_int64, []),
     "lz_attn_policy_pack": (ctypes.c_int, [ctypes.POINTER(LzAttnPolicy), VP, ctypes.c_int64]),
     "lz_rollout_policy_attn": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),

@@ -15,8 +15,12 @@ and finally ``RolloutBuffer.compute_returns_and_advantage``.
 the C oracle reproduces bit for bit; ``precision="bf16"`` selects the faster bf16-MFMA
 kernel ``lz_rollout_policy``, the attention policies run bf16 only), the Gaussian
 sample (Philox), the action-space clip, the env step with
-auto-reset, SB3's truncation bootstrap, and VecNormalize's observation normalisation
-(statistics frozen for the K steps and updated once from the K steps' moments).
+auto-reset, SB3's truncation bootstrap, and VecNormalize's observation normalisation.
+With a training VecNormalize the float32 kernel follows SB3's order exactly: each
+step's batch updates obs_rms before that step's observations are normalised
+(``lz_rollout_policy_f32_vn``: one launch per step, the statistics update between
+launches); ``vecnorm_update="rollout"`` (and the bf16 / attention kernels) keep the
+statistics frozen for the K steps and update them once from the pooled moments.
 ``compute_returns_and_advantage`` is ``lz_gae``.  The buffers come back as
 time-major device tensors in SB3's RolloutBuffer layout ([K, N, ...]).
 
@@ -468,7 +472,15 @@ class FusedRolloutCollector:
     backend:       gym_lorenz.core.BatchedEnv (float32, autoreset)
     state_dict:    SB3 ActorCriticPolicy / ActorCriticMlp state_dict
     obs_rms:       gym_lorenz.vec_normalize.DeviceRunningMeanStd or None
-    training:      update obs_rms after each rollout (VecNormalize.training)
+    training:      update obs_rms (VecNormalize.training)
+    vecnorm_update: how a training obs_rms is updated.  "step" (the default for the
+                   float32 MlpPolicy): SB3's order -- every step's batch updates obs_rms
+                   before that step's observations (and the truncated steps' terminal
+                   observations) are normalised (lz_rollout_policy_f32_vn: one launch
+                   per step + the statistics update between).  "rollout" (opt-in; the
+                   only mode of the bf16 / attention kernels): the K steps run in one
+                   launch with the rollout-start statistics and one update from the K
+                   steps' pooled moments afterwards -- faster, not SB3's trajectory.
     precision:     MlpPolicy arithmetic: "fp32" (default; SB3's float32 forward,
                    lz_rollout_policy_f32) or "bf16" (bf16 MFMA operands, fp32
                    accumulation, lz_rollout_policy: ~2.5x faster, ~1e-2 off SB3).  The
@@ -479,7 +491,7 @@ class FusedRolloutCollector:
     def __init__(self, backend, state_dict=None, gamma=0.99, gae_lambda=0.95, obs_rms=None,
                  clip_obs=10.0, norm_eps=1e-8, training=True, bootstrap=True,
                  deterministic=False, capture_terminal=0, group=None, frame_stack=1,
-                 precision=None):
+                 precision=None, vecnorm_update=None):
         if backend.tdtype != torch.float32:
             raise ValueError("the fused policy rollout runs float32 env handles")
         self.env = backend
@@ -494,6 +506,9 @@ class FusedRolloutCollector:
         if precision not in (None, "fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
         self.precision = precision
+        if vecnorm_update not in (None, "step", "rollout"):
+            raise ValueError("vecnorm_update must be 'step' or 'rollout'")
+        self.vecnorm_update = vecnorm_update
         self.f32 = False
         self.blob = None
         self.attention = False
@@ -531,7 +546,27 @@ class FusedRolloutCollector:
             blob = (pack_policy_f32 if self.f32 else pack_policy)(state_dict, self.O, self.A)
         if (self.attention or self.attention_ln) and self.precision == "fp32":
             raise ValueError("the attention actor-critics run bf16 only (precision='bf16')")
+        if self.vecnorm_update == "step" and not self.f32:
+            raise ValueError("vecnorm_update='step' runs the float32 MlpPolicy kernel")
         self.blob = torch.from_numpy(blob).to(self.device)
+
+    @property
+    def per_step_vecnorm(self):
+        """True when the collect updates obs_rms in SB3's per-step order."""
+        return (self.obs_rms is not None and self.training and self.f32
+                and self.vecnorm_update != "rollout")
+
+    def _rms_update_obs(self, x):
+        """VecNormalize.reset()'s obs_rms.update(obs) in the per-step kernel's moment order."""
+        rms = self.obs_rms
+        x = x.reshape(x.shape[0], self.O).contiguous()
+        if self.group is None:
+            nat.check(nat.lib.lz_rms_update_obs(rms._h, x.data_ptr(), x.shape[0], None))
+            return
+        mom = torch.empty((1 + 2 * self.O,), dtype=torch.float64, device=self.device)
+        nat.check(nat.lib.lz_rms_update_obs(rms._h, x.data_ptr(), x.shape[0], mom.data_ptr()))
+        dist.all_reduce(mom, group=self.group)
+        nat.check(nat.lib.lz_rms_update(rms._h, ctypes.c_void_p(mom.data_ptr())))
 
     def reset(self):
         """VecEnv.reset(): fresh episodes; the next rollout starts from their obs."""
@@ -543,7 +578,10 @@ class FusedRolloutCollector:
         self.last_stack[:, -self.O:] = obs
         self.last_episode_starts.fill_(1.0)
         if self.obs_rms is not None and self.training:
-            self.obs_rms.update(self.last_obs, self.group)
+            if self.per_step_vecnorm:
+                self._rms_update_obs(self.last_obs)
+            else:
+                self.obs_rms.update(self.last_obs, self.group)
         return self.last_obs
 
     def collect(self, K):
@@ -562,7 +600,8 @@ class FusedRolloutCollector:
         done = torch.empty((K, n), dtype=torch.uint8, device=dev)
         last_val = torch.empty((n,), dtype=f32, device=dev)
         obs_last = torch.empty((n, O), dtype=f32, device=dev)
-        want_mom = self.obs_rms is not None and self.training
+        per_step = self.per_step_vecnorm
+        want_mom = self.obs_rms is not None and self.training and not per_step
         mom = torch.empty((1 + 2 * O,), dtype=torch.float64, device=dev) if want_mom else None
         didx = tobs = ndone = None
         if self.capture_terminal:
@@ -574,7 +613,7 @@ class FusedRolloutCollector:
         r.flags = ((nat.POLICY_DETERMINISTIC if self.deterministic else 0)
                    | (nat.POLICY_BOOTSTRAP if self.bootstrap else 0))
         r.blob, r.obs_in, r.obs_last = _p(self.blob), _p(self.last_obs), _p(obs_last)
-        r.obs_norm = _p(self.obs_rms.state) if self.obs_rms is not None else None
+        r.obs_norm = _p(self.obs_rms.state) if self.obs_rms is not None and not per_step else None
         r.norm_eps, r.clip_obs, r.gamma = self.norm_eps, self.clip_obs, self.gamma
         r.act_low, r.act_high = self.act_low, self.act_high
         r.obs_buf, r.act_buf, r.logp_buf, r.val_buf = _p(obs_buf), _p(act_buf), _p(logp), _p(val)
@@ -594,6 +633,25 @@ class FusedRolloutCollector:
             nat.check(nat.lib.lz_rollout_policy_attn_stack(self.env._h, ctypes.byref(r),
                                                            self.frame_stack, _p(self.last_stack),
                                                            _p(stack_out)))
+        elif per_step:
+            state = ctypes.c_void_p(self.obs_rms.state.data_ptr())
+            if self.group is None:
+                nat.check(nat.lib.lz_rollout_policy_f32_vn(self.env._h, ctypes.byref(r), state))
+            else:  # every step's batch moments all-reduced before its update
+                mom = torch.empty((1 + 2 * O,), dtype=torch.float64, device=dev)
+                rh = self.obs_rms._h
+                nat.check(nat.lib.lz_rms_set_stream(rh, ctypes.c_void_p(caller.cuda_stream)))
+                for k in range(K + 1):
+                    nat.check(nat.lib.lz_policy_step_f32(self.env._h, ctypes.byref(r), k, state,
+                                                         ctypes.c_void_p(mom.data_ptr()) if k < K
+                                                         else None))
+                    if k < K:
+                        if es != caller:
+                            caller.wait_stream(es)
+                        dist.all_reduce(mom, group=self.group)
+                        nat.check(nat.lib.lz_rms_update(rh, ctypes.c_void_p(mom.data_ptr())))
+                        if es != caller:
+                            es.wait_stream(caller)
         else:
             launch = (nat.lib.lz_rollout_policy_attn if self.attention else
                       nat.lib.lz_rollout_policy_f32 if self.f32 else nat.lib.lz_rollout_policy)

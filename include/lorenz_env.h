@@ -366,6 +366,31 @@ lz_status lz_rollout_policy(lz_handle* h, const lz_policy_rollout_args* r);
  * code/lorenz_pmsm/test_evaluate.py:117-120's deterministic closed loop). */
 lz_status lz_rollout_policy_f32(lz_handle* h, const lz_policy_rollout_args* r);
 
+/* The same collect under VecNormalize(training=True) in SB3's own order (SB3 2.7.1
+ * VecNormalize.step_wait inside collect_rollouts; code/lorenz_pmsm/train.py:170-181
+ * A2C n_steps=16 behind VecNormalize(norm_obs=True, norm_reward=False, clip_obs=10)):
+ * step k's observation is normalised with obs_rms already updated by step k's whole
+ * batch, and a truncated step's terminal observation (bootstrap value) with the
+ * statistics that step produced.  One launch per step (the update is a reduction over
+ * the batch between two steps) plus a closing launch:
+ *   k = 0 .. K-1: [bootstrap of step k-1] normalise obs with obs_rms_state, policy,
+ *                 sample, clip, env step (raw obs -> r->obs_last); then obs_rms_state
+ *                 is updated in place from float64 tile moments of the raw step obs
+ *                 (moments_out == NULL), or moments_out (device double [1 + 2*O]) gets
+ *                 the batch moments (n, sums, sums of squares) for the caller's
+ *                 all-reduce + lz_rms_update (multi-GPU);
+ *   k = K:        the bootstrap of step K-1 and r->last_values.
+ * obs_rms_state: the lz_rms state (lz_rms_state: mean[O], var[O], count, contiguous),
+ * read and written; r->obs_norm NULL or the same pointer; r->obs_moments NULL.  The
+ * batch moments are float64 sums in one fixed order (lz_internal.h PStepArgs; restated
+ * by the oracle) -- SB3 sums float32 rows with np.mean / np.var.  Step k reads
+ * r->obs_in (k = 0) or r->obs_last.  Call k = 0 .. K in order on one stream. */
+lz_status lz_policy_step_f32(lz_handle* h, const lz_policy_rollout_args* r, int32_t k,
+                             double* obs_rms_state, double* moments_out);
+/* k = 0 .. K of lz_policy_step_f32 with in-place statistics (single GPU). */
+lz_status lz_rollout_policy_f32_vn(lz_handle* h, const lz_policy_rollout_args* r,
+                                   double* obs_rms_state);
+
 /* The actor-critic of the reference's flagship PPO script, code/train.py:52-112:
  * policy_kwargs = dict(features_extractor_class=AttentionFeaturesExtractor,
  * features_extractor_kwargs=dict(features_dim=64), net_arch=dict(pi=[128, 128],
@@ -480,6 +505,10 @@ lz_status lz_rms_state(lz_rms* r, double** mean, double** var, double** count);
 lz_status lz_rms_moments(lz_rms* r, const void* x, int32_t dtype, int64_t n, double* moments_out);
 /* RunningMeanStd.update_from_moments with those moments (possibly all-reduced). */
 lz_status lz_rms_update(lz_rms* r, const double* moments);
+/* RunningMeanStd.update(x) for x float32 [n, dim] (dim <= 8) in lz_policy_step_f32's
+ * moment order (VecNormalize.reset() of the SB3-exact collect); with moments_out
+ * non-NULL only the batch moments are written (all-reduce, then lz_rms_update). */
+lz_status lz_rms_update_obs(lz_rms* r, const float* x, int64_t n, double* moments_out);
 /* y (float32 [n, dim]) = clip((x - mean if center else x) / sqrt(var + eps), -clip, clip)
  * (VecNormalize.normalize_obs with center=1, normalize_reward with center=0). */
 lz_status lz_rms_normalize(lz_rms* r, const void* x, int32_t dtype, int64_t n, float* y,

@@ -716,3 +716,38 @@ void orc_mlp_f32(int64_t n, int O, int A, int H, const float* x, const float* pi
 void orc_tanh_tab_v(int64_t n, const float* x, float* out) {
   for (int64_t i = 0; i < n; ++i) out[i] = orc_tanh_tab(x[i]);
 }
+
+/* ---- SB3-exact VecNormalize of the fused float32 rollout (lz_policy_step_f32).
+ * The batch moments of x [n, O] float32 in the device's fixed order (gym-lorenz_amd/
+ * csrc/lz_internal.h PStepArgs; k_policy_step_f32 / k_obs_tile_moments + k_vn_tile_update):
+ * per tile of 32 envs (0.0 past n) a 32-lane butterfly v_l += v_(l ^ m), m = 16 .. 1, of
+ * (double)x (sums) or (double)x * (double)x (squares); per column, accumulator t < 256
+ * sums the partials of tiles t, t + 256, ... from 0.0 in order; then the tree
+ * a[t] += a[t + m], m = 128 .. 1.  tot[2 O] = (sums[O], sums of squares[O]).
+ * SB3 2.7.1 RunningMeanStd.update (common/running_mean_std.py) takes np.mean / np.var
+ * of the float32 rows instead; the statistics built on these sums follow
+ * update_from_moments (the caller, oracle/__init__.py vn_rms_update). */
+void orc_vn_tile_totals(const float* x, int64_t n, int O, double* tot) {
+  const int64_t ntiles = (n + 31) / 32;
+  for (int c = 0; c < 2 * O; ++c) {
+    const int j = c % O, sq = c >= O;
+    double acc[256];
+    for (int t = 0; t < 256; ++t) acc[t] = 0.0;
+    for (int64_t tile = 0; tile < ntiles; ++tile) {
+      double v[32], w[32];
+      for (int l = 0; l < 32; ++l) {
+        const int64_t i = tile * 32 + l;
+        const double d = i < n ? (double)x[i * O + j] : 0.0;
+        v[l] = sq ? d * d : d;
+      }
+      for (int m = 16; m >= 1; m >>= 1) {
+        for (int l = 0; l < 32; ++l) w[l] = v[l] + v[l ^ m];
+        for (int l = 0; l < 32; ++l) v[l] = w[l];
+      }
+      acc[tile % 256] += v[0];
+    }
+    for (int m = 128; m >= 1; m >>= 1)
+      for (int t = 0; t < m; ++t) acc[t] += acc[t + m];
+    tot[c] = acc[0];
+  }
+}

@@ -227,8 +227,9 @@ def test_f32_vs_sb3_fp32_forward(gl, pol):
 
 
 def test_f32_vecnormalize_moments(gl, pol):
-    """Training statistics from the f32 kernel's register moments: equal to float64
-    sums over the raw step outputs (the lz_rollout twin's obs) to 1e-12."""
+    """vecnorm_update="rollout" (the pooled opt-in): training statistics from the f32
+    kernel's register moments, equal to float64 sums over the raw step outputs (the
+    lz_rollout twin's obs) to 1e-12; the policy saw the rollout-start statistics."""
     from gym_lorenz.vec_normalize import DeviceRunningMeanStd
 
     n, K = 3001, 7
@@ -237,7 +238,7 @@ def test_f32_vecnormalize_moments(gl, pol):
     _, sd = _random_policy(pol, 6, 2, seed=5)
     rms = DeviceRunningMeanStd(6, envp.device)
     col = pol.FusedRolloutCollector(envp, sd, bootstrap=False, obs_rms=rms, training=True,
-                                    precision="fp32")
+                                    precision="fp32", vecnorm_update="rollout")
     col.reset()
     envr.reset()
     mean0, var0 = rms.mean.copy(), rms.var.copy()
