@@ -383,12 +383,13 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
     net = (ActorCriticAttn(stack * O, A, seed=0, layer_norm=ln) if attn
            else ActorCriticMlp(O, A, seed=0))
     rms = None if attn else DeviceRunningMeanStd(O, device)
-    f32 = not attn and args.precision == "fp32"
-    per_step = f32 and args.vecnorm_update == "step"
+    f32 = args.precision == "fp32"
+    per_step = f32 and not attn and args.vecnorm_update == "step"
     col = FusedRolloutCollector(env, net.state_dict(), gamma=0.99, gae_lambda=0.95, obs_rms=rms,
                                 clip_obs=10.0, training=True, bootstrap=True, frame_stack=stack,
                                 precision="fp32" if f32 else "bf16",
-                                vecnorm_update=("step" if per_step else "rollout") if f32 else None)
+                                vecnorm_update=("step" if per_step else "rollout")
+                                if f32 and not attn else None)
     assert col.per_step_vecnorm == per_step
     stream = torch.cuda.Stream(device)
     with torch.cuda.stream(stream):
@@ -448,18 +449,22 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32 MFMA (f32 accumulate), f32 env" if f32 else "bf16 MFMA (fp32 accumulate), f32 env",
+        "precision_note": ("float32 end to end, bit-exact vs the C oracle (SB3's own precision)"
+                           if f32 else "bf16 operands (opt-in, ~1e-2 off SB3's float32)"),
         "data": "synthetic: on-device Philox initial states and Gaussian action samples; "
                 "SB3-initialised (orthogonal) random policy weights",
         "config": {
             "workload": ("%s with code/lorenz_filter/train.py's PPO actor-critic on "
                          "VecFrameStack(4) (attention + residual + LayerNorm extractor, pi/vf "
-                         "[128,128] Tanh): %d-step fused rollout (lz_rollout_policy_attn_stack: "
+                         "[128,128] Tanh): %d-step fused rollout (lz_rollout_policy_attn_stack" +
+                         ("_f32, float32 as SB3" if f32 else ", bf16 MFMA") + ": "
                          "frame stack + extractor + nets + sample + clip + env step + bootstrap), "
                          "GAE (lz_gae); %d envs total, %d per GPU" if ln else
                          "%s with code/train.py's PPO actor-critic (AttentionFeaturesExtractor "
                          "fc1 + 4-head self-attention over 8 tokens + post_fc 64, then pi/vf "
                          "[128,128] Tanh) in the loop: %d-step fused rollout "
-                         "(lz_rollout_policy_attn: extractor + nets + DiagGaussian sample + clip "
+                         "(lz_rollout_policy_attn" + ("_f32, float32 as SB3" if f32 else ", bf16 MFMA")
+                         + ": extractor + nets + DiagGaussian sample + clip "
                          "+ env step + truncation bootstrap), GAE (lz_gae); %d envs total, %d per "
                          "GPU" if attn else
                          "%s with the SB3 A2C/PPO MlpPolicy (pi/vf [128,128] Tanh) in the loop: "
@@ -486,7 +491,11 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         "roofline": {
             "bound": "mfma", "achieved": achieved, "peak": peak,
             "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-            "kernel": ("_ZN2lz16k_rollout_policyINS_%sLi4ELi32ELi4ELi4EEEvNS_5KArgsENS_5PArgsE"
+            "kernel": ("_ZN2lz25k_rollout_policy_attn_f32INS_%sLb1ELi4ELi4EEEvNS_5KArgsENS_5PArgsE"
+                       if ln and f32 else
+                       "_ZN2lz25k_rollout_policy_attn_f32INS_%sLb0ELi1ELi8EEEvNS_5KArgsENS_5PArgsE"
+                       if attn and f32 else
+                       "_ZN2lz16k_rollout_policyINS_%sLi4ELi32ELi4ELi4EEEvNS_5KArgsENS_5PArgsE"
                        if ln else
                        "_ZN2lz16k_rollout_policyINS_%sLi4ELi32ELi3EEEvNS_5KArgsENS_5PArgsE"
                        if attn else

@@ -111,31 +111,33 @@ struct lz_handle {
   uint8_t* hs_dev;     // lz_step_host: its device address
   size_t hs_in, hs_out;  // bytes of the input / output parts
   // lz_resident_step: mailbox in mapped coherent host memory (cmd | resp | act | noise
-  // || obs | rew | done), its device address, the server's own stream
+  // || obs | rew | done || published state planes) and its device address
   uint8_t* rs_pin;
   uint8_t* rs_dev;
-  hipStream_t rs_stream;
-  hipEvent_t rs_ev;
-  bool rs_active;       // a k_resident launch may be running
-  int rs_use_noise;     // ... serving injected noise
-  int64_t rs_seq;       // number of the last request posted
-  uint64_t rs_idle;     // idle exit, wall-clock ticks
+  bool rs_member;       // registered with its device's resident server
+  bool rs_active;       // ... whose launch may be running
+  bool rs_pub_valid;    // the published planes are this launch's (a request was served)
+  int rs_use_noise;     // serving injected noise
+  int64_t rs_seq;       // number of the last request posted (= served, after the reply)
 };
 
-// Stop the resident step server (if any) and wait for it: every other call on the
-// handle starts with this, so the server's register-held state is back in the planes
-// and the handle's stream ordering is the plain one again.
+// Stop the resident step server serving the handle (if it runs) and wait for it: every
+// other call on the handle starts with this, so the server's register-held state is
+// back in the planes and the handle's stream ordering is the plain one again.
+// (rs_member changes only in calls on this handle; rs_active -- another thread's
+// lz_resident_step may relaunch the server with this handle -- is read under the lock)
 #define RESIDENT_QUIESCE(h)                           \
   do {                                                \
-    if ((h)->rs_active) {                             \
-      const lz_status q_ = resident_stop(h);          \
+    if ((h)->rs_member) {                             \
+      const lz_status q_ = resident_quiesce(h);       \
       if (q_ != LZ_OK) return q_;                     \
     }                                                 \
   } while (0)
 
 extern "C" {
 
-static lz_status resident_stop(lz_handle* h);
+static lz_status resident_quiesce(lz_handle* h);
+static void resident_leave(lz_handle* h);
 
 int32_t lz_abi_version(void) { return LZ_ABI_VERSION; }
 
@@ -310,9 +312,7 @@ lz_status lz_create(const lz_config* cfg_in, lz_handle** out) {
 lz_status lz_destroy(lz_handle* h) {
   if (!h) return LZ_OK;
   (void)hipSetDevice(h->cfg.device);
-  if (h->rs_active) (void)resident_stop(h);
-  if (h->rs_stream) (void)hipStreamDestroy(h->rs_stream);
-  if (h->rs_ev) (void)hipEventDestroy(h->rs_ev);
+  if (h->rs_member) resident_leave(h);
   if (h->rs_pin) (void)hipHostFree(h->rs_pin);
   for (int p = 0; p < lz::kMaxPlanes; ++p)
     if (h->planes[p]) (void)hipFree(h->planes[p]);
@@ -515,9 +515,10 @@ lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, 
   return LZ_OK;
 }
 
-// ---- resident step server (lz_resident_step)
+// ---- resident step server (lz_resident_step; lz_internal.h ResBox / ResMember)
 // mailbox layout (bytes): cmd int64 @0, resp int64 @128 (own cache lines), actions
-// float32 [n, A] @256, noise double [n, 3] @kRsNoise, then obs | reward | done @kRsOut
+// float32 [n, A] @256, noise double [n, 3] @kRsNoise, then obs | reward | done @kRsOut,
+// then the published state planes (plane p at rs_pub_off + p * kRsPubStride(n))
 constexpr size_t kRsCmd = 0, kRsResp = 128, kRsAct = 256;
 constexpr size_t kRsNoise = kRsAct + 64 * 4 * 4, kRsOut = kRsNoise + 64 * 3 * 8;
 constexpr int kRsMaxEnvs = 64;
@@ -528,82 +529,168 @@ static size_t rs_rew_off(const lz_handle* h) {
 static size_t rs_done_off(const lz_handle* h) {
   return rs_rew_off(h) + align16((size_t)h->cfg.num_envs * (h->f64 ? 8 : 4));
 }
+static size_t rs_pub_stride(const lz_handle* h) { return align16((size_t)h->cfg.num_envs * 8); }
+static size_t rs_pub_off(const lz_handle* h) { return rs_done_off(h) + align16((size_t)h->cfg.num_envs); }
+static size_t rs_bytes(const lz_handle* h) {
+  return rs_pub_off(h) + (size_t)h->desc.n_planes * rs_pub_stride(h);
+}
 
 static volatile int64_t* rs_word(const lz_handle* h, size_t off) {
   return reinterpret_cast<volatile int64_t*>(h->rs_pin + off);
 }
 
-// handles whose server may be running, so that process exit without lz_destroy posts
-// their stop commands first (an atexit handler registered at the first launch: it runs
-// before the HIP runtime's own exit-time teardown, which was registered earlier).
-constexpr int kRsLiveMax = 1024;
+// One server per device: the registered handles, the stream (one hardware queue) its
+// launch polls on, the member table it reads.  g_rs_mu guards every field and the
+// membership; calls on different handles may come from different threads.
+constexpr int kRsMaxDevices = 64;
+struct RsServer {
+  bool init;
+  bool active;           // a launch may be running
+  int n;
+  lz_handle* members[lz::kRsMaxHandles];
+  hipStream_t stream;
+  hipEvent_t ev;
+  lz::ResMember* table_host;  // pinned staging of the member table
+  lz::ResMember* table_dev;
+  uint64_t idle;         // idle exit, wall-clock ticks
+};
 static std::mutex g_rs_mu;  // trivially destructible
-static lz_handle* g_rs_live[kRsLiveMax];
-static int g_rs_n;
+static RsServer g_rs[kRsMaxDevices];
 
-static void rs_live_add(lz_handle* h) {
-  std::lock_guard<std::mutex> lk(g_rs_mu);
-  for (int i = 0; i < g_rs_n; ++i)
-    if (g_rs_live[i] == h) return;
-  if (g_rs_n < kRsLiveMax) g_rs_live[g_rs_n++] = h;
-}
-static void rs_live_remove(lz_handle* h) {
-  std::lock_guard<std::mutex> lk(g_rs_mu);
-  for (int i = 0; i < g_rs_n; ++i)
-    if (g_rs_live[i] == h) {
-      g_rs_live[i] = g_rs_live[--g_rs_n];
-      return;
-    }
+static RsServer& rs_server(const lz_handle* h) { return g_rs[h->cfg.device]; }
+
+static lz_status rs_server_init(RsServer& sv, int device) {
+  if (sv.init) return LZ_OK;
+  hipStream_t st = nullptr;
+  hipEvent_t ev = nullptr;
+  lz::ResMember* th = nullptr;
+  lz::ResMember* td = nullptr;
+  const size_t tb = sizeof(lz::ResMember) * lz::kRsMaxHandles;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&th), tb) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&td), tb) != hipSuccess) {
+    if (st) (void)hipStreamDestroy(st);
+    if (ev) (void)hipEventDestroy(ev);
+    if (th) (void)hipHostFree(th);
+    return fail(LZ_ERR_OOM, "resident server setup failed");
+  }
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0)
+    khz = 100000;
+  const char* e = std::getenv("LZ_RESIDENT_IDLE_US");
+  // short: a device-wide synchronize (torch.cuda.synchronize()) waits for the idle exit,
+  // and a caller that leaves > 1 ms between steps pays one relaunch (~20 us)
+  const double idle_us = e ? std::atof(e) : 1000.0;
+  sv.stream = st;
+  sv.ev = ev;
+  sv.table_host = th;
+  sv.table_dev = td;
+  sv.idle = (uint64_t)(idle_us * khz / 1000.0);
+  sv.n = 0;
+  sv.active = false;
+  sv.init = true;
+  return LZ_OK;
 }
 
+// the launch has ended (stop command or idle exit): every member's state is in its
+// planes and its tick in the other ping-pong slot
+static void rs_server_ended(RsServer& sv) {
+  for (int i = 0; i < sv.n; ++i) {
+    lz_handle* m = sv.members[i];
+    m->rs_active = false;
+    m->rs_pub_valid = false;
+    m->parity ^= 1;
+  }
+  sv.active = false;
+}
+
+static lz_status rs_server_stop(RsServer& sv) {
+  if (!sv.active) return LZ_OK;
+  // one mailbox's stop command makes every wave leave; the word is restored after
+  lz_handle* m0 = sv.members[0];
+  __atomic_store_n(const_cast<int64_t*>(rs_word(m0, kRsCmd)), (int64_t)-1, __ATOMIC_RELEASE);
+  const hipError_t e = hipStreamSynchronize(sv.stream);
+  __atomic_store_n(const_cast<int64_t*>(rs_word(m0, kRsCmd)), m0->rs_seq, __ATOMIC_RELEASE);
+  rs_server_ended(sv);
+  if (e != hipSuccess) return fail(LZ_ERR_HIP, "resident stop: %s", hipGetErrorString(e));
+  return LZ_OK;
+}
+
+// process exit without lz_destroy: post the stop commands first (an atexit handler
+// registered at the first launch runs before the HIP runtime's own exit-time teardown,
+// which was registered earlier).  try_lock: a thread that died holding the lock must not
+// hang the exit; the servers are then stopped without it.
 static void resident_unload() {
-  for (int i = 0; i < g_rs_n; ++i)
-    __atomic_store_n(const_cast<int64_t*>(rs_word(g_rs_live[i], kRsCmd)), (int64_t)-1,
+  bool locked = false;
+  for (int k = 0; k < 100 && !(locked = g_rs_mu.try_lock()); ++k) usleep(100);
+  bool any = false;
+  for (int d = 0; d < kRsMaxDevices; ++d) {
+    RsServer& sv = g_rs[d];
+    if (!sv.init || !sv.active || sv.n == 0) continue;
+    __atomic_store_n(const_cast<int64_t*>(rs_word(sv.members[0], kRsCmd)), (int64_t)-1,
                      __ATOMIC_RELEASE);
-  if (g_rs_n > 0) usleep(2000);  // a poll period is ~2 us; they exit on sight
+    any = true;
+  }
+  if (any) usleep(2000);  // a poll period is ~2 us; the waves exit on sight
+  if (locked) g_rs_mu.unlock();
 }
 
-static lz_status resident_launch(lz_handle* h, int64_t next, int use_noise) {
-  KArgs a;
-  fill_common(h, a);
-  lz::ResBox box;
-  box.cmd = reinterpret_cast<const int64_t*>(h->rs_dev + kRsCmd);
-  box.resp = reinterpret_cast<int64_t*>(h->rs_dev + kRsResp);
-  box.act = reinterpret_cast<const float*>(h->rs_dev + kRsAct);
-  box.noise = reinterpret_cast<const double*>(h->rs_dev + kRsNoise);
-  box.obs = h->rs_dev + kRsOut;
-  box.rew = h->rs_dev + rs_rew_off(h);
-  box.done = h->rs_dev + rs_done_off(h);
-  box.next = next;
-  box.idle_ticks = h->rs_idle;
-  box.use_noise = use_noise;
-  // after everything already queued on the handle's stream (reset, set_state, ...)
-  HIP_TRY(hipEventRecord(h->rs_ev, h->stream));
-  HIP_TRY(hipStreamWaitEvent(h->rs_stream, h->rs_ev, 0));
-  const int e = lz::launch_resident(h->cfg.system, h->f64, a, box, h->rs_stream);
+static lz_status rs_server_launch(RsServer& sv) {
+  for (int i = 0; i < sv.n; ++i) {
+    lz_handle* m = sv.members[i];
+    lz::ResMember& r = sv.table_host[i];
+    std::memset(&r, 0, sizeof r);
+    fill_common(m, r.a);
+    r.system = m->cfg.system;
+    r.f64 = m->f64;
+    lz::ResBox& box = r.box;
+    box.cmd = reinterpret_cast<const int64_t*>(m->rs_dev + kRsCmd);
+    box.resp = reinterpret_cast<int64_t*>(m->rs_dev + kRsResp);
+    box.act = reinterpret_cast<const float*>(m->rs_dev + kRsAct);
+    box.noise = reinterpret_cast<const double*>(m->rs_dev + kRsNoise);
+    box.obs = m->rs_dev + kRsOut;
+    box.rew = m->rs_dev + rs_rew_off(m);
+    box.done = m->rs_dev + rs_done_off(m);
+    for (int p = 0; p < m->desc.n_planes; ++p) {
+      box.pub[p] = m->rs_dev + rs_pub_off(m) + (size_t)p * rs_pub_stride(m);
+      box.pub_es[p] = plane_elem(m->cfg.system, m->f64, p);
+    }
+    box.next = m->rs_seq + 1;  // the requester's pending request, the others' next one
+    box.use_noise = m->rs_use_noise;
+    // after everything already queued on the member's stream (reset, set_state, ...)
+    HIP_TRY(hipEventRecord(sv.ev, m->stream));
+    HIP_TRY(hipStreamWaitEvent(sv.stream, sv.ev, 0));
+  }
+  HIP_TRY(hipMemcpyAsync(sv.table_dev, sv.table_host, sizeof(lz::ResMember) * sv.n,
+                         hipMemcpyHostToDevice, sv.stream));
+  const int e = lz::launch_resident_multi(sv.table_dev, sv.n, sv.idle, sv.stream);
   if (e != 0) return fail(LZ_ERR_HIP, "resident launch: %s", hipGetErrorString((hipError_t)e));
-  h->rs_active = true;
-  h->rs_use_noise = use_noise;
-  rs_live_add(h);
+  sv.active = true;
+  for (int i = 0; i < sv.n; ++i) sv.members[i]->rs_active = true;
   static const int registered = std::atexit(resident_unload);
   (void)registered;
   return LZ_OK;
 }
 
-// the launch has ended (stop command or idle exit): its state is in the planes and its
-// tick in the other ping-pong slot
-static void resident_ended(lz_handle* h) {
-  h->rs_active = false;
-  h->parity ^= 1;
-  rs_live_remove(h);
+static lz_status resident_quiesce(lz_handle* h) {
+  std::lock_guard<std::mutex> lk(g_rs_mu);
+  if (!h->rs_active) return LZ_OK;
+  (void)hipSetDevice(h->cfg.device);
+  return rs_server_stop(rs_server(h));
 }
 
-static lz_status resident_stop(lz_handle* h) {
-  __atomic_store_n(const_cast<int64_t*>(rs_word(h, kRsCmd)), (int64_t)-1, __ATOMIC_RELEASE);
-  const hipError_t e = hipStreamSynchronize(h->rs_stream);
-  resident_ended(h);
-  if (e != hipSuccess) return fail(LZ_ERR_HIP, "resident stop: %s", hipGetErrorString(e));
-  return LZ_OK;
+// lz_destroy: stop the server if it serves the handle, drop the membership
+static void resident_leave(lz_handle* h) {
+  std::lock_guard<std::mutex> lk(g_rs_mu);
+  RsServer& sv = rs_server(h);
+  if (h->rs_active) (void)rs_server_stop(sv);
+  for (int i = 0; i < sv.n; ++i)
+    if (sv.members[i] == h) {
+      sv.members[i] = sv.members[--sv.n];
+      break;
+    }
+  h->rs_member = false;
 }
 
 lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noise, void* obs_out,
@@ -624,41 +711,51 @@ lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noi
     return fail(LZ_ERR_STATE, "lz_resident_step: the handle's stream is being captured "
                               "(a synchronous host round trip cannot be captured)");
   const size_t es = h->f64 ? 8 : 4;
-  if (!h->rs_pin) {
-    const size_t bytes = rs_done_off(h) + align16((size_t)n);
-    if (hipHostMalloc(reinterpret_cast<void**>(&h->rs_pin), bytes,
-                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+  if (!h->rs_pin) {  // built in locals, assigned to the handle once complete
+    const size_t bytes = rs_bytes(h);
+    uint8_t* pin = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&pin), bytes, hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipSuccess)
       return fail(LZ_ERR_OOM, "lz_resident_step: mailbox (%zu B)", bytes);
-    std::memset(h->rs_pin, 0, bytes);
+    std::memset(pin, 0, bytes);
     void* dp = nullptr;
-    if (hipHostGetDevicePointer(&dp, h->rs_pin, 0) != hipSuccess || !dp)
+    if (hipHostGetDevicePointer(&dp, pin, 0) != hipSuccess || !dp) {
+      (void)hipHostFree(pin);
       return fail(LZ_ERR_HIP, "lz_resident_step: no device address for the mailbox");
+    }
+    h->rs_pin = pin;
     h->rs_dev = static_cast<uint8_t*>(dp);
-    HIP_TRY(hipStreamCreateWithFlags(&h->rs_stream, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&h->rs_ev, hipEventDisableTiming));
-    int khz = 0;
-    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->cfg.device) != hipSuccess ||
-        khz <= 0)
-      khz = 100000;
-    const char* ev = std::getenv("LZ_RESIDENT_IDLE_US");
-    // short: a device-wide synchronize (torch.cuda.synchronize()) waits for the idle
-    // exit, and a caller that leaves > 1 ms between steps pays one relaunch (~20 us)
-    const double idle_us = ev ? std::atof(ev) : 1000.0;
-    h->rs_idle = (uint64_t)(idle_us * khz / 1000.0);
     h->rs_seq = 0;
+  }
+  std::unique_lock<std::mutex> lk(g_rs_mu);
+  RsServer& sv = rs_server(h);
+  {
+    const lz_status q = rs_server_init(sv, h->cfg.device);
+    if (q != LZ_OK) return q;
+  }
+  if (!h->rs_member) {
+    if (sv.n >= lz::kRsMaxHandles) {
+      // more handles than server waves: this one steps by launches (same results)
+      lk.unlock();
+      return lz_step_host(h, actions, noise, obs_out, rew_out, done_out);
+    }
+    const lz_status q = rs_server_stop(sv);  // relaunched below with the new member
+    if (q != LZ_OK) return q;
+    sv.members[sv.n++] = h;
+    h->rs_member = true;
   }
   const int use_noise = noise != nullptr;
   if (h->rs_active && use_noise != h->rs_use_noise) {
-    const lz_status q = resident_stop(h);
+    const lz_status q = rs_server_stop(sv);
     if (q != LZ_OK) return q;
   }
+  h->rs_use_noise = use_noise;
   const int64_t seq = h->rs_seq + 1;
   if (needs_act) std::memcpy(h->rs_pin + kRsAct, actions, (size_t)n * h->desc.action_dim * 4);
   if (noise) std::memcpy(h->rs_pin + kRsNoise, noise, (size_t)n * 3 * 8);
   __atomic_store_n(const_cast<int64_t*>(rs_word(h, kRsCmd)), seq, __ATOMIC_RELEASE);
-  h->rs_seq = seq;
-  if (!h->rs_active) {
-    const lz_status q = resident_launch(h, seq, use_noise);
+  if (!sv.active) {
+    const lz_status q = rs_server_launch(sv);
     if (q != LZ_OK) return q;
   }
   volatile int64_t* resp = rs_word(h, kRsResp);
@@ -666,16 +763,19 @@ lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noi
     if (__atomic_load_n(const_cast<int64_t*>(resp), __ATOMIC_ACQUIRE) == seq) break;
     if ((spin & 4095u) == 0) {
       // the server may have exited (idle) before it saw this request
-      const hipError_t q = hipStreamQuery(h->rs_stream);
+      const hipError_t q = hipStreamQuery(sv.stream);
       if (q == hipErrorNotReady) continue;
       if (__atomic_load_n(const_cast<int64_t*>(resp), __ATOMIC_ACQUIRE) == seq) break;
-      resident_ended(h);
+      rs_server_ended(sv);
       if (q != hipSuccess) return fail(LZ_ERR_HIP, "resident server: %s", hipGetErrorString(q));
-      const lz_status r = resident_launch(h, seq, use_noise);
+      const lz_status r = rs_server_launch(sv);
       if (r != LZ_OK) return r;
     }
     __builtin_ia32_pause();
   }
+  h->rs_seq = seq;
+  h->rs_pub_valid = true;
+  lk.unlock();
   std::memcpy(obs_out, h->rs_pin + kRsOut, (size_t)n * h->desc.obs_dim * es);
   std::memcpy(rew_out, h->rs_pin + rs_rew_off(h), (size_t)n * es);
   std::memcpy(done_out, h->rs_pin + rs_done_off(h), (size_t)n);
@@ -686,6 +786,25 @@ lz_status lz_resident_stop(lz_handle* h) {
   if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
   HIP_TRY(hipSetDevice(h->cfg.device));
   RESIDENT_QUIESCE(h);
+  return LZ_OK;
+}
+
+lz_status lz_resident_read_state(lz_handle* h, int32_t plane, void* host_dst) {
+  if (!h || !host_dst) return fail(LZ_ERR_INVALID, "handle/host_dst is NULL");
+  const int es = plane_elem(h->cfg.system, h->f64, plane);
+  if (!es) return fail(LZ_ERR_INVALID, "invalid plane %d", plane);
+  const size_t bytes = (size_t)h->cfg.num_envs * es;
+  {
+    std::lock_guard<std::mutex> lk(g_rs_mu);
+    if (h->rs_active && h->rs_pub_valid) {  // the server's copy after its last request
+      std::memcpy(host_dst, h->rs_pin + rs_pub_off(h) + (size_t)plane * rs_pub_stride(h), bytes);
+      return LZ_OK;
+    }
+  }
+  RESIDENT_QUIESCE(h);
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  HIP_TRY(hipMemcpyAsync(host_dst, h->planes[plane], bytes, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
   return LZ_OK;
 }
 
@@ -847,14 +966,16 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
 }
 
 // arch: 0 = MlpPolicy (bf16), 1 = attention extractor, 2 = residual + LayerNorm attention
-// on VecFrameStack(n_stack) observations, 3 = MlpPolicy in float32
+// on VecFrameStack(n_stack) observations, 3 = MlpPolicy in float32, 4 / 5 = arch 1 / 2 in
+// float32
 static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, int arch,
                                 int n_stack = 1, const float* stack_in = nullptr,
                                 float* stack_out = nullptr) {
   if (!h || !r) return fail(LZ_ERR_INVALID, "handle/args is NULL");
   RESIDENT_QUIESCE(h);
-  const bool attn = arch == 1 || arch == 2;
-  if (arch == 2) {
+  const bool attn = arch == 1 || arch == 2 || arch == 4 || arch == 5;
+  const bool stacked = arch == 2 || arch == 5;
+  if (stacked) {
     if (n_stack != 1 && n_stack != 4) return fail(LZ_ERR_UNSUPPORTED, "n_stack must be 1 or 4");
     if (!stack_in || !stack_out) return fail(LZ_ERR_INVALID, "stack_in / stack_out must be non-NULL");
     if (r->obs_norm || r->obs_moments)
@@ -863,6 +984,11 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
     if (sys != LZ_SYS_LORENZ3 && sys != LZ_SYS_PMSM && sys != LZ_SYS_HR)
       return fail(LZ_ERR_UNSUPPORTED, "the frame-stacked rollout runs LORENZ3 / PMSM / HR");
     if (n_stack * h->desc.obs_dim > lz::kLnMaxIn) return fail(LZ_ERR_UNSUPPORTED, "stacked obs > 32 dims");
+  }
+  if (arch == 4) {
+    const int sys = h->cfg.system;
+    if (sys != LZ_SYS_LORENZ3 && sys != LZ_SYS_PMSM && sys != LZ_SYS_HR)
+      return fail(LZ_ERR_UNSUPPORTED, "the float32 attention rollout runs LORENZ3 / PMSM / HR");
   }
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_rollout_policy before the first lz_reset");
   if (h->f64) return fail(LZ_ERR_UNSUPPORTED, "the policy rollout runs float32 handles only");
@@ -876,7 +1002,8 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
   if (!(r->act_low <= r->act_high)) return fail(LZ_ERR_INVALID, "act_low > act_high");
   HIP_TRY(hipSetDevice(h->cfg.device));
   const int64_t n = h->cfg.num_envs;
-  const lz::PolShape sh = attn        ? lz::attn_policy_shape(n, h->num_cus)
+  const lz::PolShape sh = arch >= 4   ? lz::attn_f32_policy_shape(n, h->num_cus, arch == 5)
+                         : attn      ? lz::attn_policy_shape(n, h->num_cus)
                          : arch == 3 ? lz::f32_policy_shape(n, h->num_cus)
                                      : lz::policy_shape(n, h->cfg.reserved[0], h->num_cus);
   const int W = sh.waves, grid = sh.grid;
@@ -919,7 +1046,9 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
   p.partials = r->obs_moments ? h->pol_part : nullptr;
   p.stack_in = stack_in;
   p.stack_out = stack_out;
-  int e = arch == 2 ? lz::launch_rollout_policy_attn_ln(h->cfg.system, n_stack, a, p, sh, h->stream)
+  int e = arch >= 4 ? lz::launch_rollout_policy_attn_f32(h->cfg.system, arch == 5, n_stack, a, p, sh,
+                                                        h->stream)
+          : arch == 2 ? lz::launch_rollout_policy_attn_ln(h->cfg.system, n_stack, a, p, sh, h->stream)
           : arch == 1 ? lz::launch_rollout_policy_attn(h->cfg.system, a, p, sh, h->stream)
           : arch == 3 ? lz::launch_rollout_policy_f32(h->cfg.system, a, p, sh, h->stream)
                       : lz::launch_rollout_policy(h->cfg.system, a, p, sh, h->stream);
@@ -1053,6 +1182,15 @@ lz_status lz_rollout_policy_f32_vn(lz_handle* h, const lz_policy_rollout_args* r
 lz_status lz_rollout_policy_attn_stack(lz_handle* h, const lz_policy_rollout_args* r,
                                        int32_t n_stack, const float* stack_in, float* stack_out) {
   return rollout_policy(h, r, 2, n_stack, stack_in, stack_out);
+}
+
+lz_status lz_rollout_policy_attn_f32(lz_handle* h, const lz_policy_rollout_args* r) {
+  return rollout_policy(h, r, 4);
+}
+
+lz_status lz_rollout_policy_attn_stack_f32(lz_handle* h, const lz_policy_rollout_args* r,
+                                           int32_t n_stack, const float* stack_in, float* stack_out) {
+  return rollout_policy(h, r, 5, n_stack, stack_in, stack_out);
 }
 
 int32_t lz_plane_elem_size(const lz_handle* h, int32_t plane) {

@@ -185,6 +185,58 @@ constexpr int kF32LogStd = 2 * kF32Net;
 constexpr int kF32Tanh = kF32LogStd + 64;           // tanh table: 72 segments x 8 floats
 constexpr int kF32BlobBytes = kF32Tanh + 72 * 32;   // 147904 B (resident in LDS)
 
+// The attention actor-critics at SB3's precision (float32 operands and accumulation;
+// lz_attn_policy_pack_f32 / lz_attn_ln_policy_pack_f32 -> k_rollout_policy_attn_f32).
+// Every product-sum runs on v_mfma_f32_16x16x4_f32 (a k-ordered fmaf chain: lane group
+// G = lane >> 4 supplies k = G of each k-step) with the weights as the A operand: a wave
+// holds 16 envs (column c = lane & 15), every 16-unit output tile lands as lane group G,
+// register i = unit 4G + i -- token t = fc1 tile t, head G's key / query / value dims
+// in lane group G -- and that layout is the next projection's k order (k-step s takes
+// register s: input 4G + s), so nothing moves between lanes and each lane group runs
+// one head's softmax.  Blob (bytes; "[tile][quad][64 lanes] f32x4" = 4 k-steps per lane
+// per 16-B LDS read; biases, LayerNorm affine and head rows in natural order):
+//   extractor: fc1 [8 tiles][2 quads][64] (k-step s: input 4s + G, zero past the input
+//              width) + bias [128]; keys, values, queries (x 0.5 = 1/sqrt(4), exact),
+//              out_proj: [64] f32x4 each (k-step s: token dim 4G + s) + biases [16];
+//              LayerNorm weight / bias [16]; post_attention_fc [4 tiles][8 tokens][64]
+//              (token i's 4 k-steps) + bias [64]
+//   net 0 (pi) / net 1 (vf): layer 1 [8 tiles][4 quads][64] (k-step q = 4f + s: feature
+//              16f + 4G + s), layer 2 [8 tiles][8 quads][64], b1 / b2 [128], head rows
+//              [4][128], head bias [4]
+//   log_std / Normal constants float[16], the tanh table (kF32Tanh's)
+// Both nets do not fit in LDS with the extractor (54 + 2 x 100 KB): the workgroup keeps
+// the extractor, the constants and ONE net slot, and LDS-DMAs pi / vf into the slot.
+constexpr int kAFMaxIn = 32;                                // fc1 inputs: 8 k-steps, 2 quads
+constexpr int kAFFc1W = 0;
+constexpr int kAFFc1B = kAFFc1W + 8 * 2 * 64 * 16;
+constexpr int kAFKW = kAFFc1B + 128 * 4;
+constexpr int kAFVW = kAFKW + 64 * 16;
+constexpr int kAFQW = kAFVW + 64 * 16;
+constexpr int kAFOW = kAFQW + 64 * 16;
+constexpr int kAFKB = kAFOW + 64 * 16;
+constexpr int kAFVB = kAFKB + 16 * 4;
+constexpr int kAFQB = kAFVB + 16 * 4;
+constexpr int kAFOB = kAFQB + 16 * 4;
+constexpr int kAFGam = kAFOB + 16 * 4;
+constexpr int kAFBet = kAFGam + 16 * 4;
+constexpr int kAFPostW = kAFBet + 16 * 4;
+constexpr int kAFPostB = kAFPostW + 4 * 8 * 64 * 16;
+constexpr int kAFExt = kAFPostB + 64 * 4;                   // 54,400 B
+constexpr int kAFN1 = 0;
+constexpr int kAFN2 = kAFN1 + 8 * 4 * 64 * 16;
+constexpr int kAFNB1 = kAFN2 + 8 * 8 * 64 * 16;
+constexpr int kAFNB2 = kAFNB1 + 128 * 4;
+constexpr int kAFNH = kAFNB2 + 128 * 4;
+constexpr int kAFNHB = kAFNH + 4 * 128 * 4;
+constexpr int kAFNet = 100 * 1024;                          // 101,392 B padded to whole 1-KiB DMA pieces
+static_assert(kAFNHB + 16 <= kAFNet, "attention net slot");
+constexpr int kAFPi = kAFExt, kAFVf = kAFExt + kAFNet;
+constexpr int kAFConst = 64 + 72 * 32;                      // log_std consts + tanh table
+constexpr int kAFLogStd = kAFExt + 2 * kAFNet;
+constexpr int kAFTanh = kAFLogStd + 64;
+constexpr int kAFBlobBytes = kAFLogStd + kAFConst;          // 261,568 B (device)
+constexpr int kAFLdsBytes = kAFExt + kAFConst + kAFNet;     // 159,168 B (LDS)
+
 struct PArgs {
   const uint8_t* blob;     // device copy of the packed policy
   const float* obs_in;     // [N, O] raw observation at rollout start
@@ -270,14 +322,20 @@ lz_status set_error(lz_status s, const char* msg);
 int launch_reset(int system, int f64, const KArgs& a, void* stream);
 int launch_step(int system, int f64, const KArgs& a, void* stream);
 
-// Resident step server of a small handle (lz_resident_step, n <= 64 envs, one wave):
-// the device addresses of its mailbox in mapped, coherent host memory.  The kernel
-// holds the state in registers, polls *cmd (system-scope loads), serves request
-// `next`, `next + 1`, ... each exactly as one k_step launch would (step_body), writes
-// obs | reward | done into the mailbox and then *resp = the request's number (release,
-// system scope).  It stores the state back and exits on cmd == -1 or after idle_ticks
-// wall-clock ticks without a request; the host relaunches it when a request finds it
-// gone.
+// Resident step server (lz_resident_step): ONE launch per process and device serves
+// every handle that steps through lz_resident_step -- one wave per handle (n <= 64 envs
+// each, up to kRsMaxHandles handles), so a DummyVecEnv of several drop-in envs shares one
+// polling launch on one stream (one hardware queue) instead of one per handle.  Each
+// wave holds its handle's state in registers, polls the handle's mailbox in mapped,
+// coherent host memory (*cmd, system-scope loads), serves request `next`, `next + 1`, ...
+// each exactly as one k_step launch would (step_body), writes obs | reward | done and
+// the handle's state planes (pub: the copy lz_resident_read_state returns without
+// stopping the server) into the mailbox and then *resp = the request's number (release,
+// system scope).  The waves leave together: on cmd == -1 in any mailbox, or when no
+// mailbox has seen a request for idle_ticks wall-clock ticks; each stores its state back
+// to the planes.  The host relaunches the server (with every registered handle) when a
+// request finds it gone.
+constexpr int kRsMaxHandles = 16;
 struct ResBox {
   const int64_t* cmd;   // host -> device: request number, -1 = stop
   int64_t* resp;        // device -> host: number of the last request served
@@ -286,11 +344,18 @@ struct ResBox {
   void* obs;            // T [n, O]
   void* rew;            // T [n]
   uint8_t* done;        // [n]
+  void* pub[kMaxPlanes];  // the published state planes [n] each (nullptr past n_planes)
+  int32_t pub_es[kMaxPlanes];  // their element sizes
   int64_t next;         // first request this launch serves
-  uint64_t idle_ticks;  // wall_clock64() ticks
   int32_t use_noise;
 };
-int launch_resident(int system, int f64, const KArgs& a, const ResBox& box, void* stream);
+struct ResMember {      // one wave of the server
+  KArgs a;
+  ResBox box;
+  int32_t system, f64;
+};
+// table: device copy of n members; one workgroup of 64 n threads
+int launch_resident_multi(const ResMember* table, int n, uint64_t idle_ticks, void* stream);
 int launch_rollout(int system, int f64, const KArgs& a, void* stream);
 int launch_step_vecnorm(int system, int f64, const KArgs& a, const VArgs& v, void* stream);
 // Launch shape of the policy rollout (one workgroup per CU: the weights fill LDS).
@@ -341,6 +406,12 @@ int launch_rollout_policy_attn(int system, const KArgs& a, const PArgs& p, const
 // n_stack 1 or 4, same shape as attn_policy_shape
 int launch_rollout_policy_attn_ln(int system, int n_stack, const KArgs& a, const PArgs& p,
                                   const PolShape& sh, void* stream);
+// the attention actor-critics in float32 (kAF* blob): ln = 0 code/train.py's extractor,
+// 1 the residual + LayerNorm variant on VecFrameStack(n_stack = 1 or 4); systems LORENZ3 /
+// PMSM / HR; attn_f32_policy_shape's grid (16 envs per wave, 8 or 4 waves)
+PolShape attn_f32_policy_shape(int64_t n, int num_cus, int ln);
+int launch_rollout_policy_attn_f32(int system, int ln, int n_stack, const KArgs& a, const PArgs& p,
+                                   const PolShape& sh, void* stream);
 int launch_policy_moments_final(const double* partials, int nparts, int width, double count,
                                 double* out, void* stream);
 

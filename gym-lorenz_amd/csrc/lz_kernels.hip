@@ -899,39 +899,66 @@ static int dispatch(int which, int system, int f64, const KArgs& a, void* stream
 }
 
 // ------------------------------------------------------------------ resident step server
-// lz_resident_step (lz_internal.h ResBox): the per-env drop-in classes step ONE env per
-// env.step() call, and a launch + stream synchronisation per call costs 20-27 us
-// (profiles/r01/dropin).  This kernel stays on the GPU between calls: lane 0 polls the
-// host's command word over PCIe, the wave serves the request with the same step_body
-// as k_step (state in registers, tick += 1 per request, injected noise staged through
-// LDS), and the reply goes straight into host memory.  Bounded: it exits on the stop
-// command or after idle_ticks without one.
+// lz_resident_step (lz_internal.h ResBox / ResMember): the per-env drop-in classes step
+// ONE env per env.step() call, and a launch + stream synchronisation per call costs
+// 20-27 us (profiles/r01/dropin).  This kernel stays on the GPU between calls, one wave
+// per registered handle: lane 0 polls its handle's command word over PCIe, the wave
+// serves the request with the same step_body as k_step (state in registers, tick += 1
+// per request, injected noise staged through LDS), and the reply goes straight into host
+// memory.  Bounded: every wave leaves on a stop command in any mailbox or after
+// idle_ticks without a request in any mailbox (the shared flag / clock in LDS), so the
+// launch ends as a whole and a relaunch includes every handle.
+struct ResShared {
+  int exit_;
+  unsigned long long last;  // wall_clock64() of the latest request served by any wave
+};
+
 template <class Sys, typename T>
-__global__ __launch_bounds__(64) void k_resident(KArgs a, ResBox box) {
-  const int lane = (int)threadIdx.x;
+__device__ void resident_serve(const ResMember& m, ResShared* sh, double* s_nz, uint64_t idle_ticks) {
+  const KArgs& a = m.a;
+  const ResBox& box = m.box;
+  const int lane = (int)(threadIdx.x & 63u);
   const bool live = lane < a.n;
-  __shared__ double s_nz[64 * 3];
   Sys sys;
   sys.setup(a);
   int32_t steps = 0;
   if (live) {
     sys.load(a, lane);
     if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[lane];
+    // the published copy starts as the planes (every plane, byte for byte)
+    for (int p = 0; p < kMaxPlanes; ++p) {
+      const int es = box.pub_es[p];
+      if (es == 8) static_cast<uint64_t*>(box.pub[p])[lane] = static_cast<const uint64_t*>(a.pl[p])[lane];
+      else if (es == 4) static_cast<uint32_t*>(box.pub[p])[lane] = static_cast<const uint32_t*>(a.pl[p])[lane];
+    }
   }
   uint64_t tick = *a.tick_in;
   if (lane == 0) *a.counter_next = 0;  // as k_step leaves it for the launch that follows
   KArgs b = a;
   b.noise = box.use_noise ? s_nz : nullptr;
   b.term_obs = nullptr;
+  KArgs pubk = a;  // sys.store into the published planes
+#pragma unroll
+  for (int p = 0; p < kMaxPlanes; ++p) pubk.pl[p] = box.pub[p];
   int64_t next = box.next;
-  uint64_t t_last = wall_clock64();
   for (;;) {
     int64_t c = 0;
     if (lane == 0) {
       for (;;) {
         c = __hip_atomic_load(box.cmd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (c == next || c < 0) break;
-        if (wall_clock64() - t_last > box.idle_ticks) {
+        if (c == next) break;
+        if (c < 0) {  // stop: every wave leaves
+          __hip_atomic_store(&sh->exit_, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          break;
+        }
+        if (__hip_atomic_load(&sh->exit_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+          c = -2;
+          break;
+        }
+        const unsigned long long last =
+            __hip_atomic_load(&sh->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (wall_clock64() - last > idle_ticks) {
+          __hip_atomic_store(&sh->exit_, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           c = -2;
           break;
         }
@@ -966,12 +993,17 @@ __global__ __launch_bounds__(64) void k_resident(KArgs a, ResBox box) {
       for (int j = 0; j < Sys::O; ++j) static_cast<T*>(box.obs)[lane * Sys::O + j] = o[j];
       static_cast<T*>(box.rew)[lane] = rew;
       box.done[lane] = d;
+      sys.store(pubk, lane);
+      if (a.count_steps) static_cast<int32_t*>(pubk.pl[Sys::kStepPlane])[lane] = steps;
     }
     tick += 1;
     // the outputs of the whole wave reach host memory before the reply (release)
-    if (lane == 0) __hip_atomic_store(box.resp, next, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0) {
+      __hip_atomic_store(box.resp, next, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_fetch_max(&sh->last, (unsigned long long)wall_clock64(), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     ++next;
-    t_last = wall_clock64();
   }
   if (live) {
     sys.store(a, lane);
@@ -980,33 +1012,45 @@ __global__ __launch_bounds__(64) void k_resident(KArgs a, ResBox box) {
   if (lane == 0) *a.tick_out = tick;
 }
 
-template <class Sys, typename T>
-static int launch_res(const KArgs& a, const ResBox& box, hipStream_t s) {
-  hipLaunchKernelGGL((k_resident<Sys, T>), dim3(1), dim3(64), 0, s, a, box);
-  return (int)hipGetLastError();
+__global__ __launch_bounds__(64 * kRsMaxHandles) void k_resident_multi(const ResMember* __restrict__ table,
+                                                                       uint64_t idle_ticks) {
+  __shared__ ResShared sh;
+  __shared__ double s_nz[kRsMaxHandles][64 * 3];
+  // wave-uniform to the compiler too: the member's fields are scalar loads, and the
+  // PMSM bias table pointer can feed its scalar load (SysPMSM::sload2)
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (threadIdx.x == 0) {
+    sh.exit_ = 0;
+    sh.last = wall_clock64();
+  }
+  __syncthreads();
+  const ResMember& m = table[wave];
+  const int key = m.system * 2 + m.f64;
+  switch (key) {  // wave-uniform: each wave runs its own handle's system
+    case LZ_SYS_LORENZ3 * 2: resident_serve<SysL3<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_LORENZ3 * 2 + 1: resident_serve<SysL3<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_LORENZ4 * 2: resident_serve<SysL4<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_LORENZ4 * 2 + 1: resident_serve<SysL4<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_PMSM * 2: resident_serve<SysPMSM, float>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_HR * 2: resident_serve<SysHR<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_HR * 2 + 1: resident_serve<SysHR<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_T1 * 2: resident_serve<SysT1<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_T1 * 2 + 1: resident_serve<SysT1<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_T2 * 2: resident_serve<SysT2<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_T2 * 2 + 1: resident_serve<SysT2<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_TP * 2: resident_serve<SysTP<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_TP * 2 + 1: resident_serve<SysTP<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_SC * 2: resident_serve<SysSC<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_SC * 2 + 1: resident_serve<SysSC<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
+    default: break;
+  }
 }
 
-int launch_resident(int system, int f64, const KArgs& a, const ResBox& box, void* stream) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  switch (system) {
-    case LZ_SYS_LORENZ3:
-      return f64 ? launch_res<SysL3<double>, double>(a, box, s) : launch_res<SysL3<float>, float>(a, box, s);
-    case LZ_SYS_LORENZ4:
-      return f64 ? launch_res<SysL4<double>, double>(a, box, s) : launch_res<SysL4<float>, float>(a, box, s);
-    case LZ_SYS_PMSM:
-      return launch_res<SysPMSM, float>(a, box, s);
-    case LZ_SYS_HR:
-      return f64 ? launch_res<SysHR<double>, double>(a, box, s) : launch_res<SysHR<float>, float>(a, box, s);
-    case LZ_SYS_T1:
-      return f64 ? launch_res<SysT1<double>, double>(a, box, s) : launch_res<SysT1<float>, float>(a, box, s);
-    case LZ_SYS_T2:
-      return f64 ? launch_res<SysT2<double>, double>(a, box, s) : launch_res<SysT2<float>, float>(a, box, s);
-    case LZ_SYS_TP:
-      return f64 ? launch_res<SysTP<double>, double>(a, box, s) : launch_res<SysTP<float>, float>(a, box, s);
-    case LZ_SYS_SC:
-      return f64 ? launch_res<SysSC<double>, double>(a, box, s) : launch_res<SysSC<float>, float>(a, box, s);
-  }
-  return (int)hipErrorInvalidValue;
+int launch_resident_multi(const ResMember* table, int n, uint64_t idle_ticks, void* stream) {
+  if (n < 1 || n > kRsMaxHandles) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_resident_multi, dim3(1), dim3(64 * n), 0, static_cast<hipStream_t>(stream), table,
+                     idle_ticks);
+  return (int)hipGetLastError();
 }
 
 // lz_step_vecnorm's envs per workgroup: kVnBlock on the fused path, kBlock on the split

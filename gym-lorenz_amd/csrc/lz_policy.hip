@@ -720,33 +720,20 @@ __device__ __forceinline__ float tanh_tab(float x, const float* tab) {
   return __builtin_copysignf(y, x);
 }
 
-// One net on the wave's 32-env tile.  xs[s] = this lane's layer-1 input for k-step s
-// (obs[2s + h] of env lane & 31).  Returns the NH head rows in head[] on every lane
-// (both halves hold the same values).
-template <int KS1, int NH>
-__device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int lane, float* head,
-                                        const float* ttab) {
-  asm volatile("" ::: "memory");
+// Layer 2 (128 -> 128, tanh_tab) and the NH head rows of a float32 net, from layer 1's
+// activations a1[4] (accumulator layout: tile t register g of half h = unit 32t +
+// row(g, h)).  w2 [4 out tiles][16 quads][64 lanes][4] (k-step q: input unit 32 (q >> 4)
+// + row(q & 15, h)), b2 [4][2][16], head rows [NH][2 halves][64], head bias [NH].
+// Returns the head rows in head[] on every lane (both halves hold the same values).
+template <int NH>
+__device__ __forceinline__ void mlp_f32_tail(const uint8_t* w2p, const uint8_t* b2p, const uint8_t* whp,
+                                             const uint8_t* bhp, const f32x16* a1, int lane,
+                                             float* head, const float* ttab) {
   const int h = lane >> 5;
-  const f32x4* w1 = reinterpret_cast<const f32x4*>(net + kF32W1) + lane;
-  const f32x4* w2 = reinterpret_cast<const f32x4*>(net + kF32W2) + lane;
-  const f32x16* b1 = reinterpret_cast<const f32x16*>(net + kF32B1) + h;
-  const f32x16* b2 = reinterpret_cast<const f32x16*>(net + kF32B2) + h;
-  const float* wh = reinterpret_cast<const float*>(net + kF32H) + h * 64;
-  const float* bh = reinterpret_cast<const float*>(net + kF32HB);
-  f32x16 a1[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const f32x4 w = w1[t * 64];
-    f32x16 c = b1[2 * t];
-#pragma unroll
-    for (int s = 0; s < KS1; ++s) c = mfma_f32(w[s], xs[s], c);
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      c[g] = tanh_tab(c[g], ttab);
-    }
-    a1[t] = c;
-  }
+  const f32x4* w2 = reinterpret_cast<const f32x4*>(w2p) + lane;
+  const f32x16* b2 = reinterpret_cast<const f32x16*>(b2p) + h;
+  const float* wh = reinterpret_cast<const float*>(whp) + h * 64;
+  const float* bh = reinterpret_cast<const float*>(bhp);
   float acc[NH];
 #pragma unroll
   for (int j = 0; j < NH; ++j) acc[j] = 0.0f;  // first step fmaf(w, v, +0)
@@ -781,6 +768,32 @@ __device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int
     const float o = __shfl_xor(acc[j], 32, 64);
     head[j] = (acc[j] + o) + bh[j];  // IEEE add commutes: both halves get the same bits
   }
+}
+
+// One net on the wave's 32-env tile.  xs[s] = this lane's layer-1 input for k-step s
+// (obs[2s + h] of env lane & 31).  Returns the NH head rows in head[] on every lane
+// (both halves hold the same values).
+template <int KS1, int NH>
+__device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int lane, float* head,
+                                        const float* ttab) {
+  asm volatile("" ::: "memory");
+  const int h = lane >> 5;
+  const f32x4* w1 = reinterpret_cast<const f32x4*>(net + kF32W1) + lane;
+  const f32x16* b1 = reinterpret_cast<const f32x16*>(net + kF32B1) + h;
+  f32x16 a1[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f32x4 w = w1[t * 64];
+    f32x16 c = b1[2 * t];
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) c = mfma_f32(w[s], xs[s], c);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      c[g] = tanh_tab(c[g], ttab);
+    }
+    a1[t] = c;
+  }
+  mlp_f32_tail<NH>(net + kF32W2, net + kF32B2, net + kF32H, net + kF32HB, a1, lane, head, ttab);
 }
 
 // this lane's layer-1 inputs from the env-owning lane (half 0) of its env
@@ -1260,6 +1273,568 @@ __global__ __launch_bounds__(W * 64) void k_policy_step_f32(KArgs a, PArgs p, PS
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The attention actor-critics at SB3's precision: code/train.py:52-112 (PPO, the
+// AttentionFeaturesExtractor shared by pi and vf) and code/lorenz_filter/train.py:54-132
+// (the residual + LayerNorm variant on VecFrameStack(4)), float32 end to end -- the
+// oracle (lz_oracle.c orc_attn_f32) restates every operation in this order, bit for bit.
+// Layout (lz_internal.h kAF*): v_mfma_f32_16x16x4_f32, 16 envs per wave, lane group
+// G = lane >> 4 holds units 4G .. 4G+3 of every 16-unit tile, which is also the k order
+// of the next projection -- so token t is fc1 tile t, lane group G holds head G's query,
+// keys and values and runs head G's softmax, and nothing moves between lanes:
+//   fc1 + ReLU            (relu keeps NaN)
+//   K, V, Q per token     Q with the exact 1/sqrt(4) = 0.5 folded (torch scales q)
+//   attention, head G     scores as fmaf chains, NaN-propagating max, exp_att, the sum in
+//                         key order, one division 1 / sum, weights e_j * (1 / sum), outputs
+//                         as fmaf chains over the keys (torch: softmax, then weights @ v)
+//   out_proj
+//   [LayerNorm]           (x + attn): per lane group the sum of its 4 dims in order, the
+//                         groups' partials combined by a lane-16 then a lane-32 swap
+//                         ((p0 + p1) + (p2 + p3) on every lane), * 1/16; the biased
+//                         variance the same way; rstd = 1 / sqrtf(var + 1e-5);
+//                         fmaf(z * rstd, w, b)
+//   post_fc + ReLU, the pi / vf nets (layer 1 over the 64 features, tanh_tab, layer 2,
+//   tanh_tab) and the heads (per lane group an fmaf chain over its units, the groups
+//   combined like the LayerNorm sums, then the bias).
+// All four lanes of an env (c, c + 16, c + 32, c + 48) also run the env step, the sample
+// and the frame stack redundantly (step_body's lead flag: only lane group 0 takes a slot
+// in the compact done list; only lane group 0 stores), so every lane has the inputs its
+// k-steps need without a shuffle.
+// Both nets do not fit in LDS beside the extractor: the workgroup keeps the extractor,
+// the constants and ONE net slot, and LDS-DMAs (global_load_lds_dwordx4, 1 KiB per wave
+// instruction, no VGPR staging) pi into it while the step's features are extracted and
+// vf while the env steps.  The value of the step and the truncation bootstrap of the
+// PREVIOUS step (its terminal input extracted while vf lands) run from the vf slot after
+// the env step; the last step's bootstrap and the last values close the tile.  8 waves
+// (two per SIMD), every wave of the workgroup in lockstep through the swaps.
+
+// exp(x) for the softmax (x <= 0, or NaN): orc_exp_f32's operations exactly
+__device__ __forceinline__ float exp_att(float x) {
+  const float k = __builtin_rintf(x * 1.44269504088896341f);
+  float r = fmaf(k, -0.693145751953125f, x);
+  r = fmaf(k, -1.42860682030941723e-6f, r);
+  float p = fmaf(1.38888892e-3f, r, 8.33333377e-3f);
+  p = fmaf(p, r, 4.16666679e-2f);
+  p = fmaf(p, r, 1.66666672e-1f);
+  p = fmaf(p, r, 0.5f);
+  p = fmaf(p, r, 1.0f);
+  p = fmaf(p, r, 1.0f);
+  float y = __builtin_ldexpf(p, (int)k);
+  y = x < -86.0f ? 0.0f : y;
+  return x != x ? x : y;
+}
+
+__device__ __forceinline__ float relu_f(float v) { return v < 0.0f ? 0.0f : v; }  // NaN kept
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// (p0 + p1) + (p2 + p3) of the four lane groups' values, on every lane (IEEE addition
+// commutes, so each lane's order gives the same bits)
+__device__ __forceinline__ float group_sum4(float v) {
+  v = v + __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+// the 64 features (4 tiles) of one input; xs[s] = this lane group's fc1 input of k-step
+// s (input 4s + G)
+template <int KS, bool kLn>
+__device__ __forceinline__ void attn16_extract(const uint8_t* ext, const float* xs, int lane,
+                                               f32x4* feat) {
+  asm volatile("" ::: "memory");
+  const int G = lane >> 4;
+  constexpr int KQ = (KS + 3) / 4;
+  const f32x4* wf = reinterpret_cast<const f32x4*>(ext + kAFFc1W) + lane;
+  const f32x4* bf = reinterpret_cast<const f32x4*>(ext + kAFFc1B) + G;
+  // token t = fc1 tile t, computed twice (for the keys / values first, then again for
+  // the query and the residual): 8 KS MFMAs instead of 32 registers held through the
+  // attention
+  auto token = [&](int t) __attribute__((always_inline)) {
+    asm volatile("" ::: "memory");  // keep the LDS weight loads of different tiles apart
+    f32x4 c = bf[4 * t];
+#pragma unroll
+    for (int qd = 0; qd < KQ; ++qd) {
+      const f32x4 w = wf[(t * 2 + qd) * 64];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (4 * qd + e < KS) c = mfma16(w[e], xs[4 * qd + e], c);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] = relu_f(c[r]);
+    return c;
+  };
+  const f32x4 wk = reinterpret_cast<const f32x4*>(ext + kAFKW)[lane];
+  const f32x4 wv = reinterpret_cast<const f32x4*>(ext + kAFVW)[lane];
+  const f32x4 bk = reinterpret_cast<const f32x4*>(ext + kAFKB)[G];
+  const f32x4 bv = reinterpret_cast<const f32x4*>(ext + kAFVB)[G];
+  f32x4 K[kAttTokens], V[kAttTokens];  // head G's 4 key / value dims of each token
+#pragma unroll
+  for (int T = 0; T < kAttTokens; ++T) {
+    const f32x4 tk = token(T);
+    f32x4 ck = bk, cv = bv;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      ck = mfma16(wk[s], tk[s], ck);
+      cv = mfma16(wv[s], tk[s], cv);
+    }
+    K[T] = ck;
+    V[T] = cv;
+  }
+  const f32x4 wq = reinterpret_cast<const f32x4*>(ext + kAFQW)[lane];
+  const f32x4 wo = reinterpret_cast<const f32x4*>(ext + kAFOW)[lane];
+  const f32x4 bq = reinterpret_cast<const f32x4*>(ext + kAFQB)[G];
+  const f32x4 bo = reinterpret_cast<const f32x4*>(ext + kAFOB)[G];
+  const f32x4 gam = reinterpret_cast<const f32x4*>(ext + kAFGam)[G];
+  const f32x4 bet = reinterpret_cast<const f32x4*>(ext + kAFBet)[G];
+  const f32x4* wp = reinterpret_cast<const f32x4*>(ext + kAFPostW) + lane;
+  f32x4 post[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) post[u] = reinterpret_cast<const f32x4*>(ext + kAFPostB)[4 * u + G];
+#pragma unroll
+  for (int i = 0; i < kAttTokens; ++i) {
+    asm volatile("" ::: "memory");  // one query token's weights in flight at a time
+    f32x4 pw[4];  // token i's post_fc weights, issued ahead of the attention math
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pw[u] = wp[(u * 8 + i) * 64];
+    const f32x4 tk = token(i);
+    f32x4 q = bq;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) q = mfma16(wq[s], tk[s], q);
+    float sc[kAttTokens];
+#pragma unroll
+    for (int j = 0; j < kAttTokens; ++j) {
+      float t = q[0] * K[j][0];
+      t = fmaf(q[1], K[j][1], t);
+      t = fmaf(q[2], K[j][2], t);
+      t = fmaf(q[3], K[j][3], t);
+      sc[j] = t;
+    }
+    float m = sc[0];
+#pragma unroll
+    for (int j = 1; j < kAttTokens; ++j) m = (m != m || m >= sc[j]) ? m : sc[j];
+    float e[kAttTokens], sum = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kAttTokens; ++j) {
+      e[j] = exp_att(sc[j] - m);
+      sum = j == 0 ? e[0] : sum + e[j];
+    }
+    const float r = 1.0f / sum;
+    float o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      float acc = (e[0] * r) * V[0][d];
+#pragma unroll
+      for (int j = 1; j < kAttTokens; ++j) acc = fmaf(e[j] * r, V[j][d], acc);
+      o[d] = acc;
+    }
+    f32x4 y = bo;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) y = mfma16(wo[s], o[s], y);
+    float u[4];
+    if constexpr (kLn) {
+      float z[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) z[d] = y[d] + tk[d];
+      const float mean = group_sum4(((z[0] + z[1]) + z[2]) + z[3]) * 0.0625f;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) z[d] = z[d] - mean;
+      float s2 = z[0] * z[0];
+#pragma unroll
+      for (int d = 1; d < 4; ++d) s2 = fmaf(z[d], z[d], s2);
+      const float rstd = 1.0f / sqrtf(group_sum4(s2) * 0.0625f + 1e-5f);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) u[d] = fmaf(z[d] * rstd, gam[d], bet[d]);
+    } else {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) u[d] = y[d];
+    }
+#pragma unroll
+    for (int uu = 0; uu < 4; ++uu) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) post[uu] = mfma16(pw[uu][s], u[s], post[uu]);
+    }
+  }
+#pragma unroll
+  for (int uu = 0; uu < 4; ++uu) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) post[uu][r] = relu_f(post[uu][r]);
+    feat[uu] = post[uu];
+  }
+}
+
+// one [128, 128] Tanh net + NH head rows on the 64 features (a kAFN* net slot)
+template <int NH>
+__device__ __forceinline__ void attn16_net(const uint8_t* net, const f32x4* feat, int lane,
+                                           float* head, const float* ttab) {
+  asm volatile("" ::: "memory");
+  const int G = lane >> 4;
+  const f32x4* w1 = reinterpret_cast<const f32x4*>(net + kAFN1) + lane;
+  const f32x4* b1 = reinterpret_cast<const f32x4*>(net + kAFNB1) + G;
+  f32x4 a1[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    asm volatile("" ::: "memory");
+    f32x4 w[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) w[f] = w1[(t * 4 + f) * 64];
+    f32x4 c = b1[4 * t];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) c = mfma16(w[f][s], feat[f][s], c);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] = tanh_tab(c[r], ttab);
+    a1[t] = c;
+  }
+  const f32x4* w2 = reinterpret_cast<const f32x4*>(net + kAFN2) + lane;
+  const f32x4* b2 = reinterpret_cast<const f32x4*>(net + kAFNB2) + G;
+  const f32x4* wh = reinterpret_cast<const f32x4*>(net + kAFNH) + G;
+  const float* bh = reinterpret_cast<const float*>(net + kAFNHB);
+  float acc[NH];
+#pragma unroll
+  for (int j = 0; j < NH; ++j) acc[j] = 0.0f;  // first step fmaf(w, v, +0)
+#pragma unroll 1
+  for (int t = 0; t < 8; ++t) {
+    asm volatile("" ::: "memory");
+    f32x4 w[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) w[q] = w2[(t * 8 + q) * 64];
+    f32x4 c = b2[4 * t];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) c = mfma16(w[q][s], a1[q][s], c);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = tanh_tab(c[r], ttab);
+#pragma unroll
+      for (int j = 0; j < NH; ++j) acc[j] = fmaf(wh[j * 32 + 4 * t][r], v, acc[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NH; ++j) head[j] = group_sum4(acc[j]) + bh[j];
+}
+
+typedef __attribute__((address_space(3))) void* las_p;
+// 1 KiB per wave instruction from global (L2-resident weights: default cache policy)
+// into LDS at M0 + 16 lane; issued from inline asm, so hipcc neither sees nor waits for
+// it -- the caller waits with vmcnt(0) and a barrier before reading the slot.
+__device__ __forceinline__ void dma16_keep(const void* g, uint32_t m0) {
+  uint32_t saved;  // M0 is a reserved register hipcc may hold a value in: save/restore
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(saved)
+               : "v"(g), "s"(m0)
+               : "memory");
+}
+
+template <class Sys, bool kLn, int S, int W>
+__global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PArgs p) {
+  constexpr int E = 16;
+  constexpr int O = Sys::O, A = Sys::A;
+  constexpr int SO = S * O, KS = (SO + 3) / 4;
+  static_assert(kLn || S == 1, "frame stacking is the LayerNorm variant's");
+  static_assert(SO <= kAFMaxIn && O <= kPolMaxObs && A <= kPolMaxAct, "policy tile shape");
+  constexpr int SZ = SO - O;  // the stack's older frames
+  __shared__ __attribute__((aligned(16))) uint8_t s_lds[kAFLdsBytes];
+  __shared__ double s_norm[2 * kPolMaxObs];
+  const int tid = (int)threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, G = lane >> 4, col = lane & 15;
+  {
+    const f4v* src = reinterpret_cast<const f4v*>(p.blob);
+    f4v* dst = reinterpret_cast<f4v*>(s_lds);
+    for (int v = tid; v < kAFExt / 16; v += W * 64) dst[v] = src[v];
+    const f4v* sc = reinterpret_cast<const f4v*>(p.blob + kAFLogStd);
+    f4v* dc = reinterpret_cast<f4v*>(s_lds + kAFExt);
+    for (int v = tid; v < kAFConst / 16; v += W * 64) dc[v] = sc[v];
+  }
+  if (tid < O) {
+    s_norm[tid] = p.norm ? p.norm[tid] : 0.0;
+    s_norm[kPolMaxObs + tid] = p.norm ? sqrt(p.norm[O + tid] + p.eps) : 1.0;
+  }
+  const uint64_t tick = *a.tick_in;
+  if (blockIdx.x == 0 && tid == 0) {
+    *a.counter_next = 0;
+    *a.tick_out = tick + a.tick_adv;
+  }
+  __syncthreads();
+  const uint8_t* s_ext = s_lds;
+  const float* cst = reinterpret_cast<const float*>(s_lds + kAFExt);
+  const float* g_scale = cst + 4;
+  const float* g_var2 = cst + 8;
+  const float* g_lscale = cst + 12;
+  const float* ttab = cst + 16;
+  const uint8_t* s_net = s_lds + kAFExt + kAFConst;
+  const uint32_t m0_net = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(las_p)(const_cast<uint8_t*>(s_net)));
+  const uint8_t* g_pi = p.blob + kAFPi;
+  const uint8_t* g_vf = p.blob + kAFVf;
+  auto net_dma = [&](const uint8_t* g) {  // this wave's share of the 100 1-KiB pieces
+    const int wv = __builtin_amdgcn_readfirstlane(wave);  // M0 takes a wave-uniform SGPR
+    for (int c = wv; c < kAFNet / 1024; c += W)
+      dma16_keep(g + c * 1024 + lane * 16, (uint32_t)__builtin_amdgcn_readfirstlane(m0_net + 1024u * c));
+  };
+  const bool norm = p.norm != nullptr;
+  const double* mu = s_norm;
+  const double* sd = s_norm + kPolMaxObs;
+  const bool det = (p.pflags & LZ_POLICY_DETERMINISTIC) != 0;
+  const bool boot = (p.pflags & LZ_POLICY_BOOTSTRAP) != 0;
+  const float gamma = p.gamma;
+  double mom_r[O];  // pooled obs moments (code/train.py's variant): group 0 sums, 1 squares
+#pragma unroll
+  for (int j = 0; j < O; ++j) mom_r[j] = 0.0;
+  Sys sys;
+  sys.setup(a);
+  float* obs_buf = static_cast<float*>(a.obs);
+  float* rew_buf = static_cast<float*>(a.rew);
+  const int64_t ntiles = (a.n + E - 1) / E;
+  const int64_t per_round = (int64_t)gridDim.x * W;
+  const int64_t rounds = (ntiles + per_round - 1) / per_round;
+  // this lane group's fc1 inputs: input 4s + G of the stacked / normalised input
+  auto inputs = [&](const float* src, float* xs) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      float v = 0.0f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        if (4 * s + g < SO) v = G == g ? src[4 * s + g < SO ? 4 * s + g : 0] : v;
+      xs[s] = v;
+    }
+  };
+  // kLn: the stack the policy sees (st with the deferred zeroing applied) / the stacked
+  // terminal observation of a pending bootstrap
+  auto cur_stack = [&](const float* stv, bool z, float* out) {
+#pragma unroll
+    for (int j = 0; j < SO; ++j) out[j] = (j < SZ && z) ? 0.0f : stv[j];
+  };
+  auto term_stack = [&](const float* stv, const float* tf, float* out) {
+#pragma unroll
+    for (int j = 0; j < SO; ++j) out[j] = j < SZ ? stv[j < SZ ? j : 0] : tf[j < SZ ? 0 : j - SZ];
+  };
+  for (int64_t rd = 0; rd < rounds; ++rd) {
+    const int64_t tile = (rd * gridDim.x + blockIdx.x) * W + wave;
+    const bool active = tile < ntiles;  // wave-uniform; inactive waves still swap the slot
+    const int64_t i = tile * E + col;
+    const bool valid = active && i < a.n;  // all four lanes of the env compute it
+    const bool own = valid && G == 0;      // ... lane group 0 stores it
+    int32_t steps = 0;
+    bool any_reset = false;
+    // pt: the raw terminal obs of a pending bootstrap.  kLn: st is the rolled stack with
+    // the zeroing of a done env's older frames deferred (zf) until the bootstrap of the
+    // step has read [st[0 .. SZ), pt] (SB3's stacked terminal observation)
+    float o[O], st[kLn ? SO : 1], pt[O];
+    bool zf = false;
+#pragma unroll
+    for (int j = 0; j < O; ++j) o[j] = pt[j] = 0.0f;
+    if (valid) {
+      sys.load(a, i);
+      if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
+#pragma unroll
+      for (int j = 0; j < O; ++j) o[j] = p.obs_in[i * O + j];
+    }
+    if constexpr (kLn) {
+#pragma unroll
+      for (int j = 0; j < SO; ++j) st[j] = valid ? p.stack_in[i * SO + j] : 0.0f;
+    }
+    bool pend = false;  // this env's step truncated: its bootstrap value comes next step
+    float prew = 0.0f;  // ... and its reward before the bootstrap
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    for (int k = 0; k < a.K; ++k) {
+      const int64_t off = (int64_t)k * a.n + i;
+      // [1] pi into the slot, meanwhile the features of this step's input
+      __syncthreads();
+      net_dma(g_pi);
+      const bool pb = pend;
+      const bool any_pb = __ballot(pb) != 0ull;
+      f32x4 F[4], Ft[4];
+      if (active) {
+        float xs[KS];
+        if constexpr (kLn) {
+          float cs[SO];
+          cur_stack(st, zf, cs);
+          if (own) {
+#pragma unroll
+            for (int j = 0; j < SO; ++j) obs_buf[off * SO + j] = cs[j];
+          }
+          inputs(cs, xs);
+        } else {
+          float x[O];
+          normalize<O>(o, x, norm, mu, sd, p.clip);
+          if (own) {
+#pragma unroll
+            for (int j = 0; j < O; ++j) obs_buf[off * O + j] = x[j];
+          }
+          inputs(x, xs);
+        }
+        attn16_extract<KS, kLn>(s_ext, xs, lane, F);
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA pieces have landed
+      __syncthreads();
+      // [2] the policy head: sample (every lane of the env, same Philox draw), log-prob, clip
+      float act_c[A];
+#pragma unroll
+      for (int j = 0; j < A; ++j) act_c[j] = 0.0f;
+      if (active) {
+        float mean[A];
+        attn16_net<A>(s_net, F, lane, mean, ttab);
+        if (valid) {
+          float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+          if (!det) {
+            if constexpr (A <= 2) normal2(a.seed, (uint64_t)(a.gid0 + i), tick + (uint64_t)k, z);
+            else normal4(a.seed, (uint64_t)(a.gid0 + i), tick + (uint64_t)k, z);
+          }
+          float lp = 0.0f;
+#pragma unroll
+          for (int j = 0; j < A; ++j) {
+            const float aj = det ? mean[j] : mean[j] + z[j] * g_scale[j];
+            const float dd = aj - mean[j];
+            const float lpj = (-(dd * dd)) / g_var2[j] - g_lscale[j] - 0.91893853320467274f;
+            lp = j == 0 ? lpj : lp + lpj;
+            act_c[j] = clip(aj, p.act_lo, p.act_hi);
+            if (own) p.act[off * A + j] = aj;
+          }
+          if (own) p.logp[off] = lp;
+        }
+      }
+      // [3] vf into the slot while the previous step's pending terminal input is
+      //     extracted and the env steps (which overwrites pt)
+      __syncthreads();
+      net_dma(g_vf);
+      float rew = 0.0f;
+      bool pn = false;
+      if (active) {
+        if (any_pb) {
+          float xt[KS];
+          if constexpr (kLn) {
+            float ts[SO];
+            term_stack(st, pt, ts);
+            inputs(ts, xt);
+          } else {
+            float x[O];
+            normalize<O>(pt, x, norm, mu, sd, p.clip);
+            inputs(x, xt);
+          }
+          attn16_extract<KS, kLn>(s_ext, xt, lane, Ft);
+        }
+        if constexpr (kLn) {  // the deferred zeroing, now that the bootstrap has its input
+#pragma unroll
+          for (int j = 0; j < SZ; ++j) st[j] = zf ? 0.0f : st[j];
+        }
+        float on[O], ot[O];
+        bool did_reset;
+        const uint8_t df = step_body<Sys, float, true, true>(sys, steps, a, i, valid, act_c,
+                                                             tick + (uint64_t)k, k, on, rew,
+                                                             did_reset, ot, G == 0);
+        any_reset = any_reset || did_reset;
+        pn = boot && valid && (df & LZ_DONE_TRUNCATED) && !(df & LZ_DONE_TERMINATED);
+        if (pn) {
+#pragma unroll
+          for (int j = 0; j < O; ++j) pt[j] = ot[j];
+        }
+        if constexpr (kLn) {
+          // VecFrameStack (SB3 StackedObservations.update): roll by O, the new frame last;
+          // a done env's older frames become zeros (deferred: zf) -- its stacked terminal
+          // observation is [rolled older frames, terminal frame]
+#pragma unroll
+          for (int j = 0; j < SZ; ++j) st[j] = st[j + O];
+#pragma unroll
+          for (int j = 0; j < O; ++j) st[SZ + j] = on[j];
+          zf = df != 0;
+        } else {
+          if (p.partials && valid && G < 2) {
+#pragma unroll
+            for (int j = 0; j < O; ++j) {
+              const double v = (double)on[j];
+              mom_r[j] += G ? v * v : v;
+            }
+          }
+        }
+        if (own) {
+          rew_buf[off] = rew;
+          a.done[off] = df;
+        }
+#pragma unroll
+        for (int j = 0; j < O; ++j) o[j] = on[j];
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      __syncthreads();
+      // [4] V(this step's input); the previous step's truncation bootstrap
+      if (active) {
+        float v[1];
+        attn16_net<1>(s_net, F, lane, v, ttab);
+        if (own) p.val[off] = v[0];
+        if (any_pb) {
+          float vt[1];
+          attn16_net<1>(s_net, Ft, lane, vt, ttab);
+          if (own && pb) rew_buf[off - a.n] = prew + gamma * vt[0];
+        }
+      }
+      pend = pn;
+      prew = rew;
+    }
+    // the slot holds vf: the last step's bootstrap and the last values
+    if (active) {
+      const bool pb = pend;
+      const bool any_pb = __ballot(pb) != 0ull;
+      f32x4 F[4];
+      float xs[KS];
+      float cs[kLn ? SO : 1];
+      if constexpr (kLn) {
+        cur_stack(st, zf, cs);
+        inputs(cs, xs);
+      } else {
+        float x[O];
+        normalize<O>(o, x, norm, mu, sd, p.clip);
+        inputs(x, xs);
+      }
+      attn16_extract<KS, kLn>(s_ext, xs, lane, F);
+      float vl[1];
+      attn16_net<1>(s_net, F, lane, vl, ttab);
+      if (any_pb) {
+        float xt[KS];
+        if constexpr (kLn) {
+          float ts[SO];
+          term_stack(st, pt, ts);
+          inputs(ts, xt);
+        } else {
+          float x[O];
+          normalize<O>(pt, x, norm, mu, sd, p.clip);
+          inputs(x, xt);
+        }
+        attn16_extract<KS, kLn>(s_ext, xt, lane, F);
+        float vt[1];
+        attn16_net<1>(s_net, F, lane, vt, ttab);
+        if (own && pb) rew_buf[(int64_t)(a.K - 1) * a.n + i] = prew + gamma * vt[0];
+      }
+      if (own) {
+        p.last_val[i] = vl[0];
+#pragma unroll
+        for (int j = 0; j < O; ++j) p.obs_last[i * O + j] = o[j];
+        sys.store(a, i);
+        if (any_reset) sys.store_autoreset_extra(a, i);
+        if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
+        if constexpr (kLn) {
+#pragma unroll
+          for (int j = 0; j < SO; ++j) p.stack_out[i * SO + j] = cs[j];
+        }
+      }
+    }
+  }
+  if (!kLn && p.partials) {  // fixed-order butterfly over the wave: deterministic
+    double* dst = p.partials + ((int64_t)blockIdx.x * W + wave) * (2 * O);
+#pragma unroll
+    for (int j = 0; j < 2 * O; ++j) {
+      double v = (j < O ? G == 0 : G == 1) ? mom_r[j < O ? j : j - O] : 0.0;
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+      if (lane == 0) dst[j] = v;
+    }
+  }
+}
+
 // obs moments: out = (count, column sums, column sums of squares) from the per-wave
 // partials, summed in a fixed order.  One workgroup per column (the column loop ran in
 // a single workgroup before: 22.9 us per collect at 262,144 envs, 2.8% of K=16); the
@@ -1492,6 +2067,21 @@ int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, const PolS
   return (int)hipErrorInvalidValue;
 }
 
+// waves of 16 envs, one workgroup per CU (the LDS holds one): 8 (two per SIMD) for
+// code/train.py's extractor, 4 (one per SIMD, 512 registers) for the LayerNorm variant,
+// whose stacked input and LayerNorm spill at 256 registers; LZ_ATTN_F32_WAVES=4|8 forces
+PolShape attn_f32_policy_shape(int64_t n, int num_cus, int ln) {
+  static const int forced = [] {
+    const char* e = std::getenv("LZ_ATTN_F32_WAVES");
+    const int w = e ? std::atoi(e) : 0;
+    return w == 4 || w == 8 ? w : 0;
+  }();
+  PolShape s = {16, forced ? forced : (ln ? 4 : 8), 0, 0};
+  const int64_t groups = ((n + 15) / 16 + s.waves - 1) / s.waves;
+  s.grid = (int)(groups < num_cus ? groups : num_cus);
+  return s;
+}
+
 PolShape attn_policy_shape(int64_t n, int num_cus) {
   PolShape s = {32, 4, 3, 0};
   const int64_t groups = ((n + 31) / 32 + 3) / 4;
@@ -1530,6 +2120,32 @@ static int launch_pol_attn_ln(int n_stack, const KArgs& a, const PArgs& p, const
   else if (n_stack == 1) hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, kAttnLn, 1>), grid, block, 0, s, a, p);
   else return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
+}
+
+template <class Sys>
+static int launch_pol_attn_f32(int ln, int n_stack, const KArgs& a, const PArgs& p, const PolShape& sh,
+                               hipStream_t s) {
+  const dim3 grid((unsigned)sh.grid), block(sh.waves * 64);
+#define LZ_ATTN_F32(LN, S_)                                                                        \
+  if (sh.waves == 8) hipLaunchKernelGGL((k_rollout_policy_attn_f32<Sys, LN, S_, 8>), grid, block, 0, s, a, p); \
+  else hipLaunchKernelGGL((k_rollout_policy_attn_f32<Sys, LN, S_, 4>), grid, block, 0, s, a, p);
+  if (!ln) { LZ_ATTN_F32(false, 1) }
+  else if (n_stack == 4) { LZ_ATTN_F32(true, 4) }
+  else if (n_stack == 1) { LZ_ATTN_F32(true, 1) }
+  else return (int)hipErrorInvalidValue;
+#undef LZ_ATTN_F32
+  return (int)hipGetLastError();
+}
+
+int launch_rollout_policy_attn_f32(int system, int ln, int n_stack, const KArgs& a, const PArgs& p,
+                                   const PolShape& grid, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (system) {  // code/train.py's learner is HR; lorenz_filter's is HR on VecFrameStack(4)
+    case LZ_SYS_LORENZ3: return launch_pol_attn_f32<SysL3<float>>(ln, n_stack, a, p, grid, s);
+    case LZ_SYS_PMSM: return launch_pol_attn_f32<SysPMSM>(ln, n_stack, a, p, grid, s);
+    case LZ_SYS_HR: return launch_pol_attn_f32<SysHR<float>>(ln, n_stack, a, p, grid, s);
+  }
+  return (int)hipErrorInvalidValue;
 }
 
 int launch_rollout_policy_attn_ln(int system, int n_stack, const KArgs& a, const PArgs& p,
@@ -1869,6 +2485,82 @@ void pack_attn(uint8_t* b, const lz_attn_policy* p, const float* ln_w, const flo
   }
 }
 
+// The attention actor-critics in float32 (kAF* layout, lz_internal.h; 16x16x4 tiles:
+// lane (r = lane & 15, G = lane >> 4) holds A[row r][k = G] of every k-step): ln_w ==
+// nullptr for code/train.py's extractor, else code/lorenz_filter/train.py's residual +
+// LayerNorm variant (fc1 over <= 32 stacked inputs).  Nothing is folded or rescaled
+// except Q's exact 1/sqrt(4) = 0.5.
+void pack_attn_f32(uint8_t* b, const lz_attn_policy* p, const float* ln_w, const float* ln_b) {
+  using lz::kPolHidden;
+  const int I = p->obs_dim;
+  float* f1 = reinterpret_cast<float*>(b + lz::kAFFc1W);
+  float* fk = reinterpret_cast<float*>(b + lz::kAFKW);
+  float* fv = reinterpret_cast<float*>(b + lz::kAFVW);
+  float* fq = reinterpret_cast<float*>(b + lz::kAFQW);
+  float* fo = reinterpret_cast<float*>(b + lz::kAFOW);
+  float* fp = reinterpret_cast<float*>(b + lz::kAFPostW);
+  for (int lane = 0; lane < 64; ++lane) {
+    const int r = lane & 15, G = lane >> 4;
+    for (int t = 0; t < lz::kAttTokens; ++t)  // fc1 tile t = token t; k-step s: input 4s + G
+      for (int s = 0; s < 8; ++s) {
+        const int k = 4 * s + G;
+        f1[((t * 2 + s / 4) * 64 + lane) * 4 + s % 4] = k < I ? p->fc1_w[(16 * t + r) * I + k] : 0.0f;
+      }
+    for (int s = 0; s < 4; ++s) {  // k-step s: token / attention-output dim 4G + s
+      const int d = 4 * G + s;
+      fk[lane * 4 + s] = p->in_proj_w[(16 + r) * 16 + d];
+      fv[lane * 4 + s] = p->in_proj_w[(32 + r) * 16 + d];
+      fq[lane * 4 + s] = 0.5f * p->in_proj_w[r * 16 + d];
+      fo[lane * 4 + s] = p->out_proj_w[r * 16 + d];
+    }
+    for (int u = 0; u < 4; ++u)
+      for (int i = 0; i < lz::kAttTokens; ++i)
+        for (int s = 0; s < 4; ++s)
+          fp[((u * 8 + i) * 64 + lane) * 4 + s] = p->post_w[(16 * u + r) * kPolHidden + 16 * i + 4 * G + s];
+  }
+  float* c1 = reinterpret_cast<float*>(b + lz::kAFFc1B);
+  for (int u = 0; u < kPolHidden; ++u) c1[u] = p->fc1_b[u];
+  for (int d = 0; d < 16; ++d) {
+    reinterpret_cast<float*>(b + lz::kAFKB)[d] = p->in_proj_b[16 + d];
+    reinterpret_cast<float*>(b + lz::kAFVB)[d] = p->in_proj_b[32 + d];
+    reinterpret_cast<float*>(b + lz::kAFQB)[d] = 0.5f * p->in_proj_b[d];
+    reinterpret_cast<float*>(b + lz::kAFOB)[d] = p->out_proj_b[d];
+    reinterpret_cast<float*>(b + lz::kAFGam)[d] = ln_w ? ln_w[d] : 1.0f;
+    reinterpret_cast<float*>(b + lz::kAFBet)[d] = ln_b ? ln_b[d] : 0.0f;
+  }
+  for (int f = 0; f < lz::kAttFeat; ++f) reinterpret_cast<float*>(b + lz::kAFPostB)[f] = p->post_b[f];
+  const float* W1[2] = {p->pi_w1, p->vf_w1};
+  const float* B1[2] = {p->pi_b1, p->vf_b1};
+  const float* W2[2] = {p->pi_w2, p->vf_w2};
+  const float* B2[2] = {p->pi_b2, p->vf_b2};
+  const float* W3[2] = {p->act_w, p->val_w};
+  const float* B3[2] = {p->act_b, p->val_b};
+  const int rows3[2] = {p->act_dim, 1};
+  for (int n = 0; n < 2; ++n) {
+    uint8_t* net = b + (n == 0 ? lz::kAFPi : lz::kAFVf);
+    float* g1 = reinterpret_cast<float*>(net + lz::kAFN1);
+    float* g2 = reinterpret_cast<float*>(net + lz::kAFN2);
+    for (int lane = 0; lane < 64; ++lane) {
+      const int r = lane & 15, G = lane >> 4;
+      for (int t = 0; t < 8; ++t) {
+        for (int f = 0; f < 4; ++f)  // layer 1: k-step 4f + s = feature 16f + 4G + s
+          for (int s = 0; s < 4; ++s)
+            g1[((t * 4 + f) * 64 + lane) * 4 + s] = W1[n][(16 * t + r) * lz::kAttFeat + 16 * f + 4 * G + s];
+        for (int q = 0; q < 8; ++q)  // layer 2: k-step 4q + s = unit 16q + 4G + s
+          for (int s = 0; s < 4; ++s)
+            g2[((t * 8 + q) * 64 + lane) * 4 + s] = W2[n][(16 * t + r) * kPolHidden + 16 * q + 4 * G + s];
+      }
+    }
+    for (int u = 0; u < kPolHidden; ++u) {
+      reinterpret_cast<float*>(net + lz::kAFNB1)[u] = B1[n][u];
+      reinterpret_cast<float*>(net + lz::kAFNB2)[u] = B2[n][u];
+      for (int j = 0; j < rows3[n]; ++j)
+        reinterpret_cast<float*>(net + lz::kAFNH)[j * kPolHidden + u] = W3[n][j * kPolHidden + u];
+    }
+    for (int j = 0; j < rows3[n]; ++j) reinterpret_cast<float*>(net + lz::kAFNHB)[j] = B3[n][j];
+  }
+}
+
 void pack_gauss(float* ls, int act_dim, const float* log_std) {
   // [log_std(4)][scale(4)][2 scale^2 (4)][log scale (4)]: torch Normal's
   // scale = exp(log_std), var = scale**2 (the kernel divides by 2 * var), log(scale)
@@ -2072,6 +2764,42 @@ lz_status lz_episode_starts(int64_t n, int32_t K, const uint8_t* done, const flo
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pfail(LZ_ERR_HIP, hipGetErrorString(e));
   return LZ_OK;
+}
+
+int64_t lz_attn_policy_f32_blob_bytes(void) { return lz::kAFBlobBytes; }
+
+static lz_status pack_attn_f32_checked(const lz_attn_policy* p, const float* ln_w, const float* ln_b,
+                                       void* host_blob, int64_t cap, int max_in) {
+  if (!p || !host_blob) return pfail(LZ_ERR_INVALID, "policy/blob is NULL");
+  if (cap < lz::kAFBlobBytes) return pfail(LZ_ERR_INVALID, "blob capacity too small");
+  if (p->obs_dim < 1 || p->obs_dim > max_in || p->act_dim < 1 || p->act_dim > lz::kPolMaxAct)
+    return pfail(LZ_ERR_UNSUPPORTED, max_in == lz::kPolMaxObs
+                                         ? "policy supports obs_dim 1..8 and act_dim 1..4"
+                                         : "policy supports input dims 1..32 and act_dim 1..4");
+  const float* req[] = {p->fc1_w, p->fc1_b, p->in_proj_w, p->in_proj_b, p->out_proj_w,
+                        p->out_proj_b, p->post_w, p->post_b, p->pi_w1, p->pi_b1, p->pi_w2,
+                        p->pi_b2, p->vf_w1, p->vf_b1, p->vf_w2, p->vf_b2, p->act_w, p->act_b,
+                        p->val_w, p->val_b, p->log_std};
+  for (const float* q : req)
+    if (!q) return pfail(LZ_ERR_INVALID, "a policy weight pointer is NULL");
+  uint8_t* b = static_cast<uint8_t*>(host_blob);
+  std::memset(b, 0, lz::kAFBlobBytes);
+  pack_attn_f32(b, p, ln_w, ln_b);
+  pack_gauss(reinterpret_cast<float*>(b + lz::kAFLogStd), p->act_dim, p->log_std);
+  float* tt = reinterpret_cast<float*>(b + lz::kAFTanh);
+  for (int k = 0; k < 72; ++k)
+    for (int j = 0; j < 8; ++j) tt[8 * k + j] = std::ldexp(kTanhTab[8 * k + j], -3 * j);
+  return LZ_OK;
+}
+
+lz_status lz_attn_policy_pack_f32(const lz_attn_policy* p, void* host_blob, int64_t cap) {
+  return pack_attn_f32_checked(p, nullptr, nullptr, host_blob, cap, lz::kPolMaxObs);
+}
+
+lz_status lz_attn_ln_policy_pack_f32(const lz_attn_ln_policy* p, void* host_blob, int64_t cap) {
+  if (!p) return pfail(LZ_ERR_INVALID, "policy is NULL");
+  if (!p->ln_w || !p->ln_b) return pfail(LZ_ERR_INVALID, "layer_norm weight / bias is NULL");
+  return pack_attn_f32_checked(&p->attn, p->ln_w, p->ln_b, host_blob, cap, lz::kAFMaxIn);
 }
 
 }  // extern "C"

@@ -158,6 +158,7 @@ _SIGS = {
     "lz_step_host": (ctypes.c_int, [VP, VP, VP, VP, VP, VP]),
     "lz_resident_step": (ctypes.c_int, [VP, VP, VP, VP, VP, VP]),
     "lz_resident_stop": (ctypes.c_int, [VP]),
+    "lz_resident_read_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
     "lz_get_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
     "lz_set_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
     "lz_plane_elem_size": (ctypes.c_int32, [VP, ctypes.c_int32]),
@@ -196,6 +197,12 @@ _SIGS = {
     "lz_attn_ln_policy_pack": (ctypes.c_int, [ctypes.POINTER(LzAttnLnPolicy), VP, ctypes.c_int64]),
     "lz_rollout_policy_attn_stack": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs),
                                                     ctypes.c_int32, VP, VP]),
+    "lz_attn_policy_f32_blob_bytes": (ctypes.c_int64, []),
+    "lz_attn_policy_pack_f32": (ctypes.c_int, [ctypes.POINTER(LzAttnPolicy), VP, ctypes.c_int64]),
+    "lz_attn_ln_policy_pack_f32": (ctypes.c_int, [ctypes.POINTER(LzAttnLnPolicy), VP, ctypes.c_int64]),
+    "lz_rollout_policy_attn_f32": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
+    "lz_rollout_policy_attn_stack_f32": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs),
+                                                        ctypes.c_int32, VP, VP]),
     "lz_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP, ctypes.c_double,
                               ctypes.c_double, VP, VP, ctypes.c_int32, VP]),
     "lz_episode_starts": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, VP, VP, VP, VP,

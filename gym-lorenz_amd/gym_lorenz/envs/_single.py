@@ -71,7 +71,14 @@ class SingleEnvCore:
         return self._obs_h[0].copy(), self._rew_h[0], int(self._done_h[0])
 
     def plane(self, p):
-        return self.be.get_state(p).cpu().numpy()[0]
+        # lz_resident_read_state: while the resident server serves this env, its copy of
+        # the state after the last step (the server keeps running -- test_evaluate.py:
+        # 123-125 reads state1 / state2 after every step); otherwise a device copy
+        dt = self.be.plane_dtype(p)
+        out = np.empty((1,), {torch.float64: np.float64, torch.float32: np.float32,
+                              torch.int32: np.int32}[dt])
+        nat.check(nat.lib.lz_resident_read_state(self.be._h, int(p), out.ctypes.data))
+        return out[0]
 
     def planes(self, first, count):
         return np.array([self.plane(first + j) for j in range(count)])

@@ -12,8 +12,9 @@ and finally ``RolloutBuffer.compute_returns_and_advantage``.
 ``FusedRolloutCollector.collect(K)`` does all K steps in ONE kernel launch
 (``lz_rollout_policy_f32``): the two 6->128->128 MLPs at SB3's own precision
 (float32 operands and accumulation on f32-input MFMA, a deterministic operation order
-the C oracle reproduces bit for bit; ``precision="bf16"`` selects the faster bf16-MFMA
-kernel ``lz_rollout_policy``, the attention policies run bf16 only), the Gaussian
+the C oracle reproduces bit for bit -- likewise code/train.py's and code/lorenz_filter/
+train.py's attention actor-critics, ``lz_rollout_policy_attn_f32`` / ``_attn_stack_f32``;
+``precision="bf16"`` selects the faster bf16-MFMA kernels), the Gaussian
 sample (Philox), the action-space clip, the env step with
 auto-reset, SB3's truncation bootstrap, and VecNormalize's observation normalisation.
 With a training VecNormalize the float32 kernel follows SB3's order exactly: each
@@ -387,6 +388,53 @@ def pack_policy(state_dict, obs_dim, act_dim):
     return blob
 
 
+def _attn_struct(state_dict, in_dim, act_dim, features_dim, ln):
+    if features_dim != 64:
+        raise ValueError("the fused kernel implements features_dim=64 (code/train.py:100)")
+    keys = [_fe_key(state_dict, k) for k in ATTN_FE_KEYS] + list(KEYS)
+    if ln:
+        keys += [_fe_key(state_dict, "layer_norm.weight"), _fe_key(state_dict, "layer_norm.bias")]
+    for key in KEYS:
+        if key not in state_dict:
+            raise KeyError("policy state_dict lacks %r" % key)
+    arrs = [np.ascontiguousarray(_np(state_dict[k]), dtype=np.float32) for k in keys]
+    F = features_dim
+    shapes = [(HIDDEN, in_dim), (HIDDEN,), (48, 16), (48,), (16, 16), (16,), (F, HIDDEN), (F,)] + [
+        (HIDDEN, F), (HIDDEN,), (HIDDEN, HIDDEN), (HIDDEN,)] * 2 + [
+        (act_dim, HIDDEN), (act_dim,), (1, HIDDEN), (1,), (act_dim,)] + ([(16,), (16,)] if ln else [])
+    for key, a, shp in zip(keys, arrs, shapes):
+        if a.shape != shp:
+            raise ValueError("%s has shape %s, expected %s" % (key, a.shape, shp))
+    p = nat.LzAttnPolicy()
+    p.obs_dim, p.act_dim = int(in_dim), int(act_dim)
+    for f, a in zip(_ATTN_FE_FIELDS + _FIELDS, arrs):
+        setattr(p, f, a.ctypes.data)
+    if not ln:
+        return p, arrs
+    q = nat.LzAttnLnPolicy()
+    q.attn = p
+    q.ln_w, q.ln_b = arrs[-2].ctypes.data, arrs[-1].ctypes.data
+    return q, arrs
+
+
+def pack_attn_policy_f32(state_dict, obs_dim, act_dim, features_dim=64):
+    """lz_attn_policy_pack_f32: code/train.py's attention actor-critic at SB3's float32
+    precision (lz_rollout_policy_attn_f32) -> uint8 numpy blob (host; needs no GPU)."""
+    p, _keep = _attn_struct(state_dict, obs_dim, act_dim, features_dim, False)
+    blob = np.zeros(int(nat.lib.lz_attn_policy_f32_blob_bytes()), np.uint8)
+    nat.check(nat.lib.lz_attn_policy_pack_f32(ctypes.byref(p), blob.ctypes.data, blob.size))
+    return blob
+
+
+def pack_attn_ln_policy_f32(state_dict, in_dim, act_dim, features_dim=64):
+    """lz_attn_ln_policy_pack_f32: code/lorenz_filter/train.py's residual + LayerNorm
+    policy at float32 precision (in_dim = the stacked observation width)."""
+    p, _keep = _attn_struct(state_dict, in_dim, act_dim, features_dim, True)
+    blob = np.zeros(int(nat.lib.lz_attn_policy_f32_blob_bytes()), np.uint8)
+    nat.check(nat.lib.lz_attn_ln_policy_pack_f32(ctypes.byref(p), blob.ctypes.data, blob.size))
+    return blob
+
+
 def pack_attn_policy(state_dict, obs_dim, act_dim, features_dim=64):
     """lz_attn_policy_pack: SB3 state_dict of code/train.py's attention actor-critic ->
     uint8 numpy blob (host; needs no GPU)."""
@@ -481,11 +529,11 @@ class FusedRolloutCollector:
                    only mode of the bf16 / attention kernels): the K steps run in one
                    launch with the rollout-start statistics and one update from the K
                    steps' pooled moments afterwards -- faster, not SB3's trajectory.
-    precision:     MlpPolicy arithmetic: "fp32" (default; SB3's float32 forward,
-                   lz_rollout_policy_f32) or "bf16" (bf16 MFMA operands, fp32
-                   accumulation, lz_rollout_policy: ~2.5x faster, ~1e-2 off SB3).  The
-                   attention actor-critics (code/train.py, code/lorenz_filter/train.py)
-                   run bf16 whatever this says (None = default for the policy kind).
+    precision:     policy arithmetic: "fp32" (default; SB3's float32 forward --
+                   lz_rollout_policy_f32, and for the attention actor-critics of
+                   code/train.py / code/lorenz_filter/train.py lz_rollout_policy_attn_f32 /
+                   _attn_stack_f32) or "bf16" (bf16 MFMA operands, fp32 accumulation:
+                   lz_rollout_policy / _attn / _attn_stack, ~2.5-5x faster, ~1e-2 off SB3).
     """
 
     def __init__(self, backend, state_dict=None, gamma=0.99, gae_lambda=0.95, obs_rms=None,
@@ -535,26 +583,25 @@ class FusedRolloutCollector:
         if self.frame_stack > 1 and not self.attention_ln:
             raise ValueError("frame_stack > 1 runs code/lorenz_filter/train.py's policy "
                              "(the residual + LayerNorm attention extractor)")
+        self.f32 = self.precision != "bf16"
         if self.attention_ln:
             if self.obs_rms is not None:
                 raise ValueError("the LayerNorm attention rollout takes raw observations")
-            blob = pack_attn_ln_policy(state_dict, self.frame_stack * self.O, self.A)
+            blob = (pack_attn_ln_policy_f32 if self.f32 else pack_attn_ln_policy)(
+                state_dict, self.frame_stack * self.O, self.A)
         elif self.attention:
-            blob = pack_attn_policy(state_dict, self.O, self.A)
+            blob = (pack_attn_policy_f32 if self.f32 else pack_attn_policy)(state_dict, self.O, self.A)
         else:
-            self.f32 = self.precision != "bf16"
             blob = (pack_policy_f32 if self.f32 else pack_policy)(state_dict, self.O, self.A)
-        if (self.attention or self.attention_ln) and self.precision == "fp32":
-            raise ValueError("the attention actor-critics run bf16 only (precision='bf16')")
-        if self.vecnorm_update == "step" and not self.f32:
+        if self.vecnorm_update == "step" and (not self.f32 or self.attention or self.attention_ln):
             raise ValueError("vecnorm_update='step' runs the float32 MlpPolicy kernel")
         self.blob = torch.from_numpy(blob).to(self.device)
 
     @property
     def per_step_vecnorm(self):
         """True when the collect updates obs_rms in SB3's per-step order."""
-        return (self.obs_rms is not None and self.training and self.f32
-                and self.vecnorm_update != "rollout")
+        return (self.obs_rms is not None and self.training and self.f32 and not self.attention
+                and not self.attention_ln and self.vecnorm_update != "rollout")
 
     def _rms_update_obs(self, x):
         """VecNormalize.reset()'s obs_rms.update(obs) in the per-step kernel's moment order."""
@@ -630,9 +677,10 @@ class FusedRolloutCollector:
             es.wait_stream(caller)
         if self.attention_ln:
             stack_out = torch.empty((n, SO), dtype=f32, device=dev)
-            nat.check(nat.lib.lz_rollout_policy_attn_stack(self.env._h, ctypes.byref(r),
-                                                           self.frame_stack, _p(self.last_stack),
-                                                           _p(stack_out)))
+            launch = (nat.lib.lz_rollout_policy_attn_stack_f32 if self.f32
+                      else nat.lib.lz_rollout_policy_attn_stack)
+            nat.check(launch(self.env._h, ctypes.byref(r), self.frame_stack, _p(self.last_stack),
+                             _p(stack_out)))
         elif per_step:
             state = ctypes.c_void_p(self.obs_rms.state.data_ptr())
             if self.group is None:
@@ -653,7 +701,8 @@ class FusedRolloutCollector:
                         if es != caller:
                             es.wait_stream(caller)
         else:
-            launch = (nat.lib.lz_rollout_policy_attn if self.attention else
+            launch = ((nat.lib.lz_rollout_policy_attn_f32 if self.f32 else nat.lib.lz_rollout_policy_attn)
+                      if self.attention else
                       nat.lib.lz_rollout_policy_f32 if self.f32 else nat.lib.lz_rollout_policy)
             nat.check(launch(self.env._h, ctypes.byref(r)))
         if es != caller:

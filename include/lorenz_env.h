@@ -244,21 +244,30 @@ lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, 
                        void* rew_out, uint8_t* done_out);
 
 /* lz_step_host's contract (same arguments, same results bit for bit -- the same step
- * body, tick for tick) served by a RESIDENT kernel: the first call launches a one-wave
- * server on a stream of its own that keeps the state in registers and polls a mailbox
- * in mapped host memory; each call posts its request there and spins until the reply
- * lands in host memory -- no launch, no stream synchronisation per step (the
- * reference's per-env callers step one env per env.step(), code/train.py:98-100,
- * gym_run.py).  Handles of at most 64 envs without LZ_FLAG_AUTORESET
- * (LZ_ERR_UNSUPPORTED otherwise).  The server exits by itself after
- * LZ_RESIDENT_IDLE_US (default 1000) microseconds without a request and is
- * relaunched by the next call (a device-wide synchronize waits for that exit); every
- * other call on the handle stops it first (its state goes back to the planes), as
- * does lz_resident_stop.  Synchronous: LZ_ERR_STATE while the handle's stream is
- * being captured into a graph. */
+ * body, tick for tick) served by a RESIDENT kernel: one launch per process and device
+ * serves every handle that calls this (one wave per handle, up to 16 handles; a
+ * DummyVecEnv of several drop-in envs -- code/train.py:98-100 -- shares the one launch
+ * and its one stream), keeps each handle's state in registers and polls the handles'
+ * mailboxes in mapped host memory; each call posts its request there and spins until
+ * the reply lands in host memory -- no launch, no stream synchronisation per step.  A
+ * handle joining the server restarts it (its state goes back to the planes and every
+ * handle is relaunched); a 17th handle steps through lz_step_host instead.  Handles of
+ * at most 64 envs without LZ_FLAG_AUTORESET (LZ_ERR_UNSUPPORTED otherwise).  The server
+ * exits after LZ_RESIDENT_IDLE_US (default 1000) microseconds without a request to ANY
+ * of its handles and is relaunched by the next call (a device-wide synchronize waits
+ * for that exit); every other call on a served handle stops it first (all states go
+ * back to the planes), as does lz_resident_stop.  Synchronous: LZ_ERR_STATE while the
+ * handle's stream is being captured into a graph. */
 lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noise,
                            void* obs_out, void* rew_out, uint8_t* done_out);
 lz_status lz_resident_stop(lz_handle* h);
+/* Host copy of one state plane (N elements, lz_plane_elem_size bytes each) -- what the
+ * per-env drop-in classes' state1 / state2 / state_master ... attributes return
+ * (code/lorenz_pmsm/test_evaluate.py:123-125 reads them after every step).  While the
+ * resident server serves the handle this is its published copy after the last request
+ * (no device interaction, the server keeps running); otherwise the plane is copied from
+ * the device (synchronous). */
+lz_status lz_resident_read_state(lz_handle* h, int32_t plane, void* host_dst);
 
 /* K fused steps in ONE launch, state held in registers.  Time-major buffers:
  *   actions T [K, N, action_dim]; obs_out T [K, N, obs_dim]; rew_out T [K, N];
@@ -460,6 +469,27 @@ lz_status lz_attn_ln_policy_pack(const lz_attn_ln_policy* p, void* host_blob, in
  * stack_in / stack_out: [N, n_stack*O] float32 device (may alias). */
 lz_status lz_rollout_policy_attn_stack(lz_handle* h, const lz_policy_rollout_args* r,
                                        int32_t n_stack, const float* stack_in, float* stack_out);
+
+/* The two attention actor-critics at the precision the reference trains them in (torch
+ * float32; code/train.py:101-112, code/lorenz_filter/train.py:117-127): float32
+ * operands and accumulation everywhere (f32-input MFMA = k-ordered fmaf chains), the
+ * softmax exp / LayerNorm / tanh as fixed IEEE operation sequences -- deterministic and
+ * reproduced bit for bit by the C oracle (orc_attn_f32), which agrees with torch's
+ * nn.MultiheadAttention / nn.LayerNorm float32 modules to ~1e-6.  Nothing is folded
+ * (out_proj runs as its own layer).  hidden 128, features_dim 64.  Host-only packers;
+ * obs_dim 1..8 (lz_attn_policy_pack_f32) or stacked input dims 1..32
+ * (lz_attn_ln_policy_pack_f32, attn.obs_dim = n_stack * env obs_dim). */
+int64_t lz_attn_policy_f32_blob_bytes(void);
+lz_status lz_attn_policy_pack_f32(const lz_attn_policy* p, void* host_blob, int64_t cap);
+lz_status lz_attn_ln_policy_pack_f32(const lz_attn_ln_policy* p, void* host_blob, int64_t cap);
+/* lz_rollout_policy_attn / lz_rollout_policy_attn_stack with those blobs (systems
+ * LORENZ3 / PMSM / HR).  The kernel keeps the extractor and one net in LDS and swaps the
+ * pi / vf nets into it by LDS-DMA twice per step; a truncated step's bootstrap value is
+ * added to its reward by the next step's launch segment (same result). */
+lz_status lz_rollout_policy_attn_f32(lz_handle* h, const lz_policy_rollout_args* r);
+lz_status lz_rollout_policy_attn_stack_f32(lz_handle* h, const lz_policy_rollout_args* r,
+                                           int32_t n_stack, const float* stack_in,
+                                           float* stack_out);
 
 /* SB3 RolloutBuffer.compute_returns_and_advantage over time-major [K, N] float32
  * buffers (float32 arithmetic in NumPy's order): advantages and returns out.

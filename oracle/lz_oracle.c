@@ -751,3 +751,171 @@ void orc_vn_tile_totals(const float* x, int64_t n, int O, double* tot) {
     tot[c] = acc[0];
   }
 }
+
+/* ---- f3: the attention actor-critics at SB3's precision (float32), in the fused
+ * kernel's operation order (gym-lorenz_amd/csrc/lz_policy.hip attn16_extract /
+ * attn16_net; every product-sum a k-ordered fmaf chain -- what v_mfma_f32_16x16x4_f32
+ * computes: k-step s of a 16-unit tile takes input 4G + s from lane group G = 0..3, in
+ * that order).  code/train.py:52-95 AttentionFeaturesExtractor: x = relu(fc1(obs))
+ * viewed as 8 tokens of 16; nn.MultiheadAttention(16, 4 heads) self-attention (q scaled
+ * by 1/sqrt(4)); post_attention_fc(128 -> 64) + ReLU; code/lorenz_filter/train.py:54-103
+ * adds x_seq = layer_norm(x_seq + attn_output) before post_attention_fc.  Then the pi /
+ * vf [128, 128] Tanh nets on the 64 features (tanh_tab) and the two heads. */
+
+/* exp(x) for the softmax (x <= 0, or NaN): rint(x log2 e) range reduction, a degree-6
+ * Taylor polynomial in fmaf, ldexp; 0 below -86 (the result stays a normal number). */
+float orc_exp_f32(float x) {
+  if (x != x) return x;
+  if (x < -86.0f) return 0.0f;
+  const float k = rintf(x * 1.44269504088896341f);
+  float r = fmaf(k, -0.693145751953125f, x);
+  r = fmaf(k, -1.42860682030941723e-6f, r);
+  float p = fmaf(1.38888892e-3f, r, 8.33333377e-3f);
+  p = fmaf(p, r, 4.16666679e-2f);
+  p = fmaf(p, r, 1.66666672e-1f);
+  p = fmaf(p, r, 0.5f);
+  p = fmaf(p, r, 1.0f);
+  p = fmaf(p, r, 1.0f);
+  return ldexpf(p, (int)k);
+}
+
+typedef struct {
+  const float *fc1_w, *fc1_b, *in_w, *in_b, *out_w, *out_b, *post_w, *post_b, *ln_w, *ln_b;
+} orc_attn_ext;
+
+/* acc + sum_{s < 4} sum_{G < 4} w[4G + s] * v[4G + s]: one 16-dim k order (4 k-steps) */
+static inline float dot16(float acc, const float* w, const float* v) {
+  for (int s = 0; s < 4; ++s)
+    for (int G = 0; G < 4; ++G) acc = fmaf(w[4 * G + s], v[4 * G + s], acc);
+  return acc;
+}
+
+/* (p0 + p1) + (p2 + p3), p_G = ((v[4G] + v[4G+1]) + v[4G+2]) + v[4G+3] (sq: the squares,
+ * v[4G]^2 then fmaf) -- the kernel's per-lane-group partials and two lane swaps */
+static inline float sum16(const float* v, int sq) {
+  float p[4];
+  for (int G = 0; G < 4; ++G) {
+    const float* z = v + 4 * G;
+    if (sq) {
+      p[G] = z[0] * z[0];
+      for (int d = 1; d < 4; ++d) p[G] = fmaf(z[d], z[d], p[G]);
+    } else {
+      p[G] = ((z[0] + z[1]) + z[2]) + z[3];
+    }
+  }
+  return (p[0] + p[1]) + (p[2] + p[3]);
+}
+
+/* x [in_dim] -> feat [64] */
+static void attn_ext_one(const orc_attn_ext* e, int in_dim, const float* x, float* feat) {
+  float tok[128], kk[8][16], vv[8][16];
+  const int KS = (in_dim + 3) / 4;
+  for (int u = 0; u < 128; ++u) {
+    float acc = e->fc1_b[u];
+    for (int s = 0; s < KS; ++s)
+      for (int G = 0; G < 4; ++G) {
+        const int k = 4 * s + G;
+        acc = fmaf(k < in_dim ? e->fc1_w[u * in_dim + k] : 0.0f, k < in_dim ? x[k] : 0.0f, acc);
+      }
+    tok[u] = acc < 0.0f ? 0.0f : acc;
+  }
+  for (int T = 0; T < 8; ++T)
+    for (int o = 0; o < 16; ++o) {
+      kk[T][o] = dot16(e->in_b[16 + o], e->in_w + (16 + o) * 16, tok + 16 * T);
+      vv[T][o] = dot16(e->in_b[32 + o], e->in_w + (32 + o) * 16, tok + 16 * T);
+    }
+  float post[64];
+  for (int f = 0; f < 64; ++f) post[f] = e->post_b[f];
+  for (int i = 0; i < 8; ++i) {
+    float q[16], att[16], y[16], u[16];
+    for (int o = 0; o < 16; ++o) {  /* 1/sqrt(head dim) = 0.5 folded (exact) */
+      float w[16];
+      for (int d = 0; d < 16; ++d) w[d] = 0.5f * e->in_w[o * 16 + d];
+      q[o] = dot16(0.5f * e->in_b[o], w, tok + 16 * i);
+    }
+    for (int hd = 0; hd < 4; ++hd) {
+      float sc[8], ex[8], m, sum = 0.0f, r;
+      for (int j = 0; j < 8; ++j) {
+        float t = q[4 * hd] * kk[j][4 * hd];
+        for (int c = 1; c < 4; ++c) t = fmaf(q[4 * hd + c], kk[j][4 * hd + c], t);
+        sc[j] = t;
+      }
+      m = sc[0];
+      for (int j = 1; j < 8; ++j) m = (m != m || m >= sc[j]) ? m : sc[j];
+      for (int j = 0; j < 8; ++j) {
+        ex[j] = orc_exp_f32(sc[j] - m);
+        sum = j == 0 ? ex[0] : sum + ex[j];
+      }
+      r = 1.0f / sum;
+      for (int c = 0; c < 4; ++c) {
+        float acc = (ex[0] * r) * vv[0][4 * hd + c];
+        for (int j = 1; j < 8; ++j) acc = fmaf(ex[j] * r, vv[j][4 * hd + c], acc);
+        att[4 * hd + c] = acc;
+      }
+    }
+    for (int o = 0; o < 16; ++o) y[o] = dot16(e->out_b[o], e->out_w + o * 16, att);
+    if (e->ln_w) {  /* LayerNorm(16) of (token + attention), eps 1e-5, biased variance */
+      float z[16], mean, rstd;
+      for (int d = 0; d < 16; ++d) z[d] = y[d] + tok[16 * i + d];
+      mean = sum16(z, 0) * 0.0625f;
+      for (int d = 0; d < 16; ++d) z[d] = z[d] - mean;
+      rstd = 1.0f / sqrtf(sum16(z, 1) * 0.0625f + 1e-5f);
+      for (int d = 0; d < 16; ++d) u[d] = fmaf(z[d] * rstd, e->ln_w[d], e->ln_b[d]);
+    } else {
+      for (int d = 0; d < 16; ++d) u[d] = y[d];
+    }
+    for (int f = 0; f < 64; ++f) post[f] = dot16(post[f], e->post_w + f * 128 + 16 * i, u);
+  }
+  for (int f = 0; f < 64; ++f) feat[f] = post[f] < 0.0f ? 0.0f : post[f];
+}
+
+/* one [128, 128] Tanh net + head on the 64 features (the kernel's attn16_net order):
+ * layer k orders 16-dim blocks f (then s, G) in turn; the head is a per-lane-group fmaf
+ * chain over units 16t + 4G + r (t, then r) from +0, the groups combined as sum16 */
+static void attn_net_one(int R, const float* feat, const float* w1, const float* b1, const float* w2,
+                         const float* b2, const float* w3, const float* b3, float* out) {
+  float a1[128], a2[128];
+  for (int u = 0; u < 128; ++u) {
+    float acc = b1[u];
+    for (int f = 0; f < 4; ++f) acc = dot16(acc, w1 + u * 64 + 16 * f, feat + 16 * f);
+    a1[u] = orc_tanh_tab(acc);
+  }
+  for (int u = 0; u < 128; ++u) {
+    float acc = b2[u];
+    for (int q = 0; q < 8; ++q) acc = dot16(acc, w2 + u * 128 + 16 * q, a1 + 16 * q);
+    a2[u] = orc_tanh_tab(acc);
+  }
+  for (int r = 0; r < R; ++r) {
+    float part[4];
+    for (int G = 0; G < 4; ++G) {
+      float acc = 0.0f;
+      for (int t = 0; t < 8; ++t)
+        for (int c = 0; c < 4; ++c) {
+          const int k = 16 * t + 4 * G + c;
+          acc = fmaf(w3[r * 128 + k], a2[k], acc);
+        }
+      part[G] = acc;
+    }
+    out[r] = ((part[0] + part[1]) + (part[2] + part[3])) + b3[r];
+  }
+}
+
+/* x [n, in_dim] (the policy input: normalised obs, or the VecFrameStack) -> mean [n, A],
+ * value [n], feat [n, 64] (nullable).  ln_w == NULL: code/train.py's extractor. */
+void orc_attn_f32(int64_t n, int in_dim, int A, const float* x, const float* fc1_w, const float* fc1_b,
+                  const float* in_w, const float* in_b, const float* out_w, const float* out_b,
+                  const float* post_w, const float* post_b, const float* ln_w, const float* ln_b,
+                  const float* pi_w1, const float* pi_b1, const float* pi_w2, const float* pi_b2,
+                  const float* vf_w1, const float* vf_b1, const float* vf_w2, const float* vf_b2,
+                  const float* act_w, const float* act_b, const float* val_w, const float* val_b,
+                  float* mean, float* value, float* feat_out) {
+  const orc_attn_ext e = {fc1_w, fc1_b, in_w, in_b, out_w, out_b, post_w, post_b, ln_w, ln_b};
+  for (int64_t i = 0; i < n; ++i) {
+    float feat[64];
+    attn_ext_one(&e, in_dim, x + i * in_dim, feat);
+    if (feat_out)
+      for (int f = 0; f < 64; ++f) feat_out[i * 64 + f] = feat[f];
+    attn_net_one(A, feat, pi_w1, pi_b1, pi_w2, pi_b2, act_w, act_b, mean + i * A);
+    attn_net_one(1, feat, vf_w1, vf_b1, vf_w2, vf_b2, val_w, val_b, value + i);
+  }
+}

@@ -1,5 +1,6 @@
-"""GPU parity of the fused rollout with code/train.py's attention actor-critic
-(lz_rollout_policy_attn: AttentionFeaturesExtractor shared by pi/vf, code/train.py:52-112).
+"""GPU parity of the bf16 opt-in (precision="bf16") of the fused rollout with
+code/train.py's attention actor-critic (lz_rollout_policy_attn: AttentionFeaturesExtractor
+shared by pi/vf, code/train.py:52-112); the float32 default is test_gpu_policy_attn_f32.py.
 
 Bars (as test_gpu_policy.py):
   * env part: bit-exact vs the action-driven lz_rollout fed with the policy's own
@@ -40,6 +41,12 @@ def _np(t):
     return t.detach().cpu().numpy()
 
 
+def _col(pol, *args, **kw):
+    """The bf16 kernels (this file's restatements are bf16)."""
+    kw.setdefault("precision", "bf16")
+    return pol.FusedRolloutCollector(*args, **kw)
+
+
 def _random_attn(pol, O, A, seed, scale=0.3):
     net = pol.ActorCriticAttn(O, A, seed=seed)
     g = torch.Generator().manual_seed(seed + 1)
@@ -60,7 +67,7 @@ def test_attn_rollout_env_part_bitexact(gl, pol, system, n, K, kw):
     envr = gl.BatchedEnv(system, n, seed=11, **kw)
     O, A = envp.obs_dim, envp.action_dim
     _, sd = _random_attn(pol, O, A, seed=3)
-    col = pol.FusedRolloutCollector(envp, sd, bootstrap=False, capture_terminal=K * n)
+    col = _col(pol, envp, sd, bootstrap=False, capture_terminal=K * n)
     assert col.attention
     obs0 = _np(col.reset())
     assert np.array_equal(obs0, _np(envr.reset()))
@@ -95,7 +102,7 @@ def test_attn_forward_vs_torch(gl, pol, system):
     O, A = env.obs_dim, env.action_dim
     _, sd = _random_attn(pol, O, A, seed=7)
     rms = DeviceRunningMeanStd(O, env.device) if system == "pmsm" else None
-    col = pol.FusedRolloutCollector(env, sd, bootstrap=False, deterministic=True, obs_rms=rms)
+    col = _col(pol, env, sd, bootstrap=False, deterministic=True, obs_rms=rms)
     col.reset()
     if rms is not None:
         col.collect(K)  # statistics warm-up, then frozen: last_values use the same stats
@@ -130,7 +137,7 @@ def test_attn_bf16_vs_fp32_sb3_init(gl, pol):
     env = gl.BatchedEnv("hr", n, seed=15)
     O, A = env.obs_dim, env.action_dim
     net = pol.ActorCriticAttn(O, A, seed=3)
-    col = pol.FusedRolloutCollector(env, net.state_dict(), bootstrap=False, deterministic=True)
+    col = _col(pol, env, net.state_dict(), bootstrap=False, deterministic=True)
     col.reset()
     b = col.collect(K)
     obs = b.observations.reshape(-1, O).cpu()
@@ -153,8 +160,8 @@ def test_attn_bootstrap_and_log_prob(gl, pol):
     eb = gl.BatchedEnv("hr", n, seed=21, max_episode_steps=4)
     _, sd = _random_attn(pol, 6, 2, seed=4)
     sd["log_std"] = torch.tensor([-0.5, 0.25])
-    ca = pol.FusedRolloutCollector(ea, sd, gamma=gamma, bootstrap=True, capture_terminal=K * n)
-    cb = pol.FusedRolloutCollector(eb, sd, gamma=gamma, bootstrap=False)
+    ca = _col(pol, ea, sd, gamma=gamma, bootstrap=True, capture_terminal=K * n)
+    cb = _col(pol, eb, sd, gamma=gamma, bootstrap=False)
     ca.reset()
     cb.reset()
     ba, bb = ca.collect(K), cb.collect(K)
@@ -231,7 +238,7 @@ def test_attn_ln_framestack_rollout_bitexact(gl, pol, system, n, K, kw):
     envr = gl.BatchedEnv(system, n, seed=11, **kw)
     O, A = envp.obs_dim, envp.action_dim
     _, sd = _random_attn_ln(pol, 4 * O, A, seed=3)
-    col = pol.FusedRolloutCollector(envp, sd, bootstrap=False, capture_terminal=K * n,
+    col = _col(pol, envp, sd, bootstrap=False, capture_terminal=K * n,
                                     frame_stack=4)
     assert col.attention_ln
     obs0 = _np(col.reset())
@@ -260,9 +267,9 @@ def test_attn_ln_forward_and_bootstrap(gl, pol):
     ea = gl.BatchedEnv("hr", n, seed=21, max_episode_steps=4, add_filter=True)
     eb = gl.BatchedEnv("hr", n, seed=21, max_episode_steps=4, add_filter=True)
     _, sd = _random_attn_ln(pol, 24, 2, seed=4)
-    ca = pol.FusedRolloutCollector(ea, sd, gamma=gamma, bootstrap=True, deterministic=True,
+    ca = _col(pol, ea, sd, gamma=gamma, bootstrap=True, deterministic=True,
                                    capture_terminal=K * n, frame_stack=4)
-    cb = pol.FusedRolloutCollector(eb, sd, gamma=gamma, bootstrap=False, deterministic=True,
+    cb = _col(pol, eb, sd, gamma=gamma, bootstrap=False, deterministic=True,
                                    frame_stack=4)
     obs0 = _np(ca.reset())
     cb.reset()
@@ -300,7 +307,7 @@ def test_attn_ln_sb3_init_vs_fp32(gl, pol):
     n, K = 8192, 4
     env = gl.BatchedEnv("hr", n, seed=15, add_filter=True)
     net = pol.ActorCriticAttn(24, 2, seed=3, layer_norm=True)
-    col = pol.FusedRolloutCollector(env, net.state_dict(), bootstrap=False, deterministic=True,
+    col = _col(pol, env, net.state_dict(), bootstrap=False, deterministic=True,
                                     frame_stack=4)
     col.reset()
     b = col.collect(K)

@@ -239,3 +239,101 @@ def test_resident_refused_under_capture(gl):
     nat.check(nat.lib.lz_set_stream(be._h, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     _step(nat.lib.lz_resident_step, be, act, None, (o, r, d))  # fine outside the capture
     be.close()
+
+
+def _plane_host(be, p):
+    import gym_lorenz._native as nat
+
+    out = np.zeros((be.num_envs,), np.float64 if be.tdtype == torch.float64 else np.float32)
+    nat.check(nat.lib.lz_resident_read_state(be._h, int(p), out.ctypes.data))
+    return out
+
+
+_MIX = [("lorenz3", "float64", {}, False), ("pmsm", "float32", {"add_noise": True}, True),
+        ("hr", "float64", {"add_noise": True}, False), ("lorenz4", "float64", {}, False),
+        ("pmsm", "float64", {}, False), ("hr", "float32", {"add_noise": True, "add_filter": True}, True),
+        ("lorenz3", "float32", {}, False), ("pmsm", "float32", {"add_noise": True}, False)]
+
+
+def test_resident_eight_handles_round_robin(gl):
+    """A DummyVecEnv of 8 drop-in envs (code/train.py:98-100 with several env fns, one
+    step() call per env in turn): 8 handles of mixed systems / dtypes share ONE resident
+    launch (one wave each).  Every handle stays bit-identical to its lz_step_host twin,
+    and the published states (lz_resident_read_state, code/lorenz_pmsm/test_evaluate.py:
+    123-125 reads them after every step) equal the twin's planes while the server runs."""
+    import gym_lorenz._native as nat
+
+    pairs = [_pair(s, 1, dt, **kw) for s, dt, kw, _ in _MIX]
+    bufs = [(_bufs(a), _bufs(b)) for a, b in pairs]
+    rng = np.random.default_rng(17)
+    t_res, t_host = [], []
+    for k in range(300):
+        for i, ((a, b), (ba, bb)) in enumerate(zip(pairs, bufs)):
+            act = rng.uniform(-1, 1, (1, max(a.action_dim, 1))).astype(np.float32)
+            nz = rng.standard_normal((1, 3)) if _MIX[i][3] else None
+            t0 = time.perf_counter()
+            x = _step(nat.lib.lz_step_host, a, act, nz, ba)
+            t1 = time.perf_counter()
+            y = _step(nat.lib.lz_resident_step, b, act, nz, bb)
+            t2 = time.perf_counter()
+            if k >= 20:
+                t_host.append(t1 - t0)
+                t_res.append(t2 - t1)
+            for p, q in zip(x, y):
+                assert bits_equal(p, q), (i, k)
+            if k % 25 == 7:  # published copy, no stop
+                for pl in range(2):
+                    assert bits_equal(a.get_state(pl).cpu().numpy(), _plane_host(b, pl)), (i, k, pl)
+    print("8 handles round robin: median step lz_step_host %.1f us, resident %.1f us"
+          % (1e6 * np.median(t_host), 1e6 * np.median(t_res)))
+    for a, b in pairs:
+        nat.check(nat.lib.lz_resident_stop(b._h))
+        for pl in range(2):
+            assert bits_equal(a.get_state(pl).cpu().numpy(), b.get_state(pl).cpu().numpy())
+        a.close(), b.close()
+
+
+def test_resident_member_churn(gl):
+    """Handles joining (a restart with every state written back), a plain call on one
+    member (stops the server for all), a member closing while others are served, and a
+    17th handle (steps through lz_step_host): all stay bit-identical to their twins."""
+    import gym_lorenz._native as nat
+
+    pairs, bufs = [], []
+    rng = np.random.default_rng(23)
+
+    def add(n):
+        for _ in range(n):
+            pairs.append(_pair("pmsm", 1, "float32", add_noise=True))
+            bufs.append((_bufs(pairs[-1][0]), _bufs(pairs[-1][1])))
+
+    def rounds(m):
+        for k in range(m):
+            for (a, b), (ba, bb) in zip(pairs, bufs):
+                if a is None:
+                    continue
+                act = rng.uniform(-1, 1, (1, 2)).astype(np.float32)
+                x = _step(nat.lib.lz_step_host, a, act, None, ba)
+                y = _step(nat.lib.lz_resident_step, b, act, None, bb)
+                for p, q in zip(x, y):
+                    assert bits_equal(p, q), k
+
+    add(3)
+    rounds(20)
+    add(5)  # joins: restart
+    rounds(20)
+    a, b = pairs[2]
+    act = torch.zeros((1, 2), device=a.device)
+    oa, _, _ = a.step(act)  # plain lz_step on a served handle: stops the server first
+    ob, _, _ = b.step(act)
+    assert bits_equal(oa.cpu().numpy(), ob.cpu().numpy())
+    rounds(20)
+    a, b = pairs[4]
+    a.close(), b.close()  # a member leaves while the others are served
+    pairs[4] = (None, None)
+    rounds(20)
+    add(10)  # 17 live handles: the last ones fall back to lz_step_host
+    rounds(20)
+    for a, b in pairs:
+        if a is not None:
+            a.close(), b.close()
