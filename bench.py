@@ -169,7 +169,7 @@ def fp32_drift(gl, torch, device):
     (b) the free-running max abs error curve (chaotic growth; reported only)."""
     import numpy as np
 
-    n, T = 4096, 200
+    n, T = 4096, 1000  # north_star's horizon: 1000 steps
     f64 = gl.BatchedEnv("lorenz3", n, dtype="float64", seed=99, autoreset=False, device=device)
     f32 = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=99, autoreset=False, device=device)
     f64.reset()
@@ -196,7 +196,7 @@ def fp32_drift(gl, torch, device):
     nonfin_agree = bool(torch.equal(torch.isfinite(o64).all(-1).all(0),
                                     torch.isfinite(o32).all(-1).all(0)))
     curve = {}
-    for k in (1, 10, 50, 100, 200):
+    for k in (1, 10, 50, 100, 200, 500, 1000):
         e = err[k - 1][bounded]
         curve[str(k)] = float(e.max().item()) if e.numel() else None
     for e in (f64, f32, tf):
@@ -518,6 +518,20 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
     }
 
 
+def describe_launches(tm, rollout):
+    """What one timed window of measure_steps actually launched: hipGraph replays and
+    eager launches (the driver's --steps 20 is 0 replays of a 64-step graph + 20 eager)."""
+    per_win = tm["launches"] // tm["windows"]
+    if rollout:
+        return ("per timed window: %d eager %d-step lz_rollout launches (x%d windows)"
+                % (per_win, tm["T"], tm["windows"]))
+    if tm["graph"]:
+        L = tm["graph_len"]
+        return ("per timed window: %d hipGraph replays of %d lz_step launches + %d eager "
+                "lz_step launches (x%d windows)" % (per_win // L, L, per_win % L, tm["windows"]))
+    return "per timed window: %d eager lz_step launches (x%d windows)" % (per_win, tm["windows"])
+
+
 def fp64_line(args, gl, nat, torch, dist, device, n):
     """The same step benchmark at the reference's precision: float64 LORENZ3, the kernel
     that is bit-identical to dynamic.py (tests/test_gpu_parity.py::
@@ -535,7 +549,7 @@ def fp64_line(args, gl, nat, torch, dist, device, n):
         "dtype": "f64",
         "config": {"workload": "dynamic.py 3-state Lorenz env step (lz_step, float64, "
                                "bit-identical to the reference), %d envs on 1 GPU" % n,
-                   "launch": "hipGraph of %d lz_step launches" % tm["graph_len"]},
+                   "launch": describe_launches(tm, False)},
         "timing": tm["timing"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -747,6 +761,7 @@ def main():
     launch_s = ev_ms / 1e3 / nl
     achieved = bytes_step * n * T / launch_s / 1e9
     ref_env = SYSTEM_INFO[args.system][0]
+    launch_desc = describe_launches(tm, rollout)
     if rollout:
         workload = ("%s: %d-step fused on-device rollout (lz_rollout, fp32, state in VGPRs), "
                     "%d envs total, %d per GPU, time-major [K,N,.] rollout buffers"
@@ -773,8 +788,7 @@ def main():
             "workload": workload, "system": args.system, "envs_total": total,
             "envs_per_gpu": n, "mode": args.mode,
             "parallelism": "env shard x%d (contiguous global ids, no collective on step)" % world,
-            "launch": ("hipGraph of %d lz_step launches" % L) if graph else
-                      ("%d-step lz_rollout launches" % T if rollout else "eager"),
+            "launch": launch_desc,
         },
         "timing": tm["timing"],
         "roofline": {
@@ -791,6 +805,10 @@ def main():
     if traffic is not None:
         out["roofline"]["traffic"] = traffic["bytes_per_launch"]
         out["roofline"]["traffic_source"] = traffic["source"]
+        out["roofline"]["traffic_kernel_sha256"] = traffic["kernel_code_sha256"]
+    else:
+        out["roofline"]["traffic_note"] = ("null: no committed PMC summary for this kernel "
+                                           "build (code hash) and shard size")
     headline = args.system == "lorenz3" and not rollout
     if rank == 0 and world == 1 and headline and not args.no_drift:
         out["fp32_drift"] = fp32_drift(gl, torch, device)
@@ -810,18 +828,28 @@ def load_traffic(kernel, n):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload
     (profiles/<round>/*pmc_summary.json, written by tools/pmc_summary.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950-calibrated), if one matches
-    this kernel and shard size; otherwise null."""
+    this kernel and shard size AND was measured on the same build of the kernel: the
+    summary's kernel_code_sha256 (tools/kernel_hash.py: the kernel's gfx950 machine code
+    + descriptor) must equal the running library's -- a changed kernel reports null
+    until it is re-measured."""
     import glob
 
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from kernel_hash import kernel_code_sha256
+
+    live = kernel_code_sha256(kernel)
+    if live is None:
+        return None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc_summary.json"),
                               recursive=True), reverse=True):  # newest round first
         try:
             d = json.load(open(f))
         except Exception:  # noqa: BLE001
             continue
-        if d.get("kernel") == kernel and d.get("envs_per_gpu") == n:
+        if (d.get("kernel") == kernel and d.get("envs_per_gpu") == n
+                and d.get("kernel_code_sha256") == live):
             return {"bytes_per_launch": d["hbm_bytes_per_launch"],
-                    "source": os.path.relpath(f, ROOT)}
+                    "source": os.path.relpath(f, ROOT), "kernel_code_sha256": live}
     return None
 
 

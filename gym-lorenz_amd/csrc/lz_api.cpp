@@ -107,6 +107,8 @@ struct lz_handle {
   int vn_pending;      // lz_step_vecnorm left totals for lz_vecnorm_apply's updates
   int32_t* vn_nd_out;  // lz_step_vecnorm's n_done_out, published by lz_vecnorm_apply
   int32_t* vn_counter; // ... from this done cursor (the step's)
+  uint64_t gen;        // launches on the handle (every parity flip)
+  uint64_t vn_gen;     // gen right after the lz_step_vecnorm that set vn_pending / vn_nd_out
   uint8_t* hs_pin;     // lz_step_host: mapped host staging (actions | noise || obs | rew | done)
   uint8_t* hs_dev;     // lz_step_host: its device address
   size_t hs_in, hs_out;  // bytes of the input / output parts
@@ -434,6 +436,7 @@ lz_status lz_reset(lz_handle* h, const uint8_t* mask, const void* init, void* ob
   const int e = lz::launch_reset(h->cfg.system, h->f64, a, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "reset launch: %s", hipGetErrorString((hipError_t)e));
   h->parity ^= 1;
+  ++h->gen;
   h->was_reset = true;
   return LZ_OK;
 }
@@ -468,6 +471,7 @@ lz_status lz_step(lz_handle* h, const void* actions, const double* noise, void* 
   if (n_done_out)
     HIP_TRY(hipMemcpyAsync(n_done_out, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
   h->parity ^= 1;
+  ++h->gen;
   return LZ_OK;
 }
 
@@ -601,6 +605,7 @@ static void rs_server_ended(RsServer& sv) {
     m->rs_active = false;
     m->rs_pub_valid = false;
     m->parity ^= 1;
+    ++m->gen;
   }
   sv.active = false;
 }
@@ -870,11 +875,13 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
   const int e = lz::launch_step_vecnorm(h->cfg.system, h->f64, a, v, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "step launch: %s", hipGetErrorString((hipError_t)e));
   h->parity ^= 1;
+  ++h->gen;
   h->vn_pending = (vn->flags & LZ_VN_TRAINING) && !(vn->flags & LZ_VN_DEFER);
   // without a second launch the done count is published by the paired lz_vecnorm_apply
   const bool second = (vn->flags & LZ_VN_DEFER) || ((vn->flags & LZ_VN_TRAINING) && !v.fused);
   h->vn_nd_out = second ? nullptr : n_done_out;
   h->vn_counter = a.counter;
+  h->vn_gen = h->gen;
   return LZ_OK;
 }
 
@@ -893,6 +900,14 @@ lz_status lz_vecnorm_apply(lz_handle* h, const lz_vecnorm* vn, const void* obs_r
   const bool term = terminal_obs_raw != nullptr || term_norm != nullptr;
   if (term && (!terminal_obs_raw || !term_norm || !n_done))
     return fail(LZ_ERR_INVALID, "terminal_obs_raw, n_done and term_norm go together");
+  if ((h->vn_pending || h->vn_nd_out) && h->gen != h->vn_gen) {
+    // another launch since lz_step_vecnorm reused its done cursor (and may have
+    // overwritten the moment partials): publishing / updating now would be silently wrong
+    h->vn_pending = 0;
+    h->vn_nd_out = nullptr;
+    return fail(LZ_ERR_STATE, "lz_vecnorm_apply must directly follow its lz_step_vecnorm "
+                              "(another launch on the handle came in between)");
+  }
   HIP_TRY(hipSetDevice(h->cfg.device));
   const int O = h->desc.obs_dim;
   if ((vn->flags & LZ_VN_DEFER) && (vn->flags & LZ_VN_TRAINING)) {
@@ -962,6 +977,7 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
   if (n_done_out)
     HIP_TRY(hipMemcpyAsync(n_done_out, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
   h->parity ^= 1;
+  ++h->gen;
   return LZ_OK;
 }
 
@@ -1061,6 +1077,7 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
   if (r->n_done)
     HIP_TRY(hipMemcpyAsync(r->n_done, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
   h->parity ^= 1;
+  ++h->gen;
   return LZ_OK;
 }
 
@@ -1160,6 +1177,7 @@ lz_status lz_policy_step_f32(lz_handle* h, const lz_policy_rollout_args* r, int3
   if (e != 0) return fail(LZ_ERR_HIP, "policy step launch: %s", hipGetErrorString((hipError_t)e));
   if (!fin) {
     h->parity ^= 1;  // the launch advanced the RNG tick by one (ping-pong)
+    ++h->gen;
     e = lz::launch_vn_tile_update(st.tiles, ntiles, O, (double)n, st.snap, obs_rms_state, moments_out,
                                   h->stream);
     if (e != 0) return fail(LZ_ERR_HIP, "statistics update launch: %s", hipGetErrorString((hipError_t)e));
@@ -1198,26 +1216,35 @@ int32_t lz_plane_elem_size(const lz_handle* h, int32_t plane) {
   return plane_elem(h->cfg.system, h->f64, plane);
 }
 
-lz_status lz_get_state(lz_handle* h, int32_t plane, void* dst) {
-  if (!h || !dst) return fail(LZ_ERR_INVALID, "handle/dst is NULL");
-  RESIDENT_QUIESCE(h);
+static lz_status plane_access(lz_handle* h, int32_t plane, void* buf, const int64_t* indices, int64_t count,
+                              bool set) {
+  if (!h || !buf) return fail(LZ_ERR_INVALID, "handle/%s is NULL", set ? "src" : "dst");
   const int es = plane_elem(h->cfg.system, h->f64, plane);
   if (!es) return fail(LZ_ERR_INVALID, "invalid plane %d", plane);
+  if (!indices && count != 0 && count != h->cfg.num_envs)
+    return fail(LZ_ERR_INVALID, "whole-plane access (indices NULL) with count %lld != 0 / num_envs",
+                (long long)count);
+  if (indices && (count < 0 || count > ((int64_t)1 << 40)))
+    return fail(LZ_ERR_INVALID, "index count %lld out of range", (long long)count);
+  RESIDENT_QUIESCE(h);
   HIP_TRY(hipSetDevice(h->cfg.device));
-  HIP_TRY(hipMemcpyAsync(dst, h->planes[plane], (size_t)h->cfg.num_envs * es, hipMemcpyDeviceToDevice,
-                         h->stream));
+  if (!indices) {
+    const size_t bytes = (size_t)h->cfg.num_envs * es;
+    HIP_TRY(set ? hipMemcpyAsync(h->planes[plane], buf, bytes, hipMemcpyDeviceToDevice, h->stream)
+                : hipMemcpyAsync(buf, h->planes[plane], bytes, hipMemcpyDeviceToDevice, h->stream));
+    return LZ_OK;
+  }
+  HIP_TRY((hipError_t)lz::launch_plane_index(set, es, h->planes[plane], h->cfg.num_envs, indices, count, buf,
+                                             h->stream));
   return LZ_OK;
 }
 
-lz_status lz_set_state(lz_handle* h, int32_t plane, const void* src) {
-  if (!h || !src) return fail(LZ_ERR_INVALID, "handle/src is NULL");
-  RESIDENT_QUIESCE(h);
-  const int es = plane_elem(h->cfg.system, h->f64, plane);
-  if (!es) return fail(LZ_ERR_INVALID, "invalid plane %d", plane);
-  HIP_TRY(hipSetDevice(h->cfg.device));
-  HIP_TRY(hipMemcpyAsync(h->planes[plane], src, (size_t)h->cfg.num_envs * es, hipMemcpyDeviceToDevice,
-                         h->stream));
-  return LZ_OK;
+lz_status lz_get_state(lz_handle* h, int32_t plane, void* dst, const int64_t* indices, int64_t count) {
+  return plane_access(h, plane, dst, indices, count, false);
+}
+
+lz_status lz_set_state(lz_handle* h, int32_t plane, const void* src, const int64_t* indices, int64_t count) {
+  return plane_access(h, plane, const_cast<void*>(src), indices, count, true);
 }
 
 }  // extern "C"

@@ -357,6 +357,10 @@ struct ResMember {      // one wave of the server
 // table: device copy of n members; one workgroup of 64 n threads
 int launch_resident_multi(const ResMember* table, int n, uint64_t idle_ticks, void* stream);
 int launch_rollout(int system, int f64, const KArgs& a, void* stream);
+// gather (scatter = false: buf[i] = plane[idx[i]]) / scatter (plane[idx[i]] = buf[i]) of
+// es-byte elements; indices outside [0, n) skipped / read as zero
+int launch_plane_index(bool scatter, int es, void* plane, int64_t n, const int64_t* idx, int64_t count,
+                       void* buf, void* stream);
 int launch_step_vecnorm(int system, int f64, const KArgs& a, const VArgs& v, void* stream);
 // Launch shape of the policy rollout (one workgroup per CU: the weights fill LDS).
 //   >= 131,072 envs: 64 envs per wave (two 32-env MFMA column tiles, every lane steps

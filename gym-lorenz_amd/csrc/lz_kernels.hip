@@ -1125,4 +1125,50 @@ int launch_rollout(int system, int f64, const KArgs& a, void* stream) {
   return dispatch(2, system, f64, a, stream);
 }
 
+// Indexed plane access (lz_get_state / lz_set_state with indices): one lane per index,
+// elements of E bytes.  Indices outside [0, n) are skipped by the scatter and read as
+// zero bits by the gather -- no fault; the host wrappers validate before launching.
+template <typename E>
+__global__ __launch_bounds__(256) void k_plane_gather(const E* __restrict__ plane, int64_t n,
+                                                      const int64_t* __restrict__ idx, int64_t count,
+                                                      E* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  const int64_t j = idx[i];
+  dst[i] = (j >= 0 && j < n) ? plane[j] : E(0);
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void k_plane_scatter(E* __restrict__ plane, int64_t n,
+                                                       const int64_t* __restrict__ idx, int64_t count,
+                                                       const E* __restrict__ src) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  const int64_t j = idx[i];
+  if (j >= 0 && j < n) plane[j] = src[i];
+}
+
+int launch_plane_index(bool scatter, int es, void* plane, int64_t n, const int64_t* idx, int64_t count,
+                       void* buf, void* stream) {
+  if (count <= 0) return 0;
+  const dim3 g((unsigned)((count + 255) / 256));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (es == 8) {
+    if (scatter)
+      hipLaunchKernelGGL(k_plane_scatter<uint64_t>, g, dim3(256), 0, s, static_cast<uint64_t*>(plane), n, idx,
+                         count, static_cast<const uint64_t*>(buf));
+    else
+      hipLaunchKernelGGL(k_plane_gather<uint64_t>, g, dim3(256), 0, s, static_cast<const uint64_t*>(plane), n,
+                         idx, count, static_cast<uint64_t*>(buf));
+  } else {
+    if (scatter)
+      hipLaunchKernelGGL(k_plane_scatter<uint32_t>, g, dim3(256), 0, s, static_cast<uint32_t*>(plane), n, idx,
+                         count, static_cast<const uint32_t*>(buf));
+    else
+      hipLaunchKernelGGL(k_plane_gather<uint32_t>, g, dim3(256), 0, s, static_cast<const uint32_t*>(plane), n,
+                         idx, count, static_cast<uint32_t*>(buf));
+  }
+  return (int)hipGetLastError();
+}
+
 }  // namespace lz

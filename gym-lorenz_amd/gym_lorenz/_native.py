@@ -159,8 +159,8 @@ _SIGS = {
     "lz_resident_step": (ctypes.c_int, [VP, VP, VP, VP, VP, VP]),
     "lz_resident_stop": (ctypes.c_int, [VP]),
     "lz_resident_read_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
-    "lz_get_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
-    "lz_set_state": (ctypes.c_int, [VP, ctypes.c_int32, VP]),
+    "lz_get_state": (ctypes.c_int, [VP, ctypes.c_int32, VP, VP, ctypes.c_int64]),
+    "lz_set_state": (ctypes.c_int, [VP, ctypes.c_int32, VP, VP, ctypes.c_int64]),
     "lz_plane_elem_size": (ctypes.c_int32, [VP, ctypes.c_int32]),
     "lz_rms_create": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_double,
                                      ctypes.POINTER(VP)]),

@@ -220,15 +220,49 @@ class BatchedEnv:
             return torch.int32
         return torch.float64 if es == 8 else torch.float32
 
-    def get_state(self, plane):
-        t = torch.empty((self.num_envs,), dtype=self.plane_dtype(plane), device=self.device)
-        nat.check(nat.lib.lz_get_state(self._h, int(plane), _ptr(t)))
+    def _env_ids(self, indices):
+        """Validated device int64 env ids (lz_get_state / lz_set_state skip, not fault
+        on, out-of-range ids: reject them here instead)."""
+        idx = torch.as_tensor(indices, dtype=torch.int64).reshape(-1)
+        if idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= self.num_envs):
+            raise IndexError("env index out of range [0, %d)" % self.num_envs)
+        return idx.to(self.device)
+
+    def get_state(self, plane, indices=None):
+        """The whole plane, or (indices: env ids) a device gather of those envs."""
+        if indices is None:
+            t = torch.empty((self.num_envs,), dtype=self.plane_dtype(plane), device=self.device)
+            nat.check(nat.lib.lz_get_state(self._h, int(plane), _ptr(t), None, 0))
+            return t
+        idx = self._env_ids(indices)
+        t = torch.empty((idx.numel(),), dtype=self.plane_dtype(plane), device=self.device)
+        if idx.numel() == 0:  # (a NULL index list would mean the whole plane)
+            return t
+        nat.check(nat.lib.lz_get_state(self._h, int(plane), _ptr(t), _ptr(idx), idx.numel()))
+        self._last_plane = idx
         return t
 
-    def set_state(self, plane, values):
-        t = self._check_dev(values, self.plane_dtype(plane), (self.num_envs,), "plane")
-        nat.check(nat.lib.lz_set_state(self._h, int(plane), _ptr(t)))
-        self._last_plane = t
+    def set_state(self, plane, values, indices=None):
+        """The whole plane, or (indices) a device scatter of values[i] into env
+        indices[i] (repeated ids: the last occurrence wins, as numpy assignment)."""
+        if indices is None:
+            t = self._check_dev(values, self.plane_dtype(plane), (self.num_envs,), "plane")
+            nat.check(nat.lib.lz_set_state(self._h, int(plane), _ptr(t), None, 0))
+            self._last_plane = t
+            return
+        idx = self._env_ids(indices)
+        if idx.numel() == 0:
+            return
+        v = torch.as_tensor(values, dtype=self.plane_dtype(plane)).reshape(-1).to(self.device)
+        v = torch.broadcast_to(v, idx.shape).contiguous()
+        if idx.numel() > 1:  # keep the last occurrence of a repeated id
+            order = torch.arange(idx.numel(), device=idx.device)
+            last = torch.full((self.num_envs,), -1, dtype=torch.int64, device=idx.device)
+            last.scatter_reduce_(0, idx, order, reduce="amax")
+            keep = last[idx] == order
+            idx, v = idx[keep].contiguous(), v[keep].contiguous()
+        nat.check(nat.lib.lz_set_state(self._h, int(plane), _ptr(v), _ptr(idx), idx.numel()))
+        self._last_plane = (v, idx)
 
     def set_seed(self, seed):
         """Philox key for subsequent on-device resets and noise (VecEnv.seed)."""

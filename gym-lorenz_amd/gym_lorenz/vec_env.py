@@ -297,30 +297,37 @@ class LorenzVecEnv(VecEnvBase):
         return list(indices)
 
     def get_attr(self, attr_name, indices=None):
+        """SB3 VecEnv.get_attr: state attributes read as a device gather of the requested
+        envs only (lz_get_state with indices)."""
         idx = self._indices(indices)
         attrs = _STATE_ATTRS[self.system]
         if attr_name in attrs:
             first, cnt = attrs[attr_name]
-            cols = [self.backend.get_state(first + j).cpu().numpy() for j in range(cnt)]
+            ids = None if indices is None else idx
+            cols = [self.backend.get_state(first + j, ids).cpu().numpy() for j in range(cnt)]
             vals = np.stack(cols, axis=1)
-            return [vals[i] if cnt > 1 else vals[i, 0] for i in idx]
+            rows = range(len(idx))
+            return [vals[r] if cnt > 1 else vals[r, 0] for r in rows]
         if attr_name in ("observation_space", "action_space", "render_mode", "metadata", "spec"):
             return [getattr(self, attr_name) for _ in idx]
         raise AttributeError("LorenzVecEnv: unknown env attribute %r" % attr_name)
 
     def set_attr(self, attr_name, value, indices=None):
+        """SB3 VecEnv.set_attr: every requested env gets `value` (the reference's
+        `base_env.state1 = np.array([10, -10, 15])`, code/lorenz_pmsm/test_evaluate.py:
+        100-102), written as a device scatter into those envs only (lz_set_state with
+        indices) -- the other envs' state is not touched."""
         idx = self._indices(indices)
         attrs = _STATE_ATTRS[self.system]
         if attr_name not in attrs:
             raise AttributeError("LorenzVecEnv: attribute %r is not settable" % attr_name)
         first, cnt = attrs[attr_name]
-        v = np.asarray(value)
+        v = np.asarray(value, dtype=np.float64)
+        if cnt > 1 and v.shape[-1:] != (cnt,):
+            raise ValueError("%s takes %d components, got shape %s" % (attr_name, cnt, v.shape))
         for j in range(cnt):
-            col = self.backend.get_state(first + j)
             vj = v[..., j] if cnt > 1 else v
-            col[torch.as_tensor(idx, device=col.device)] = torch.as_tensor(
-                np.broadcast_to(vj, (len(idx),)).copy(), dtype=col.dtype, device=col.device)
-            self.backend.set_state(first + j, col)
+            self.backend.set_state(first + j, np.broadcast_to(vj, (len(idx),)).copy(), idx)
 
     def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
         idx = self._indices(indices)

@@ -507,10 +507,21 @@ lz_status lz_gae(int64_t n, int32_t K, const float* rew, const float* values,
 lz_status lz_episode_starts(int64_t n, int32_t K, const uint8_t* done, const float* last_in,
                             float* starts, float* last_out, int32_t device, void* hip_stream);
 
-/* Copy one SoA state plane (N elements, T or int32 / float32 as listed above)
- * between the handle and a device buffer. */
-lz_status lz_get_state(lz_handle* h, int32_t plane, void* dst);
-lz_status lz_set_state(lz_handle* h, int32_t plane, const void* src);
+/* Read / write one SoA state plane (T or int32 / float32 elements as listed above),
+ * stream-ordered on the handle's stream, device buffers:
+ *   indices == NULL: the whole plane, N elements (count 0 or N);
+ *   indices != NULL: a device int64 [count] list of env ids -- lz_get_state gathers
+ *     dst[i] = plane[indices[i]], lz_set_state scatters plane[indices[i]] = src[i]
+ *     (one launch, O(count) bytes: a single env's attribute is written without a
+ *     whole-plane round trip).  Ids outside [0, N) are skipped by the scatter and read
+ *     as zero bits by the gather (validate on the host); with repeated ids in a scatter
+ *     it is unspecified which value lands.
+ * Replaces the per-env attribute reads / writes of a DummyVecEnv caller:
+ * VecEnv.get_attr / set_attr(name, value, indices) and the injection
+ * `base_env.state1 = np.array([10, -10, 15])` in code/lorenz_pmsm/test_evaluate.py:100-102. */
+lz_status lz_get_state(lz_handle* h, int32_t plane, void* dst, const int64_t* indices, int64_t count);
+lz_status lz_set_state(lz_handle* h, int32_t plane, const void* src, const int64_t* indices,
+                       int64_t count);
 
 /* Element size in bytes of a plane (4 or 8), or 0 for an invalid plane. */
 int32_t lz_plane_elem_size(const lz_handle* h, int32_t plane);

@@ -69,7 +69,7 @@ static int run_l3(int64_t n, int K) {
   float* st = malloc(n * 3 * 4);
   float* x = malloc(n * 4);
   for (int j = 0; j < 3; ++j) {  /* the device-drawn initial states, plane by plane */
-    CHECK(lz_get_state(h, LZ_L3_X + j, d_x));
+    CHECK(lz_get_state(h, LZ_L3_X + j, d_x, NULL, 0));
     CHECK(lz_sync(h));
     HCHECK(hipMemcpy(x, d_x, n * 4, hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < n; ++i) st[i * 3 + j] = x[i];

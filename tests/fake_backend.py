@@ -88,19 +88,24 @@ class FakeBackend:
     def done_list(self):
         return torch.from_numpy(self._done_idx), torch.from_numpy(self._term)
 
-    def get_state(self, plane):
+    def _col(self, plane):
         if self.system_name == "lorenz3":
-            return torch.from_numpy(self.st[:, plane].copy())
+            return self.st[:, plane]
         cols = {**{j: self.S.st[:, j] for j in range(6)}, 6: self.S.lam, 7: self.S.m, 8: self.S.v,
                 9: self.S.adam_step, 10: self.S.cur_step}
-        return torch.from_numpy(np.array(cols[plane]))
+        return cols[plane]
 
-    def set_state(self, plane, values):
+    def get_state(self, plane, indices=None):
+        col = self._col(plane)
+        return torch.from_numpy(np.array(col if indices is None else col[np.asarray(indices)]))
+
+    def set_state(self, plane, values, indices=None):
         v = np.asarray(values.cpu() if isinstance(values, torch.Tensor) else values)
-        if self.system_name == "lorenz3":
-            self.st[:, plane] = v
+        col = self._col(plane)  # a view: writes land in the state
+        if indices is None:
+            col[:] = v
         else:
-            self.S.st[:, plane] = v
+            col[np.asarray(indices)] = v
 
     def set_seed(self, seed):
         self.seed = seed

@@ -329,6 +329,42 @@ def test_shard_invariance(gl):
         assert np.array_equal(df, np.concatenate([x[2] for x in outs]))
 
 
+def test_cfg3_shard_geometry(gl):
+    """BASELINE configs[2]'s real split: 8 ranks x 131,072 LORENZ3 envs at
+    global_env_offset = r * 131,072 (run one after another on this GPU) reproduce one
+    1,048,576-env handle bit for bit over 30 steps with auto-reset (a 7-step TimeLimit,
+    so resets fire and their draws are keyed by the global env id): observations,
+    rewards, done bytes and the compact done lists (shard ids + offset)."""
+    S, R, T = 131_072, 8, 30
+    full = gl.BatchedEnv("lorenz3", S * R, dtype="float32", seed=21, max_episode_steps=7)
+    parts = [gl.BatchedEnv("lorenz3", S, dtype="float32", seed=21, max_episode_steps=7,
+                           global_env_offset=r * S) for r in range(R)]
+    of = full.reset()
+    for r, p in enumerate(parts):
+        assert torch.equal(p.reset().view(torch.int32), of[r * S:(r + 1) * S].view(torch.int32))
+    g = torch.Generator(device="cuda").manual_seed(8)
+    resets = 0
+    for k in range(T):
+        a = torch.rand((S * R, 3), generator=g, device="cuda") * 2 - 1
+        of, rf, df = full.step(a)
+        fidx, fterm = full.done_list()
+        resets += fidx.numel()
+        for r, p in enumerate(parts):
+            sl = slice(r * S, (r + 1) * S)
+            o, rw, d = p.step(a[sl])
+            assert torch.equal(o.view(torch.int32), of[sl].view(torch.int32)), (k, r)
+            assert torch.equal(rw.view(torch.int32), rf[sl].view(torch.int32)), (k, r)
+            assert torch.equal(d, df[sl]), (k, r)
+            pidx, pterm = p.done_list()
+            m = (fidx >= r * S) & (fidx < (r + 1) * S)
+            assert torch.equal(pidx + r * S, fidx[m]), (k, r)
+            assert torch.equal(pterm.view(torch.int32), fterm[m].view(torch.int32)), (k, r)
+    assert resets == 4 * S * R  # truncations at steps 7, 14, 21, 28
+    full.close()
+    for p in parts:
+        p.close()
+
+
 @pytest.mark.parametrize("system,dtype,n", [("lorenz3", "float32", 1000), ("pmsm", "float32", 1000),
                                             ("hr", "float64", 1000), ("lorenz4", "float32", 1000),
                                             ("lorenz3", "float32", 40001),

@@ -251,7 +251,7 @@ def _plane_host(be, p):
 
 _MIX = [("lorenz3", "float64", {}, False), ("pmsm", "float32", {"add_noise": True}, True),
         ("hr", "float64", {"add_noise": True}, False), ("lorenz4", "float64", {}, False),
-        ("pmsm", "float64", {}, False), ("hr", "float32", {"add_noise": True, "add_filter": True}, True),
+        ("lorenz4", "float32", {}, False), ("hr", "float32", {"add_noise": True, "add_filter": True}, True),
         ("lorenz3", "float32", {}, False), ("pmsm", "float32", {"add_noise": True}, False)]
 
 

@@ -207,3 +207,40 @@ def test_vecnorm_abi_errors(gl):
     assert nat.lib.lz_step_vecnorm(be._h, ctypes.byref(vn), *args) == nat.LZ_ERR_INVALID
     vn = v._vn_args()
     assert nat.lib.lz_step_vecnorm(be._h, ctypes.byref(vn), *args[:6], None) == nat.LZ_ERR_INVALID
+
+
+def test_vecnorm_apply_refused_after_another_launch(gl):
+    """lz_step_vecnorm leaves its done cursor and moment partials for the paired
+    lz_vecnorm_apply; a launch in between (here a plain lz_step, which reuses the cursor)
+    makes the apply refuse with LZ_ERR_STATE instead of publishing a wrong done count or
+    stale statistics.  The next proper step_vecnorm + apply pair works again."""
+    from gym_lorenz import _native as nat
+
+    n = 4096
+    dev = _vn(gl, n, norm_obs=True, norm_reward=False, clip_obs=10.0)
+    dev.reset()
+    be = dev.venv.backend
+    vn = dev._vn_args()
+    o = be.obs_dim
+    buf = [torch.empty((n, o), device="cuda"), torch.empty((n,), device="cuda"),
+           torch.empty((n,), dtype=torch.uint8, device="cuda"),
+           torch.empty((n + 1,), dtype=torch.int32, device="cuda"),
+           torch.empty((n, o), device="cuda"), torch.empty((n, o), device="cuda"),
+           torch.empty((n,), device="cuda"), torch.empty((n,), dtype=torch.uint8, device="cuda"),
+           torch.empty((n, o), device="cuda")]
+    p = [t.data_ptr() for t in buf]
+    acts = torch.zeros((n, 2), device="cuda")
+    nat.check(nat.lib.lz_step_vecnorm(be._h, vn, acts.data_ptr(), p[0], p[1], p[2], p[3], p[4],
+                                      p[3] + 4 * n))
+    be.step(acts)  # another launch on the handle
+    st = nat.lib.lz_vecnorm_apply(be._h, vn, p[0], p[1], p[2], p[5], p[6], p[7], p[4],
+                                  p[3] + 4 * n, p[8])
+    assert st == nat.LZ_ERR_STATE
+    # a proper pair goes through
+    nat.check(nat.lib.lz_step_vecnorm(be._h, vn, acts.data_ptr(), p[0], p[1], p[2], p[3], p[4],
+                                      p[3] + 4 * n))
+    nat.check(nat.lib.lz_vecnorm_apply(be._h, vn, p[0], p[1], p[2], p[5], p[6], p[7], p[4],
+                                       p[3] + 4 * n, p[8]))
+    torch.cuda.synchronize()
+    obs, rew, done, infos = dev.step(np.zeros((n, 2), np.float32))  # the wrapper still works
+    assert obs.shape == (n, o)

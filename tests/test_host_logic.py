@@ -89,6 +89,14 @@ def test_vecenv_attrs_methods_seed():
     assert len(s1) == n and s1[0].shape == (3,)
     v.set_attr("state1", [1.0, 2.0, 3.0], indices=[2])
     assert np.array_equal(v.get_attr("state1", indices=2)[0], [1, 2, 3])
+    after = v.get_attr("state1")
+    for i in range(n):  # only env 2 was written
+        if i != 2:
+            assert np.array_equal(after[i], s1[i])
+    got = v.get_attr("state1", indices=[5, 2])  # in the order asked
+    assert np.array_equal(got[0], s1[5]) and np.array_equal(got[1], [1, 2, 3])
+    with pytest.raises(ValueError):
+        v.set_attr("state1", [1.0, 2.0], indices=[2])  # wrong component count
     assert v.get_attr("lambda_coef")[0] == 0.0
     assert v.env_is_wrapped(object) == [False] * n
     assert v.seed(123)[:2] == [123, 124] and be.seed == 123

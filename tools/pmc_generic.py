@@ -17,6 +17,8 @@ import sys
 
 from pmc_summary import per_kernel
 
+from kernel_hash import kernel_code_sha256  # noqa: E402  (tools/)
+
 FETCH_FACTOR = 0.5000092188517252
 WRITE_FACTOR = 1.0
 
@@ -40,6 +42,8 @@ def main():
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, "
                   "kernel-trace only; average over the profiled launches",
     }
+    # the traffic is valid for exactly this build of the kernel (bench.py load_traffic)
+    res["kernel_code_sha256"] = kernel_code_sha256(res["kernel"])
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: res[k] for k in ("kernel", "hbm_bytes_per_launch", "algorithmic_bytes",
                                           "traffic_over_algorithmic")}))

@@ -16,6 +16,8 @@ import json
 import os
 import sys
 
+from kernel_hash import kernel_code_sha256  # noqa: E402  (tools/)
+
 FETCH_FACTOR = 0.5000092188517252  # tools/pmc_generic.py (r01 calibration)
 SIMDS = 1024
 
@@ -82,6 +84,8 @@ def main():
                   "SQ issue/wait set; SQ instruction mix + GRBM_GUI_ACTIVE), kernel trace only; "
                   "averages over the profiled dispatches (tools/step_counters.sh)",
     }
+    # the traffic is valid for exactly this build of the kernel (bench.py load_traffic)
+    res["kernel_code_sha256"] = kernel_code_sha256(res["kernel"])
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({"kernel": match, "avg_us": avg_ns / 1e3, "traffic_x": res["traffic_over_algorithmic"],
                       **{k: v for k, v in d.items() if k != "wave_cycles_split"},

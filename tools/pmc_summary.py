@@ -16,6 +16,8 @@ import json
 import os
 import sys
 
+from kernel_hash import kernel_code_sha256  # noqa: E402  (tools/)
+
 GIB = 1 << 30
 STEP = "k_step<lz::SysL3<float>, float, 0>"
 STEP_MANGLED = "_ZN2lz6k_stepINS_5SysL3IfEEfLi0EEEvNS_5KArgsE"
@@ -67,6 +69,8 @@ def main():
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                   "measured/known factors from tools/pmc_calib (1 GiB streams)",
     }
+    # the traffic is valid for exactly this build of the kernel (bench.py load_traffic)
+    res["kernel_code_sha256"] = kernel_code_sha256(res["kernel"])
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -41,7 +41,34 @@ def main():
         e = gl.make("lorenz_pmsm-v0")
         e.reset(seed=0)
         res["lorenz_pmsm-v0 (fp32)"] = timed(e, np.zeros(2, np.float32), 5000)
+        # code/lorenz_pmsm/test_evaluate.py:119-125: every step followed by reads of
+        # base_env.state1 / state2 (the published copy while the server runs)
+        base = e.unwrapped
+        act = np.zeros(2, np.float32)
+        for _ in range(50):
+            e.step(act)
+        t0 = time.perf_counter()
+        for _ in range(5000):
+            e.step(act)
+            _ = base.state1[0] - base.state2[0], base.state1[1] - base.state2[1]
+        res["lorenz_pmsm-v0 step + state1/state2 reads (test_evaluate loop)"] = (
+            (time.perf_counter() - t0) / 5000 * 1e6)
         e.close()
+        # DummyVecEnv([env_fn] * 8) (code/train.py:98-100 with several env fns): one
+        # step() per env in turn; per env-step
+        envs = [gl.make("lorenz_pmsm-v0") for _ in range(8)]
+        for i, x in enumerate(envs):
+            x.reset(seed=i)
+        for _ in range(50):
+            for x in envs:
+                x.step(act)
+        t0 = time.perf_counter()
+        for _ in range(1000):
+            for x in envs:
+                x.step(act)
+        res["8 lorenz_pmsm-v0 envs round robin (per env-step)"] = (time.perf_counter() - t0) / 8000 * 1e6
+        for x in envs:
+            x.close()
         out[label] = res
     # the C call alone (no gymnasium / class overhead): lorenz3 fp64, 1 env
     import gym_lorenz._native as nat
