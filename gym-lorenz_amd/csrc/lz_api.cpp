@@ -556,6 +556,8 @@ struct RsServer {
   hipEvent_t ev;
   lz::ResMember* table_host;  // pinned staging of the member table
   lz::ResMember* table_dev;
+  int64_t* bell;         // the doorbell: mapped, coherent host memory (own cache line)
+  const int64_t* bell_dev;
   uint64_t idle;         // idle exit, wall-clock ticks
 };
 static std::mutex g_rs_mu;  // trivially destructible
@@ -569,16 +571,24 @@ static lz_status rs_server_init(RsServer& sv, int device) {
   hipEvent_t ev = nullptr;
   lz::ResMember* th = nullptr;
   lz::ResMember* td = nullptr;
+  int64_t* bell = nullptr;
+  void* bell_dev = nullptr;
   const size_t tb = sizeof(lz::ResMember) * lz::kRsMaxHandles;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&th), tb) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&td), tb) != hipSuccess) {
+      hipMalloc(reinterpret_cast<void**>(&td), tb) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&bell), 128, hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer(&bell_dev, bell, 0) != hipSuccess || !bell_dev) {
     if (st) (void)hipStreamDestroy(st);
     if (ev) (void)hipEventDestroy(ev);
     if (th) (void)hipHostFree(th);
+    if (td) (void)hipFree(td);
+    if (bell) (void)hipHostFree(bell);
     return fail(LZ_ERR_OOM, "resident server setup failed");
   }
+  *bell = 0;
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0)
     khz = 100000;
@@ -590,6 +600,8 @@ static lz_status rs_server_init(RsServer& sv, int device) {
   sv.ev = ev;
   sv.table_host = th;
   sv.table_dev = td;
+  sv.bell = bell;
+  sv.bell_dev = static_cast<const int64_t*>(bell_dev);
   sv.idle = (uint64_t)(idle_us * khz / 1000.0);
   sv.n = 0;
   sv.active = false;
@@ -615,6 +627,7 @@ static lz_status rs_server_stop(RsServer& sv) {
   // one mailbox's stop command makes every wave leave; the word is restored after
   lz_handle* m0 = sv.members[0];
   __atomic_store_n(const_cast<int64_t*>(rs_word(m0, kRsCmd)), (int64_t)-1, __ATOMIC_RELEASE);
+  __atomic_fetch_add(sv.bell, 1, __ATOMIC_RELEASE);
   const hipError_t e = hipStreamSynchronize(sv.stream);
   __atomic_store_n(const_cast<int64_t*>(rs_word(m0, kRsCmd)), m0->rs_seq, __ATOMIC_RELEASE);
   rs_server_ended(sv);
@@ -635,6 +648,7 @@ static void resident_unload() {
     if (!sv.init || !sv.active || sv.n == 0) continue;
     __atomic_store_n(const_cast<int64_t*>(rs_word(sv.members[0], kRsCmd)), (int64_t)-1,
                      __ATOMIC_RELEASE);
+    __atomic_fetch_add(sv.bell, 1, __ATOMIC_RELEASE);
     any = true;
   }
   if (any) usleep(2000);  // a poll period is ~2 us; the waves exit on sight
@@ -669,7 +683,7 @@ static lz_status rs_server_launch(RsServer& sv) {
   }
   HIP_TRY(hipMemcpyAsync(sv.table_dev, sv.table_host, sizeof(lz::ResMember) * sv.n,
                          hipMemcpyHostToDevice, sv.stream));
-  const int e = lz::launch_resident_multi(sv.table_dev, sv.n, sv.idle, sv.stream);
+  const int e = lz::launch_resident_multi(sv.table_dev, sv.n, sv.bell_dev, sv.idle, sv.stream);
   if (e != 0) return fail(LZ_ERR_HIP, "resident launch: %s", hipGetErrorString((hipError_t)e));
   sv.active = true;
   for (int i = 0; i < sv.n; ++i) sv.members[i]->rs_active = true;
@@ -759,6 +773,7 @@ lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noi
   if (needs_act) std::memcpy(h->rs_pin + kRsAct, actions, (size_t)n * h->desc.action_dim * 4);
   if (noise) std::memcpy(h->rs_pin + kRsNoise, noise, (size_t)n * 3 * 8);
   __atomic_store_n(const_cast<int64_t*>(rs_word(h, kRsCmd)), seq, __ATOMIC_RELEASE);
+  __atomic_fetch_add(sv.bell, 1, __ATOMIC_RELEASE);  // after the command (x86: ordered)
   if (!sv.active) {
     const lz_status q = rs_server_launch(sv);
     if (q != LZ_OK) return q;

@@ -901,20 +901,21 @@ static int dispatch(int which, int system, int f64, const KArgs& a, void* stream
 // ------------------------------------------------------------------ resident step server
 // lz_resident_step (lz_internal.h ResBox / ResMember): the per-env drop-in classes step
 // ONE env per env.step() call, and a launch + stream synchronisation per call costs
-// 20-27 us (profiles/r01/dropin).  This kernel stays on the GPU between calls, one wave
-// per registered handle: lane 0 polls its handle's command word over PCIe, the wave
-// serves the request with the same step_body as k_step (state in registers, tick += 1
-// per request, injected noise staged through LDS), and the reply goes straight into host
-// memory.  Bounded: every wave leaves on a stop command in any mailbox or after
-// idle_ticks without a request in any mailbox (the shared flag / clock in LDS), so the
-// launch ends as a whole and a relaunch includes every handle.
+// 20-27 us (profiles/r01/dropin).  This kernel stays on the GPU between calls: one wave
+// per registered handle serves that handle's requests with the same step_body as k_step
+// (state in registers, tick += 1 per request, injected noise staged through LDS), the
+// reply going straight into host memory; one poller wave watches the doorbell and hands
+// request numbers to the member waves through LDS.  Bounded: every wave leaves on a stop
+// command in any mailbox or after idle_ticks without a doorbell (the shared flag in LDS),
+// so the launch ends as a whole and a relaunch includes every handle.
 struct ResShared {
   int exit_;
-  unsigned long long last;  // wall_clock64() of the latest request served by any wave
+  unsigned long long last;          // wall_clock64() of the latest doorbell / reply
+  int64_t req[kRsMaxHandles];       // the newest request number posted to each member
 };
 
 template <class Sys, typename T>
-__device__ void resident_serve(const ResMember& m, ResShared* sh, double* s_nz, uint64_t idle_ticks) {
+__device__ __forceinline__ void resident_serve(const ResMember& m, int wave, ResShared* sh, double* s_nz) {
   const KArgs& a = m.a;
   const ResBox& box = m.box;
   const int lane = (int)(threadIdx.x & 63u);
@@ -943,22 +944,13 @@ __device__ void resident_serve(const ResMember& m, ResShared* sh, double* s_nz, 
   int64_t next = box.next;
   for (;;) {
     int64_t c = 0;
-    if (lane == 0) {
+    if (lane == 0) {  // LDS only: the poller reads host memory
       for (;;) {
-        c = __hip_atomic_load(box.cmd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (c == next) break;
-        if (c < 0) {  // stop: every wave leaves
-          __hip_atomic_store(&sh->exit_, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__hip_atomic_load(&sh->req[wave], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= next) {
+          c = next;
           break;
         }
         if (__hip_atomic_load(&sh->exit_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-          c = -2;
-          break;
-        }
-        const unsigned long long last =
-            __hip_atomic_load(&sh->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (wall_clock64() - last > idle_ticks) {
-          __hip_atomic_store(&sh->exit_, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           c = -2;
           break;
         }
@@ -1012,8 +1004,49 @@ __device__ void resident_serve(const ResMember& m, ResShared* sh, double* s_nz, 
   if (lane == 0) *a.tick_out = tick;
 }
 
-__global__ __launch_bounds__(64 * kRsMaxHandles) void k_resident_multi(const ResMember* __restrict__ table,
-                                                                       uint64_t idle_ticks) {
+// The poller wave: one system-scope load of the doorbell per poll; when it has moved,
+// lane i loads member i's command word and publishes it to the member through LDS.  A
+// request posted after the command loads rings the doorbell again, so none is missed.
+__device__ void resident_poll(const ResMember* __restrict__ table, int n, const int64_t* bell,
+                              ResShared* sh, uint64_t idle_ticks) {
+  const int lane = (int)(threadIdx.x & 63u);
+  const int64_t* cmd = lane < n ? table[lane].box.cmd : nullptr;
+  int64_t seen = -1;  // the first pass scans every mailbox (a request may predate the launch)
+  for (;;) {
+    int64_t b = 0;
+    if (lane == 0) b = __hip_atomic_load(bell, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    b = __shfl(b, 0, 64);
+    if (b != seen) {
+      seen = b;
+      bool stop = false;
+      if (lane < n) {
+        const int64_t c = __hip_atomic_load(cmd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (c < 0) stop = true;
+        else __hip_atomic_store(&sh->req[lane], c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (lane == 0)
+        __hip_atomic_fetch_max(&sh->last, (unsigned long long)wall_clock64(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (__ballot(stop)) break;  // stop: every wave leaves
+      continue;
+    }
+    bool idle = false;
+    if (lane == 0) {
+      const unsigned long long last =
+          __hip_atomic_load(&sh->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      idle = wall_clock64() - last > idle_ticks;
+    }
+    if (__shfl((int)idle, 0, 64)) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (lane == 0) __hip_atomic_store(&sh->exit_, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// kWaves: the register budget -- up to 7 handles (8 waves, 2 per SIMD: 256 VGPRs, the
+// float64 RK4 bodies do not spill) or up to 15 (16 waves: 128 VGPRs)
+template <int kWaves>
+__global__ __launch_bounds__(64 * kWaves) void k_resident_multi(
+    const ResMember* __restrict__ table, int n, const int64_t* bell, uint64_t idle_ticks) {
   __shared__ ResShared sh;
   __shared__ double s_nz[kRsMaxHandles][64 * 3];
   // wave-uniform to the compiler too: the member's fields are scalar loads, and the
@@ -1023,33 +1056,43 @@ __global__ __launch_bounds__(64 * kRsMaxHandles) void k_resident_multi(const Res
     sh.exit_ = 0;
     sh.last = wall_clock64();
   }
+  if ((int)threadIdx.x < n) sh.req[threadIdx.x] = table[threadIdx.x].box.next - 1;
   __syncthreads();
+  if (wave == n) {
+    resident_poll(table, n, bell, &sh, idle_ticks);
+    return;
+  }
   const ResMember& m = table[wave];
   const int key = m.system * 2 + m.f64;
   switch (key) {  // wave-uniform: each wave runs its own handle's system
-    case LZ_SYS_LORENZ3 * 2: resident_serve<SysL3<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_LORENZ3 * 2 + 1: resident_serve<SysL3<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_LORENZ4 * 2: resident_serve<SysL4<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_LORENZ4 * 2 + 1: resident_serve<SysL4<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_PMSM * 2: resident_serve<SysPMSM, float>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_HR * 2: resident_serve<SysHR<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_HR * 2 + 1: resident_serve<SysHR<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_T1 * 2: resident_serve<SysT1<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_T1 * 2 + 1: resident_serve<SysT1<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_T2 * 2: resident_serve<SysT2<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_T2 * 2 + 1: resident_serve<SysT2<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_TP * 2: resident_serve<SysTP<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_TP * 2 + 1: resident_serve<SysTP<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_SC * 2: resident_serve<SysSC<float>, float>(m, &sh, s_nz[wave], idle_ticks); break;
-    case LZ_SYS_SC * 2 + 1: resident_serve<SysSC<double>, double>(m, &sh, s_nz[wave], idle_ticks); break;
+    case LZ_SYS_LORENZ3 * 2: resident_serve<SysL3<float>, float>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_LORENZ3 * 2 + 1: resident_serve<SysL3<double>, double>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_LORENZ4 * 2: resident_serve<SysL4<float>, float>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_LORENZ4 * 2 + 1: resident_serve<SysL4<double>, double>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_PMSM * 2: resident_serve<SysPMSM, float>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_HR * 2: resident_serve<SysHR<float>, float>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_HR * 2 + 1: resident_serve<SysHR<double>, double>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_T1 * 2: resident_serve<SysT1<float>, float>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_T1 * 2 + 1: resident_serve<SysT1<double>, double>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_T2 * 2: resident_serve<SysT2<float>, float>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_T2 * 2 + 1: resident_serve<SysT2<double>, double>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_TP * 2: resident_serve<SysTP<float>, float>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_TP * 2 + 1: resident_serve<SysTP<double>, double>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_SC * 2: resident_serve<SysSC<float>, float>(m, wave, &sh, s_nz[wave]); break;
+    case LZ_SYS_SC * 2 + 1: resident_serve<SysSC<double>, double>(m, wave, &sh, s_nz[wave]); break;
     default: break;
   }
 }
 
-int launch_resident_multi(const ResMember* table, int n, uint64_t idle_ticks, void* stream) {
-  if (n < 1 || n > kRsMaxHandles) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_resident_multi, dim3(1), dim3(64 * n), 0, static_cast<hipStream_t>(stream), table,
-                     idle_ticks);
+int launch_resident_multi(const ResMember* table, int n, const int64_t* bell, uint64_t idle_ticks,
+                          void* stream) {
+  if (n < 1 || n > kRsMaxHandles || !bell) return (int)hipErrorInvalidValue;
+  if (n + 1 <= 8)
+    hipLaunchKernelGGL(k_resident_multi<8>, dim3(1), dim3(64 * (n + 1)), 0, static_cast<hipStream_t>(stream),
+                       table, n, bell, idle_ticks);
+  else
+    hipLaunchKernelGGL(k_resident_multi<kRsMaxHandles + 1>, dim3(1), dim3(64 * (n + 1)), 0,
+                       static_cast<hipStream_t>(stream), table, n, bell, idle_ticks);
   return (int)hipGetLastError();
 }
 

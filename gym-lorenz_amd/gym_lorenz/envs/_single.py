@@ -40,6 +40,16 @@ class SingleEnvCore:
         # the host buffers' addresses, looked up once (ndarray.ctypes costs ~0.5 us a call)
         self._p = (self._act_h.ctypes.data, self._noise_h.ctypes.data, self._obs_h.ctypes.data,
                    self._rew_h.ctypes.data, self._done_h.ctypes.data)
+        # state reads (test_evaluate.py:123-125 reads state1 / state2 several times after
+        # every step): one host buffer + address per plane, and the values cached until
+        # the next step / reset / write
+        npdt = {torch.float64: np.float64, torch.float32: np.float32, torch.int32: np.int32}
+        self._pbuf = []
+        for q in range(self.be.info.n_planes):
+            b = np.zeros((1,), npdt[self.be.plane_dtype(q)])
+            self._pbuf.append((b, b.ctypes.data))
+        self._ver = 0
+        self._pcache = {}
 
     def _unpack(self):
         raw = self.be.packed.cpu().numpy()  # one D2H copy: obs | rew | done
@@ -49,6 +59,7 @@ class SingleEnvCore:
         return obs, rew, done
 
     def reset(self, init):
+        self._ver += 1
         init_t = torch.as_tensor(np.asarray(init, dtype=self._np_dtype).reshape(1, -1))
         self.be.reset(init=init_t)
         return self._unpack()[0]
@@ -62,6 +73,7 @@ class SingleEnvCore:
             self._act_h[...] = np.asarray(action, dtype=np.float32).reshape(1, -1)
         nz = None
         p = self._p
+        self._ver += 1
         if noise is not None:
             self._noise_h[...] = np.asarray(noise, dtype=np.float64).reshape(1, 3)
             nz = p[1]
@@ -74,16 +86,23 @@ class SingleEnvCore:
         # lz_resident_read_state: while the resident server serves this env, its copy of
         # the state after the last step (the server keeps running -- test_evaluate.py:
         # 123-125 reads state1 / state2 after every step); otherwise a device copy
-        dt = self.be.plane_dtype(p)
-        out = np.empty((1,), {torch.float64: np.float64, torch.float32: np.float32,
-                              torch.int32: np.int32}[dt])
-        nat.check(nat.lib.lz_resident_read_state(self.be._h, int(p), out.ctypes.data))
-        return out[0]
+        b, addr = self._pbuf[p]
+        st = nat.lib.lz_resident_read_state(self.be._h, p, addr)
+        if st:
+            nat.check(st)
+        return b[0]
 
     def planes(self, first, count):
-        return np.array([self.plane(first + j) for j in range(count)])
+        key = (first, count)
+        hit = self._pcache.get(key)
+        if hit is not None and hit[0] == self._ver:
+            return hit[1].copy()
+        vals = np.array([self.plane(first + j) for j in range(count)])
+        self._pcache[key] = (self._ver, vals)
+        return vals.copy()
 
     def set_planes(self, first, values, dtype=None):
+        self._ver += 1
         values = np.asarray(values).reshape(-1)
         for j, v in enumerate(values):
             self.be.set_state(first + j, torch.tensor([v], dtype=self.be.plane_dtype(first + j)))

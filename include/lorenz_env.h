@@ -245,13 +245,15 @@ lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, 
 
 /* lz_step_host's contract (same arguments, same results bit for bit -- the same step
  * body, tick for tick) served by a RESIDENT kernel: one launch per process and device
- * serves every handle that calls this (one wave per handle, up to 16 handles; a
+ * serves every handle that calls this (one wave per handle, up to 15 handles; a
  * DummyVecEnv of several drop-in envs -- code/train.py:98-100 -- shares the one launch
- * and its one stream), keeps each handle's state in registers and polls the handles'
- * mailboxes in mapped host memory; each call posts its request there and spins until
- * the reply lands in host memory -- no launch, no stream synchronisation per step.  A
+ * and its one stream), keeps each handle's state in registers; each call posts its
+ * request into the handle's mailbox in mapped host memory, rings the server's one
+ * doorbell word (one poller wave watches it and wakes the handle's wave through LDS) and
+ * spins until the reply lands in host memory -- no launch, no stream synchronisation per
+ * step.  A
  * handle joining the server restarts it (its state goes back to the planes and every
- * handle is relaunched); a 17th handle steps through lz_step_host instead.  Handles of
+ * handle is relaunched); a 16th handle steps through lz_step_host instead.  Handles of
  * at most 64 envs without LZ_FLAG_AUTORESET (LZ_ERR_UNSUPPORTED otherwise).  The server
  * exits after LZ_RESIDENT_IDLE_US (default 1000) microseconds without a request to ANY
  * of its handles and is relaunched by the next call (a device-wide synchronize waits

@@ -296,7 +296,7 @@ def test_resident_eight_handles_round_robin(gl):
 def test_resident_member_churn(gl):
     """Handles joining (a restart with every state written back), a plain call on one
     member (stops the server for all), a member closing while others are served, and a
-    17th handle (steps through lz_step_host): all stay bit-identical to their twins."""
+    16th and 17th handle (step through lz_step_host): all stay bit-identical to their twins."""
     import gym_lorenz._native as nat
 
     pairs, bufs = [], []
@@ -332,7 +332,7 @@ def test_resident_member_churn(gl):
     a.close(), b.close()  # a member leaves while the others are served
     pairs[4] = (None, None)
     rounds(20)
-    add(10)  # 17 live handles: the last ones fall back to lz_step_host
+    add(10)  # 17 live handles: the 16th and 17th fall back to lz_step_host
     rounds(20)
     for a, b in pairs:
         if a is not None:
