@@ -1604,15 +1604,45 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
       xs[s] = v;
     }
   };
-  // kLn: the stack the policy sees (st with the deferred zeroing applied) / the stacked
-  // terminal observation of a pending bootstrap
-  auto cur_stack = [&](const float* stv, bool z, float* out) {
+  // kLn: the frame stack lives distributed like the fc1 inputs it feeds -- lane group G
+  // holds entries 4s + G (s < KS) of its env's stack, 1/4 of it.  The policy's input
+  // (the deferred zeroing applied) / the stacked terminal observation of a pending
+  // bootstrap ([older frames, terminal frame]) are then per-lane selects.
+  auto cur_stack = [&](const float* stv, bool z, float* xs) {
 #pragma unroll
-    for (int j = 0; j < SO; ++j) out[j] = (j < SZ && z) ? 0.0f : stv[j];
+    for (int s = 0; s < KS; ++s) xs[s] = (z && 4 * s + G < SZ) ? 0.0f : stv[s];
   };
-  auto term_stack = [&](const float* stv, const float* tf, float* out) {
+  auto frame_at = [&](const float* f, int q) {  // f[q] for a lane-varying q in [0, O)
+    float v = 0.0f;
 #pragma unroll
-    for (int j = 0; j < SO; ++j) out[j] = j < SZ ? stv[j < SZ ? j : 0] : tf[j < SZ ? 0 : j - SZ];
+    for (int j = 0; j < O; ++j) v = q == j ? f[j] : v;
+    return v;
+  };
+  auto term_stack = [&](const float* stv, const float* tf, float* xs) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int q = 4 * s + G;
+      xs[s] = q < SZ ? stv[s] : (q < SO ? frame_at(tf, q - SZ) : 0.0f);
+    }
+  };
+  // VecFrameStack roll (SB3 StackedObservations.update): entry q takes q + O, the new
+  // frame lands in the last O.  Entry q + O lives in lane group (G + O) & 3, slot
+  // s + O / 4 (+1 when G + O % 4 wraps): one lane permute per slot pair.
+  auto roll_stack = [&](float* stv, const float* nf) {
+    const int src = (((G + O) & 3) << 4) | col;
+    const bool carry = G + (O & 3) >= 4;
+    float nst[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      constexpr int D = O / 4;
+      const float va = __shfl(s + D < KS ? stv[s + D < KS ? s + D : 0] : 0.0f, src, 64);
+      const float vb = __shfl(s + D + 1 < KS ? stv[s + D + 1 < KS ? s + D + 1 : 0] : 0.0f, src, 64);
+      const int q = 4 * s + G;
+      const float v = carry ? vb : va;
+      nst[s] = q < SZ ? v : (q < SO ? frame_at(nf, q - SZ) : 0.0f);
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) stv[s] = nst[s];
   };
   for (int64_t rd = 0; rd < rounds; ++rd) {
     const int64_t tile = (rd * gridDim.x + blockIdx.x) * W + wave;
@@ -1625,7 +1655,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
     // pt: the raw terminal obs of a pending bootstrap.  kLn: st is the rolled stack with
     // the zeroing of a done env's older frames deferred (zf) until the bootstrap of the
     // step has read [st[0 .. SZ), pt] (SB3's stacked terminal observation)
-    float o[O], st[kLn ? SO : 1], pt[O];
+    float o[O], st[kLn ? KS : 1], pt[O];
     bool zf = false;
 #pragma unroll
     for (int j = 0; j < O; ++j) o[j] = pt[j] = 0.0f;
@@ -1637,7 +1667,8 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
     }
     if constexpr (kLn) {
 #pragma unroll
-      for (int j = 0; j < SO; ++j) st[j] = valid ? p.stack_in[i * SO + j] : 0.0f;
+      for (int s = 0; s < KS; ++s)
+        st[s] = (valid && 4 * s + G < SO) ? p.stack_in[i * SO + (4 * s + G < SO ? 4 * s + G : 0)] : 0.0f;
     }
     bool pend = false;  // this env's step truncated: its bootstrap value comes next step
     float prew = 0.0f;  // ... and its reward before the bootstrap
@@ -1653,13 +1684,12 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
       if (active) {
         float xs[KS];
         if constexpr (kLn) {
-          float cs[SO];
-          cur_stack(st, zf, cs);
-          if (own) {
+          cur_stack(st, zf, xs);
+          if (valid) {  // every lane group stores its entries of the stacked row
 #pragma unroll
-            for (int j = 0; j < SO; ++j) obs_buf[off * SO + j] = cs[j];
+            for (int s = 0; s < KS; ++s)
+              if (4 * s + G < SO) obs_buf[off * SO + 4 * s + G] = xs[s];
           }
-          inputs(cs, xs);
         } else {
           float x[O];
           normalize<O>(o, x, norm, mu, sd, p.clip);
@@ -1709,9 +1739,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
         if (any_pb) {
           float xt[KS];
           if constexpr (kLn) {
-            float ts[SO];
-            term_stack(st, pt, ts);
-            inputs(ts, xt);
+            term_stack(st, pt, xt);
           } else {
             float x[O];
             normalize<O>(pt, x, norm, mu, sd, p.clip);
@@ -1721,7 +1749,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
         }
         if constexpr (kLn) {  // the deferred zeroing, now that the bootstrap has its input
 #pragma unroll
-          for (int j = 0; j < SZ; ++j) st[j] = zf ? 0.0f : st[j];
+          for (int s = 0; s < KS; ++s) st[s] = (zf && 4 * s + G < SZ) ? 0.0f : st[s];
         }
         float on[O], ot[O];
         bool did_reset;
@@ -1738,10 +1766,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
           // VecFrameStack (SB3 StackedObservations.update): roll by O, the new frame last;
           // a done env's older frames become zeros (deferred: zf) -- its stacked terminal
           // observation is [rolled older frames, terminal frame]
-#pragma unroll
-          for (int j = 0; j < SZ; ++j) st[j] = st[j + O];
-#pragma unroll
-          for (int j = 0; j < O; ++j) st[SZ + j] = on[j];
+          roll_stack(st, on);
           zf = df != 0;
         } else {
           if (p.partials && valid && G < 2) {
@@ -1781,10 +1806,8 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
       const bool any_pb = __ballot(pb) != 0ull;
       f32x4 F[4];
       float xs[KS];
-      float cs[kLn ? SO : 1];
       if constexpr (kLn) {
-        cur_stack(st, zf, cs);
-        inputs(cs, xs);
+        cur_stack(st, zf, xs);
       } else {
         float x[O];
         normalize<O>(o, x, norm, mu, sd, p.clip);
@@ -1796,9 +1819,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
       if (any_pb) {
         float xt[KS];
         if constexpr (kLn) {
-          float ts[SO];
-          term_stack(st, pt, ts);
-          inputs(ts, xt);
+          term_stack(st, pt, xt);
         } else {
           float x[O];
           normalize<O>(pt, x, norm, mu, sd, p.clip);
@@ -1816,9 +1837,12 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
         sys.store(a, i);
         if (any_reset) sys.store_autoreset_extra(a, i);
         if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
-        if constexpr (kLn) {
+      }
+      if constexpr (kLn) {
+        if (valid) {
 #pragma unroll
-          for (int j = 0; j < SO; ++j) p.stack_out[i * SO + j] = cs[j];
+          for (int s = 0; s < KS; ++s)
+            if (4 * s + G < SO) p.stack_out[i * SO + 4 * s + G] = xs[s];
         }
       }
     }
