@@ -491,7 +491,7 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         "roofline": {
             "bound": "mfma", "achieved": achieved, "peak": peak,
             "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-            "kernel": ("_ZN2lz25k_rollout_policy_attn_f32INS_%sLb1ELi4ELi4EEEvNS_5KArgsENS_5PArgsE"
+            "kernel": ("_ZN2lz25k_rollout_policy_attn_f32INS_%sLb1ELi4ELi8EEEvNS_5KArgsENS_5PArgsE"
                        if ln and f32 else
                        "_ZN2lz25k_rollout_policy_attn_f32INS_%sLb0ELi1ELi8EEEvNS_5KArgsENS_5PArgsE"
                        if attn and f32 else

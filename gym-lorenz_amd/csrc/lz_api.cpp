@@ -120,7 +120,9 @@ struct lz_handle {
   bool rs_active;       // ... whose launch may be running
   bool rs_pub_valid;    // the published planes are this launch's (a request was served)
   int rs_use_noise;     // serving injected noise
-  int64_t rs_seq;       // number of the last request posted (= served, after the reply)
+  int64_t rs_seq;       // number of the last request served (after the reply)
+  int64_t rs_posted;    // number of the last request posted (its command-line word)
+  int rs_slot;          // its word in the server's command line (= its wave)
 };
 
 // Stop the resident step server serving the handle (if it runs) and wait for it: every
@@ -520,10 +522,10 @@ lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, 
 }
 
 // ---- resident step server (lz_resident_step; lz_internal.h ResBox / ResMember)
-// mailbox layout (bytes): cmd int64 @0, resp int64 @128 (own cache lines), actions
-// float32 [n, A] @256, noise double [n, 3] @kRsNoise, then obs | reward | done @kRsOut,
+// mailbox layout (bytes): resp int64 @128 (own cache line; the request number goes to the
+// server's command line), actions float32 [n, A] @256, noise double [n, 3] @kRsNoise, then obs | reward | done @kRsOut,
 // then the published state planes (plane p at rs_pub_off + p * kRsPubStride(n))
-constexpr size_t kRsCmd = 0, kRsResp = 128, kRsAct = 256;
+constexpr size_t kRsResp = 128, kRsAct = 256;
 constexpr size_t kRsNoise = kRsAct + 64 * 4 * 4, kRsOut = kRsNoise + 64 * 3 * 8;
 constexpr int kRsMaxEnvs = 64;
 
@@ -556,8 +558,9 @@ struct RsServer {
   hipEvent_t ev;
   lz::ResMember* table_host;  // pinned staging of the member table
   lz::ResMember* table_dev;
-  int64_t* bell;         // the doorbell: mapped, coherent host memory (own cache line)
-  const int64_t* bell_dev;
+  int64_t* cmds;         // the command line: word k = member k's last posted request
+                         // (mapped, coherent host memory, one 128-B line)
+  const int64_t* cmds_dev;
   uint64_t idle;         // idle exit, wall-clock ticks
 };
 static std::mutex g_rs_mu;  // trivially destructible
@@ -571,24 +574,25 @@ static lz_status rs_server_init(RsServer& sv, int device) {
   hipEvent_t ev = nullptr;
   lz::ResMember* th = nullptr;
   lz::ResMember* td = nullptr;
-  int64_t* bell = nullptr;
-  void* bell_dev = nullptr;
+  int64_t* cmds = nullptr;
+  void* cmds_dev = nullptr;
   const size_t tb = sizeof(lz::ResMember) * lz::kRsMaxHandles;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&th), tb) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&td), tb) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&bell), 128, hipHostMallocMapped | hipHostMallocCoherent) !=
+      hipHostMalloc(reinterpret_cast<void**>(&cmds), 128, hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
-      hipHostGetDevicePointer(&bell_dev, bell, 0) != hipSuccess || !bell_dev) {
+      hipHostGetDevicePointer(&cmds_dev, cmds, 0) != hipSuccess || !cmds_dev) {
     if (st) (void)hipStreamDestroy(st);
     if (ev) (void)hipEventDestroy(ev);
     if (th) (void)hipHostFree(th);
     if (td) (void)hipFree(td);
-    if (bell) (void)hipHostFree(bell);
+    if (cmds) (void)hipHostFree(cmds);
     return fail(LZ_ERR_OOM, "resident server setup failed");
   }
-  *bell = 0;
+  static_assert(lz::kRsMaxHandles * sizeof(int64_t) <= 128, "one command line");
+  std::memset(cmds, 0, 128);
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0)
     khz = 100000;
@@ -600,8 +604,8 @@ static lz_status rs_server_init(RsServer& sv, int device) {
   sv.ev = ev;
   sv.table_host = th;
   sv.table_dev = td;
-  sv.bell = bell;
-  sv.bell_dev = static_cast<const int64_t*>(bell_dev);
+  sv.cmds = cmds;
+  sv.cmds_dev = static_cast<const int64_t*>(cmds_dev);
   sv.idle = (uint64_t)(idle_us * khz / 1000.0);
   sv.n = 0;
   sv.active = false;
@@ -626,10 +630,9 @@ static lz_status rs_server_stop(RsServer& sv) {
   if (!sv.active) return LZ_OK;
   // one mailbox's stop command makes every wave leave; the word is restored after
   lz_handle* m0 = sv.members[0];
-  __atomic_store_n(const_cast<int64_t*>(rs_word(m0, kRsCmd)), (int64_t)-1, __ATOMIC_RELEASE);
-  __atomic_fetch_add(sv.bell, 1, __ATOMIC_RELEASE);
+  __atomic_store_n(&sv.cmds[0], (int64_t)-1, __ATOMIC_RELEASE);
   const hipError_t e = hipStreamSynchronize(sv.stream);
-  __atomic_store_n(const_cast<int64_t*>(rs_word(m0, kRsCmd)), m0->rs_seq, __ATOMIC_RELEASE);
+  __atomic_store_n(&sv.cmds[0], m0->rs_posted, __ATOMIC_RELEASE);
   rs_server_ended(sv);
   if (e != hipSuccess) return fail(LZ_ERR_HIP, "resident stop: %s", hipGetErrorString(e));
   return LZ_OK;
@@ -646,9 +649,7 @@ static void resident_unload() {
   for (int d = 0; d < kRsMaxDevices; ++d) {
     RsServer& sv = g_rs[d];
     if (!sv.init || !sv.active || sv.n == 0) continue;
-    __atomic_store_n(const_cast<int64_t*>(rs_word(sv.members[0], kRsCmd)), (int64_t)-1,
-                     __ATOMIC_RELEASE);
-    __atomic_fetch_add(sv.bell, 1, __ATOMIC_RELEASE);
+    __atomic_store_n(&sv.cmds[0], (int64_t)-1, __ATOMIC_RELEASE);
     any = true;
   }
   if (any) usleep(2000);  // a poll period is ~2 us; the waves exit on sight
@@ -664,7 +665,9 @@ static lz_status rs_server_launch(RsServer& sv) {
     r.system = m->cfg.system;
     r.f64 = m->f64;
     lz::ResBox& box = r.box;
-    box.cmd = reinterpret_cast<const int64_t*>(m->rs_dev + kRsCmd);
+    m->rs_slot = i;
+    __atomic_store_n(&sv.cmds[i], m->rs_posted, __ATOMIC_RELEASE);
+    box.cmd = sv.cmds_dev + i;
     box.resp = reinterpret_cast<int64_t*>(m->rs_dev + kRsResp);
     box.act = reinterpret_cast<const float*>(m->rs_dev + kRsAct);
     box.noise = reinterpret_cast<const double*>(m->rs_dev + kRsNoise);
@@ -683,7 +686,7 @@ static lz_status rs_server_launch(RsServer& sv) {
   }
   HIP_TRY(hipMemcpyAsync(sv.table_dev, sv.table_host, sizeof(lz::ResMember) * sv.n,
                          hipMemcpyHostToDevice, sv.stream));
-  const int e = lz::launch_resident_multi(sv.table_dev, sv.n, sv.bell_dev, sv.idle, sv.stream);
+  const int e = lz::launch_resident_multi(sv.table_dev, sv.n, sv.idle, sv.stream);
   if (e != 0) return fail(LZ_ERR_HIP, "resident launch: %s", hipGetErrorString((hipError_t)e));
   sv.active = true;
   for (int i = 0; i < sv.n; ++i) sv.members[i]->rs_active = true;
@@ -707,6 +710,7 @@ static void resident_leave(lz_handle* h) {
   for (int i = 0; i < sv.n; ++i)
     if (sv.members[i] == h) {
       sv.members[i] = sv.members[--sv.n];
+      sv.members[i]->rs_slot = i;  // (the relaunch rewrites the command line)
       break;
     }
   h->rs_member = false;
@@ -745,6 +749,7 @@ lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noi
     h->rs_pin = pin;
     h->rs_dev = static_cast<uint8_t*>(dp);
     h->rs_seq = 0;
+    h->rs_posted = 0;
   }
   std::unique_lock<std::mutex> lk(g_rs_mu);
   RsServer& sv = rs_server(h);
@@ -760,6 +765,7 @@ lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noi
     }
     const lz_status q = rs_server_stop(sv);  // relaunched below with the new member
     if (q != LZ_OK) return q;
+    h->rs_slot = sv.n;
     sv.members[sv.n++] = h;
     h->rs_member = true;
   }
@@ -772,8 +778,9 @@ lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noi
   const int64_t seq = h->rs_seq + 1;
   if (needs_act) std::memcpy(h->rs_pin + kRsAct, actions, (size_t)n * h->desc.action_dim * 4);
   if (noise) std::memcpy(h->rs_pin + kRsNoise, noise, (size_t)n * 3 * 8);
-  __atomic_store_n(const_cast<int64_t*>(rs_word(h, kRsCmd)), seq, __ATOMIC_RELEASE);
-  __atomic_fetch_add(sv.bell, 1, __ATOMIC_RELEASE);  // after the command (x86: ordered)
+  h->rs_posted = seq;
+  // the inputs are in the mailbox before the command word changes (release; x86 TSO)
+  __atomic_store_n(&sv.cmds[h->rs_slot], seq, __ATOMIC_RELEASE);
   if (!sv.active) {
     const lz_status q = rs_server_launch(sv);
     if (q != LZ_OK) return q;

@@ -326,23 +326,23 @@ int launch_step(int system, int f64, const KArgs& a, void* stream);
 // every handle that steps through lz_resident_step -- one wave per handle (n <= 64 envs
 // each, up to kRsMaxHandles handles) plus ONE poller wave, so a DummyVecEnv of several
 // drop-in envs shares one launch on one stream (one hardware queue).  The host posts a
-// request as: inputs into the handle's mailbox (mapped, coherent host memory), *cmd = the
-// request's number (release), then ++*bell, the server's one doorbell word.  The poller
-// alone reads host memory while idle -- the doorbell, one system-scope load per poll;
-// when it moves, every member's *cmd in one wave-wide load -- and hands each new request
-// number to its member wave through LDS; the member waves wait on LDS, not on PCIe (N
-// waves polling host memory slowed every request: 5.3 -> 11.4 us at 8 handles, 24.9 at
-// 16, profiles/r03/resident).  A member wave holds its handle's state in registers,
-// serves request `next`, `next + 1`, ... each exactly as one k_step launch would
-// (step_body), writes obs | reward | done and the handle's state planes (pub: the copy
-// lz_resident_read_state returns without stopping the server) into the mailbox and then
-// *resp = the request's number (release, system scope).  All waves leave together: on
-// cmd == -1 in any mailbox, or after idle_ticks wall-clock ticks without a doorbell; each
-// member stores its state back to the planes.  The host relaunches the server (with every
-// registered handle) when a request finds it gone.
+// request as: inputs into the handle's mailbox (mapped, coherent host memory), then the
+// request's number into the handle's word of the server's command line (release).  The
+// poller alone reads host memory while idle -- the whole command line in one wave-wide
+// load per poll -- and hands each new request number to its member wave through LDS;
+// the member waves wait on LDS, not on PCIe (N waves polling host memory slowed every
+// request: 5.3 -> 11.4 us at 8 handles, 24.9 at 16, profiles/r03/resident).  A member
+// wave holds its handle's state in registers, serves request `next`, `next + 1`, ... each
+// exactly as one k_step launch would (step_body), writes obs | reward | done and the
+// handle's state planes (pub: the copy lz_resident_read_state returns without stopping
+// the server) into the mailbox and then *resp = the request's number (release, system
+// scope).  All waves leave together: on -1 in any command word, or after idle_ticks
+// wall-clock ticks without a new request; each member stores its state back to the
+// planes.  The host relaunches the server (with every registered handle) when a request
+// finds it gone.
 constexpr int kRsMaxHandles = 15;  // + the poller: 16 waves, one 1024-thread workgroup
 struct ResBox {
-  const int64_t* cmd;   // host -> device: request number, -1 = stop
+  const int64_t* cmd;   // host -> device: request number, -1 = stop (the server's command line)
   int64_t* resp;        // device -> host: number of the last request served
   const float* act;     // [n, A]
   const double* noise;  // [n, 3] (with use_noise)
@@ -359,10 +359,8 @@ struct ResMember {      // one wave of the server
   ResBox box;
   int32_t system, f64;
 };
-// table: device copy of n members; bell: the doorbell (device address of mapped host
-// memory); one workgroup of 64 (n + 1) threads, wave n the poller
-int launch_resident_multi(const ResMember* table, int n, const int64_t* bell, uint64_t idle_ticks,
-                          void* stream);
+// table: device copy of n members; one workgroup of 64 (n + 1) threads, wave n the poller
+int launch_resident_multi(const ResMember* table, int n, uint64_t idle_ticks, void* stream);
 int launch_rollout(int system, int f64, const KArgs& a, void* stream);
 // gather (scatter = false: buf[i] = plane[idx[i]]) / scatter (plane[idx[i]] = buf[i]) of
 // es-byte elements; indices outside [0, n) skipped / read as zero

@@ -2091,16 +2091,19 @@ int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, const PolS
   return (int)hipErrorInvalidValue;
 }
 
-// waves of 16 envs, one workgroup per CU (the LDS holds one): 8 (two per SIMD) for
-// code/train.py's extractor, 4 (one per SIMD, 512 registers) for the LayerNorm variant,
-// whose stacked input and LayerNorm spill at 256 registers; LZ_ATTN_F32_WAVES=4|8 forces
+// waves of 16 envs, one workgroup per CU (the LDS holds one): 8 (two per SIMD, 256
+// registers) for both extractors -- the LayerNorm variant ran 4 (one per SIMD, 512
+// registers) until its frame stack was distributed over the lane groups; then 8 waves
+// measured 5.96e8 vs 4.50e8 env-steps/s at HR 32,768 x 2048 (profiles/r03/attn_f32) with
+// 20 spilled VGPRs; LZ_ATTN_F32_WAVES=4|8 forces
 PolShape attn_f32_policy_shape(int64_t n, int num_cus, int ln) {
   static const int forced = [] {
     const char* e = std::getenv("LZ_ATTN_F32_WAVES");
     const int w = e ? std::atoi(e) : 0;
     return w == 4 || w == 8 ? w : 0;
   }();
-  PolShape s = {16, forced ? forced : (ln ? 4 : 8), 0, 0};
+  (void)ln;
+  PolShape s = {16, forced ? forced : 8, 0, 0};
   const int64_t groups = ((n + 15) / 16 + s.waves - 1) / s.waves;
   s.grid = (int)(groups < num_cus ? groups : num_cus);
   return s;
