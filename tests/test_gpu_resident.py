@@ -178,6 +178,34 @@ def test_resident_does_not_block_torch(gl):
     env.close()
 
 
+def test_eight_live_handles_do_not_block_torch(gl):
+    """With the server resident for 8 handles (one launch, 9 waves polling LDS / one the
+    command line), torch kernels on torch's stream run without waiting for it."""
+    x = torch.ones(1024, device="cuda")
+    for _ in range(3):
+        x = x + 1
+    torch.cuda.synchronize()
+    envs = []
+    for _ in range(8):
+        e = gl.LorenzDynamicEnv()
+        e.reset()
+        e.step(np.zeros(3, np.float32))
+        envs.append(e)
+    s = torch.cuda.current_stream()
+    worst = 0.0
+    for _ in range(20):
+        for e in envs:
+            e.step(np.zeros(3, np.float32))  # the server stays resident
+        t0 = time.perf_counter()
+        x = x + 1
+        s.synchronize()
+        worst = max(worst, time.perf_counter() - t0)
+    assert worst < 0.002, worst  # not serialised behind the server (its idle exit is 1 ms)
+    assert float(x[0]) == 24.0
+    for e in envs:
+        e.close()
+
+
 def test_dropin_resident_matches_step_host(gl, monkeypatch):
     """The drop-in class with LZ_RESIDENT=0 (lz_step_host) and the default (resident)."""
     outs = []

@@ -1,9 +1,10 @@
 """Host code under AddressSanitizer + UndefinedBehaviorSanitizer, no GPU:
 
   * the CPU oracle (oracle/lz_oracle.c): every function on exact-size heap buffers;
-  * the library's host-side C-ABI (lz_api.cpp, the policy packer, argument checks and
-    error paths of lz_rms / lz_gae / lz_frame_stack), built with
-    `hipcc -Xarch_host -fsanitize=...` (device code unsanitized, never launched here).
+  * the library's host-side C-ABI (lz_api.cpp, the policy packers in lz_pack.cpp,
+    argument checks and error paths of lz_rms / lz_frame_stack), built with
+    `hipcc -Xarch_host -fsanitize=...` (device code unsanitized, never launched here;
+    the kernel-only translation units are linked from the library build).
 """
 import os
 import shutil
@@ -38,13 +39,16 @@ def test_host_abi_under_asan_ubsan(tmp_path):
               "-fPIC", "-I", INC, "-I", CSRC]
     san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
            "-Xarch_host", "-fno-sanitize-recover=all"]
-    kern = os.path.join(ROOT, "gym-lorenz_amd", "build", "lz_kernels.o")
-    if not os.path.exists(kern):  # kernels + launchers: built unsanitized (device code)
-        kern = str(tmp_path / "k.o")
-        subprocess.check_call(common + ["-O3", "-c", os.path.join(CSRC, "lz_kernels.hip"),
-                                        "-o", kern])
-    objs = [kern]
-    for f in ("lz_rms.hip", "lz_policy.hip", "lz_wrappers.hip", "lz_api.cpp"):
+    # the kernel translation units (device code, never launched here) come unsanitized
+    # from the library build; every file with host-side C-ABI logic is rebuilt sanitized
+    objs = []
+    for f in ("lz_kernels", "lz_policy"):
+        o = os.path.join(ROOT, "gym-lorenz_amd", "build", f + ".o")
+        if not os.path.exists(o):
+            o = str(tmp_path / (f + ".o"))
+            subprocess.check_call(common + ["-O3", "-c", os.path.join(CSRC, f + ".hip"), "-o", o])
+        objs.append(o)
+    for f in ("lz_rms.hip", "lz_wrappers.hip", "lz_pack.cpp", "lz_api.cpp"):
         o = str(tmp_path / (f + ".o"))
         lang = ["-x", "hip"] if f.endswith(".cpp") else []
         subprocess.check_call(common + san + lang + ["-c", os.path.join(CSRC, f), "-o", o])

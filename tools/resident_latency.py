@@ -4,7 +4,8 @@ class overhead): microseconds per lz_resident_step for
   * N handles registered, only handle 0 stepped (the others' waves poll idle);
   * N handles stepped in runs of 8 calls each;
 next to lz_step_host.  Separates the cost of idle polling waves from the cost of
-switching between handles."""
+switching between handles.  At 8 handles also: a small torch kernel + synchronize on
+torch's stream with and without the server resident."""
 import json
 import os
 import sys
@@ -41,6 +42,34 @@ def run(fn, hs, order, reps):
     return (time.perf_counter() - t0) / (reps * len(order)) * 1e6
 
 
+def torch_latency(hs):
+    """Median microseconds of one small torch kernel + stream synchronize on torch's own
+    stream: with no server, then while the server polls for the live handles."""
+    import torch
+
+    x = torch.ones(1024, device="cuda")
+    s = torch.cuda.current_stream()
+
+    def med(live):
+        ts = []
+        for _ in range(300):
+            if live:
+                nat.lib.lz_resident_step(*hs[0][1])  # keeps the server resident
+            t0 = time.perf_counter()
+            x.add_(1.0)
+            s.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e6
+
+    for be, _, _ in hs:
+        nat.check(nat.lib.lz_resident_stop(be._h))
+    idle = med(False)
+    for be, args, _ in hs:
+        nat.lib.lz_resident_step(*args)
+    return {"torch kernel + sync, no server": idle,
+            "torch kernel + sync, server live for %d handles" % len(hs): med(True)}
+
+
 def main():
     res = {}
     for n in (1, 2, 4, 8, 16):
@@ -52,6 +81,8 @@ def main():
             if fn == "lz_resident_step":
                 row[fn + " handle 0 only"] = run(fn, hs, [0] * 64, 100)
                 row[fn + " runs of 8"] = run(fn, hs, [i for i in range(n) for _ in range(8)], 50)
+        if n == 8:
+            row.update(torch_latency(hs))
         res["%d handles" % n] = row
         for be, _, _ in hs:
             be.close()
