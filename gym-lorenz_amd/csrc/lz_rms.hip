@@ -483,18 +483,18 @@ __global__ __launch_bounds__(256) void k_vn_tile_update(const double* tiles, int
   const double* cs = tiles + (int64_t)d * ntiles;
   const double* cq = tiles + (int64_t)(O + d) * ntiles;
   double a = 0.0, b = 0.0;
-  // the same in-order sums, with 8 rows of loads issued before their adds (the plain
+  // the same in-order sums, with 16 rows of loads issued before their adds (the plain
   // loop left one load in flight per add: 12 us at 8,192 tiles)
   int64_t r = t;
-  for (; r + 7 * 256 < ntiles; r += 8 * 256) {
-    double va[8], vb[8];
+  for (; r + 15 * 256 < ntiles; r += 16 * 256) {
+    double va[16], vb[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       va[u] = cs[r + u * 256];
       vb[u] = cq[r + u * 256];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       a += va[u];
       b += vb[u];
     }
