@@ -808,18 +808,18 @@ static inline bool rollout_split(const KArgs& a) {
   return std::is_same<Sys, SysL3<float>>::value && a.n >= 32768;
 }
 
-template <class Sys, typename T, int D>
+template <class Sys, typename T, int D, int DS = D>  // DS: the split-lane kernel's distance
 static void launch_rollout_d(const KArgs& a, hipStream_t s) {
   if (a.n < 2 * 256 * kBlock) {  // < 2 full workgroups per CU: one-wave groups
     if (rollout_split<Sys>(a)) {
       const dim3 g((unsigned)((a.n + 31) / 32));
       if constexpr (never_terminates<Sys>::value && !Sys::kNoise) {
         if (no_done<Sys>(a) && !(a.variant & 2048)) {  // variant bit 2048: keep the done path (A/B)
-          hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, D, true>), g, dim3(64), 0, s, a);
+          hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true>), g, dim3(64), 0, s, a);
           return;
         }
       }
-      hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, D>), g, dim3(64), 0, s, a);
+      hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS>), g, dim3(64), 0, s, a);
     } else {
       hipLaunchKernelGGL((k_rollout<Sys, T, 64, D>), dim3((unsigned)((a.n + 63) / 64)), dim3(64),
                          0, s, a);
@@ -861,6 +861,9 @@ static int launch_all(int which, const KArgs& a, hipStream_t s) {
     }
   } else if constexpr (kVariants) {
     if (a.variant & 1024) launch_rollout_d<Sys, T, 3>(a, s);  // A/B: prefetch distance 3
+    // A/B: split-lane distance 15 (vmcnt allows 59 ops in flight): no change at 32,768 -
+    // 131,071 envs (profiles/r03/rollout/ab_split_dma_distance_15_rejected.json)
+    else if (a.variant & 4096) launch_rollout_d<Sys, T, kDmaDist, 15>(a, s);
     else launch_rollout_d<Sys, T, kDmaDist>(a, s);
   } else {
     launch_rollout_d<Sys, T, kDmaDist>(a, s);

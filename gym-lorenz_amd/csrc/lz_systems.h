@@ -21,6 +21,17 @@ template <typename T>
 __device__ __forceinline__ T clip(T x, T lo, T hi) {
   return x < lo ? lo : (x > hi ? hi : x);
 }
+// np.clip with NONZERO bounds: float32 through IEEE 754-2019 maximum / minimum
+// (v_maximum3_f32 / v_minimum3_f32 on gfx950, NaN-propagating): the value clip() gives
+// (bounds away from 0, so no signed-zero case) except a NaN's payload, in 2 instructions
+// instead of 2 compares + 2 selects; float64 keeps clip() (no native f64 maximum).
+template <typename T>
+__device__ __forceinline__ T clip_nz(T x, T lo, T hi) {
+  if constexpr (std::is_same<T, float>::value)
+    return __builtin_elementwise_minimum(__builtin_elementwise_maximum(x, lo), hi);
+  else
+    return clip(x, lo, hi);
+}
 
 template <typename T>
 __device__ __forceinline__ T ld(const void* p, int64_t i) {
@@ -113,8 +124,8 @@ struct SysL3 {
   // step(): dynamic.py:61-90
   // act: float32 (SB3 hands np.float32 actions; np.clip keeps f32, then promotes)
   __device__ bool step(const float* act, bool, const double*, T* o, T& rew, const KArgs&) {
-    const T u1 = clip((T)act[0], -cl, cl), u2 = clip((T)act[1], -cl, cl),
-            u3 = clip((T)act[2], -cl, cl);
+    const T u1 = clip_nz((T)act[0], -cl, cl), u2 = clip_nz((T)act[1], -cl, cl),
+            u3 = clip_nz((T)act[2], -cl, cl);
     T fx, fy, fz;
     rhs(fx, fy, fz);                 // :70-72, all from the old state
     x = (x + fx * dt) + u1;          // :73
@@ -304,8 +315,8 @@ struct SysPMSM {
   // step(): :76-184
   __device__ bool step(const float* act, bool use_nz, const double* nz, float* o, float& rew,
                        const KArgs& a) {
-    const float a1 = clip(act[0], -1.0f, 1.0f) * fmax;     // :81-82
-    const float a2 = clip(act[1], -1.0f, 1.0f) * fmax;
+    const float a1 = clip_nz(act[0], -1.0f, 1.0f) * fmax;  // :81-82
+    const float a2 = clip_nz(act[1], -1.0f, 1.0f) * fmax;
     float d1[3], d2[3];
     rhs(s1, 0.0f, 0.0f, false, nullptr, d1);                      // :88
     rhs(s2, a1, a2, use_nz, nz, d2);                               // :89-90
@@ -497,8 +508,8 @@ struct SysHR {
   __device__ void reset_obs(T* o) const {  // :71-78 (error clipped in reset only)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      o[j] = clip((m[j] - s[j]) / sc, (T)-1, (T)1);
-      o[3 + j] = clip(m[j] / ms, (T)-1, (T)1);
+      o[j] = clip_nz((m[j] - s[j]) / sc, (T)-1, (T)1);
+      o[3 + j] = clip_nz(m[j] / ms, (T)-1, (T)1);
     }
   }
   __device__ void noise_from_normals(const float* z, double* nz) const {  // :136 N(0, sigma)
@@ -514,8 +525,8 @@ struct SysHR {
       fa1 = f1m * fa1 + falpha * f1;
       f0 = fa0; f1 = fa1;
     }
-    const float a1 = clip(f0, -1.0f, 1.0f) * 100.0f;       // :92-93 np.float32 * 100.0
-    const float a2 = clip(f1, -1.0f, 1.0f) * 100.0f;
+    const float a1 = clip_nz(f0, -1.0f, 1.0f) * 100.0f;    // :92-93 np.float32 * 100.0
+    const float a2 = clip_nz(f1, -1.0f, 1.0f) * 100.0f;
     if constexpr (std::is_same<T, float>::value && LZ_HR_PACKED) {
       rk4_pair(m, s, a1, a2);                              // both systems, packed f32
     } else {
@@ -550,7 +561,7 @@ struct SysHR {
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {                          // :150-156
-      o[3 + j] = clip(o[3 + j], (T)-1, (T)1);
+      o[3 + j] = clip_nz(o[3 + j], (T)-1, (T)1);
       te = te || (fabs(e[j]) > tterm);                     // :174
     }
     const float q = act[0] * act[0] + act[1] * act[1];     // np.square + np.sum (f32)
@@ -611,7 +622,7 @@ struct SysT1 {
   }
   __device__ void noise_from_normals(const float*, double* nz) const { nz[0] = nz[1] = nz[2] = 0.0; }
   __device__ bool step(const float* act, bool, const double*, T* o, T& rew, const KArgs&) {
-    const float u1 = clip(act[0], -cl, cl), u2 = clip(act[1], -cl, cl);  // :71-72
+    const float u1 = clip_nz(act[0], -cl, cl), u2 = clip_nz(act[1], -cl, cl);  // :71-72
     T f[3];
     pmsm3_rhs(v[0], v[1], v[2], pa, pb, f);                              // :78-80
     v[0] = (v[0] + f[0] * dt) + (T)u1;                                   // :84
@@ -676,9 +687,9 @@ struct SysT2 {
   }
   __device__ void noise_from_normals(const float*, double* nz) const { nz[0] = nz[1] = nz[2] = 0.0; }
   __device__ bool step(const float* act, bool, const double*, T* o, T& rew, const KArgs&) {
-    const float g1 = clip(act[0], -cl, cl) * gain;   // :182-184, :210-213 u*100 in f32
-    const float g2 = clip(act[1], -cl, cl) * gain;
-    const float g3 = clip(act[2], -cl, cl) * gain;
+    const float g1 = clip_nz(act[0], -cl, cl) * gain;   // :182-184, :210-213 u*100 in f32
+    const float g2 = clip_nz(act[1], -cl, cl) * gain;
+    const float g3 = clip_nz(act[2], -cl, cl) * gain;
     T f[4];
     rhs(m, f);                                       // :189-192
 #pragma unroll
@@ -747,8 +758,8 @@ struct SysTP {
   }
   __device__ bool step(const float* act, bool use_nz, const double* nz, T* o, T& rew,
                        const KArgs&) {
-    const float g1 = clip(act[0], -cl, cl) * gain;   // :78-79, :91-92 u*20 in f32
-    const float g2 = clip(act[1], -cl, cl) * gain;
+    const float g1 = clip_nz(act[0], -cl, cl) * gain;   // :78-79, :91-92 u*20 in f32
+    const float g2 = clip_nz(act[1], -cl, cl) * gain;
     T f[3];
     pmsm3_rhs(m[0], m[1], m[2], pa, pb, f);          // :87-89
 #pragma unroll
