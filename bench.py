@@ -61,9 +61,6 @@ def parse():
     p.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                    help="--mode policy --policy mlp: fp32 = SB3's float32 forward "
                         "(lz_rollout_policy_f32), bf16 = the bf16-MFMA kernel")
-    p.add_argument("--vn-launch", choices=["one", "two"], default="one",
-                   help="--mode vecnorm: lz_step_vecnorm_fused (one launch per step, where the "
-                        "grid can be resident at once) or lz_step_vecnorm + lz_vecnorm_apply")
     p.add_argument("--vecnorm-update", choices=["step", "rollout"], default="step",
                    help="--mode policy --policy mlp fp32: step = SB3's VecNormalize order (obs_rms "
                         "updated by every step's batch before it is normalised; one launch per "
@@ -272,21 +269,9 @@ def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
     h = env._h
     env.reset()
     nd = didx.data_ptr() + 4 * n
-    # one launch per step (lz_step_vecnorm_fused) where the grid can be resident at once,
-    # else (or --vn-launch two) the two-call form
-    single = [args.vn_launch == "one"]
 
     def one(k):
         r = k % R
-        if single[0]:
-            st = nat.lib.lz_step_vecnorm_fused(
-                h, vn, acts[r].data_ptr(), raw_o[r].data_ptr(), raw_r[r].data_ptr(),
-                done[r].data_ptr(), didx.data_ptr(), tobs.data_ptr(), nd, obs_n[r].data_ptr(),
-                rew_n[r].data_ptr(), dones[r].data_ptr(), tn.data_ptr())
-            if st != nat.LZ_ERR_UNSUPPORTED:
-                nat.check(st)
-                return
-            single[0] = False
         nat.check(nat.lib.lz_step_vecnorm(h, vn, acts[r].data_ptr(), raw_o[r].data_ptr(),
                                           raw_r[r].data_ptr(), done[r].data_ptr(), didx.data_ptr(),
                                           tobs.data_ptr(), nd))
@@ -324,23 +309,15 @@ def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
     step_s = ev0.elapsed_time(ev1) / 1e3 / steps
     info = env.info
     es = 4
-    # lz_step's bytes + the float64 returns (read + written) + the normalised obs /
-    # reward / bool dones written; the two-call form also re-reads the raw obs / reward /
-    # done it wrote (not algorithmically needed: counted only for it)
-    bytes_step = info.bytes_per_env_step + 16 + (1 if single[0] else 2) * (O * es + es + 1)
+    bytes_step = info.bytes_per_env_step + 16 + 2 * (O * es + es + 1)
     achieved = bytes_step * n / step_s / 1e9
     obs_rms.close()
     ret_rms.close()
-    # PMC bytes of the kernel(s) (tools/pmc_r03.sh summaries), when committed for this
-    # system, size and kernel build
-    if args.system != "pmsm":
-        tr = [None]
-    elif single[0]:
-        tr = [load_traffic("_ZN2lz10k_step_vn1INS_7SysPMSMEfEEvNS_5KArgsENS_5VArgsE", n)]
-    else:
-        tr = [load_traffic(k, n) for k in (
-            "_ZN2lz9k_step_vnINS_7SysPMSMEfLi24EEEvNS_5KArgsENS_5VArgsE",
-            "_ZN12_GLOBAL__N_110k_vn_applyIfLi6ELb1EEEvNS_11VnApplyArgsE")]
+    # PMC bytes of the two kernels (tools/pmc_vecnorm.sh summaries), when committed for
+    # this system and size
+    tr = [load_traffic(k, n) for k in (
+        "_ZN2lz9k_step_vnINS_7SysPMSMEfLi24EEEvNS_5KArgsENS_5VArgsE",
+        "_ZN12_GLOBAL__N_110k_vn_applyIfLi6ELb1EEEvNS_11VnApplyArgsE")] if args.system == "pmsm" else [None]
     traffic = sum(t["bytes_per_launch"] for t in tr) if all(tr) else None
     return {
         "metric": METRIC, "value": total * steps / elapsed, "unit": "env-steps/s",
@@ -355,10 +332,8 @@ def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
                 "pre-generated on device" % (arange, arange),
         "config": {
             "workload": "VecNormalize(norm_obs, norm_reward, clip_obs=10) over %s, fused step "
-                        "(%s, no host sync), %d envs"
-                        % (SYSTEM_INFO[args.system][0],
-                           "lz_step_vecnorm_fused: 1 kernel" if single[0] else
-                           "lz_step_vecnorm + lz_vecnorm_apply: 2 kernels", n),
+                        "(lz_step_vecnorm + lz_vecnorm_apply: 2 kernels, no host sync), %d envs"
+                        % (SYSTEM_INFO[args.system][0], n),
             "system": args.system, "envs_total": total, "envs_per_gpu": n, "mode": "vecnorm",
             "parallelism": "env shard x%d (per-rank statistics)" % world,
             "launch": "hipGraph of %d steps" % L},
@@ -366,13 +341,11 @@ def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "traffic_source": [t["source"] for t in tr] if traffic else None,
-            "kernel": ("k_step_vn1 (step + statistics + normalised outputs, one launch)"
-                       if single[0] else "k_step_vn + k_vn_apply (one fused VecNormalize step)"),
+            "kernel": "k_step_vn + k_vn_apply (one fused VecNormalize step)",
             "avg_launch_us": step_s * 1e6, "bytes_per_env_step": bytes_step,
             "note": "achieved = algorithmic bytes of the whole fused step (lz_step's + 16 B of "
-                    "float64 returns + normalised obs/reward/dones written; the two-kernel form "
-                    "also counts its re-read of the raw obs/reward/done) / HIP-event time per "
-                    "step"},
+                    "float64 returns + the normalise pass: raw obs/reward/done read, normalised "
+                    "obs/reward/dones written) / HIP-event time per step"},
     }
 
 
@@ -752,7 +725,6 @@ def main():
         start = rank * n
     kw = {"add_noise": True, "alpha": 0.5} if args.system == "pmsm" else {}
     env = gl.BatchedEnv(args.system, n, dtype="float32", seed=0, global_env_offset=start,
-                        variant=int(os.environ.get("LZ_BENCH_VARIANT", "0")),  # A/B tools only
                         autoreset=True, device=local, max_episode_steps=args.max_episode_steps,
                         **kw)
     if args.mode == "policy":

@@ -104,7 +104,6 @@ struct lz_handle {
   float* ps_term;
   int32_t* ps_cursor;
   uint8_t* vn_ws;      // lz_step_vecnorm moment partials (lazily allocated)
-  int32_t* vn_bar;     // lz_step_vecnorm_fused block counters [2] (in / out, self-resetting)
   int vn_pending;      // lz_step_vecnorm left totals for lz_vecnorm_apply's updates
   int32_t* vn_nd_out;  // lz_step_vecnorm's n_done_out, published by lz_vecnorm_apply
   int32_t* vn_counter; // ... from this done cursor (the step's)
@@ -329,7 +328,6 @@ lz_status lz_destroy(lz_handle* h) {
   if (h->ps_term) (void)hipFree(h->ps_term);
   if (h->ps_cursor) (void)hipFree(h->ps_cursor);
   if (h->vn_ws) (void)hipFree(h->vn_ws);
-  if (h->vn_bar) (void)hipFree(h->vn_bar);
   if (h->hs_pin) (void)hipHostFree(h->hs_pin);  // hs_dev is its mapped device address
   delete h;
   return LZ_OK;
@@ -967,81 +965,6 @@ lz_status lz_vecnorm_apply(lz_handle* h, const lz_vecnorm* vn, const void* obs_r
       vn->clip_obs, vn->clip_reward, obs_norm, rew_norm, dones_out, term ? term_norm : nullptr,
       upd, counter, nd_out, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "normalise launch: %s", hipGetErrorString((hipError_t)e));
-  return LZ_OK;
-}
-
-lz_status lz_step_vecnorm_fused(lz_handle* h, const lz_vecnorm* vn, const void* actions, void* obs_out,
-                                void* rew_out, uint8_t* done_out, int32_t* done_idx_out,
-                                void* terminal_obs_out, int32_t* n_done_out, float* obs_norm,
-                                float* rew_norm, uint8_t* dones_out, float* term_norm) {
-  if (!h) return fail(LZ_ERR_INVALID, "handle is NULL");
-  RESIDENT_QUIESCE(h);
-  if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_step_vecnorm_fused before the first lz_reset");
-  const lz_status c = check_vecnorm(h, vn);
-  if (c != LZ_OK) return c;
-  const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4 && h->cfg.system != LZ_SYS_SC;
-  if ((needs_act && !actions) || !obs_out || !rew_out || !done_out || !done_idx_out ||
-      !terminal_obs_out || !n_done_out || !obs_norm || !rew_norm || !dones_out || !term_norm)
-    return fail(LZ_ERR_INVALID, "every buffer of lz_step_vecnorm_fused must be non-NULL");
-  const int64_t n = h->cfg.num_envs;
-  const int64_t n_wg = (n + 1023) / 1024;
-  if (vn->flags & LZ_VN_DEFER)
-    return fail(LZ_ERR_UNSUPPORTED, "lz_step_vecnorm_fused: LZ_VN_DEFER needs the two-call form "
-                                    "(the moments are all-reduced between the calls)");
-  if (n_wg > h->num_cus || n_wg > lz::vn_fuse_max_wg())
-    return fail(LZ_ERR_UNSUPPORTED, "lz_step_vecnorm_fused: %lld envs need %lld workgroups, more "
-                "than can be resident at once (%d)", (long long)n, (long long)n_wg, h->num_cus);
-  HIP_TRY(hipSetDevice(h->cfg.device));
-  if (!h->vn_ws) {
-    const int64_t max_wg = (n + lz::kBlock - 1) / lz::kBlock;
-    const size_t bytes = (size_t)(max_wg + 3) * 2 * (lz::kVnMaxObs + 1) * sizeof(double);
-    if (hipMalloc(reinterpret_cast<void**>(&h->vn_ws), bytes) != hipSuccess)
-      return fail(LZ_ERR_OOM, "vecnorm workspace (%zu B)", bytes);
-  }
-  if (!h->vn_bar) {
-    int32_t* b = nullptr;
-    if (hipMalloc(reinterpret_cast<void**>(&b), 2 * sizeof(int32_t)) != hipSuccess)
-      return fail(LZ_ERR_OOM, "vecnorm arrival counters");
-    if (hipMemsetAsync(b, 0, 2 * sizeof(int32_t), h->stream) != hipSuccess) {
-      (void)hipFree(b);
-      return fail(LZ_ERR_HIP, "vecnorm arrival counters: memset");
-    }
-    h->vn_bar = b;
-  }
-  KArgs a;
-  fill_common(h, a);
-  a.act = actions;
-  a.obs = obs_out;
-  a.rew = rew_out;
-  a.done = done_out;
-  a.done_idx32 = done_idx_out;
-  a.term_obs = terminal_obs_out;
-  a.vec_ok = (!needs_act || aligned16(actions)) && aligned16(obs_out) && aligned16(obs_norm);
-  lz::VArgs v;
-  std::memset(&v, 0, sizeof v);
-  v.returns = vn->returns;
-  v.part = reinterpret_cast<double*>(h->vn_ws);
-  v.fused = 1;
-  v.n_done_out = n_done_out;
-  v.obs_state = lz::rms_state(vn->obs_rms);
-  v.ret_state = lz::rms_state(vn->ret_rms);
-  v.gamma = vn->gamma;
-  v.flags = vn->flags;
-  v.n_wg = (int32_t)n_wg;
-  v.obs_n = obs_norm;
-  v.rew_n = rew_norm;
-  v.dones01 = dones_out;
-  v.term_n = term_norm;
-  v.bar = h->vn_bar;
-  v.eps = vn->epsilon;
-  v.clip_obs = vn->clip_obs;
-  v.clip_rew = vn->clip_reward;
-  const int e = lz::launch_step_vecnorm1(h->cfg.system, h->f64, a, v, h->stream);
-  if (e != 0) return fail(LZ_ERR_HIP, "step launch: %s", hipGetErrorString((hipError_t)e));
-  h->parity ^= 1;
-  ++h->gen;
-  h->vn_pending = 0;
-  h->vn_nd_out = nullptr;
   return LZ_OK;
 }
 

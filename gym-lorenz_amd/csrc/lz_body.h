@@ -66,8 +66,7 @@ template <class Sys, typename T, bool kRollout, bool kKeepTerm = false, bool kNo
 __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KArgs& a, int64_t i,
                                              bool live, const float* act, uint64_t tick, int k,
                                              T* o, T& rew, bool& did_reset,
-                                             T* o_term = nullptr, bool lead = true,
-                                             int32_t* pos_out = nullptr) {
+                                             T* o_term = nullptr, bool lead = true) {
   uint8_t dflag = 0;
   did_reset = false;
   if constexpr (kNoDone) {
@@ -100,7 +99,6 @@ __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KAr
   // compact list of done envs: ballot + one atomic per wave (all lanes reach this)
   if (a.term_obs) {
     const int32_t pos = wave_compact(dflag != 0 && lead, a.counter);
-    if (pos_out) *pos_out = pos;
     if (pos >= 0) {
       if constexpr (kRollout) {
         if (pos < a.term_cap) {

@@ -80,17 +80,7 @@ struct VArgs {
   uint32_t flags;      // LZ_VN_*
   int32_t n_wg;
   int32_t fused;       // the normalise pass reduces the partials itself (n_wg small)
-  // single-launch mode (lz_step_vecnorm_fused, k_step_vn1): the normalise pass runs in
-  // the step kernel after a grid-wide arrival count (n_wg <= the CUs: co-resident)
-  float* obs_n;        // [N, O] normalised obs
-  float* rew_n;        // [N] normalised reward
-  uint8_t* dones01;    // [N] SB3 bool dones
-  float* term_n;       // [n_done, O] normalised terminal rows
-  int32_t* bar;        // [2] blocks in / out (self-resetting: the last block out zeroes both)
-  double eps, clip_obs, clip_rew;
 };
-// lz_step_vecnorm_fused: one launch of k_step_vn1 (see lz_kernels.hip)
-int launch_step_vecnorm1(int system, int f64, const KArgs& a, const VArgs& v, void* stream);
 
 // Policy-in-the-loop rollout (lz_policy.hip): SB3 ActorCriticPolicy (MlpPolicy,
 // net_arch pi=[128,128] vf=[128,128], Tanh, DiagGaussian) packed as bf16 MFMA

@@ -123,18 +123,9 @@ constexpr int step_block() {  // bits 3-4 of V: workgroup size
 // order (no cross-workgroup synchronisation inside the step: an in-kernel last-arriver
 // reduction needs every workgroup to wait for its stores' acknowledgements before
 // taking a ticket, which measured 4x the step time at 1M envs).
-template <int O, int SB, typename T, bool kCoh = false>
+template <int O, int SB, typename T>
 __device__ __forceinline__ void vn_epilogue(const T* s_obs, const double* s_ret, int nb, int tid,
                                             const VArgs& v) {
-  // kCoh (single launch): device-scope stores, read by the other workgroups in-kernel
-  auto bar = [] __device__() {  // kCoh: LDS-only (the raw-output stores stay in flight)
-    if constexpr (kCoh) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else __syncthreads();
-  };
-  auto put = [&](int64_t at, double t) __attribute__((always_inline)) {
-    if constexpr (kCoh) __hip_atomic_store(v.part + at, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else v.part[at] = t;
-  };
   constexpr int C = O + 1;
   constexpr int G = SB / 32;                   // 32-lane groups
   constexpr int CP = C <= 8 ? 8 : 16;          // column slots
@@ -157,13 +148,13 @@ __device__ __forceinline__ void vn_epilogue(const T* s_obs, const double* s_ret,
     red[c][q * 32 + j] = s;
     red[C + c][q * 32 + j] = sq;
   }
-  bar();
+  __syncthreads();
   if constexpr (Q == 1) {
     if (tid < 2 * C) {
       double t = 0.0;
 #pragma unroll
       for (int k = 0; k < 32; ++k) t += red[tid][k];
-      put((int64_t)tid * v.n_wg + blockIdx.x, t);
+      v.part[(int64_t)tid * v.n_wg + blockIdx.x] = t;
     }
   } else {
     __shared__ double red2[2 * C][Q];
@@ -174,12 +165,12 @@ __device__ __forceinline__ void vn_epilogue(const T* s_obs, const double* s_ret,
       for (int k = 0; k < 32; ++k) t += red[c][q * 32 + k];
       red2[c][q] = t;
     }
-    bar();
+    __syncthreads();
     if (tid < 2 * C) {
       double t = red2[tid][0];
 #pragma unroll
       for (int q = 1; q < Q; ++q) t += red2[tid][q];
-      put((int64_t)tid * v.n_wg + blockIdx.x, t);
+      v.part[(int64_t)tid * v.n_wg + blockIdx.x] = t;
     }
   }
 }
@@ -333,232 +324,6 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
     static_assert(kLds, "the VecNormalize epilogue reads the LDS obs tile");
     if (v.flags & LZ_VN_TRAINING) vn_epilogue<Sys::O, SB, T>(s_obs, s_ret, nb, tid, v);
   }
-}
-
-// lz_step_vecnorm_fused: SB3 VecNormalize.step_wait in ONE launch (training or not,
-// n_wg <= the CU count so that every workgroup is resident at once; not LZ_VN_DEFER).
-// The step as step_tile<kVN>, then:
-//   training: the workgroup's moment partials go out as device-scope stores FIRST (the
-//   per-XCD L2s are not coherent inside a kernel), it waits for those stores alone
-//   (vmcnt(0) before any bulk store is issued), counts itself in (one device-scope
-//   atomic), issues its state / raw obs / reward / done stores, and waits until every
-//   workgroup has counted in; then it reduces the partials (vn_col_totals with
-//   device-scope loads: the order and the bits of the two-launch path) and derives the
-//   updated statistics itself (block 0 writes them back -- every block read the old
-//   ones before counting in);
-//   then the normalised obs straight from the LDS obs tile, the normalised reward, the
-//   bool dones and the normalised terminal rows of this workgroup's done envs (their
-//   compact-list slots are known to their lanes).
-// Against the two launches: no second kernel boundary and no re-read of the raw obs.
-// The wait is bounded (20 ms of wall clock): a grid that could not become resident
-// leaves NaN statistics instead of hanging.
-template <class Sys, typename T, int V>
-__device__ __forceinline__ void step_tile_vn1(const KArgs& a, const VArgs& v) {
-  constexpr int SB = step_block<V>();
-  constexpr int O = Sys::O, C = O + 1, W = 2 * C;
-  __shared__ __attribute__((aligned(16))) float s_act[SB * Sys::A];
-  __shared__ __attribute__((aligned(16))) T s_obs[SB * O];
-  __shared__ double s_ret[SB];
-  __shared__ double s_old[2 * O + 4];
-  __shared__ double s_st[2 * O + 1];
-  __shared__ double s_red[LZ_VN_RED(W)];
-  __shared__ double s_tot[W];
-  const int tid = (int)threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * SB;
-  const int64_t i = base + tid;
-  const int nb = (int)((a.n - base) < SB ? (a.n - base) : SB);
-  const bool live = tid < nb;
-  const bool vec = a.vec_ok != 0;
-  const bool training = (v.flags & LZ_VN_TRAINING) != 0;
-  const uint64_t tick = *a.tick_in;
-  if (blockIdx.x == 0 && tid == 0) {
-    *a.counter_next = 0;
-    *a.tick_out = tick + a.tick_adv;
-  }
-  // the statistics before this step (block 0 overwrites them only after every block
-  // has counted in, i.e. after every block has read them here)
-  if (tid < 2 * O + 1) s_old[tid] = v.obs_state[tid];
-  if (tid < 3) s_old[2 * O + 1 + tid] = v.ret_state[tid];
-  Sys sys;
-  sys.setup(a);
-  int32_t steps = 0;
-  double ret_in = 0.0;
-  if (live) {
-    sys.load(a, i);
-    if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
-    ret_in = v.returns[i];
-  }
-  float act[Sys::A];
-  if constexpr (Sys::kUsesAction) {
-    stage_in<true, float, Sys::A, SB>(s_act, static_cast<const float*>(a.act) + base * Sys::A, nb, tid, vec);
-    wg_barrier<false>();
-    if (live) {
-#pragma unroll
-      for (int j = 0; j < Sys::A; ++j) act[j] = s_act[tid * Sys::A + j];
-    }
-  }
-  T o[O], ot[O];
-  T rew = (T)0;
-  bool did_reset;
-  int32_t pos = -1;
-  const uint8_t dflag = step_body<Sys, T, false, true>(sys, steps, a, i, live, act, tick, 0, o, rew,
-                                                       did_reset, ot, true, &pos);
-  double rn = 0.0;
-  if (live) {
-    double r0 = ret_in;
-    if (training) r0 = r0 * v.gamma + (double)(float)rew;
-    rn = r0;
-    v.returns[i] = dflag ? 0.0 : r0;
-#pragma unroll
-    for (int j = 0; j < O; ++j) s_obs[tid * O + j] = o[j];
-  }
-  s_ret[tid] = rn;
-  // v.bar[0] counts the blocks in, v.bar[1] out; the last block out zeroes both, so any
-  // launch finds them at 0 whatever ran on the handle in between
-  int32_t* bar = v.bar;
-  // the raw outputs (lz_step's): this thread's state / reward / done and its chunks of
-  // the block's raw obs rows (LDS tile -> 16-B vectors)
-  auto raw_out = [&]() __attribute__((always_inline)) {
-    if (live) {
-      sys.store(a, i);
-      if (did_reset) sys.store_autoreset_extra(a, i);
-      if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
-      gstore<true>(static_cast<T*>(a.rew) + i, rew);
-      gstore<true>(a.done + i, dflag);
-    }
-    stage_out<true, T, O, SB>(static_cast<T*>(a.obs) + base * O, s_obs, nb, tid, vec);
-  };
-  wg_barrier<false>();  // s_obs / s_ret complete
-  const bool w0 = tid < 64;  // wave 0 writes the partials and counts the block in
-  if (!training || !w0) raw_out();  // in flight during the epilogue and the wait
-  if (training) {
-    vn_epilogue<O, SB, T, true>(s_obs, s_ret, nb, tid, v);
-    if (w0) {
-      // wave 0 has issued nothing but the partials since its loads: vmcnt(0) waits for
-      // them alone, then the block counts in and wave 0 issues its raw outputs
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (tid == 0) __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      raw_out();
-    }
-  }
-  double mean[O], sd[O], rsd;
-  if (training) {
-    if (tid == 0) {  // every block counted in (bounded: 20 ms of wall clock)
-      const uint64_t t0 = wall_clock64();
-      bool late = false;
-      while (!(a.variant & 8192) &&
-             __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)gridDim.x) {
-        __builtin_amdgcn_s_sleep(2);
-        if (wall_clock64() - t0 > 2000000ull) {
-          late = true;
-          break;
-        }
-      }
-      if (late) s_old[0] = __builtin_nan("");  // visible, never silently wrong
-      if (__hip_atomic_fetch_add(bar + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-          (int32_t)gridDim.x - 1) {  // every block is past the wait
-        __hip_atomic_store(bar, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(bar + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    wg_barrier<false>();
-    if (a.variant & 16384) {  // TIMING A/B ONLY: no reduction
-      if (tid < W) s_tot[tid] = 1.0;
-      __syncthreads();
-    } else {
-      vn_col_totals<W, true>(v.part, v.n_wg, s_red, s_tot);
-    }
-    const double bc = (double)a.n;
-    if (tid < O) {
-      double nm = s_old[tid], nv = s_old[O + tid];
-      if (v.flags & LZ_VN_NORM_OBS)
-        rms_new(s_old[tid], s_old[O + tid], s_old[2 * O], bc, s_tot[tid], s_tot[O + 1 + tid], nm, nv);
-      s_st[tid] = nm;
-      s_st[O + tid] = sqrt(nv + v.eps);
-      if (blockIdx.x == 0 && (v.flags & LZ_VN_NORM_OBS)) {
-        v.obs_state[tid] = nm;
-        v.obs_state[O + tid] = nv;
-        if (tid == 0) v.obs_state[2 * O] = s_old[2 * O] + bc;
-      }
-    }
-    if (tid == 64) {
-      const double* r = s_old + 2 * O + 1;
-      double nm, nv;
-      rms_new(r[0], r[1], r[2], bc, s_tot[O], s_tot[2 * O + 1], nm, nv);
-      s_st[2 * O] = sqrt(nv + v.eps);
-      if (blockIdx.x == 0) {
-        v.ret_state[0] = nm;
-        v.ret_state[1] = nv;
-        v.ret_state[2] = r[2] + bc;
-      }
-    }
-    if (blockIdx.x == 0 && tid == 0 && v.n_done_out)
-      *v.n_done_out = __hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    wg_barrier<false>();
-#pragma unroll
-    for (int d = 0; d < O; ++d) {
-      mean[d] = s_st[d];
-      sd[d] = s_st[O + d];
-    }
-    rsd = s_st[2 * O];
-  } else {
-#pragma unroll
-    for (int d = 0; d < O; ++d) {
-      mean[d] = s_old[d];
-      sd[d] = sqrt(s_old[O + d] + v.eps);
-    }
-    rsd = sqrt(s_old[2 * O + 2] + v.eps);
-  }
-  const bool nobs = (v.flags & LZ_VN_NORM_OBS) != 0;
-  const bool nrew = (v.flags & LZ_VN_NORM_REWARD) != 0;
-  // normalised obs from the LDS tile, written as the raw obs were
-  if (a.variant & 32768) return;  // TIMING A/B ONLY
-  if (vec && nb == SB) {
-    constexpr int kVec = SB * O / 4;
-    f4v* gv = reinterpret_cast<f4v*>(v.obs_n + base * O);
-    for (int q = tid; q < kVec; q += SB) {
-      float y[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int el = 4 * q + e;
-        const float x = (float)s_obs[el];
-        y[e] = nobs ? rms_norm_sd((double)x, mean[el % O], sd[el % O], true, v.clip_obs) : x;
-      }
-      gstore<true>(gv + q, (f4v){y[0], y[1], y[2], y[3]});
-    }
-  } else {
-    for (int e = tid; e < nb * O; e += SB) {
-      const float x = (float)s_obs[e];
-      v.obs_n[base * O + e] = nobs ? rms_norm_sd((double)x, mean[e % O], sd[e % O], true, v.clip_obs) : x;
-    }
-  }
-  if (live) {
-    const float rw = (float)rew;
-    gstore<true>(v.rew_n + i, nrew ? rms_norm_sd((double)rw, 0.0, rsd, false, v.clip_rew) : rw);
-    gstore<true>(v.dones01 + i, (uint8_t)(dflag != 0));
-    if (pos >= 0 && v.term_n) {
-#pragma unroll
-      for (int j = 0; j < O; ++j) {
-        const float x = (float)ot[j];
-        v.term_n[(int64_t)pos * O + j] = nobs ? rms_norm_sd((double)x, mean[j], sd[j], true, v.clip_obs) : x;
-      }
-    }
-  }
-  if (!training && v.n_done_out) {
-    // eval (no arrival wait): the last block to finish publishes the done count (every
-    // block's compact-list atomics returned before it counts in)
-    wg_barrier<false>();
-    if (tid == 0 && __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                        (int32_t)gridDim.x - 1) {
-      *v.n_done_out = __hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(bar, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-template <class Sys, typename T>
-__global__ __launch_bounds__(1024) void k_step_vn1(KArgs a, VArgs v) {
-  step_tile_vn1<Sys, T, 24>(a, v);
 }
 
 // Occupancy hint per system (Sys::kStepWaves, default none): a register-heavy step body
@@ -1373,36 +1138,6 @@ static int launch_vn(const KArgs& a, const VArgs& v, hipStream_t s) {
     hipLaunchKernelGGL((k_vn_colsum<Sys::O>), dim3(v.fused ? 1 : 2 * (Sys::O + 1)),
                        dim3(kVnColBlock), 0, s, v, a.n, a.counter, v.n_done_out);
   return (int)hipGetLastError();
-}
-
-template <class Sys, typename T>
-static int launch_vn1(const KArgs& a, const VArgs& v, hipStream_t s) {
-  static_assert(Sys::O <= kVnMaxObs, "obs too wide for the VecNormalize epilogue");
-  hipLaunchKernelGGL((k_step_vn1<Sys, T>), dim3((unsigned)((a.n + 1023) / 1024)), dim3(1024), 0, s, a, v);
-  return (int)hipGetLastError();
-}
-
-int launch_step_vecnorm1(int system, int f64, const KArgs& a, const VArgs& v, void* stream) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  switch (system) {
-    case LZ_SYS_LORENZ3:
-      return f64 ? launch_vn1<SysL3<double>, double>(a, v, s) : launch_vn1<SysL3<float>, float>(a, v, s);
-    case LZ_SYS_LORENZ4:
-      return f64 ? launch_vn1<SysL4<double>, double>(a, v, s) : launch_vn1<SysL4<float>, float>(a, v, s);
-    case LZ_SYS_PMSM:
-      return launch_vn1<SysPMSM, float>(a, v, s);
-    case LZ_SYS_HR:
-      return f64 ? launch_vn1<SysHR<double>, double>(a, v, s) : launch_vn1<SysHR<float>, float>(a, v, s);
-    case LZ_SYS_T1:
-      return f64 ? launch_vn1<SysT1<double>, double>(a, v, s) : launch_vn1<SysT1<float>, float>(a, v, s);
-    case LZ_SYS_T2:
-      return f64 ? launch_vn1<SysT2<double>, double>(a, v, s) : launch_vn1<SysT2<float>, float>(a, v, s);
-    case LZ_SYS_TP:
-      return f64 ? launch_vn1<SysTP<double>, double>(a, v, s) : launch_vn1<SysTP<float>, float>(a, v, s);
-    case LZ_SYS_SC:
-      return f64 ? launch_vn1<SysSC<double>, double>(a, v, s) : launch_vn1<SysSC<float>, float>(a, v, s);
-  }
-  return (int)hipErrorInvalidValue;
 }
 
 int launch_step_vecnorm(int system, int f64, const KArgs& a, const VArgs& v, void* stream) {

@@ -49,56 +49,39 @@ __device__ __forceinline__ float rms_norm(double v, double mean, double var, boo
 // of the butterfly measured slower) and no lane-strided global loads (one cache line
 // per lane: measured 4 us per 262k-env step).  red: LZ_VN_RED(W) doubles of LDS.
 #define LZ_VN_RED(W) ((W) * 257 + 256)
-// kCoherent: the partials were written by other workgroups of the SAME launch (the
-// single-launch VecNormalize step): device-scope atomic loads, which bypass the
-// per-XCD L2s that are not coherent with each other inside a kernel -- same order, same
-// bits.
-template <int W, bool kCoherent = false>
+template <int W>
 __device__ __forceinline__ void vn_col_totals(const double* part, int n_wg, double* red,
                                               double* out) {
   constexpr int CS = W <= 16 ? 16 : 32, S = 256 / CS, RUN = 256 / S;
   static_assert(W <= 32, "too many partial columns");
-  const int t = (int)threadIdx.x;  // threads >= 256 (larger workgroups) only synchronise
-  // kCoherent (in-kernel): LDS-only barriers, so that the workgroup's global stores stay
-  // in flight (__syncthreads() also waits for every store of every wave)
-  auto bar = [] __device__() {
-    if constexpr (kCoherent) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else __syncthreads();
-  };
+  const int t = (int)threadIdx.x;
   double acc[W];
 #pragma unroll
   for (int c = 0; c < W; ++c) acc[c] = 0.0;
-  for (int r = t; t < 256 && r < n_wg; r += 256) {
+  for (int r = t; r < n_wg; r += 256) {
 #pragma unroll
-    for (int c = 0; c < W; ++c) {
-      if constexpr (kCoherent)
-        acc[c] += __hip_atomic_load(part + (int64_t)c * n_wg + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        acc[c] += part[(int64_t)c * n_wg + r];
-    }
+    for (int c = 0; c < W; ++c) acc[c] += part[(int64_t)c * n_wg + r];
   }
-  if (t < 256) {
 #pragma unroll
-    for (int c = 0; c < W; ++c) red[c * 257 + t] = acc[c];
-  }
-  bar();
+  for (int c = 0; c < W; ++c) red[c * 257 + t] = acc[c];
+  __syncthreads();
   double* run = red + W * 257;
   const int c = t % CS, sg = t / CS;
-  if (t < 256 && c < W) {
+  if (c < W) {
     const double* x = red + c * 257 + sg * RUN;
     double v = x[0];
 #pragma unroll
     for (int k = 1; k < RUN; ++k) v += x[k];
     run[sg * CS + c] = v;
   }
-  bar();
+  __syncthreads();
   if (t < W) {
     double v = run[t];
 #pragma unroll
     for (int k = 1; k < S; ++k) v += run[k * CS + t];
     out[t] = v;
   }
-  bar();
+  __syncthreads();
 }
 
 }  // namespace lz

@@ -178,7 +178,6 @@ _SIGS = {
     "lz_step_vecnorm": (ctypes.c_int, [VP, ctypes.POINTER(LzVecNorm), VP, VP, VP, VP, VP, VP, VP]),
     "lz_vecnorm_apply": (ctypes.c_int, [VP, ctypes.POINTER(LzVecNorm), VP, VP, VP, VP, VP, VP, VP,
                                         VP, VP]),
-    "lz_step_vecnorm_fused": (ctypes.c_int, [VP, ctypes.POINTER(LzVecNorm)] + [VP] * 11),
     "lz_policy_blob_bytes": (ctypes.c_int64, []),
     "lz_policy_pack": (ctypes.c_int, [ctypes.POINTER(LzMlpPolicy), VP, ctypes.c_int64]),
     "lz_policy_pack_hidden": (ctypes.c_int, [ctypes.POINTER(LzMlpPolicy), ctypes.c_int32, VP,

@@ -31,7 +31,6 @@ statistic per step, RCCL over xGMI).
 Statistics are saved / loaded as .npz (no pickle).
 """
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -165,9 +164,6 @@ class LorenzVecNormalize:
         self.returns = torch.zeros((self.num_envs,), dtype=torch.float64, device=self.device)
         self._moments = torch.zeros((2 * obs_dim + 4,), dtype=torch.float64, device=self.device)
         self._fused = isinstance(be, BatchedEnv) and be.compact
-        # one launch per step (lz_step_vecnorm_fused) where every step workgroup can be
-        # resident at once; LZ_VN_ONE=0 keeps the two-call form (A/B, parity tests)
-        self._one = os.environ.get("LZ_VN_ONE", "1") != "0"
         self._layout = self._vn = self._last = None
         self.old_obs = None
         self.old_reward = None
@@ -273,22 +269,13 @@ class LorenzVecNormalize:
         vn = self._vn[1]
         acts = be._check_dev(venv.device_actions(self._actions), torch.float32,
                              (n, be.action_dim), "actions")
-        one = self._one and self.group is None
-        if one:  # step + statistics + normalised outputs in one launch
-            st = nat.lib.lz_step_vecnorm_fused(be._h, vn, acts.data_ptr(), p_obs, p_rew, p_done,
-                                               p_idx, p_tobs, p_nd, p_on, p_rn, p_dones, p_tn)
-            if st == nat.LZ_ERR_UNSUPPORTED:  # too many envs to be resident at once
-                self._one = one = False
-            else:
-                nat.check(st)
-        if not one:
-            nat.check(nat.lib.lz_step_vecnorm(be._h, vn, acts.data_ptr(), p_obs, p_rew, p_done,
-                                              p_idx, p_tobs, p_nd))
-            if self.group is not None and self.training:
-                dist.all_reduce(self._moments, group=self.group)
-            nat.check(nat.lib.lz_vecnorm_apply(be._h, vn, p_obs, p_rew, p_done, p_on, p_rn,
-                                               p_dones, p_tobs, p_nd, p_tn))
+        nat.check(nat.lib.lz_step_vecnorm(be._h, vn, acts.data_ptr(), p_obs, p_rew, p_done, p_idx,
+                                          p_tobs, p_nd))
         be._last_actions = acts
+        if self.group is not None and self.training:
+            dist.all_reduce(self._moments, group=self.group)
+        nat.check(nat.lib.lz_vecnorm_apply(be._h, vn, p_obs, p_rew, p_done, p_on, p_rn, p_dones,
+                                           p_tobs, p_nd, p_tn))
 
         def view(k):
             a, nb, dt, shp = offs[k]

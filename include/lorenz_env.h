@@ -624,20 +624,6 @@ lz_status lz_vecnorm_apply(lz_handle* h, const lz_vecnorm* vn, const void* obs_r
                            float* rew_norm, uint8_t* dones_out, const void* terminal_obs_raw,
                            const int32_t* n_done, float* term_norm);
 
-/* lz_step_vecnorm + lz_vecnorm_apply in ONE launch (same arguments and results, bit
- * for bit): the step kernel's workgroups count themselves in after writing their
- * moment partials, each reduces them in the two-call path's fixed order and normalises
- * its own rows from LDS.  Needs every workgroup (1024 envs each) resident at once:
- * LZ_ERR_UNSUPPORTED above (CUs x 1024) envs and with LZ_VN_DEFER (a multi-GPU caller
- * all-reduces between the two calls) -- use the two calls then.  Synchronisation is
- * bounded: a grid that cannot become resident (other work occupying the CUs) produces
- * NaN statistics instead of hanging.  dones_out and term_norm are required here. */
-lz_status lz_step_vecnorm_fused(lz_handle* h, const lz_vecnorm* vn, const void* actions,
-                                void* obs_out, void* rew_out, uint8_t* done_out,
-                                int32_t* done_idx_out, void* terminal_obs_out,
-                                int32_t* n_done_out, float* obs_norm, float* rew_norm,
-                                uint8_t* dones_out, float* term_norm);
-
 /* ------------------------------------------------------------------------------
  * VecFrameStack(venv, n_stack) on the device (SB3 2.7.1 common/vec_env/
  * stacked_observations.py StackedObservations, 1-D Box, channels-last), as the

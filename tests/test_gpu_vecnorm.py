@@ -244,55 +244,3 @@ def test_vecnorm_apply_refused_after_another_launch(gl):
     torch.cuda.synchronize()
     obs, rew, done, infos = dev.step(np.zeros((n, 2), np.float32))  # the wrapper still works
     assert obs.shape == (n, o)
-
-
-@pytest.mark.parametrize("env_id,n,dtype,training,norm_reward", [
-    ("lorenz_pmsm-v0", 20000 + 37, "float32", True, True),    # ragged, 20 workgroups
-    ("lorenz_pmsm-v0", 1 << 18, "float32", True, True),       # 256 workgroups = the CUs
-    ("lorenz_pmsm-v0", 300, "float32", False, False),         # eval: no arrival wait
-    ("lorenz_transient-v0", 5000, "float32", True, True),     # obs_dim 8
-    ("lorenz_dynamic-v0", 4096 + 5, "float64", True, True),   # fp64 env
-])
-def test_single_launch_equals_two_calls(gl, env_id, n, dtype, training, norm_reward):
-    """lz_step_vecnorm_fused (one launch: the workgroups count themselves in after their
-    moment partials, each reduces them and normalises its own rows) against the
-    two-call form, bit for bit: normalised obs / rewards / dones / terminal
-    observations, the raw obs, and the statistics, over 30 steps with truncations."""
-    runs = []
-    for single in (True, False):
-        vn = _vn(gl, n, env_id, mes=7, dtype=dtype, norm_obs=True, norm_reward=norm_reward,
-                 clip_obs=10.0, training=training)
-        vn._one = single
-        vn.reset()
-        rng = np.random.default_rng(1)
-        A = vn.action_space.shape[0]
-        out = []
-        for k in range(30):
-            o, r, d, infos = vn.step(rng.uniform(-1, 1, (n, A)).astype(np.float32))
-            term = [infos[i]["terminal_observation"] for i in np.nonzero(d)[0][:50]]
-            out.append((o.copy(), r.copy(), d.copy(), _np(vn.get_original_obs()).copy(),
-                        np.array(term, np.float32).reshape(-1)))
-        st = (vn.obs_rms.mean, vn.obs_rms.var, np.array([vn.obs_rms.count]), vn.ret_rms.mean,
-              vn.ret_rms.var)
-        assert vn._one == single  # the single launch was not refused
-        runs.append((out, [np.asarray(x).copy() for x in st]))
-        vn.close()
-    (a_out, a_st), (b_out, b_st) = runs
-    for k, (x, y) in enumerate(zip(a_out, b_out)):
-        for p, q in zip(x, y):
-            assert np.array_equal(np.asarray(p).view(np.uint8), np.asarray(q).view(np.uint8)), k
-    saw = sum(int(x[2].sum()) for x in a_out)
-    assert saw > 0  # terminal rows were normalised
-    for p, q in zip(a_st, b_st):
-        assert np.array_equal(p.view(np.uint8), q.view(np.uint8))
-
-
-def test_single_launch_refused_above_resident_grid(gl):
-    """Above CUs x 1024 envs the single launch is refused (LZ_ERR_UNSUPPORTED) and the
-    wrapper keeps the two-call form; results stay those of the two calls."""
-    n = (1 << 18) + 1024 * 8
-    vn = _vn(gl, n, norm_obs=True, norm_reward=True, clip_obs=10.0)
-    vn.reset()
-    vn.step(np.zeros((n, 2), np.float32))
-    assert vn._one is False
-    vn.close()
