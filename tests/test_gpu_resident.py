@@ -365,3 +365,41 @@ def test_resident_member_churn(gl):
     for a, b in pairs:
         if a is not None:
             a.close(), b.close()
+
+
+def test_resident_two_threads(gl):
+    """Drop-in envs stepped from two Python threads at once (ctypes releases the GIL
+    during the call; the server's membership and command line are guarded by one
+    mutex): every env stays bit-identical to its lz_step_host twin."""
+    import threading
+
+    import gym_lorenz._native as nat
+
+    pairs = [_pair("pmsm", 1, "float32", add_noise=True) for _ in range(4)]
+    errors = []
+
+    def worker(idx, seed):
+        try:
+            rng = np.random.default_rng(seed)
+            mine = pairs[idx::2]
+            bufs = [(_bufs(a), _bufs(b)) for a, b in mine]
+            for k in range(300):
+                for (a, b), (ba, bb) in zip(mine, bufs):
+                    act = rng.uniform(-1, 1, (1, 2)).astype(np.float32)
+                    x = _step(nat.lib.lz_step_host, a, act, None, ba)
+                    y = _step(nat.lib.lz_resident_step, b, act, None, bb)
+                    for p, q in zip(x, y):
+                        if not bits_equal(p, q):
+                            errors.append((idx, k))
+                            return
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(j, 40 + j)) for j in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors[:3]
+    for a, b in pairs:
+        a.close(), b.close()
