@@ -1180,26 +1180,27 @@ template <typename E>
 __global__ __launch_bounds__(256) void k_plane_gather(const E* __restrict__ plane, int64_t n,
                                                       const int64_t* __restrict__ idx, int64_t count,
                                                       E* __restrict__ dst) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= count) return;
-  const int64_t j = idx[i];
-  dst[i] = (j >= 0 && j < n) ? plane[j] : E(0);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256) {
+    const int64_t j = idx[i];
+    dst[i] = (j >= 0 && j < n) ? plane[j] : E(0);
+  }
 }
 
 template <typename E>
 __global__ __launch_bounds__(256) void k_plane_scatter(E* __restrict__ plane, int64_t n,
                                                        const int64_t* __restrict__ idx, int64_t count,
                                                        const E* __restrict__ src) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= count) return;
-  const int64_t j = idx[i];
-  if (j >= 0 && j < n) plane[j] = src[i];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256) {
+    const int64_t j = idx[i];
+    if (j >= 0 && j < n) plane[j] = src[i];
+  }
 }
 
 int launch_plane_index(bool scatter, int es, void* plane, int64_t n, const int64_t* idx, int64_t count,
                        void* buf, void* stream) {
   if (count <= 0) return 0;
-  const dim3 g((unsigned)((count + 255) / 256));
+  const int64_t want = (count + 255) / 256;
+  const dim3 g((unsigned)(want < 65536 ? want : 65536));  // grid-stride beyond 16M ids
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (es == 8) {
     if (scatter)
