@@ -272,7 +272,8 @@ def test_resident_refused_under_capture(gl):
 def _plane_host(be, p):
     import gym_lorenz._native as nat
 
-    out = np.zeros((be.num_envs,), np.float64 if be.tdtype == torch.float64 else np.float32)
+    npdt = {torch.float64: np.float64, torch.float32: np.float32, torch.int32: np.int32}
+    out = np.zeros((be.num_envs,), npdt[be.plane_dtype(p)])
     nat.check(nat.lib.lz_resident_read_state(be._h, int(p), out.ctypes.data))
     return out
 
@@ -403,3 +404,27 @@ def test_resident_two_threads(gl):
     assert not errors, errors[:3]
     for a, b in pairs:
         a.close(), b.close()
+
+
+def test_read_state_after_idle_exit(gl, monkeypatch):
+    """lz_resident_read_state while the server runs (its published copy) and after its
+    idle exit (the planes): both equal the lz_step_host twin's state, and stepping on
+    afterwards relaunches the server with the same trajectory."""
+    import gym_lorenz._native as nat
+
+    monkeypatch.setenv("LZ_RESIDENT_IDLE_US", "300")
+    a, b = _pair("hr", 1, "float64", add_noise=True)
+    ba, bb = _bufs(a), _bufs(b)
+    rng = np.random.default_rng(8)
+    for k in range(40):
+        act = rng.uniform(-1, 1, (1, 2)).astype(np.float32)
+        x = _step(nat.lib.lz_step_host, a, act, None, ba)
+        y = _step(nat.lib.lz_resident_step, b, act, None, bb)
+        for p, q in zip(x, y):
+            assert bits_equal(p, q), k
+        if k % 10 == 9:
+            if k % 20 == 19:
+                time.sleep(0.003)  # > the idle limit: the server has exited
+            for pl in range(9):  # HR: master (3), slave (3), sigma, filter (2)
+                assert bits_equal(a.get_state(pl).cpu().numpy(), _plane_host(b, pl)), (k, pl)
+    a.close(), b.close()
