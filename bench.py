@@ -526,9 +526,12 @@ def describe_launches(tm, rollout):
         return ("per timed window: %d eager %d-step lz_rollout launches (x%d windows)"
                 % (per_win, tm["T"], tm["windows"]))
     if tm["graph"]:
-        L = tm["graph_len"]
-        return ("per timed window: %d hipGraph replays of %d lz_step launches + %d eager "
-                "lz_step launches (x%d windows)" % (per_win // L, L, per_win % L, tm["windows"]))
+        L, G = tm["graph_len"], tm.get("graph_rem", 0)
+        rem = per_win % L
+        extra = ("1 hipGraph replay of %d lz_step launches + " % G) if G and rem >= G else ""
+        return ("per timed window: %d hipGraph replays of %d lz_step launches + %s%d eager "
+                "lz_step launches (x%d windows)"
+                % (per_win // L, L, extra, rem - (G if extra else 0), tm["windows"]))
     return "per timed window: %d eager lz_step launches (x%d windows)" % (per_win, tm["windows"])
 
 
@@ -608,11 +611,21 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
         nat.check(nat.lib.lz_set_stream(h, ctypes.c_void_p(stream.cuda_stream)))
         for _ in range(max(warm, 2)):
             one()
+        graph_rem, rem_n = None, 0
         if args.launch == "graph" and not rollout:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=stream):
                 for _ in range(L):
                     one()
+            # the window's K mod L remainder as a graph too (its even part: the captured
+            # ping-pong parity), so that a short window (the driver's --steps 20) is not
+            # paced by one Python launch per step
+            rem_n = (launches % L) - (launches % L) % 2
+            if rem_n:
+                graph_rem = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph_rem, stream=stream):
+                    for _ in range(rem_n):
+                        one()
         torch.cuda.synchronize(device)
 
         def run(nlaunch):  # exactly nlaunch launches
@@ -622,7 +635,11 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
                 return
             for _ in range(nlaunch // L):
                 graph.replay()
-            for _ in range(nlaunch % L):
+            r = nlaunch % L
+            if graph_rem is not None and r >= rem_n:
+                graph_rem.replay()
+                r -= rem_n
+            for _ in range(r):
                 one()
 
         def fix_parity(nlaunch):  # untimed: an odd eager remainder flipped the parity
@@ -670,6 +687,7 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
     K = launches * T
     return {
         "steps": K, "T": T, "ring": R, "graph_len": L, "graph": graph is not None,
+        "graph_rem": rem_n if graph_rem is not None else 0,
         "warmup": warm, "launches": launches * need, "windows": need,
         "elapsed": elapsed, "ev_ms": ev_ms,
         "timing": {
