@@ -255,12 +255,11 @@ class BatchedEnv:
             return
         v = torch.as_tensor(values, dtype=self.plane_dtype(plane)).reshape(-1).to(self.device)
         v = torch.broadcast_to(v, idx.shape).contiguous()
-        if idx.numel() > 1:  # keep the last occurrence of a repeated id
-            order = torch.arange(idx.numel(), device=idx.device)
-            last = torch.full((self.num_envs,), -1, dtype=torch.int64, device=idx.device)
-            last.scatter_reduce_(0, idx, order, reduce="amax")
-            keep = last[idx] == order
-            idx, v = idx[keep].contiguous(), v[keep].contiguous()
+        if idx.numel() > 1:  # keep the last occurrence of a repeated id, O(count log count)
+            srt, perm = torch.sort(idx, stable=True)
+            last = torch.ones_like(srt, dtype=torch.bool)
+            last[:-1] = srt[1:] != srt[:-1]  # the last of each run of equal ids
+            idx, v = srt[last].contiguous(), v[perm[last]].contiguous()
         nat.check(nat.lib.lz_set_state(self._h, int(plane), _ptr(v), _ptr(idx), idx.numel()))
         self._last_plane = (v, idx)
 
