@@ -1042,7 +1042,7 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
   const int64_t n = h->cfg.num_envs;
   const lz::PolShape sh = arch >= 4   ? lz::attn_f32_policy_shape(n, h->num_cus, arch == 5)
                          : attn      ? lz::attn_policy_shape(n, h->num_cus)
-                         : arch == 3 ? lz::f32_policy_shape(n, h->num_cus)
+                         : arch == 3 ? lz::f32_policy_shape(n, h->num_cus, h->cfg.reserved[0])
                                      : lz::policy_shape(n, h->cfg.reserved[0], h->num_cus);
   const int W = sh.waves, grid = sh.grid;
   const int O = h->desc.obs_dim;
@@ -1158,7 +1158,7 @@ lz_status lz_policy_step_f32(lz_handle* h, const lz_policy_rollout_args* r, int3
   }
   const bool fin = k == r->K;
   if (k == 0) HIP_TRY(hipMemsetAsync(h->ps_cursor, 0, 2 * sizeof(int32_t), h->stream));
-  const lz::PolShape sh = lz::f32_policy_shape(n, h->num_cus);
+  const lz::PolShape sh = lz::f32_policy_shape(n, h->num_cus, h->cfg.reserved[0]);
   KArgs a;
   fill_common(h, a);
   a.obs = r->obs_buf;

@@ -398,9 +398,10 @@ inline PolShape policy_shape(int64_t n, int variant, int num_cus) {
 int launch_rollout_policy(int system, const KArgs& a, const PArgs& p, const PolShape& sh,
                           void* stream);
 // the float32 MlpPolicy (kF32* blob): 32 envs per wave, 8 waves (two per SIMD; the
-// 146 KB blob leaves room for one workgroup per CU, the obs moments live in registers),
-// 4 waves below 8 tiles per CU
-PolShape f32_policy_shape(int64_t n, int num_cus);
+// 146 KB blob leaves room for one workgroup per CU, the obs moments live in registers);
+// below 8 tiles per CU 4 tiles per workgroup on 8 waves, the pi net and the env step in
+// waves 0-3, the value net in waves 4-7 (pair = 1); the per-step kernel runs 4 waves there
+PolShape f32_policy_shape(int64_t n, int num_cus, int variant);
 int launch_rollout_policy_f32(int system, const KArgs& a, const PArgs& p, const PolShape& sh,
                               void* stream);
 // SB3-exact VecNormalize: one step of the float32 policy rollout (PStepArgs above)

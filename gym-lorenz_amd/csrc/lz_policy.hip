@@ -1117,6 +1117,219 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   }
 }
 
+// Workgroup barrier for LDS hand-overs: this wave's LDS ops complete, then s_barrier.
+// __syncthreads() would also drain vmcnt (every outstanding global store of the wave).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------------------
+// The float32 MlpPolicy rollout with the two nets in different waves (f32_policy_shape
+// pair = 1: fewer than 8 32-env tiles per CU, e.g. cfg5's 32,768 envs = 1,024 tiles).
+// With both nets in one wave such a grid has one wave per SIMD, and every MFMA chain's
+// and tanh's latency is exposed.  Here waves 0-3 (actors) each step a 32-env tile: the
+// pi net, the sample, the env step; waves 4-7 (critics; wave w + 4 shares wave w's SIMD)
+// run the value net on the same tiles: V(x_k) for the values, the truncation bootstraps
+// and V(x_K) -- two waves per SIMD, each computing what k_rollout_policy<kMlpF32>
+// computes (the same bits; the same moment partials, one per actor wave, the same tile
+// order).  Hand-over through LDS, one slot per env and no double buffer: the actor
+// writes step k's next obs, terminal obs, reward and done code between barriers M_k and
+// B_k; the critic reads them between B_k and M_{k+1}, then evaluates V(x_{k+1}) (and
+// step k's bootstraps) while the actor runs step k + 1.
+template <class Sys>
+__global__ __launch_bounds__(512) void k_rollout_policy_f32_split(KArgs a, PArgs p) {
+  constexpr int O = Sys::O, A = Sys::A, KS1 = (O + 1) / 2, T = 4;  // T tiles per workgroup
+  static_assert(O <= kPolMaxObs && A <= kPolMaxAct, "policy tile shape");
+  __shared__ __attribute__((aligned(64))) uint8_t s_blob[kF32BlobBytes];
+  __shared__ double s_norm[2 * kPolMaxObs];
+  __shared__ float s_on[T][O][32], s_ot[T][O][32], s_rew[T][32];
+  __shared__ uint32_t s_df[T][32];
+  const int tid = (int)threadIdx.x;
+  const int lane = tid & 63, h = lane >> 5, slot = lane & 31;
+  // wave-uniform in an SGPR: the actor / critic branches below hold barriers, so they
+  // must be scalar branches, never exec-masked
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tw = wave & (T - 1);
+  const bool owner = h == 0;
+  {
+    const f4v* src = reinterpret_cast<const f4v*>(p.blob);
+    f4v* dst = reinterpret_cast<f4v*>(s_blob);
+    for (int v = tid; v < kF32BlobBytes / 16; v += 2 * T * 64) dst[v] = src[v];
+  }
+  if (tid < O) {
+    s_norm[tid] = p.norm ? p.norm[tid] : 0.0;
+    s_norm[kPolMaxObs + tid] = p.norm ? sqrt(p.norm[O + tid] + p.eps) : 1.0;
+  }
+  const uint64_t tick = *a.tick_in;
+  if (blockIdx.x == 0 && tid == 0) {
+    *a.counter_next = 0;
+    *a.tick_out = tick + a.tick_adv;
+  }
+  __syncthreads();
+  const uint8_t* pi_net = s_blob;
+  const uint8_t* vf_net = s_blob + kF32Net;
+  const float* ttab = reinterpret_cast<const float*>(s_blob + kF32Tanh);
+  const float* g_scale = reinterpret_cast<const float*>(s_blob + kF32LogStd) + 4;
+  const float* g_var2 = g_scale + 4;
+  const float* g_lscale = g_scale + 8;
+  const bool norm = p.norm != nullptr;
+  const double* mu = s_norm;
+  const double* sd = s_norm + kPolMaxObs;
+  const bool det = (p.pflags & LZ_POLICY_DETERMINISTIC) != 0;
+  const bool boot = (p.pflags & LZ_POLICY_BOOTSTRAP) != 0;
+  const float gamma = p.gamma;
+  double mom_r[O];  // actors: the env's two lanes, half 0 the sums, half 1 the squares
+#pragma unroll
+  for (int j = 0; j < O; ++j) mom_r[j] = 0.0;
+  float* obs_buf = static_cast<float*>(a.obs);
+  float* rew_buf = static_cast<float*>(a.rew);
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t base = (int64_t)blockIdx.x * T; base < ntiles; base += (int64_t)gridDim.x * T) {
+    const int64_t i = (base + tw) * 32 + slot;
+    const bool live = owner && i < a.n;
+    if (wave < T) {  // ---- actor
+      Sys sys;
+      sys.setup(a);
+      int32_t steps = 0;
+      bool any_reset = false;
+      float o[O];
+#pragma unroll
+      for (int j = 0; j < O; ++j) o[j] = 0.0f;
+      if (live) {
+        sys.load(a, i);
+        if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
+#pragma unroll
+        for (int j = 0; j < O; ++j) o[j] = p.obs_in[i * O + j];
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see k_rollout_policy
+      for (int k = 0; k < a.K; ++k) {
+        lds_barrier();  // M_k: the critic has read step k - 1's hand-over
+        const int64_t off = (int64_t)k * a.n + i;
+        float x[O];
+        normalize<O>(o, x, norm, mu, sd, p.clip);
+        if (live) {
+#pragma unroll
+          for (int j = 0; j < O; ++j) obs_buf[off * O + j] = x[j];
+        }
+        float xs[KS1], mean[A];
+        f32_inputs<O, KS1>(x, lane, xs);
+        mlp_f32<KS1, A>(pi_net, xs, lane, mean, ttab);
+        float act_c[A];
+        if (live) {
+          float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+          if (!det) {
+            if constexpr (A <= 2) normal2(a.seed, (uint64_t)(a.gid0 + i), tick + (uint64_t)k, z);
+            else normal4(a.seed, (uint64_t)(a.gid0 + i), tick + (uint64_t)k, z);
+          }
+          float lp = 0.0f;
+#pragma unroll
+          for (int j = 0; j < A; ++j) {
+            const float aj = det ? mean[j] : mean[j] + z[j] * g_scale[j];
+            const float d = aj - mean[j];
+            const float lpj = (-(d * d)) / g_var2[j] - g_lscale[j] - 0.91893853320467274f;
+            lp = j == 0 ? lpj : lp + lpj;
+            act_c[j] = clip(aj, p.act_lo, p.act_hi);
+            p.act[off * A + j] = aj;
+          }
+          p.logp[off] = lp;
+        }
+        float on[O], ot[O];
+        float rew = 0.0f;
+        bool did_reset;
+        const uint8_t df = step_body<Sys, float, true, true>(sys, steps, a, i, live, act_c,
+                                                             tick + (uint64_t)k, k, on, rew,
+                                                             did_reset, ot);
+        any_reset = any_reset || did_reset;
+        if (live) {
+          a.done[off] = df;
+#pragma unroll
+          for (int j = 0; j < O; ++j) {
+            s_on[tw][j][slot] = on[j];
+            s_ot[tw][j][slot] = ot[j];
+          }
+          s_rew[tw][slot] = rew;
+          s_df[tw][slot] = df;
+        }
+        if (p.partials) {
+#pragma unroll
+          for (int j = 0; j < O; ++j) {
+            const double v = (double)__shfl(on[j], slot, 64);
+            if (i < a.n) mom_r[j] += h ? v * v : v;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < O; ++j) o[j] = on[j];
+        lds_barrier();  // B_k: step k's hand-over is written
+      }
+      if (live) {
+#pragma unroll
+        for (int j = 0; j < O; ++j) p.obs_last[i * O + j] = o[j];
+        sys.store(a, i);
+        if (any_reset) sys.store_autoreset_extra(a, i);
+        if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
+      }
+    } else {  // ---- critic
+      float o[O], ot[O];
+      float rew = 0.0f;
+      uint32_t df = 0;
+#pragma unroll
+      for (int j = 0; j < O; ++j) o[j] = live ? p.obs_in[i * O + j] : 0.0f;
+      // step kk's hand-over -> registers (between B_kk and M_{kk+1})
+      auto take = [&]() {
+        if (live) {
+#pragma unroll
+          for (int j = 0; j < O; ++j) {
+            o[j] = s_on[tw][j][slot];
+            ot[j] = s_ot[tw][j][slot];
+          }
+          rew = s_rew[tw][slot];
+          df = s_df[tw][slot];
+        }
+      };
+      // step kk's truncation bootstrap (SB3: rewards += gamma * V(terminal obs)), reward out
+      auto settle = [&](int kk) {
+        if (boot) {
+          const bool bt = live && (df & LZ_DONE_TRUNCATED) && !(df & LZ_DONE_TERMINATED);
+          if (__ballot(bt) != 0ull) {
+            float xt[O], vt[1];
+            normalize<O>(ot, xt, norm, mu, sd, p.clip);
+            value_fwd<32, O, kMlpF32>(s_blob, vf_net, xt, bt, lane, vt);
+            if (bt) rew = rew + gamma * vt[0];
+          }
+        }
+        if (live) rew_buf[(int64_t)kk * a.n + i] = rew;
+      };
+      for (int k = 0; k < a.K; ++k) {
+        if (k > 0) take();
+        lds_barrier();  // M_k
+        if (k > 0) settle(k - 1);
+        float x[O], xs[KS1], val[1];
+        normalize<O>(o, x, norm, mu, sd, p.clip);
+        f32_inputs<O, KS1>(x, lane, xs);
+        mlp_f32<KS1, 1>(vf_net, xs, lane, val, ttab);
+        if (live) p.val[(int64_t)k * a.n + i] = val[0];
+        lds_barrier();  // B_k
+      }
+      take();
+      settle(a.K - 1);
+      float x[O], vl[1];
+      normalize<O>(o, x, norm, mu, sd, p.clip);
+      value_fwd<32, O, kMlpF32>(s_blob, vf_net, x, live, lane, vl);
+      if (live) p.last_val[i] = vl[0];
+    }
+  }
+  if (wave < T && p.partials) {  // fixed-order butterfly over the wave, as k_rollout_policy
+    double* dst = p.partials + ((int64_t)blockIdx.x * T + wave) * (2 * O);
+#pragma unroll
+    for (int j = 0; j < 2 * O; ++j) {
+      double v = (j < O ? h == 0 : h == 1) ? mom_r[j < O ? j : j - O] : 0.0;
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+      if (lane == 0) dst[j] = v;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // SB3-exact VecNormalize in the float32 rollout (lz_policy_step_f32).  SB3 2.7.1's
 // collect_rollouts under VecNormalize(training=True) (code/lorenz_pmsm/train.py:170-181):
@@ -2009,7 +2222,10 @@ static int launch_pol(const KArgs& a, const PArgs& p, const PolShape& sh, hipStr
 
 template <class Sys>
 static int launch_pol_f32(const KArgs& a, const PArgs& p, const PolShape& sh, hipStream_t s) {
-  if (sh.waves == 4)
+  if (sh.pair == 1)
+    hipLaunchKernelGGL((k_rollout_policy_f32_split<Sys>), dim3((unsigned)sh.grid), dim3(8 * 64), 0, s, a,
+                       p);
+  else if (sh.waves == 4)
     hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, kMlpF32>), dim3((unsigned)sh.grid), dim3(4 * 64), 0, s,
                        a, p);
   else
@@ -2018,16 +2234,21 @@ static int launch_pol_f32(const KArgs& a, const PArgs& p, const PolShape& sh, hi
   return (int)hipGetLastError();
 }
 
-// 8 waves (two per SIMD) when there are enough 32-env tiles for every CU, else 4 (one
-// per SIMD: cfg5's 32,768 envs are 1,024 tiles = 128 eight-wave groups, half the CUs)
-PolShape f32_policy_shape(int64_t n, int num_cus) {
+// 8 waves (two per SIMD) when there are enough 32-env tiles for every CU, else 4 tiles
+// per workgroup with the nets split over 8 waves (pair = 1, k_rollout_policy_f32_split:
+// cfg5's 32,768 envs are 1,024 tiles = 128 eight-tile groups, half the CUs).
+// LZ_POL_F32_WAVES=4|8 forces the one-wave-per-tile kernel at that width, lz_config
+// reserved[0] bit 8192 keeps it at 4 waves (A/B knobs).  waves = tiles per workgroup:
+// the moment partials are one per tile-wave either way.
+PolShape f32_policy_shape(int64_t n, int num_cus, int variant) {
   const int64_t tiles = (n + 31) / 32;
-  static const int forced = [] {  // LZ_POL_F32_WAVES=4|8: A/B knob
+  static const int forced = [] {
     const char* e = std::getenv("LZ_POL_F32_WAVES");
     const int w = e ? std::atoi(e) : 0;
     return w == 4 || w == 8 ? w : 0;
   }();
   PolShape s = {32, forced ? forced : tiles >= 8 * (int64_t)num_cus ? 8 : 4, 0, 0};
+  if (!forced && s.waves == 4 && !(variant & 8192)) s.pair = 1;
   const int64_t groups = (tiles + s.waves - 1) / s.waves;
   s.grid = (int)(groups < num_cus ? groups : num_cus);
   return s;

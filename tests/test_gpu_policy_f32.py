@@ -197,6 +197,52 @@ def test_f32_truncation_bootstrap(gl, pol, orc):
     assert _eq(ra[k, e][sel], want[sel])
 
 
+@pytest.mark.parametrize("system,kw", [("pmsm", dict(add_noise=True, max_episode_steps=5)),
+                                       ("lorenz4", dict(max_episode_steps=4))])
+def test_f32_split_kernel_equals_one_wave_kernel(gl, pol, system, kw):
+    """Below 8 tiles per CU the rollout runs k_rollout_policy_f32_split (pi net + env step
+    in waves 0-3, the value net in waves 4-7); lz_config reserved[0] bit 8192 keeps the
+    one-wave-per-tile kernel.  Every output of both -- K = 16 with sampling, truncation
+    bootstraps, captured terminal obs, VecNormalize statistics, pooled moments, final
+    env state -- is bit-identical, at a ragged N (a partly dead last tile and a
+    workgroup with dead tiles)."""
+    from gym_lorenz.vec_normalize import DeviceRunningMeanStd
+
+    n, K = 3001, 16
+    out = []
+    for variant in (0, 8192):
+        env = gl.BatchedEnv(system, n, seed=41, variant=variant, **kw)
+        O, A = env.obs_dim, env.action_dim
+        _, sd = _random_policy(pol, O, A, seed=9)
+        rms = DeviceRunningMeanStd(O, env.device)
+        rng = np.random.default_rng(3)
+        rms.set_state(rng.normal(0, 2, O), rng.uniform(0.5, 30, O), 1e4)
+        col = pol.FusedRolloutCollector(env, sd, gamma=0.95, bootstrap=True, obs_rms=rms,
+                                        training=True, vecnorm_update="rollout",
+                                        capture_terminal=K * n, precision="fp32")
+        col.reset()
+        col.collect(K)
+        b = col.collect(K)
+        m = int(b.n_done.item())
+        idx = _np(b.done_idx[:m])
+        order = np.argsort(idx)
+        res = {f: _np(getattr(b, f)) for f in ("observations", "actions", "log_probs", "values",
+                                               "rewards", "dones", "last_values", "last_obs",
+                                               "obs_moments")}
+        res["done_idx"] = idx[order]
+        res["terminal_obs"] = _np(b.terminal_obs[:m])[order]
+        for j in range(64):  # every state plane (lz_plane_elem_size 0 ends the list)
+            try:
+                res["plane%d" % j] = _np(env.get_state(j))
+            except ValueError:
+                break
+        out.append(res)
+        env.close()
+    assert out[0]["done_idx"].size > 0
+    for f in out[0]:
+        assert _eq(out[0][f], out[1][f]), f
+
+
 def test_f32_vs_sb3_fp32_forward(gl, pol):
     """The fp32 twin of test_policy_bf16_vs_fp32_sb3_init: an SB3-initialised policy
     behind VecNormalize against the plain torch float32 forward SB3 computes."""
