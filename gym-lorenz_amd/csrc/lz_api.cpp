@@ -419,6 +419,7 @@ static void fill_common(const lz_handle* h, KArgs& a) {
   a.flags = h->cfg.flags;
   a.alpha = h->cfg.alpha;
   a.variant = h->cfg.reserved[0];
+  a.num_cus = h->num_cus;
   for (int j = 0; j < LZ_MAX_PARAMS; ++j) a.prm[j] = h->cfg.params[j];
   a.counter = h->counters + h->parity;
   a.counter_next = h->counters + (1 - h->parity);

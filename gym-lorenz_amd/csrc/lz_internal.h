@@ -46,6 +46,8 @@ struct KArgs {
   int32_t K;                 // rollout length
   int32_t variant;           // step-kernel tuning variant (lz_config.reserved[0])
   float alpha;               // PMSM
+  int32_t num_cus;           // compute units (k_step_multi's tile count; fills the padding
+                             // before prm, so no other kernel's argument offsets move)
   double prm[LZ_MAX_PARAMS];
 };
 

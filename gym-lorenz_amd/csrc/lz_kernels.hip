@@ -350,6 +350,115 @@ __global__ __launch_bounds__(step_block<VB>()) void k_step_vn(KArgs a, VArgs v) 
   step_tile<Sys, T, VB, true>(a, v);
 }
 
+// ------------------------------------------------------------------ multi-tile step
+// E consecutive 256-env tiles per workgroup, each lane one env of every tile (PMSM and
+// HR float32, A = 2).  k_step gives every wave ONE tile: its state loads, ~300-400
+// dependent instructions, its stores -- and at PMSM 262,144 envs all 4,096 waves are
+// resident at once, so the chip reads everything, then computes, then writes (the time
+// is the sum of the three, profiles/r03/step).  Here every tile's loads are issued at
+// entry, tile e steps as soon as its own loads have landed (the compiler waits with
+// vmcnt(#later loads)), while tiles e+1.. are still arriving and tile e-1's stores
+// drain.  Actions come straight from the row-major [N, 2] tensor, one 8-B load per lane
+// (a wave instruction reads 512 contiguous bytes); the obs tile leaves through LDS as
+// in k_step, one LDS buffer per tile (no reuse hazard between tiles).  Same step_body,
+// same per-env arithmetic: bit-identical to k_step.
+typedef float f2m __attribute__((ext_vector_type(2)));
+template <class Sys, typename T, int E>
+__global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
+  static_assert(Sys::A == 2 && Sys::kUsesAction, "k_step_multi: two-action systems");
+  constexpr int SB = kBlock;
+  __shared__ __attribute__((aligned(16))) T s_obs[E][SB * Sys::O];
+  const int tid = (int)threadIdx.x;
+  const bool vec = a.vec_ok != 0;
+  const uint64_t tick = *a.tick_in;
+  if (blockIdx.x == 0 && tid == 0) {
+    *a.counter_next = 0;
+    *a.tick_out = tick + a.tick_adv;
+  }
+  Sys sys[E];
+  int32_t steps[E];
+  float act[E][2];
+  const float* ga = static_cast<const float*>(a.act);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {  // every tile's loads, in tile order
+    const int64_t i = ((int64_t)blockIdx.x * E + e) * SB + tid;
+    sys[e].setup(a);
+    steps[e] = 0;
+    act[e][0] = act[e][1] = 0.0f;
+    if (i < a.n) {
+      sys[e].load(a, i);
+      if (a.count_steps) steps[e] = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
+      if (vec) {
+        const f2m v2 = __builtin_nontemporal_load(reinterpret_cast<const f2m*>(ga) + i);
+        act[e][0] = v2[0];
+        act[e][1] = v2[1];
+      } else {
+        act[e][0] = __builtin_nontemporal_load(ga + 2 * i);
+        act[e][1] = __builtin_nontemporal_load(ga + 2 * i + 1);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int64_t base = ((int64_t)blockIdx.x * E + e) * SB;
+    if (base >= a.n) break;  // workgroup-uniform: the trailing tiles of the last group
+    const int64_t i = base + tid;
+    const int nb = (int)((a.n - base) < SB ? (a.n - base) : SB);
+    const bool live = tid < nb;
+    T o[Sys::O];
+    T rew = (T)0;
+    bool did_reset;
+    const uint8_t dflag =
+        step_body<Sys, T, false>(sys[e], steps[e], a, i, live, act[e], tick, 0, o, rew, did_reset);
+    if (live) {
+      sys[e].store(a, i);
+      if (did_reset) sys[e].store_autoreset_extra(a, i);
+      if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps[e];
+#pragma unroll
+      for (int j = 0; j < Sys::O; ++j) s_obs[e][tid * Sys::O + j] = o[j];
+      gstore<true>(static_cast<T*>(a.rew) + i, rew);
+      gstore<true>(a.done + i, dflag);
+    }
+    wg_barrier<false>();
+    stage_out<true, T, Sys::O, SB>(static_cast<T*>(a.obs) + base * Sys::O, s_obs[e], nb, tid, vec);
+  }
+}
+
+// Tiles per workgroup of k_step_multi: variant bits 14-15 (16384 x {1, 2, 3}) force 1
+// (k_step), 2 or 4; 0 = the measured default, step_tiles_auto.
+template <class Sys>
+struct multi_step_ok {
+  static constexpr bool value = false;
+};
+template <>
+struct multi_step_ok<SysPMSM> {
+  static constexpr bool value = true;
+};
+template <>
+struct multi_step_ok<SysHR<float>> {
+  static constexpr bool value = true;
+};
+// Four tiles per workgroup only where that grid is ONE full generation of the chip (4
+// waves per SIMD, 109 VGPRs: 4 workgroups of 1,024 envs per CU, more than 3/4 of them
+// used): then k_step's 2-3 generations (HR 1M: 4,096 workgroups at 6 waves per SIMD =
+// 2.67) and their partial last one go away.  Elsewhere one wave running its tiles in
+// sequence is slower than k_step's waves running theirs in parallel (each tile is a
+// ~1.6 us dependent chain of ~400 instructions): PMSM 262,144 6.9 -> 11.3 us, HR 2M
+// 32 -> 35.6 us.  Measured (profiles/r03/multi_step/): HR 1M 17.0 -> 15.8 us, PMSM 1M
+// 24.6 -> 23.5, PMSM 786,432 19.0 -> 18.1; 917,504 a tie.
+inline int step_tiles_auto(int64_t n, int num_cus) {
+  const int64_t groups = (n + 4 * kBlock - 1) / (4 * kBlock), full = 4 * (int64_t)num_cus;
+  return (4 * groups > 3 * full && groups <= full) ? 4 : 1;
+}
+inline int step_tiles(const KArgs& a) {
+  switch ((a.variant >> 14) & 3) {
+    case 1: return 1;
+    case 2: return 2;
+    case 3: return 4;
+    default: return step_tiles_auto(a.n, a.num_cus > 0 ? a.num_cus : 256);
+  }
+}
+
 
 // ------------------------------------------------------------------ fused rollout
 // K steps in one launch, state in VGPRs.  B = envs per workgroup: 256, or 64 (one
@@ -842,9 +951,17 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
 template <class Sys, typename T, bool kVariants = false>
 static int launch_all(int which, const KArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)grid_for(a.n)), block(kBlock);
+  const int tiles = which == 1 && multi_step_ok<Sys>::value ? step_tiles(a) : 1;
   if (which == 0)
     hipLaunchKernelGGL((k_reset<Sys, T>), grid, block, 0, s, a);
-  else if (which == 1 && !kVariants) {
+  else if (tiles > 1) {
+    if constexpr (multi_step_ok<Sys>::value) {
+      const int64_t per = (int64_t)kBlock * tiles;
+      const dim3 g((unsigned)((a.n + per - 1) / per));
+      if (tiles == 2) hipLaunchKernelGGL((k_step_multi<Sys, T, 2>), g, block, 0, s, a);
+      else hipLaunchKernelGGL((k_step_multi<Sys, T, 4>), g, block, 0, s, a);
+    }
+  } else if (which == 1 && !kVariants) {
     hipLaunchKernelGGL((k_step<Sys, T, 0>), grid, block, 0, s, a);
   } else if (which == 1) {
     switch (a.variant & 31) {

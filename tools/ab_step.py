@@ -1,6 +1,7 @@
 """Interleaved A/B of lz_step kernel variants (one process, hipGraph-replayed steps,
 HIP-event timing on the launch stream; order rotated every round, a variant listed twice
-is a noise control).  Usage: AB_VARIANTS=0,32,0 python tools/ab_step.py [envs...]"""
+is a noise control).  Usage: AB_VARIANTS=0,32,0 [AB_SYSTEM=pmsm AB_NOISE=1]
+python tools/ab_step.py [envs...]"""
 import ctypes
 import json
 import os
@@ -14,7 +15,9 @@ from gym_lorenz import _native as nat  # noqa: E402
 
 
 def make(variant, n, system="lorenz3", R=16):
-    env = gl.BatchedEnv(system, n, dtype="float32", autoreset=True, variant=variant)
+    noise = os.environ.get("AB_NOISE")  # "1" / "0": force add_noise (default: the system's)
+    kw = {} if noise is None else {"add_noise": noise == "1"}
+    env = gl.BatchedEnv(system, n, dtype="float32", autoreset=True, variant=variant, **kw)
     env.reset()
     dev = env.device
     acts = torch.rand((R, n, env.action_dim), device=dev) * 2 - 1

@@ -1,6 +1,9 @@
 """Code hash of one kernel inside the built library: sha256 over the kernel's gfx950
 machine code and its kernel descriptor (<name>.kd: register counts, LDS size, launch
-attributes), read from the .so's clang offload bundles.  A PMC traffic figure measured
+attributes; its kernel_code_entry_byte_offset field -- bytes 16-23, where the code sits
+relative to the descriptor -- is zeroed, so adding an unrelated kernel to the same
+source file does not change the hash of one whose code did not change), read from the
+.so's clang offload bundles.  A PMC traffic figure measured
 for a kernel stays valid exactly as long as this hash does -- bench.py attaches a
 committed profiles/**/*pmc_summary.json's traffic only when the summary's recorded hash
 equals the running library's (tools/pmc_summary.py and tools/pmc_sq_summary.py record
@@ -68,15 +71,19 @@ def _sym_bytes(elf, want):
     return None
 
 
-def kernel_code_sha256(kernel, so_path=DEFAULT_SO):
+def kernel_code_sha256(kernel, so_path=DEFAULT_SO, mask_entry=True):
     """sha256 hex of the kernel's code + descriptor, or None when it is not in the
-    library (or the library is missing)."""
+    library (or the library is missing).  mask_entry=False: the round-3 first form
+    (descriptor hashed whole), for checking summaries recorded with it."""
     try:
         for elf in code_objects(so_path):
             code = _sym_bytes(elf, kernel)
             if code is None:
                 continue
-            kd = _sym_bytes(elf, kernel + ".kd") or b""
+            kd = bytearray(_sym_bytes(elf, kernel + ".kd") or b"")
+            if mask_entry and len(kd) >= 24:
+                kd[16:24] = bytes(8)  # kernel_code_entry_byte_offset: layout, not code
+            kd = bytes(kd)
             return hashlib.sha256(code + b"|" + kd).hexdigest()
     except (OSError, struct.error, ValueError, IndexError):
         return None
