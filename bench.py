@@ -72,6 +72,9 @@ def parse():
                         "with the AttentionFeaturesExtractor (no VecNormalize, as there); "
                         "attn_ln = code/lorenz_filter/train.py's residual + LayerNorm extractor "
                         "on VecFrameStack(4)")
+    p.add_argument("--variant", type=int, default=0,
+                   help="step-kernel tuning variant (lz_config.reserved[0]; A/B only, e.g. "
+                        "16384 / 32768 / 49152 force 1 / 2 / 4 tiles per PMSM / HR workgroup)")
     p.add_argument("--max-episode-steps", type=int, default=0,
                    help="TimeLimit truncation (auto-reset inside the kernel); 0 = none")
     return p.parse_args()
@@ -216,7 +219,20 @@ SYSTEM_INFO = {  # system -> (reference env, mangled k_step / k_rollout names, a
 }
 
 
-def kernel_name(system, mode, n, f64=False, no_done=False):
+def step_tiles(system, n, f64=False, num_cus=256, variant=0):
+    """Tiles per workgroup of the step launch: lz_kernels.hip step_tiles (variant bits
+    14-15 force 1 / 2 / 4) and step_tiles_auto (PMSM / HR float32: 4 where that grid is
+    one full chip generation, else 1)."""
+    if system not in ("pmsm", "hr") or f64:
+        return 1
+    forced = (variant >> 14) & 3
+    if forced:
+        return {1: 1, 2: 2, 3: 4}[forced]
+    groups, full = -(-n // 1024), 4 * num_cus
+    return 4 if 4 * groups > 3 * full and groups <= full else 1
+
+
+def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=0):
     """Mangled name of the dominant kernel (lz_kernels.hip launch_all / launch_rollout_d).
     no_done: a rollout launch that cannot produce a done (LORENZ3 without a TimeLimit)
     runs the done-free instantiation (kNoDone = true)."""
@@ -225,6 +241,9 @@ def kernel_name(system, mode, n, f64=False, no_done=False):
         tag = tag.replace("IfEEf", "IdEEd")
     sysname = ("7" if system == "pmsm" else "5") + tag
     if mode != "rollout":
+        tiles = step_tiles(system, n, f64, num_cus, variant)
+        if tiles > 1:
+            return "_ZN2lz12k_step_multiINS_%sLi%dEEEvNS_5KArgsE" % (sysname, tiles)
         return "_ZN2lz6k_stepINS_%sLi0EEEvNS_5KArgsE" % sysname
     D = 7  # kDmaDist
     b = "Lb%dE" % int(no_done and system == "lorenz3")
@@ -744,7 +763,7 @@ def main():
     kw = {"add_noise": True, "alpha": 0.5} if args.system == "pmsm" else {}
     env = gl.BatchedEnv(args.system, n, dtype="float32", seed=0, global_env_offset=start,
                         autoreset=True, device=local, max_episode_steps=args.max_episode_steps,
-                        **kw)
+                        variant=args.variant, **kw)
     if args.mode == "policy":
         out = bench_policy(args, gl, nat, torch, env, device, world, rank, total, n)
         env.close()
@@ -812,7 +831,9 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": kernel_name(args.system, args.mode, n, no_done=args.max_episode_steps == 0),
+            "kernel": kernel_name(args.system, args.mode, n, no_done=args.max_episode_steps == 0,
+                                  num_cus=torch.cuda.get_device_properties(device).multi_processor_count,
+                                  variant=args.variant),
             "avg_launch_us": launch_s * 1e6,
             "bytes_per_env_step": bytes_step,
             "note": "achieved = algorithmic bytes per launch (bytes_per_env_step x envs_per_gpu"

@@ -26,3 +26,29 @@ def test_hash_found_stable_distinct():
     assert kernel_hash.kernel_code_sha256(PMSM) not in (None, a)
     assert kernel_hash.kernel_code_sha256("_Z_no_such_kernel") is None
     assert kernel_hash.kernel_code_sha256(HEAD, "/nonexistent.so") is None
+
+
+def test_entry_offset_masked():
+    """The masked hash ignores only the descriptor's code-entry offset: it differs from
+    the whole-descriptor hash, and both are stable."""
+    a, b = kernel_hash.kernel_code_sha256(HEAD), kernel_hash.kernel_code_sha256(HEAD, mask_entry=False)
+    assert a and b and a != b
+    assert kernel_hash.kernel_code_sha256(HEAD, mask_entry=False) == b
+
+
+def test_bench_kernel_names_exist():
+    """Every kernel bench.py names as a line's dominant kernel is in the built library
+    (k_step_multi at the one-generation sizes, k_step elsewhere, the rollouts)."""
+    import bench
+
+    cases = [("lorenz3", "step", 1 << 20), ("pmsm", "step", 262144), ("pmsm", "step", 1 << 20),
+             ("hr", "step", 1 << 20), ("hr", "step", 1 << 21), ("lorenz4", "step", 1 << 20),
+             ("lorenz3", "rollout", 32768), ("lorenz3", "rollout", 262144)]
+    names = set()
+    for system, mode, n in cases:
+        k = bench.kernel_name(system, mode, n, no_done=True)
+        assert kernel_hash.kernel_code_sha256(k) is not None, k
+        names.add(k)
+    assert "_ZN2lz12k_step_multiINS_5SysHRIfEEfLi4EEEvNS_5KArgsE" in names
+    assert bench.step_tiles("pmsm", 262144) == 1 and bench.step_tiles("hr", 1 << 20) == 4
+    assert bench.step_tiles("hr", 1 << 21) == 1 and bench.step_tiles("lorenz3", 1 << 20) == 1
