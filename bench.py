@@ -242,16 +242,20 @@ def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=
     sysname = ("7" if system == "pmsm" else "5") + tag
     if mode != "rollout":
         tiles = step_tiles(system, n, f64, num_cus, variant)
-        if tiles > 1:
-            return "_ZN2lz12k_step_multiINS_%sLi%dEEEvNS_5KArgsE" % (sysname, tiles)
+        if tiles > 1:  # k_step_multi<Sys, T, E, kDoneT = false>
+            return "_ZN2lz12k_step_multiINS_%sLi%dELb0EEEvNS_5KArgsE" % (sysname, tiles)
         return "_ZN2lz6k_stepINS_%sLi0EEEvNS_5KArgsE" % sysname
     D = 7  # kDmaDist
     b = "Lb%dE" % int(no_done and system == "lorenz3")
-    if n < 2 * 256 * 256:  # one-wave workgroups; two lanes per env for LORENZ3 f32 >= 32,768
-        if system == "lorenz3" and n >= 32768:
-            return "_ZN2lz15k_rollout_splitINS_%sLi2ELi%dE%sEEvNS_5KArgsE" % (sysname, D, b)
-        return "_ZN2lz9k_rolloutINS_%sLi64ELi%dE%sEEvNS_5KArgsE" % (sysname, D, b)
-    return "_ZN2lz9k_rolloutINS_%sLi256ELi%dE%sEEvNS_5KArgsE" % (sysname, D, b)
+    # lz_kernels.hip launch_rollout_d: one-wave workgroups below 256 x CUs envs for
+    # LORENZ3 f32 (below 131,072 for the others); two lanes per env for LORENZ3 f32 from
+    # 32,768; temporal done stores by default (split SV = 1, k_rollout kDoneT = true)
+    one_wave_below = 256 * num_cus if system == "lorenz3" and not f64 else 2 * 256 * 256
+    if n < one_wave_below:
+        if system == "lorenz3" and not f64 and n >= 32768:
+            return "_ZN2lz15k_rollout_splitINS_%sLi2ELi%dE%sLi1EEEvNS_5KArgsE" % (sysname, D, b)
+        return "_ZN2lz9k_rolloutINS_%sLi64ELi%dE%sLb1EEEvNS_5KArgsE" % (sysname, D, b)
+    return "_ZN2lz9k_rolloutINS_%sLi256ELi%dE%sLb1EEEvNS_5KArgsE" % (sysname, D, b)
 
 
 def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):

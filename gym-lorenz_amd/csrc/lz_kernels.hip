@@ -243,6 +243,7 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
   constexpr bool NT = (V & 1) == 0;
   constexpr bool kLds = (V & 2) == 0;
   constexpr bool kFullBar = (V & 4) != 0;
+  constexpr bool kDoneT = (V & 32) != 0;  // A/B: temporal done-byte stores
   __shared__ __attribute__((aligned(16))) float s_act[kLds ? SB * Sys::A : 4];
   __shared__ __attribute__((aligned(16))) T s_obs[kLds ? SB * Sys::O : 2];
   const int tid = (int)threadIdx.x;
@@ -314,7 +315,7 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
       for (int j = 0; j < Sys::O; ++j) gstore<NT>(static_cast<T*>(a.obs) + i * Sys::O + j, o[j]);
     }
     gstore<NT>(static_cast<T*>(a.rew) + i, rew);
-    gstore<NT>(a.done + i, dflag);
+    gstore<NT && !kDoneT>(a.done + i, dflag);
   }
   if constexpr (kLds) {
     wg_barrier<kFullBar>();
@@ -363,7 +364,7 @@ __global__ __launch_bounds__(step_block<VB>()) void k_step_vn(KArgs a, VArgs v) 
 // in k_step, one LDS buffer per tile (no reuse hazard between tiles).  Same step_body,
 // same per-env arithmetic: bit-identical to k_step.
 typedef float f2m __attribute__((ext_vector_type(2)));
-template <class Sys, typename T, int E>
+template <class Sys, typename T, int E, bool kDoneT = false>
 __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
   static_assert(Sys::A == 2 && Sys::kUsesAction, "k_step_multi: two-action systems");
   constexpr int SB = kBlock;
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
 #pragma unroll
       for (int j = 0; j < Sys::O; ++j) s_obs[e][tid * Sys::O + j] = o[j];
       gstore<true>(static_cast<T*>(a.rew) + i, rew);
-      gstore<true>(a.done + i, dflag);
+      gstore<!kDoneT>(a.done + i, dflag);
     }
     wg_barrier<false>();
     stage_out<true, T, Sys::O, SB>(static_cast<T*>(a.obs) + base * Sys::O, s_obs[e], nb, tid, vec);
@@ -565,7 +566,7 @@ __device__ __forceinline__ void ladder_wait(int k) {
   }
 }
 
-template <class Sys, typename T, int B, bool FULL, int D, bool kNoDone>
+template <class Sys, typename T, int B, bool FULL, int D, bool kNoDone, bool kDoneT>
 __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any_reset,
                                              const KArgs& a, int64_t base, int tid, int nb,
                                              uint64_t tick, float* s_act, T* s_obs) {
@@ -675,7 +676,7 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
     T* gobs = static_cast<T*>(a.obs) + (off + base) * Sys::O;
     if constexpr (kDirect) {
       gstore<true>(static_cast<T*>(a.rew) + off + i, rew);
-      gstore<true>(a.done + off + i, dflag);
+      gstore<!kDoneT>(a.done + off + i, dflag);
       const co_t* src = reinterpret_cast<const co_t*>(o);
 #pragma unroll
       for (int j = 0; j < CO::N; ++j) gstore<false>(reinterpret_cast<co_t*>(gobs) + tid * CO::N + j, src[j]);
@@ -685,7 +686,7 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
 #pragma unroll
       for (int j = 0; j < Sys::O; ++j) s_obs[tid * Sys::O + j] = o[j];
       gstore<true>(static_cast<T*>(a.rew) + off + i, rew);
-      gstore<true>(a.done + off + i, dflag);
+      gstore<!kDoneT>(a.done + off + i, dflag);
     }
     wg_barrier<false>();
     if constexpr (FULL) {
@@ -705,7 +706,11 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   for (; k < a.K; ++k) run_step(k, std::false_type{});
 }
 
-template <class Sys, typename T, int B, int D, bool kNoDone = false>
+// kDoneT: temporal done-byte stores (the default: a wave's 64 done bytes are half a
+// 128-B line, merged in the L2 with the other wave's half; +5.6% mean over three
+// allocations at 262,144 envs, K = 2048, profiles/r03/done_stores/); variant bit 21 keeps
+// the non-temporal stores (A/B)
+template <class Sys, typename T, int B, int D, bool kNoDone = false, bool kDoneT = true>
 __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
   __shared__ __attribute__((aligned(16))) float s_act[dma_slots<D>() * act_slot_floats<Sys::A, B>()];  // DMA ring
   __shared__ __attribute__((aligned(16))) T s_obs[B * Sys::O];
@@ -728,9 +733,9 @@ __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
     if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
   }
   if (nb == B && a.vec_ok)
-    rollout_loop<Sys, T, B, true, D, kNoDone>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
+    rollout_loop<Sys, T, B, true, D, kNoDone, kDoneT>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
   else
-    rollout_loop<Sys, T, B, false, D, kNoDone>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
+    rollout_loop<Sys, T, B, false, D, kNoDone, kDoneT>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
   if (live) {
     sys.store(a, i);
     if (any_reset) sys.store_autoreset_extra(a, i);
@@ -779,7 +784,7 @@ __device__ __forceinline__ void store_half(T* p, const T* v) {
 // asm, so the compiler assumes the DMA writes it) -- the compiler then places the
 // lgkmcnt wait where the action is first used, and the state-only part of the step
 // (the RHS of the old state) overlaps the LDS latency.
-template <class Sys, typename T, int R, bool FULL, int D, bool kNoDone>
+template <class Sys, typename T, int R, bool FULL, int D, bool kNoDone, int SV>
 __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_reset,
                                            const KArgs& a, int64_t base, int tid, int nb,
                                            uint64_t tick, float* s_act) {
@@ -847,15 +852,20 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
                                                                   did_reset, nullptr, lead);
     any_reset = any_reset || did_reset;
     if (!live) return;
-    if (lead) gstore<true>(static_cast<T*>(a.rew) + off + i, rew);
-    else gstore<true>(a.done + off + i, kNoDone ? (uint8_t)0 : dflag);
+    if (lead) gstore<(SV & 2) == 0>(static_cast<T*>(a.rew) + off + i, rew);
+    else gstore<(SV & 1) == 0>(a.done + off + i, kNoDone ? (uint8_t)0 : dflag);
     // this lane's half row: elements [q*H, q*H + H) of env i = elements tid*H of the
     // block's contiguous obs slice
     T* p = static_cast<T*>(a.obs) + (off + base) * Sys::O + (int64_t)tid * H;
     T h[H];
 #pragma unroll
     for (int j = 0; j < H; ++j) h[j] = q ? o[H + j] : o[j];
-    store_half<T, H>(p, h);
+    if constexpr ((SV & 4) != 0) {  // A/B: plain (temporal) obs stores
+#pragma unroll
+      for (int j = 0; j < H; ++j) p[j] = h[j];
+    } else {
+      store_half<T, H>(p, h);
+    }
   };
   int k = 0;
   if constexpr (FULL && Sys::kUsesAction) {
@@ -865,7 +875,12 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
   for (; k < a.K; ++k) run_step(k, std::false_type{});
 }
 
-template <class Sys, typename T, int R, int D, bool kNoDone = false>
+// SV: temporal instead of non-temporal stores -- bit 0 the done bytes (the default: a
+// wave's 32 done bytes are a quarter of a 128-B line; temporal stores let the L2 merge
+// the four waves' quarters before the line leaves, +7.8% at 32,768 envs, K = 2048,
+// profiles/r03/done_stores/), bit 1 the rewards, bit 2 the obs half rows (A/B only,
+// variant bits 18-20 select SV = 0, 3, 4, 7)
+template <class Sys, typename T, int R, int D, bool kNoDone = false, int SV = 1>
 __global__ __launch_bounds__(64) void k_rollout_split(KArgs a) {
   constexpr int E = 64 / R;  // envs per one-wave workgroup
   __shared__ __attribute__((aligned(16))) float s_act[dma_slots<D>() * (row_dma<Sys::A, 32>() ? kRowRegionF : 64 * Sys::A)];
@@ -890,9 +905,9 @@ __global__ __launch_bounds__(64) void k_rollout_split(KArgs a) {
     if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
   }
   if (nb == E && a.vec_ok)
-    split_loop<Sys, T, R, true, D, kNoDone>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
+    split_loop<Sys, T, R, true, D, kNoDone, SV>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
   else
-    split_loop<Sys, T, R, false, D, kNoDone>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
+    split_loop<Sys, T, R, false, D, kNoDone, SV>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
   if (live && lead) {
     sys.store(a, i);
     if (any_reset) sys.store_autoreset_extra(a, i);
@@ -904,7 +919,8 @@ __global__ __launch_bounds__(64) void k_rollout_split(KArgs a) {
 static inline int64_t grid_for(int64_t n) { return (n + kBlock - 1) / kBlock; }
 
 // Two lanes per env in the small-N rollout (variant bit 256 forces one, 512 forces two):
-// by default for LORENZ3 f32 from 32,768 envs (below 131,072 the one-wave path runs).
+// by default for LORENZ3 f32 from 32,768 envs (below 256 x CUs = 65,536 the one-wave
+// path runs, launch_rollout_d).
 // Measured (profiles/r01/ab_rollout_*.json, K = 2048): +11% at 32,768 and +13% at
 // 65,536 envs; slower at 16,384 (the wave's step chain, not the SIMD count, bounds it
 // there) and for PMSM at any N (its step is 3-4x the instructions: doubling them costs
@@ -919,11 +935,27 @@ static inline bool rollout_split(const KArgs& a) {
 
 template <class Sys, typename T, int D, int DS = D>  // DS: the split-lane kernel's distance
 static void launch_rollout_d(const KArgs& a, hipStream_t s) {
-  if (a.n < 2 * 256 * kBlock) {  // < 2 full workgroups per CU: one-wave groups
+  // fewer 256-env workgroups than CUs: one-wave groups (variant bit 1<<23: the 256-lane
+  // kernel at any N, A/B).  At 65,536 envs on 256 CUs the 256-lane kernel (one wave per
+  // SIMD, 64 envs each) beats the split-lane one (two per SIMD, 32 envs each, every step
+  // computed twice) by 15% (profiles/r03/done_stores/, three allocations per variant);
+  // at 32,768 half the CUs would idle and it loses by 27%.
+  // Measured for LORENZ3 float32 only; the other systems keep the round-2 bound.
+  const int64_t cus = a.num_cus > 0 ? a.num_cus : 256;
+  const int64_t one_wave_below =
+      std::is_same<Sys, SysL3<float>>::value ? (int64_t)kBlock * cus : 2 * 256 * (int64_t)kBlock;
+  if (a.n < one_wave_below && !(a.variant & (1 << 23))) {
     if (rollout_split<Sys>(a)) {
       const dim3 g((unsigned)((a.n + 31) / 32));
       if constexpr (never_terminates<Sys>::value && !Sys::kNoise) {
         if (no_done<Sys>(a) && !(a.variant & 2048)) {  // variant bit 2048: keep the done path (A/B)
+          switch ((a.variant >> 18) & 7) {  // A/B: store policy (SV; 1 = the default)
+            case 1: hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true, 0>), g, dim3(64), 0, s, a); return;
+            case 3: hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true, 3>), g, dim3(64), 0, s, a); return;
+            case 4: hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true, 4>), g, dim3(64), 0, s, a); return;
+            case 7: hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true, 7>), g, dim3(64), 0, s, a); return;
+            default: break;
+          }
           hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true>), g, dim3(64), 0, s, a);
           return;
         }
@@ -936,8 +968,12 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
   } else {
     if constexpr (never_terminates<Sys>::value && !Sys::kNoise) {
       if (no_done<Sys>(a) && !(a.variant & 2048)) {
-        hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D, true>), dim3((unsigned)grid_for(a.n)),
-                           dim3(kBlock), 0, s, a);
+        if (a.variant & (1 << 21))  // A/B: non-temporal done stores
+          hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D, true, false>), dim3((unsigned)grid_for(a.n)),
+                             dim3(kBlock), 0, s, a);
+        else
+          hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D, true>), dim3((unsigned)grid_for(a.n)),
+                             dim3(kBlock), 0, s, a);
         return;
       }
     }
@@ -959,12 +995,14 @@ static int launch_all(int which, const KArgs& a, hipStream_t s) {
       const int64_t per = (int64_t)kBlock * tiles;
       const dim3 g((unsigned)((a.n + per - 1) / per));
       if (tiles == 2) hipLaunchKernelGGL((k_step_multi<Sys, T, 2>), g, block, 0, s, a);
+      else if (a.variant & (1 << 22))  // A/B: temporal done stores
+        hipLaunchKernelGGL((k_step_multi<Sys, T, 4, true>), g, block, 0, s, a);
       else hipLaunchKernelGGL((k_step_multi<Sys, T, 4>), g, block, 0, s, a);
     }
   } else if (which == 1 && !kVariants) {
     hipLaunchKernelGGL((k_step<Sys, T, 0>), grid, block, 0, s, a);
   } else if (which == 1) {
-    switch (a.variant & 31) {
+    switch (a.variant & 63) {
 #define LZ_STEP_V(VV)                                                                   \
   case VV:                                                                              \
     hipLaunchKernelGGL((k_step<Sys, T, VV>),                                            \
@@ -972,7 +1010,7 @@ static int launch_all(int which, const KArgs& a, hipStream_t s) {
                        dim3(step_block<VV>()), 0, s, a);                                \
     break;
       LZ_STEP_V(1) LZ_STEP_V(2) LZ_STEP_V(3) LZ_STEP_V(4) LZ_STEP_V(5)
-      LZ_STEP_V(8) LZ_STEP_V(16) LZ_STEP_V(24)
+      LZ_STEP_V(8) LZ_STEP_V(16) LZ_STEP_V(24) LZ_STEP_V(32)
 #undef LZ_STEP_V
       default: hipLaunchKernelGGL((k_step<Sys, T, 0>), grid, block, 0, s, a); break;
     }
