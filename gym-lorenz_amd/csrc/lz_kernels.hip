@@ -977,8 +977,12 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
         return;
       }
     }
-    hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D>), dim3((unsigned)grid_for(a.n)), dim3(kBlock),
-                       0, s, a);
+    if (a.variant & (1 << 21))  // A/B: non-temporal done stores
+      hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D, false, false>), dim3((unsigned)grid_for(a.n)),
+                         dim3(kBlock), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D>), dim3((unsigned)grid_for(a.n)), dim3(kBlock),
+                         0, s, a);
   }
 }
 
