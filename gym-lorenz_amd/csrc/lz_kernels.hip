@@ -879,7 +879,7 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
 // wave's 32 done bytes are a quarter of a 128-B line; temporal stores let the L2 merge
 // the four waves' quarters before the line leaves, +7.8% at 32,768 envs, K = 2048,
 // profiles/r03/done_stores/), bit 1 the rewards, bit 2 the obs half rows (A/B only,
-// variant bits 18-20 select SV = 0, 3, 4, 7)
+// variant bits 18-20 = 1, 3, 4, 7 select SV = 0, 3, 5, 7)
 template <class Sys, typename T, int R, int D, bool kNoDone = false, int SV = 1>
 __global__ __launch_bounds__(64) void k_rollout_split(KArgs a) {
   constexpr int E = 64 / R;  // envs per one-wave workgroup
@@ -952,7 +952,7 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
           switch ((a.variant >> 18) & 7) {  // A/B: store policy (SV; 1 = the default)
             case 1: hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true, 0>), g, dim3(64), 0, s, a); return;
             case 3: hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true, 3>), g, dim3(64), 0, s, a); return;
-            case 4: hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true, 4>), g, dim3(64), 0, s, a); return;
+            case 4: hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true, 5>), g, dim3(64), 0, s, a); return;
             case 7: hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true, 7>), g, dim3(64), 0, s, a); return;
             default: break;
           }
