@@ -437,9 +437,9 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         for _ in range(launches):
             one()
         torch.cuda.synchronize(device)
+        t1 = time.perf_counter()  # this rank's K steps; the job's time is the MAX over ranks
         if world > 1:
             dist.barrier()
-        t1 = time.perf_counter()
         # the dominant kernel alone (k_rollout_policy), HIP events on its stream
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * launches)]
         for j in range(launches):
@@ -685,9 +685,11 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
             run(launches)
             ev1.record(stream)
             torch.cuda.synchronize(device)
+            # stop before the closing barrier: a collective's latency is not part of the K
+            # steps (the path has none); the job's time is the MAX over ranks below
+            t1 = time.perf_counter()
             if world > 1:
                 dist.barrier()
-            t1 = time.perf_counter()
             fix_parity(launches)
             return t1 - t0, ev0.elapsed_time(ev1)
 
@@ -728,7 +730,8 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
             "timed_steps_total": K * need, "timed_seconds": elapsed,
             "window_ms_min": wms[0], "window_ms_median": wms[len(wms) // 2],
             "method": "each window = exactly `steps` env steps of every env, bracketed by "
-                      "barrier + torch.cuda.synchronize() on both sides; windows repeated "
+                      "barrier + torch.cuda.synchronize() on both sides (the clock stops "
+                      "after the closing synchronize, before the closing barrier); windows repeated "
                       "until >= %.0f ms are timed; value = windows x steps x envs / summed "
                       "window time (MAX over ranks)" % (min_window_s * 1e3),
         },
