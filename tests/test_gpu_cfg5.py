@@ -135,14 +135,15 @@ def test_cfg5_pmsm_rollout_k2048_bitexact(gl, orc):
     _run(gl, orc, "pmsm", 32768, L=2000, seed=32, lo=-1.2, hi=1.2)
 
 
-@pytest.mark.parametrize("n", [32768, 40001, 262144])
+@pytest.mark.parametrize("n", [32768, 40001, 65536, 100003, 262144])
 def test_cfg5_l3_rollout_no_timelimit_bitexact(gl, orc, n):
     """The bench's cfg5 workload as dynamic.py runs it: no TimeLimit, and the
     reference's own done (t == 10) never fires -- the launch takes the kernel without
     done bookkeeping (kNoDone).  K = 2048 oracle steps bit for bit, every done byte 0,
     the final state; and the same bits as the general kernel (variant bit 2048).
     n = 40,001 adds a ragged last workgroup (the non-DMA path of the same kernel);
-    262,144 is the 256-lane k_rollout path."""
+    65,536 (= 256 x CUs: the first size on the 256-lane kernel since round 3), 100,003
+    (its ragged last workgroup) and 262,144 run the 256-lane k_rollout path."""
     seed = 41
     gen = torch.Generator(device="cuda")
     gen.manual_seed(seed)
