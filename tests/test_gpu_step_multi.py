@@ -86,3 +86,57 @@ def test_step_multi_injected_noise(gl):
     for k in range(K):
         for a, b in zip(res[0][0][k], res[1][0][k]):
             assert bits_equal(a, b), k
+
+
+@pytest.fixture(scope="module")
+def orc():
+    import oracle
+
+    return oracle
+
+
+def _planes(be, p0, k):
+    return np.stack([_np(be.get_state(p0 + j)) for j in range(k)], 1)
+
+
+def test_hr_1m_default_multi_vs_oracle(gl, orc):
+    """The HR bench line's size (1,048,576 envs: the default launch IS k_step_multi with
+    4 tiles per workgroup): 6 float32 steps with injected noise, the whole batch bit for
+    bit against the oracle's DEV restatement."""
+    n, T = 1 << 20, 6
+    be = gl.BatchedEnv("hr", n, dtype="float32", seed=5, add_noise=True, autoreset=False)
+    be.reset()
+    init = orc.reset_draw("hr", np.float32, n, 0, 5, 0, add_noise=True)
+    st = np.ascontiguousarray(init[:, :6])
+    fa = np.zeros((n, 2), np.float32)
+    rng = np.random.default_rng(12)
+    with np.errstate(all="ignore"):
+        for k in range(T):
+            a = rng.uniform(-1.2, 1.2, (n, 2)).astype(np.float32)
+            nz = rng.normal(0, 1, (n, 3)) * init[:, 6:7]
+            o, r, d = be.step(torch.from_numpy(a).cuda(), torch.from_numpy(nz).cuda())
+            oo, rr, tt = orc.hr_step(st, fa, a, nz.astype(np.float32), True, False, orc.DEV)
+            assert bits_equal(_np(o), oo) and bits_equal(_np(r), rr), k
+            assert np.array_equal((_np(d) & 1).astype(bool), tt), k
+    assert bits_equal(_planes(be, 0, 6), st)
+    be.close()
+
+
+def test_pmsm_1m_default_multi_vs_oracle(gl, orc):
+    """PMSM at 1,048,576 envs (default launch: k_step_multi, 4 tiles): 6 steps with
+    injected noise, obs / state / lambda path bit for bit vs the oracle's DEV mode."""
+    n, T = 1 << 20, 6
+    be = gl.BatchedEnv("pmsm", n, seed=6, add_noise=True, autoreset=False)
+    be.reset()
+    S = orc.PmsmState(n)
+    S.st[:] = orc.reset_draw("pmsm", np.float32, n, 0, 6, 0)
+    rng = np.random.default_rng(13)
+    with np.errstate(all="ignore"):
+        for k in range(T):
+            a = rng.uniform(-1.2, 1.2, (n, 2)).astype(np.float32)
+            nz = rng.normal(0, 3, (n, 3))
+            o, r, d = be.step(torch.from_numpy(a).cuda(), torch.from_numpy(nz).cuda())
+            oo, rr, tt = orc.pmsm_step(S, a, nz, True, 0.5, orc.DEV)[:3]
+            assert bits_equal(_np(o), oo) and bits_equal(_np(r), rr), k
+    assert bits_equal(_planes(be, 0, 6), S.st)
+    be.close()
