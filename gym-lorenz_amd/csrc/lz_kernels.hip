@@ -682,9 +682,14 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
       for (int j = 0; j < CO::N; ++j) gstore<false>(reinterpret_cast<co_t*>(gobs) + tid * CO::N + j, src[j]);
       return;
     }
+    // the obs tile of this step: systems with actions pass a workgroup barrier at the top
+    // of every step (after the previous step's reads of the tile); systems without (LORENZ4,
+    // SC) alternate two tiles, so a wave's writes for step k+1 never meet a slower wave's
+    // reads of step k's tile, and step k+2's writes follow step k+1's barrier
+    T* so = s_obs + ((Sys::kUsesAction || (k & 1) == 0) ? 0 : B * Sys::O);
     if (live) {
 #pragma unroll
-      for (int j = 0; j < Sys::O; ++j) s_obs[tid * Sys::O + j] = o[j];
+      for (int j = 0; j < Sys::O; ++j) so[tid * Sys::O + j] = o[j];
       gstore<true>(static_cast<T*>(a.rew) + off + i, rew);
       gstore<!kDoneT>(a.done + off + i, dflag);
     }
@@ -693,9 +698,9 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
 #pragma unroll
       for (int j = 0; j < CO::N; ++j)
         gstore<true>(reinterpret_cast<co_t*>(gobs) + j * B + tid,
-                     reinterpret_cast<const co_t*>(s_obs)[j * B + tid]);
+                     reinterpret_cast<const co_t*>(so)[j * B + tid]);
     } else {
-      stage_out<true, T, Sys::O, B>(gobs, s_obs, nb, tid, false);
+      stage_out<true, T, Sys::O, B>(gobs, so, nb, tid, false);
     }
   };
   int k = 0;
@@ -712,8 +717,9 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
 // the non-temporal stores (A/B)
 template <class Sys, typename T, int B, int D, bool kNoDone = false, bool kDoneT = true>
 __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
-  __shared__ __attribute__((aligned(16))) float s_act[dma_slots<D>() * act_slot_floats<Sys::A, B>()];  // DMA ring
-  __shared__ __attribute__((aligned(16))) T s_obs[B * Sys::O];
+  // DMA ring (a placeholder for systems that take no action)
+  __shared__ __attribute__((aligned(16))) float s_act[Sys::kUsesAction ? dma_slots<D>() * act_slot_floats<Sys::A, B>() : 4];
+  __shared__ __attribute__((aligned(16))) T s_obs[(Sys::kUsesAction ? 1 : 2) * B * Sys::O];
   const int tid = (int)threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * B;
   const int64_t i = base + tid;
@@ -939,11 +945,16 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
   // kernel at any N, A/B).  At 65,536 envs on 256 CUs the 256-lane kernel (one wave per
   // SIMD, 64 envs each) beats the split-lane one (two per SIMD, 32 envs each, every step
   // computed twice) by 15% (profiles/r03/done_stores/, three allocations per variant);
-  // at 32,768 half the CUs would idle and it loses by 27%.
-  // Measured for LORENZ3 float32 only; the other systems keep the round-2 bound.
+  // at 32,768 half the CUs would idle and it loses by 27%.  LORENZ4 float32 the same
+  // way (profiles/r03/rollout_xover/, two allocations per variant): 65,536 envs 1,412 ->
+  // 908 us per 2048-step launch, 98,304 1,808 -> 1,476; 32,768 615 vs 820 (one-wave
+  // kept).  PMSM and HR (3-4x the instructions per step) are faster with one-wave groups
+  // at 32,768-98,304 (2,209 vs 2,493 / 1,823 vs 2,038 us at 65,536): the round-2 bound.
   const int64_t cus = a.num_cus > 0 ? a.num_cus : 256;
   const int64_t one_wave_below =
-      std::is_same<Sys, SysL3<float>>::value ? (int64_t)kBlock * cus : 2 * 256 * (int64_t)kBlock;
+      std::is_same<Sys, SysL3<float>>::value || std::is_same<Sys, SysL4<float>>::value
+          ? (int64_t)kBlock * cus
+          : 2 * 256 * (int64_t)kBlock;
   if (a.n < one_wave_below && !(a.variant & (1 << 23))) {
     if (rollout_split<Sys>(a)) {
       const dim3 g((unsigned)((a.n + 31) / 32));
