@@ -89,9 +89,10 @@ def test_legacy_f32_vs_oracle_and_reset_draws(gl, orc, key):
         assert np.array_equal(_np(d) & 1 != 0, dd), k
 
 
+@pytest.mark.parametrize("n", [777, 140001])  # one-wave kernel; 256-lane, ragged
 @pytest.mark.parametrize("key", ["t1", "t2", "tp", "sc"])
-def test_legacy_rollout_equals_steps(gl, key):
-    n, K = 777, 20
+def test_legacy_rollout_equals_steps(gl, key, n):
+    K = 20
     a = gl.BatchedEnv(NAMES[key], n, seed=5, max_episode_steps=6)
     b = gl.BatchedEnv(NAMES[key], n, seed=5, max_episode_steps=6)
     a.reset()
