@@ -248,9 +248,10 @@ def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=
     D = 7  # kDmaDist
     b = "Lb%dE" % int(no_done and system == "lorenz3")
     # lz_kernels.hip launch_rollout_d: one-wave workgroups below 256 x CUs envs for
-    # LORENZ3 / LORENZ4 f32 (below 131,072 for the others); two lanes per env for LORENZ3
+    # LORENZ3 f32 (3/4 of that for LORENZ4 f32, 131,072 for the others); two lanes per env for LORENZ3
     # f32 from 32,768; temporal done stores by default (split SV = 1, k_rollout kDoneT = true)
-    one_wave_below = (256 * num_cus if system in ("lorenz3", "lorenz4") and not f64
+    one_wave_below = (256 * num_cus if system == "lorenz3" and not f64
+                      else 256 * num_cus * 3 // 4 if system == "lorenz4" and not f64
                       else 2 * 256 * 256)
     if n < one_wave_below:
         if system == "lorenz3" and not f64 and n >= 32768:

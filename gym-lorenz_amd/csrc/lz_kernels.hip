@@ -950,11 +950,13 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
   // 908 us per 2048-step launch, 98,304 1,808 -> 1,476; 32,768 615 vs 820 (one-wave
   // kept).  PMSM and HR (3-4x the instructions per step) are faster with one-wave groups
   // at 32,768-98,304 (2,209 vs 2,493 / 1,823 vs 2,038 us at 65,536): the round-2 bound.
+  // LORENZ4's crossover lies lower, between 160 and 192 workgroups per 256 CUs (40,960
+  // envs: 658 vs 918 us; 49,152: 870 vs 925-1,096; 57,344: 908 vs 1,007): from 3/4 x 256 x CUs.
   const int64_t cus = a.num_cus > 0 ? a.num_cus : 256;
   const int64_t one_wave_below =
-      std::is_same<Sys, SysL3<float>>::value || std::is_same<Sys, SysL4<float>>::value
-          ? (int64_t)kBlock * cus
-          : 2 * 256 * (int64_t)kBlock;
+      std::is_same<Sys, SysL3<float>>::value   ? (int64_t)kBlock * cus
+      : std::is_same<Sys, SysL4<float>>::value ? (int64_t)kBlock * cus * 3 / 4
+                                               : 2 * 256 * (int64_t)kBlock;
   if (a.n < one_wave_below && !(a.variant & (1 << 23))) {
     if (rollout_split<Sys>(a)) {
       const dim3 g((unsigned)((a.n + 31) / 32));

@@ -371,14 +371,15 @@ def test_cfg3_shard_geometry(gl):
                                             ("lorenz3", "float32", 140000),
                                             ("pmsm", "float32", 140000),
                                             ("hr", "float32", 140000),
+                                            ("lorenz4", "float32", 49153),
                                             ("lorenz4", "float32", 65536),
                                             ("lorenz4", "float32", 70001),
                                             ("lorenz4", "float32", 140001),
                                             ("lorenz4", "float64", 140001),
                                             ("singlecontrol", "float32", 140001)])
 def test_rollout_equals_steps(gl, system, dtype, n):
-    """Fused rollout (one-wave workgroups below 131,072 envs, below 256 x CUs for LORENZ3 /
-    LORENZ4 f32 -- two lanes per env for LORENZ3 f32 from 32,768 -- 256-lane above) == K
+    """Fused rollout (one-wave workgroups below 131,072 envs, below 256 x CUs for LORENZ3
+    f32, 3/4 of that for LORENZ4 f32 -- two lanes per env for LORENZ3 f32 from 32,768 -- 256-lane above) == K
     steps.  The action-free systems (LORENZ4, singlecontrol) at 256-lane sizes cover the
     alternating obs tiles of k_rollout (a single tile raced: a fast wave's next-step writes
     against a slower wave's reads, seen at LORENZ4 70,001)."""
