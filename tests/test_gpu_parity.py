@@ -371,6 +371,8 @@ def test_cfg3_shard_geometry(gl):
                                             ("lorenz3", "float32", 140000),
                                             ("pmsm", "float32", 140000),
                                             ("hr", "float32", 140000),
+                                            ("pmsm", "float32", 140001),
+                                            ("hr", "float32", 140001),
                                             ("lorenz4", "float32", 49153),
                                             ("lorenz4", "float32", 65536),
                                             ("lorenz4", "float32", 70001),
