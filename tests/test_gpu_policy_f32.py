@@ -197,18 +197,20 @@ def test_f32_truncation_bootstrap(gl, pol, orc):
     assert _eq(ra[k, e][sel], want[sel])
 
 
+@pytest.mark.parametrize("n", [3001, 40001])  # 40,001: 313 groups on 256 CUs (grid-stride repeats)
 @pytest.mark.parametrize("system,kw", [("pmsm", dict(add_noise=True, max_episode_steps=5)),
                                        ("lorenz4", dict(max_episode_steps=4))])
-def test_f32_split_kernel_equals_one_wave_kernel(gl, pol, system, kw):
+def test_f32_split_kernel_equals_one_wave_kernel(gl, pol, system, kw, n):
     """Below 8 tiles per CU the rollout runs k_rollout_policy_f32_split (pi net + env step
     in waves 0-3, the value net in waves 4-7); lz_config reserved[0] bit 8192 keeps the
     one-wave-per-tile kernel.  Every output of both -- K = 16 with sampling, truncation
     bootstraps, captured terminal obs, VecNormalize statistics, pooled moments, final
     env state -- is bit-identical, at a ragged N (a partly dead last tile and a
-    workgroup with dead tiles)."""
+    workgroup with dead tiles), and where workgroups run a second tile group (the
+    hand-over across the group boundary)."""
     from gym_lorenz.vec_normalize import DeviceRunningMeanStd
 
-    n, K = 3001, 16
+    K = 16
     out = []
     for variant in (0, 8192):
         env = gl.BatchedEnv(system, n, seed=41, variant=variant, **kw)
