@@ -44,12 +44,16 @@ def test_bench_kernel_names_exist():
     cases = [("lorenz3", "step", 1 << 20), ("pmsm", "step", 262144), ("pmsm", "step", 1 << 20),
              ("hr", "step", 1 << 20), ("hr", "step", 1 << 21), ("lorenz4", "step", 1 << 20),
              ("lorenz3", "rollout", 32768), ("lorenz3", "rollout", 65536),
-             ("lorenz3", "rollout", 262144), ("pmsm", "rollout", 32768), ("pmsm", "rollout", 262144)]
+             ("lorenz3", "rollout", 262144), ("pmsm", "rollout", 32768), ("pmsm", "rollout", 262144),
+             ("lorenz4", "rollout", 32768), ("lorenz4", "rollout", 49152), ("lorenz4", "rollout", 65536)]
     names = set()
     for system, mode, n in cases:
         k = bench.kernel_name(system, mode, n, no_done=system == "lorenz3")
         assert kernel_hash.kernel_code_sha256(k) is not None, k
         names.add(k)
     assert "_ZN2lz12k_step_multiINS_5SysHRIfEEfLi4ELb0EEEvNS_5KArgsE" in names
+    # LORENZ4 f32 rollouts: one-wave groups below 3/4 x 256 x CUs envs, 256 lanes from there
+    assert "k_rolloutINS_5SysL4IfEEfLi64E" in bench.kernel_name("lorenz4", "rollout", 40960)
+    assert "k_rolloutINS_5SysL4IfEEfLi256E" in bench.kernel_name("lorenz4", "rollout", 49152)
     assert bench.step_tiles("pmsm", 262144) == 1 and bench.step_tiles("hr", 1 << 20) == 4
     assert bench.step_tiles("hr", 1 << 21) == 1 and bench.step_tiles("lorenz3", 1 << 20) == 1
