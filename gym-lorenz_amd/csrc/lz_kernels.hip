@@ -957,7 +957,8 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
       std::is_same<Sys, SysL3<float>>::value   ? (int64_t)kBlock * cus
       : std::is_same<Sys, SysL4<float>>::value ? (int64_t)kBlock * cus * 3 / 4
                                                : 2 * 256 * (int64_t)kBlock;
-  if (a.n < one_wave_below && !(a.variant & (1 << 23))) {
+  // variant bit 1<<24: one-wave groups at any N (A/B)
+  if ((a.n < one_wave_below || (a.variant & (1 << 24))) && !(a.variant & (1 << 23))) {
     if (rollout_split<Sys>(a)) {
       const dim3 g((unsigned)((a.n + 31) / 32));
       if constexpr (never_terminates<Sys>::value && !Sys::kNoise) {
