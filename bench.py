@@ -12,10 +12,14 @@ actions from and writing obs / reward / done into a 16-slot on-device rollout ri
          --master-port P bench.py --gpus N ...
 
 Multi-GPU: one process per GPU, contiguous shard of the global env axis per rank, no
-collective on the step path (barrier + max-over-ranks timing only).  Default
-scaling is "weak" (1,048,576 envs per GPU: N=1 is exactly the BASELINE 1M-env
-config); --scaling strong splits a fixed global env count instead.
-Rank 0 prints one JSON line.
+collective on the step path (barrier + max-over-ranks timing only).  `--gpus N` without
+a torch.distributed.run environment (no WORLD_SIZE) spawns the N rank processes itself
+(child processes started before anything touches the GPU; rank r pins cuda:r).  Default
+scaling is "strong": BASELINE's 1,048,576 envs in total, split over the N GPUs
+(configs[2]: 131,072 per GPU at N = 8; N = 1 is the 1M-env config itself); for N > 1
+the line also carries the weak 1M-per-GPU run and the step + RCCL gather of obs /
+reward / done to rank 0 (north_star's optional learner gather) in `extra_lines`.
+--scaling weak makes the weak run the headline.  Rank 0 prints one JSON line.
 """
 import argparse
 import math
@@ -34,14 +38,16 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no spars
 MFMA_F32_PEAK_TFLOPS = 157.3  # dense f32-input MFMA (= the f32 vector peak), MI355X_MICROARCH.md
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=4000)
     p.add_argument("--warmup", type=int, default=400)
     p.add_argument("--envs", type=int, default=1 << 20, help="per-GPU env count (weak) or "
                    "global env count (strong)")
-    p.add_argument("--scaling", choices=["strong", "weak"], default="weak")
+    p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                   help="strong (default): --envs is the global env count split over the GPUs "
+                        "(BASELINE configs[2]); weak: --envs per GPU")
     p.add_argument("--launch", choices=["graph", "eager"], default="graph")
     p.add_argument("--graph-len", type=int, default=64, help="steps per captured hipGraph")
     p.add_argument("--ring", type=int, default=16, help="rollout-ring slots for actions/obs")
@@ -77,7 +83,13 @@ def parse():
                         "16384 / 32768 / 49152 force 1 / 2 / 4 tiles per PMSM / HR workgroup)")
     p.add_argument("--max-episode-steps", type=int, default=0,
                    help="TimeLimit truncation (auto-reset inside the kernel); 0 = none")
-    return p.parse_args()
+    p.add_argument("--integrator", choices=["euler", "rk4"], default="euler",
+                   help="euler = the reference's (dynamic.py:70-75); rk4 = the opt-in RK4 mode "
+                        "of lorenz3 / lorenz4 (lz_config.integrator)")
+    p.add_argument("--no-gather", action="store_true",
+                   help="N > 1: skip the step + gather-to-rank-0 extra line")
+    p.add_argument("--probe-ranks", action="store_true", help=argparse.SUPPRESS)
+    return p.parse_args(argv)
 
 
 def _cpu_worker(kind, seconds):
@@ -232,29 +244,35 @@ def step_tiles(system, n, f64=False, num_cus=256, variant=0):
     return 4 if 4 * groups > 3 * full and groups <= full else 1
 
 
-def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=0):
+def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=0,
+                integrator="euler"):
     """Mangled name of the dominant kernel (lz_kernels.hip launch_all / launch_rollout_d).
     no_done: a rollout launch that cannot produce a done (LORENZ3 without a TimeLimit)
-    runs the done-free instantiation (kNoDone = true)."""
+    runs the done-free instantiation (kNoDone = true).  integrator "rk4": SysL3RK4 /
+    SysL4RK4 (lz_systems.h), which take the generic launcher bounds."""
     tag = SYSTEM_INFO[system][1]
     if f64:
         tag = tag.replace("IfEEf", "IdEEd")
-    sysname = ("7" if system == "pmsm" else "5") + tag
+    rk4 = integrator == "rk4" and system in ("lorenz3", "lorenz4")
+    if rk4:
+        tag = tag.replace("I", "RK4I", 1)
+    name = tag[: tag.index("I")] if "I" in tag else tag[: tag.index("E")]
+    sysname = str(len(name)) + tag
     if mode != "rollout":
         tiles = step_tiles(system, n, f64, num_cus, variant)
         if tiles > 1:  # k_step_multi<Sys, T, E, kDoneT = false>
             return "_ZN2lz12k_step_multiINS_%sLi%dELb0EEEvNS_5KArgsE" % (sysname, tiles)
         return "_ZN2lz6k_stepINS_%sLi0EEEvNS_5KArgsE" % sysname
     D = 7  # kDmaDist
-    b = "Lb%dE" % int(no_done and system == "lorenz3")
+    b = "Lb%dE" % int(no_done and system == "lorenz3")  # (SysL3RK4 never terminates either)
     # lz_kernels.hip launch_rollout_d: one-wave workgroups below 256 x CUs envs for
     # LORENZ3 f32 (3/4 of that for LORENZ4 f32, 131,072 for the others); two lanes per env for LORENZ3
     # f32 from 32,768; temporal done stores by default (split SV = 1, k_rollout kDoneT = true)
-    one_wave_below = (256 * num_cus if system == "lorenz3" and not f64
-                      else 256 * num_cus * 3 // 4 if system == "lorenz4" and not f64
+    one_wave_below = (256 * num_cus if system == "lorenz3" and not f64 and not rk4
+                      else 256 * num_cus * 3 // 4 if system == "lorenz4" and not f64 and not rk4
                       else 2 * 256 * 256)
     if n < one_wave_below:
-        if system == "lorenz3" and not f64 and n >= 32768:
+        if system == "lorenz3" and not f64 and not rk4 and n >= 32768:
             return "_ZN2lz15k_rollout_splitINS_%sLi2ELi%dE%sLi1EEEvNS_5KArgsE" % (sysname, D, b)
         return "_ZN2lz9k_rolloutINS_%sLi64ELi%dE%sLb1EEEvNS_5KArgsE" % (sysname, D, b)
     return "_ZN2lz9k_rolloutINS_%sLi256ELi%dE%sLb1EEEvNS_5KArgsE" % (sysname, D, b)
@@ -586,6 +604,141 @@ def fp64_line(args, gl, nat, torch, dist, device, n):
     }
 
 
+# FLOP per env-step of the RK4 mode (lz_systems.h SysL3RK4 / SysL4RK4): 4 RHS evaluations
+# (L3: 9 FLOP, L4: 4 x 12 = 2 systems), 3 stage inputs, 2 stage accumulations and the final
+# combination per component, then the observation RHS, the reward (and L3's clip + action)
+RK4_FLOP = {"lorenz3": 4 * 9 + 3 * 6 + 2 * 6 + 3 * 4 + 9 + 6 + 6,
+            "lorenz4": 2 * (4 * 12 + 3 * 8 + 2 * 8 + 4 * 3) + 2 * 12 + 8 + 8}
+
+
+def rk4_line(args, gl, nat, torch, dist, device, n):
+    """The headline step with the opt-in RK4 integrator (lz_config.integrator = RK4;
+    north_star's "RK4 substages in registers"): the same 65 B per env-step, ~4x the FLOP
+    (still < 2 FLOP/B: HBM-bound).  Bit-exact vs the oracle restatement (the reference
+    has no RK4 Lorenz: parity unpinned, tests/test_gpu_rk4.py)."""
+    env = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=0, autoreset=True,
+                        device=device.index, integrator="rk4")
+    tm = measure_steps(args, torch, dist, nat, env, device, 1, 0, False)
+    bytes_step = env.info.bytes_per_env_step
+    launch_s = tm["ev_ms"] / 1e3 / tm["launches"]
+    achieved = bytes_step * n / launch_s / 1e9
+    kname = kernel_name("lorenz3", "step", n, integrator="rk4")
+    env.close()
+    line = {
+        "metric": METRIC + " (integrator=rk4, opt-in mode)",
+        "value": n * tm["steps"] * tm["windows"] / tm["elapsed"], "unit": "env-steps/s",
+        "steps": tm["steps"], "ms_per_step": tm["elapsed"] * 1e3 / (tm["steps"] * tm["windows"]),
+        "dtype": "f32",
+        "config": {"workload": "dynamic.py 3-state Lorenz env step with the RK4 integrator "
+                               "(lz_step, float32, 4 RHS stages in registers), %d envs on 1 GPU" % n,
+                   "integrator": "rk4", "launch": describe_launches(tm, False)},
+        "timing": tm["timing"],
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": kname,
+                     "avg_launch_us": launch_s * 1e6, "bytes_per_env_step": bytes_step,
+                     "flop_per_env_step": RK4_FLOP["lorenz3"]},
+    }
+    traffic = load_traffic(kname, n)
+    if traffic is not None:
+        line["roofline"]["traffic"] = traffic["bytes_per_launch"]
+        line["roofline"]["traffic_source"] = traffic["source"]
+    return line
+
+
+def scaling_line(args, gl, nat, torch, dist, device, world, rank):
+    """N > 1: the headline step in the other scaling mode (the weak 1,048,576-per-GPU run
+    next to the strong 1M-total headline, or the reverse with --scaling weak)."""
+    from gym_lorenz.parallel import shard_bounds
+
+    if args.scaling == "strong":
+        mode, n = "weak", args.envs
+        total, start = n * world, rank * n
+    else:
+        mode, total = "strong", args.envs
+        start, n = shard_bounds(total, rank, world)
+    env = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=0, global_env_offset=start,
+                        autoreset=True, device=device.index)
+    tm = measure_steps(args, torch, dist, nat, env, device, world, rank, False)
+    launch_s = tm["ev_ms"] / 1e3 / tm["launches"]
+    achieved = env.info.bytes_per_env_step * n / launch_s / 1e9
+    env.close()
+    return {
+        "metric": METRIC + " (%s scaling)" % mode,
+        "value": total * tm["steps"] * tm["windows"] / tm["elapsed"], "unit": "env-steps/s",
+        "n_gpus": world, "scaling": mode, "steps": tm["steps"],
+        "ms_per_step": tm["elapsed"] * 1e3 / (tm["steps"] * tm["windows"]), "dtype": "f32",
+        "config": {"workload": "dynamic.py env step (lz_step, fp32), %d envs total, %d per GPU"
+                               % (total, n), "envs_total": total, "envs_per_gpu": n,
+                   "launch": describe_launches(tm, False)},
+        "timing": tm["timing"],
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "avg_launch_us": launch_s * 1e6,
+                     "kernel": kernel_name("lorenz3", "step", n)},
+    }
+
+
+def gather_line(args, gl, nat, torch, dist, device, world, rank, total, n, start, backend,
+                steps=200):
+    """N > 1: north_star's optional learner gather -- every step, lz_step on each rank's
+    shard, then ONE dist.gather of the shard's packed obs | reward | done bytes into rank
+    0 (RCCL over xGMI with the default backend: send / recv pairs into rank 0's links).
+    Timed as `steps` whole steps (barrier + synchronize on both sides, MAX over ranks);
+    the gather alone is timed the same way for its bytes/s."""
+    from gym_lorenz.parallel import shard_counts
+
+    counts = shard_counts(total, world)
+    if len(set(counts)) != 1:
+        return {"metric": "step + gather to rank 0", "skipped": "unequal shards %s" % counts}
+    env = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=0, global_env_offset=start,
+                        autoreset=True, device=device.index, compact=False)
+    env.reset()
+    a = torch.rand((n, 3), device=device) * 2 - 1
+    host = backend != "nccl"  # gloo rehearsal: the collective runs on host copies
+    src = env.packed if not host else torch.empty(env.packed.shape, dtype=torch.uint8)
+    bufs = [torch.empty_like(src) for _ in range(world)] if rank == 0 else None
+    nbytes = env.packed.numel()
+
+    def gather():
+        if host:
+            src.copy_(env.packed)
+        dist.gather(src, gather_list=bufs, dst=0)
+
+    def timed(fn, k):
+        dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        dist.barrier()
+        t = torch.tensor([t1 - t0], dtype=torch.float64, device=device if not host else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def both():
+        env.step(a, want_n_done=False)
+        gather()
+
+    timed(both, 10)
+    t_both = timed(both, steps)
+    t_gather = timed(gather, steps)
+    env.close()
+    return {
+        "metric": "env-steps/s with the per-step gather of obs | reward | done to rank 0",
+        "value": total * steps / t_both, "unit": "env-steps/s", "n_gpus": world, "steps": steps,
+        "ms_per_step": t_both * 1e3 / steps, "dtype": "f32",
+        "gather": {"us_per_step": t_gather * 1e6 / steps, "bytes_per_step": world * nbytes,
+                   "GB_per_s": world * nbytes * steps / t_gather / 1e9,
+                   "backend": "RCCL (xGMI)" if not host else "%s on host copies (rehearsal)" % backend,
+                   "collective": "one torch.distributed.gather of each rank's packed obs|reward|done "
+                                 "(%d B) into rank 0" % nbytes},
+        "config": {"workload": "dynamic.py env step (lz_step, fp32) + gather to rank 0, %d envs "
+                               "total, %d per GPU" % (total, n),
+                   "envs_total": total, "envs_per_gpu": n},
+    }
+
+
 def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min_window_s=0.2):
     """Time EXACTLY K env steps (K = --steps; rollout mode: --steps rounded down to whole
     --K launches), each timed window bracketed by a barrier + torch.cuda.synchronize()
@@ -740,17 +893,80 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
     }
 
 
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n, port, base=None):
+    """The torch.distributed.run environment of each of n rank processes on one node."""
+    base = dict(os.environ if base is None else base)
+    out = []
+    for r in range(n):
+        e = dict(base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                  "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                  "MASTER_PORT": str(port), "TORCHELASTIC_RUN_ID": "bench-self-spawn"})
+        out.append(e)
+    return out
+
+
+def spawn_ranks(n, argv):
+    """`--gpus N` without a launcher: run this script as N child processes (rank r on
+    cuda:r), the same arguments, before this process touches torch or the GPU.  Children
+    inherit stdout / stderr (rank 0 prints the JSON line); if one fails the others are
+    terminated (their exact PIDs).  Returns the exit status."""
+    import subprocess
+
+    envs = rank_envs(n, free_port())
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e)
+             for e in envs]
+    status = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                status = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except Exception:  # noqa: BLE001
+                p.kill()
+    return status
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if args.probe_ranks:  # launcher test: this rank's environment, nothing else
+        if os.environ.get("LZ_BENCH_PROBE_FAIL_RANK") == os.environ.get("RANK"):
+            sys.exit(3)
+        if os.environ.get("LZ_BENCH_PROBE_FAIL_RANK") is not None:
+            time.sleep(60)  # a healthy rank still running when another fails
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE",
+                                                          "MASTER_ADDR", "MASTER_PORT")}), flush=True)
+        return
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1 and args.gpus > 1:
-        raise SystemExit("--gpus %d needs torch.distributed.run with %d processes"
-                         % (args.gpus, args.gpus))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     headline = args.system == "lorenz3" and args.mode == "step"
     cpu = None
     if rank == 0 and world == 1 and headline and not args.no_cpu_baseline:
@@ -780,6 +996,8 @@ def main():
         total = n * world
         start = rank * n
     kw = {"add_noise": True, "alpha": 0.5} if args.system == "pmsm" else {}
+    if args.integrator == "rk4" and args.system in ("lorenz3", "lorenz4"):
+        kw["integrator"] = "rk4"
     env = gl.BatchedEnv(args.system, n, dtype="float32", seed=0, global_env_offset=start,
                         autoreset=True, device=local, max_episode_steps=args.max_episode_steps,
                         variant=args.variant, **kw)
@@ -818,13 +1036,14 @@ def main():
     achieved = bytes_step * n * T / launch_s / 1e9
     ref_env = SYSTEM_INFO[args.system][0]
     launch_desc = describe_launches(tm, rollout)
+    integ = " [integrator=rk4: the opt-in RK4 mode, not the reference's Euler]" if "integrator" in kw else ""
     if rollout:
-        workload = ("%s: %d-step fused on-device rollout (lz_rollout, fp32, state in VGPRs), "
+        workload = ("%s%s: %d-step fused on-device rollout (lz_rollout, fp32, state in VGPRs), "
                     "%d envs total, %d per GPU, time-major [K,N,.] rollout buffers"
-                    % (ref_env, T, total, n))
+                    % (ref_env, integ, T, total, n))
     else:
-        workload = ("%s step (lz_step, fp32), %d envs total, %d per GPU, actions/obs/reward/"
-                    "done in a %d-slot on-device rollout ring" % (ref_env, total, n, R))
+        workload = ("%s%s step (lz_step, fp32), %d envs total, %d per GPU, actions/obs/reward/"
+                    "done in a %d-slot on-device rollout ring" % (ref_env, integ, total, n, R))
     out = {
         "metric": METRIC,
         "value": total * K * tm["windows"] / elapsed,
@@ -852,7 +1071,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
             "kernel": kernel_name(args.system, args.mode, n, no_done=args.max_episode_steps == 0,
                                   num_cus=torch.cuda.get_device_properties(device).multi_processor_count,
-                                  variant=args.variant),
+                                  variant=args.variant, integrator=kw.get("integrator", "euler")),
             "avg_launch_us": launch_s * 1e6,
             "bytes_per_env_step": bytes_step,
             "note": "achieved = algorithmic bytes per launch (bytes_per_env_step x envs_per_gpu"
@@ -867,14 +1086,28 @@ def main():
     else:
         out["roofline"]["traffic_note"] = ("null: no committed PMC summary for this kernel "
                                            "build (code hash) and shard size")
-    headline = args.system == "lorenz3" and not rollout
+    if "integrator" in kw:
+        out["config"]["integrator"] = "rk4"
+        out["roofline"]["flop_per_env_step"] = RK4_FLOP[args.system]
+    headline = args.system == "lorenz3" and not rollout and "integrator" not in kw
+    env.close()
+    extras = []
     if rank == 0 and world == 1 and headline and not args.no_drift:
         out["fp32_drift"] = fp32_drift(gl, torch, device)
-    if rank == 0 and world == 1 and headline and not args.no_extras:
-        out["extra_lines"] = [fp64_line(args, gl, nat, torch, dist, device, n)]
+    if world == 1 and headline and not args.no_extras:
+        extras.append(fp64_line(args, gl, nat, torch, dist, device, n))
+        extras.append(rk4_line(args, gl, nat, torch, dist, device, n))
+    if world > 1 and headline and not args.no_extras:
+        # the other scaling mode at the same N, then the learner gather (every rank runs
+        # these: they time collectively)
+        extras.append(scaling_line(args, gl, nat, torch, dist, device, world, rank))
+        if not args.no_gather:
+            extras.append(gather_line(args, gl, nat, torch, dist, device, world, rank, total, n,
+                                      start, backend))
+    if extras and rank == 0:
+        out["extra_lines"] = extras
     if cpu is not None:
         out["cpu_baseline"] = cpu
-    env.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -103,6 +103,8 @@ struct lz_handle {
   double* ps_tiles;
   float* ps_term;
   int32_t* ps_cursor;
+  int32_t ps_next_k;   // the step lz_policy_step_f32 expects next (-1: none, start at 0)
+  uint64_t ps_gen;     // gen right after its previous step
   uint8_t* vn_ws;      // lz_step_vecnorm moment partials (lazily allocated)
   int vn_pending;      // lz_step_vecnorm left totals for lz_vecnorm_apply's updates
   int32_t* vn_nd_out;  // lz_step_vecnorm's n_done_out, published by lz_vecnorm_apply
@@ -209,6 +211,11 @@ lz_status lz_create(const lz_config* cfg_in, lz_handle** out) {
   if (cfg.global_env_offset < 0 || cfg.global_env_offset + cfg.num_envs > (int64_t(1) << 40))
     return fail(LZ_ERR_INVALID, "global env ids must lie in [0, 2^40)");
   if (cfg.max_episode_steps < 0) return fail(LZ_ERR_INVALID, "max_episode_steps < 0");
+  if (cfg.integrator != LZ_INT_EULER && cfg.integrator != LZ_INT_RK4)
+    return fail(LZ_ERR_INVALID, "unknown integrator %d", cfg.integrator);
+  if (cfg.integrator == LZ_INT_RK4 && cfg.system != LZ_SYS_LORENZ3 && cfg.system != LZ_SYS_LORENZ4 &&
+      cfg.system != LZ_SYS_HR)
+    return fail(LZ_ERR_UNSUPPORTED, "the RK4 integrator mode is LORENZ3 / LORENZ4 only (HR is RK4 already)");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (cfg.device < 0 || cfg.device >= ndev)
@@ -402,6 +409,13 @@ lz_status lz_sync(lz_handle* h) {
   return LZ_OK;
 }
 
+// the launchers' system argument: the system, + kSysRK4 for the RK4 integrator mode
+static int sys_key(const lz_handle* h) {
+  const int s = h->cfg.system;
+  return (h->cfg.integrator == LZ_INT_RK4 && (s == LZ_SYS_LORENZ3 || s == LZ_SYS_LORENZ4)) ? s + lz::kSysRK4
+                                                                                            : s;
+}
+
 static void fill_common(const lz_handle* h, KArgs& a) {
   std::memset(&a, 0, sizeof a);
   for (int p = 0; p < lz::kMaxPlanes; ++p) a.pl[p] = h->planes[p];
@@ -436,7 +450,7 @@ lz_status lz_reset(lz_handle* h, const uint8_t* mask, const void* init, void* ob
   a.mask = mask;
   a.init = init;
   a.obs = obs_out;
-  const int e = lz::launch_reset(h->cfg.system, h->f64, a, h->stream);
+  const int e = lz::launch_reset(sys_key(h), h->f64, a, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "reset launch: %s", hipGetErrorString((hipError_t)e));
   h->parity ^= 1;
   ++h->gen;
@@ -469,7 +483,7 @@ lz_status lz_step(lz_handle* h, const void* actions, const double* noise, void* 
   // full 256-env blocks start at 256*A*4 / 256*O*sizeof(T) byte offsets: only the
   // base pointers need 16-B alignment (ragged tail blocks take the scalar path)
   a.vec_ok = (!needs_act || aligned16(actions)) && aligned16(obs_out);
-  const int e = lz::launch_step(h->cfg.system, h->f64, a, h->stream);
+  const int e = lz::launch_step(sys_key(h), h->f64, a, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "step launch: %s", hipGetErrorString((hipError_t)e));
   if (n_done_out)
     HIP_TRY(hipMemcpyAsync(n_done_out, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
@@ -562,8 +576,18 @@ struct RsServer {
   int64_t* cmds;         // the command line: word k = member k's last posted request
                          // (mapped, coherent host memory, one 128-B line)
   const int64_t* cmds_dev;
-  uint64_t idle;         // idle exit, wall-clock ticks
+  int khz;               // wall-clock rate (ticks per ms)
 };
+
+// The idle exit in wall-clock ticks, read from LZ_RESIDENT_IDLE_US at every launch (so a
+// process can change it between launches): short by default -- a device-wide synchronize
+// (torch.cuda.synchronize()) waits for the idle exit, and a caller that leaves > 1 ms
+// between steps pays one relaunch (~20 us)
+static uint64_t rs_idle_ticks(const RsServer& sv) {
+  const char* e = std::getenv("LZ_RESIDENT_IDLE_US");
+  const double us = e ? std::atof(e) : 1000.0;
+  return (uint64_t)((us > 0 ? us : 1000.0) * sv.khz / 1000.0);
+}
 static std::mutex g_rs_mu;  // trivially destructible
 static RsServer g_rs[kRsMaxDevices];
 
@@ -597,17 +621,13 @@ static lz_status rs_server_init(RsServer& sv, int device) {
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0)
     khz = 100000;
-  const char* e = std::getenv("LZ_RESIDENT_IDLE_US");
-  // short: a device-wide synchronize (torch.cuda.synchronize()) waits for the idle exit,
-  // and a caller that leaves > 1 ms between steps pays one relaunch (~20 us)
-  const double idle_us = e ? std::atof(e) : 1000.0;
   sv.stream = st;
   sv.ev = ev;
   sv.table_host = th;
   sv.table_dev = td;
   sv.cmds = cmds;
   sv.cmds_dev = static_cast<const int64_t*>(cmds_dev);
-  sv.idle = (uint64_t)(idle_us * khz / 1000.0);
+  sv.khz = khz;
   sv.n = 0;
   sv.active = false;
   sv.init = true;
@@ -663,7 +683,7 @@ static lz_status rs_server_launch(RsServer& sv) {
     lz::ResMember& r = sv.table_host[i];
     std::memset(&r, 0, sizeof r);
     fill_common(m, r.a);
-    r.system = m->cfg.system;
+    r.system = sys_key(m);
     r.f64 = m->f64;
     lz::ResBox& box = r.box;
     m->rs_slot = i;
@@ -687,7 +707,7 @@ static lz_status rs_server_launch(RsServer& sv) {
   }
   HIP_TRY(hipMemcpyAsync(sv.table_dev, sv.table_host, sizeof(lz::ResMember) * sv.n,
                          hipMemcpyHostToDevice, sv.stream));
-  const int e = lz::launch_resident_multi(sv.table_dev, sv.n, sv.idle, sv.stream);
+  const int e = lz::launch_resident_multi(sv.table_dev, sv.n, rs_idle_ticks(sv), sv.stream);
   if (e != 0) return fail(LZ_ERR_HIP, "resident launch: %s", hipGetErrorString((hipError_t)e));
   sv.active = true;
   for (int i = 0; i < sv.n; ++i) sv.members[i]->rs_active = true;
@@ -895,7 +915,7 @@ lz_status lz_step_vecnorm(lz_handle* h, const lz_vecnorm* vn, const void* action
   v.gamma = vn->gamma;
   v.flags = vn->flags;
   v.n_wg = (int32_t)n_wg;
-  const int e = lz::launch_step_vecnorm(h->cfg.system, h->f64, a, v, h->stream);
+  const int e = lz::launch_step_vecnorm(sys_key(h), h->f64, a, v, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "step launch: %s", hipGetErrorString((hipError_t)e));
   h->parity ^= 1;
   ++h->gen;
@@ -995,7 +1015,7 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
   a.K = K;
   a.tick_adv = (uint64_t)K;
   a.vec_ok = (!needs_act || aligned16(actions)) && aligned16(obs_out) && (a.n % 4 == 0);
-  const int e = lz::launch_rollout(h->cfg.system, h->f64, a, h->stream);
+  const int e = lz::launch_rollout(sys_key(h), h->f64, a, h->stream);
   if (e != 0) return fail(LZ_ERR_HIP, "rollout launch: %s", hipGetErrorString((hipError_t)e));
   if (n_done_out)
     HIP_TRY(hipMemcpyAsync(n_done_out, a.counter, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
@@ -1031,6 +1051,8 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
   }
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_rollout_policy before the first lz_reset");
   if (h->f64) return fail(LZ_ERR_UNSUPPORTED, "the policy rollout runs float32 handles only");
+  if (sys_key(h) != h->cfg.system)
+    return fail(LZ_ERR_UNSUPPORTED, "the policy rollouts run the reference's Euler integrator only");
   if (r->K <= 0) return fail(LZ_ERR_INVALID, "K must be >= 1");
   if (!r->blob || !r->obs_in || !r->obs_last || !r->obs_buf || !r->act_buf || !r->logp_buf ||
       !r->val_buf || !r->rew_buf || !r->done_buf || !r->last_values)
@@ -1123,6 +1145,8 @@ lz_status lz_policy_step_f32(lz_handle* h, const lz_policy_rollout_args* r, int3
   RESIDENT_QUIESCE(h);
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_policy_step_f32 before the first lz_reset");
   if (h->f64) return fail(LZ_ERR_UNSUPPORTED, "the policy rollout runs float32 handles only");
+  if (sys_key(h) != h->cfg.system)
+    return fail(LZ_ERR_UNSUPPORTED, "the policy rollouts run the reference's Euler integrator only");
   if (r->K <= 0) return fail(LZ_ERR_INVALID, "K must be >= 1");
   if (k < 0 || k > r->K) return fail(LZ_ERR_INVALID, "step %d outside [0, K = %d]", k, r->K);
   if (!obs_rms_state) return fail(LZ_ERR_INVALID, "obs_rms_state must be non-NULL");
@@ -1157,6 +1181,17 @@ lz_status lz_policy_step_f32(lz_handle* h, const lz_policy_rollout_args* r, int3
     h->ps_term = term;
     h->ps_cursor = cur;
   }
+  // one collect = k = 0 .. K in order with no other launch on the handle in between: the
+  // raw terminal-obs carry (ps_term), the collect's done cursor and the RNG tick parity
+  // are carried from step to step
+  if (k > 0 && (k != h->ps_next_k || h->gen != h->ps_gen)) {
+    const int32_t want = h->ps_next_k;
+    h->ps_next_k = -1;
+    return fail(LZ_ERR_STATE,
+                "lz_policy_step_f32: step %d out of order (expected %d, or another launch on the "
+                "handle came in between); a collect calls k = 0 .. K in order",
+                k, want);
+  }
   const bool fin = k == r->K;
   if (k == 0) HIP_TRY(hipMemsetAsync(h->ps_cursor, 0, 2 * sizeof(int32_t), h->stream));
   const lz::PolShape sh = lz::f32_policy_shape(n, h->num_cus, h->cfg.reserved[0]);
@@ -1170,7 +1205,8 @@ lz_status lz_policy_step_f32(lz_handle* h, const lz_policy_rollout_args* r, int3
   a.term_cap = r->cap;
   a.K = r->K;
   a.counter = h->ps_cursor;       // one cursor for the whole collect (zeroed at k = 0)
-  a.counter_next = h->ps_cursor + 1;
+  // a step launch flips the parity (below): it zeroes the cursor slot the handle's next
+  // ordinary launch reads, as every other launch does (fill_common's counter_next)
   lz::PArgs p;
   std::memset(&p, 0, sizeof p);
   p.blob = static_cast<const uint8_t*>(r->blob);
@@ -1201,11 +1237,15 @@ lz_status lz_policy_step_f32(lz_handle* h, const lz_policy_rollout_args* r, int3
   if (!fin) {
     h->parity ^= 1;  // the launch advanced the RNG tick by one (ping-pong)
     ++h->gen;
+    h->ps_next_k = k + 1;
+    h->ps_gen = h->gen;
     e = lz::launch_vn_tile_update(st.tiles, ntiles, O, (double)n, st.snap, obs_rms_state, moments_out,
                                   h->stream);
     if (e != 0) return fail(LZ_ERR_HIP, "statistics update launch: %s", hipGetErrorString((hipError_t)e));
-  } else if (r->n_done) {
-    HIP_TRY(hipMemcpyAsync(r->n_done, h->ps_cursor, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
+  } else {
+    h->ps_next_k = -1;
+    if (r->n_done)
+      HIP_TRY(hipMemcpyAsync(r->n_done, h->ps_cursor, sizeof(int32_t), hipMemcpyDeviceToDevice, h->stream));
   }
   return LZ_OK;
 }

@@ -317,6 +317,11 @@ int launch_vn_apply(int f64, int O, int64_t n, const void* obs, const void* rew,
                     uint8_t* dones, float* term_n, const VnUpdate& upd, const int32_t* counter,
                     int32_t* n_done_out, void* stream);
 
+// The integrator picks the system's instantiation: the launchers' `system` argument is
+// lz_config.system + kSysRK4 for an LZ_INT_RK4 handle of LORENZ3 / LORENZ4 (SysL3RK4 /
+// SysL4RK4, lz_systems.h), else lz_config.system.
+constexpr int kSysRK4 = 256;
+
 // record the thread-local message lz_last_error() returns; returns s
 lz_status set_error(lz_status s, const char* msg);
 

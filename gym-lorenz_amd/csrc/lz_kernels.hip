@@ -1053,6 +1053,12 @@ static int dispatch(int which, int system, int f64, const KArgs& a, void* stream
     case LZ_SYS_LORENZ4:
       return f64 ? launch_all<SysL4<double>, double>(which, a, s)
                  : launch_all<SysL4<float>, float>(which, a, s);
+    case LZ_SYS_LORENZ3 + kSysRK4:
+      return f64 ? launch_all<SysL3RK4<double>, double>(which, a, s)
+                 : launch_all<SysL3RK4<float>, float>(which, a, s);
+    case LZ_SYS_LORENZ4 + kSysRK4:
+      return f64 ? launch_all<SysL4RK4<double>, double>(which, a, s)
+                 : launch_all<SysL4RK4<float>, float>(which, a, s);
     case LZ_SYS_PMSM:
       return launch_all<SysPMSM, float, true>(which, a, s);
     case LZ_SYS_HR:
@@ -1248,6 +1254,14 @@ __global__ __launch_bounds__(64 * kWaves) void k_resident_multi(
     case LZ_SYS_LORENZ3 * 2 + 1: resident_serve<SysL3<double>, double>(m, wave, &sh, s_nz[wave]); break;
     case LZ_SYS_LORENZ4 * 2: resident_serve<SysL4<float>, float>(m, wave, &sh, s_nz[wave]); break;
     case LZ_SYS_LORENZ4 * 2 + 1: resident_serve<SysL4<double>, double>(m, wave, &sh, s_nz[wave]); break;
+    case (LZ_SYS_LORENZ3 + kSysRK4) * 2: resident_serve<SysL3RK4<float>, float>(m, wave, &sh, s_nz[wave]); break;
+    case (LZ_SYS_LORENZ3 + kSysRK4) * 2 + 1:
+      resident_serve<SysL3RK4<double>, double>(m, wave, &sh, s_nz[wave]);
+      break;
+    case (LZ_SYS_LORENZ4 + kSysRK4) * 2: resident_serve<SysL4RK4<float>, float>(m, wave, &sh, s_nz[wave]); break;
+    case (LZ_SYS_LORENZ4 + kSysRK4) * 2 + 1:
+      resident_serve<SysL4RK4<double>, double>(m, wave, &sh, s_nz[wave]);
+      break;
     case LZ_SYS_PMSM * 2: resident_serve<SysPMSM, float>(m, wave, &sh, s_nz[wave]); break;
     case LZ_SYS_HR * 2: resident_serve<SysHR<float>, float>(m, wave, &sh, s_nz[wave]); break;
     case LZ_SYS_HR * 2 + 1: resident_serve<SysHR<double>, double>(m, wave, &sh, s_nz[wave]); break;
@@ -1320,6 +1334,10 @@ int launch_step_vecnorm(int system, int f64, const KArgs& a, const VArgs& v, voi
       return f64 ? launch_vn<SysL3<double>, double>(a, v, s) : launch_vn<SysL3<float>, float>(a, v, s);
     case LZ_SYS_LORENZ4:
       return f64 ? launch_vn<SysL4<double>, double>(a, v, s) : launch_vn<SysL4<float>, float>(a, v, s);
+    case LZ_SYS_LORENZ3 + kSysRK4:
+      return f64 ? launch_vn<SysL3RK4<double>, double>(a, v, s) : launch_vn<SysL3RK4<float>, float>(a, v, s);
+    case LZ_SYS_LORENZ4 + kSysRK4:
+      return f64 ? launch_vn<SysL4RK4<double>, double>(a, v, s) : launch_vn<SysL4RK4<float>, float>(a, v, s);
     case LZ_SYS_PMSM:
       return launch_vn<SysPMSM, float>(a, v, s);
     case LZ_SYS_HR:

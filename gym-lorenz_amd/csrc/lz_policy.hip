@@ -1368,7 +1368,12 @@ __global__ __launch_bounds__(W * 64) void k_policy_step_f32(KArgs a, PArgs p, PS
   // S_k for the update after this launch (read-only there: no race with the write-back)
   if (blockIdx.x == 0 && s.snap && tid < 2 * O + 1) s.snap[tid] = p.norm[tid];
   const uint64_t tick = *a.tick_in;
-  if (blockIdx.x == 0 && tid == 0 && !s.final_) *a.tick_out = tick + 1;
+  // a step launch flips the handle's call parity: advance the tick and zero the done
+  // cursor the handle's next launch (outside the collect) starts from
+  if (blockIdx.x == 0 && tid == 0 && !s.final_) {
+    *a.tick_out = tick + 1;
+    *a.counter_next = 0;
+  }
   __syncthreads();
   const uint8_t* pi_net = s_blob;
   const uint8_t* vf_net = s_blob + kF32Net;

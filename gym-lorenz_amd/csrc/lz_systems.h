@@ -203,6 +203,88 @@ struct SysL4 {
 };
 
 // ===========================================================================
+// LZ_INT_RK4 (lz_config.integrator): the classical RK4 step of HRSyncEnv
+// (lorenz_env_try.py:100-113 -- k1 = f(s), k2 = f(s + dt/2 k1), k3 = f(s + dt/2 k2),
+// k4 = f(s + dt k3), s += (dt/6.0) (((k1 + 2 k2) + 2 k3) + k4), python-float dt/2 and
+// dt/6.0) on the LORENZ3 / LORENZ4 right-hand sides.  The four stages stay in
+// registers, the stage sum accumulated as the stages complete (SysHR::rk4's order: the
+// same operations, one stage live).  LORENZ3 keeps dynamic.py:73-75's additive action
+// after the integration step: s' = (s + h6 sum) + u.  Everything else (reset, obs,
+// reward, done) is the Euler system's.  No reference oracle exists (the reference's
+// Lorenz envs are Euler only): oracle/lz_oracle.c orc_l3_step_rk4 / orc_l4_step_rk4
+// restate this arithmetic.
+// ===========================================================================
+template <typename T>
+struct SysL3RK4 : SysL3<T> {
+  using B = SysL3<T>;
+  T h2, h6;
+  __device__ void setup(const KArgs& a) {
+    B::setup(a);
+    h2 = (T)(a.prm[3] / 2);    // python dt/2
+    h6 = (T)(a.prm[3] / 6.0);  // python dt/6.0
+  }
+  __device__ void f(T x, T y, T z, T& fx, T& fy, T& fz) const {  // dynamic.py:70-72
+    fx = B::sg * (y - x);
+    fy = (B::rh * x - y) - x * z;
+    fz = x * y - B::be * z;
+  }
+  __device__ bool step(const float* act, bool, const double*, T* o, T& rew, const KArgs&) {
+    const T cl = B::cl;
+    const T u1 = clip_nz((T)act[0], -cl, cl), u2 = clip_nz((T)act[1], -cl, cl),
+            u3 = clip_nz((T)act[2], -cl, cl);
+    const T x = B::x, y = B::y, z = B::z;
+    T kx, ky, kz, ax, ay, az;
+    f(x, y, z, kx, ky, kz);                                               // k1
+    ax = kx; ay = ky; az = kz;
+    f(x + h2 * kx, y + h2 * ky, z + h2 * kz, kx, ky, kz);                 // k2
+    ax = ax + (T)2 * kx; ay = ay + (T)2 * ky; az = az + (T)2 * kz;
+    f(x + h2 * kx, y + h2 * ky, z + h2 * kz, kx, ky, kz);                 // k3
+    ax = ax + (T)2 * kx; ay = ay + (T)2 * ky; az = az + (T)2 * kz;
+    f(x + B::dt * kx, y + B::dt * ky, z + B::dt * kz, kx, ky, kz);        // k4
+    B::x = (x + h6 * (ax + kx)) + u1;                                     // + u: :73-75
+    B::y = (y + h6 * (ay + ky)) + u2;
+    B::z = (z + h6 * (az + kz)) + u3;
+    B::reset_obs(o);                                                      // :77-83
+    rew = -((((T)0 + fabs(o[0])) + fabs(o[1])) + fabs(o[2]));             // :84
+    return false;
+  }
+};
+
+template <typename T>
+struct SysL4RK4 : SysL4<T> {
+  using B = SysL4<T>;
+  T h2, h6;
+  __device__ void setup(const KArgs& a) {
+    B::setup(a);
+    h2 = (T)(a.prm[3] / 2);
+    h6 = (T)(a.prm[3] / 6.0);
+  }
+  __device__ void rk4(T* x) const {
+    T k[4], acc[4], y[4];
+    B::rhs(x, k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { acc[j] = k[j]; y[j] = x[j] + h2 * k[j]; }
+    B::rhs(y, k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { acc[j] = acc[j] + (T)2 * k[j]; y[j] = x[j] + h2 * k[j]; }
+    B::rhs(y, k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { acc[j] = acc[j] + (T)2 * k[j]; y[j] = x[j] + B::dt * k[j]; }
+    B::rhs(y, k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = x[j] + h6 * (acc[j] + k[j]);
+  }
+  __device__ bool step(const float*, bool, const double*, T* o, T& rew, const KArgs&) {
+    rk4(B::m);                                                            // master
+    rk4(B::s);                                                            // slave
+    B::reset_obs(o);                                                      // :333-362
+    const T r = -(((((T)0 + fabs(o[0])) + fabs(o[1])) + fabs(o[2])) + fabs(o[3]));  // :363
+    rew = r;
+    return r < (T)-1e6;                                                   // :369
+  }
+};
+
+// ===========================================================================
 // PMSM -- lorenz_env_try_pmsm.py:7-187 PMSM_Sync_Env (float32 throughout)
 // params: sigma=5.46, gamma=20, dt=1e-3, f_max=50, lambda_lr=1e-3, beta1=.9,
 //         beta2=.999, eps=1e-8, err_threshold=5, max_steps=2000, term=1000

@@ -23,6 +23,9 @@ LZ_OK, LZ_ERR_INVALID, LZ_ERR_UNSUPPORTED, LZ_ERR_HIP, LZ_ERR_STATE, LZ_ERR_OOM 
 LORENZ3, LORENZ4, PMSM, HR = range(4)
 T1, T2, TP, SC = range(4, 8)  # legacy, unregistered variants
 F32, F64 = 0, 1
+INT_EULER, INT_RK4 = 0, 1  # lz_config.integrator
+INTEGRATORS = {"euler": INT_EULER, "rk4": INT_RK4}
+ABI_VERSION = 2  # include/lorenz_env.h LZ_ABI_VERSION this binding is written against
 FLAG_AUTORESET, FLAG_ADD_NOISE, FLAG_EVAL_MODE, FLAG_ADD_FILTER = 1, 2, 4, 8
 DONE_TERMINATED, DONE_TRUNCATED = 1, 2
 MAX_PARAMS = 16
@@ -57,7 +60,8 @@ class LzConfig(ctypes.Structure):
         ("alpha", ctypes.c_float),
         ("params", ctypes.c_double * MAX_PARAMS),
         ("t_done_step", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 7),
+        ("reserved", ctypes.c_int32 * 6),  # reserved[0]: kernel tuning variant (A/B)
+        ("integrator", ctypes.c_int32),
     ]
 
 
@@ -243,6 +247,9 @@ if len(HIP_RUNTIME) != 1:
         "gym_lorenz: %d HIP runtimes are mapped in this process (%s); torch and "
         "libgym_lorenz_amd.so must share one.  Import torch (or gym_lorenz) before "
         "anything that loads a libamdhip64 directly." % (len(HIP_RUNTIME), ", ".join(HIP_RUNTIME)))
+if not os.environ.get("LZ_LIB_AB") and lib.lz_abi_version() != ABI_VERSION:
+    raise ImportError("gym_lorenz: %s has ABI version %d, this binding expects %d -- rebuild it"
+                      % (LIB_PATH, lib.lz_abi_version(), ABI_VERSION))
 for _name, (_res, _args) in _SIGS.items():
     try:
         _f = getattr(lib, _name)

@@ -31,12 +31,14 @@ class BatchedEnv:
     system's default (off, except the legacy TP / SC whose noise is unconditional).  ``dtype`` is the state /
     observation precision: "float64" reproduces the reference's fp64 arithmetic
     (LORENZ3 / LORENZ4 bit-exactly), "float32" is the fast path.  PMSM is float32.
+    ``integrator``: "euler" (the reference's, default) or "rk4" -- the opt-in RK4 mode of
+    lorenz3 / lorenz4 (lz_config.integrator, BASELINE north_star; no reference oracle).
     """
 
     def __init__(self, system, num_envs, dtype="float32", device=None, seed=0,
                  global_env_offset=0, max_episode_steps=0, autoreset=True, add_noise=None,
                  eval_mode=False, add_filter=False, alpha=None, params=None, compact=True,
-                 variant=0):
+                 variant=0, integrator="euler"):
         self.system = SYSTEMS[system] if isinstance(system, str) else int(system)
         self.system_name = {v: k for k, v in SYSTEMS.items()}[self.system]
         if not torch.cuda.is_available():
@@ -61,6 +63,12 @@ class BatchedEnv:
         if alpha is not None:
             cfg.alpha = float(alpha)
         cfg.reserved[0] = int(variant)  # step-kernel tuning variant (A/B experiments)
+        if isinstance(integrator, str):
+            if integrator not in nat.INTEGRATORS:
+                raise ValueError("integrator must be one of %s" % sorted(nat.INTEGRATORS))
+            integrator = nat.INTEGRATORS[integrator]
+        cfg.integrator = int(integrator)
+        self.integrator = {v: k for k, v in nat.INTEGRATORS.items()}.get(cfg.integrator, "?")
         if params:
             for k, v in (params.items() if isinstance(params, dict) else enumerate(params)):
                 cfg.params[int(k)] = float(v)

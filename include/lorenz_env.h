@@ -81,7 +81,8 @@
 extern "C" {
 #endif
 
-#define LZ_ABI_VERSION 1
+/* 2: lz_get_state / lz_set_state take (indices, count); lz_config.integrator */
+#define LZ_ABI_VERSION 2
 
 typedef enum lz_status {
   LZ_OK = 0,
@@ -105,6 +106,17 @@ typedef enum lz_system {
 } lz_system;
 
 typedef enum lz_dtype { LZ_DTYPE_F32 = 0, LZ_DTYPE_F64 = 1 } lz_dtype;
+
+/* lz_config.integrator.  LZ_INT_EULER is the reference's own integrator for every
+ * system (dynamic.py:70-75 forward Euler; HR is RK4 by definition, lorenz_env_try.py:
+ * 100-113, whatever this field says).  LZ_INT_RK4 is an opt-in mode of LORENZ3 and
+ * LORENZ4 (BASELINE north_star "the dynamic.py RK4 integrator ... RK4 substages in
+ * registers"): the classical four-stage step of HRSyncEnv's stage order (k1 = f(s),
+ * k2 = f(s + dt/2 k1), k3 = f(s + dt/2 k2), k4 = f(s + dt k3),
+ * s += (dt/6.0) (((k1 + 2 k2) + 2 k3) + k4)) applied to the system's own RHS, then the
+ * additive action of dynamic.py:73-75 (LORENZ3).  The reference has no RK4 Lorenz, so
+ * this mode is pinned to the build's own CPU restatement only ("parity unpinned"). */
+typedef enum lz_integrator { LZ_INT_EULER = 0, LZ_INT_RK4 = 1 } lz_integrator;
 
 /* State planes (SoA, one T or int32 element per env) addressable by
  * lz_get_state / lz_set_state.  Reference attribute in brackets. */
@@ -172,7 +184,8 @@ typedef struct lz_config {
    * replays the accumulator; the step index where it fires (-1 = never, which is the
    * case for the reference constants) is stored here by lz_create. Read-only. */
   int32_t t_done_step;
-  int32_t reserved[7];
+  int32_t reserved[6];       /* reserved[0]: kernel tuning variant (A/B experiments) */
+  int32_t integrator;        /* lz_integrator (LZ_INT_EULER = the reference, default) */
 } lz_config;
 
 typedef struct lz_info {
@@ -247,16 +260,18 @@ lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, 
  * body, tick for tick) served by a RESIDENT kernel: one launch per process and device
  * serves every handle that calls this (one wave per handle, up to 15 handles; a
  * DummyVecEnv of several drop-in envs -- code/train.py:98-100 -- shares the one launch
- * and its one stream), keeps each handle's state in registers; each call posts its
- * request into the handle's mailbox in mapped host memory, rings the server's one
- * doorbell word (one poller wave watches it and wakes the handle's wave through LDS) and
- * spins until the reply lands in host memory -- no launch, no stream synchronisation per
- * step.  A
+ * and its one stream), keeps each handle's state in registers; each call writes its
+ * inputs into the handle's mailbox in mapped host memory, then the request number into
+ * the handle's own 8-byte word of the server's command line (one 128-B line, one word
+ * per member handle; -1 in ANY word stops every wave).  One poller wave reads the whole
+ * line with one wave-wide load per poll and hands a changed word to the handle's wave
+ * through LDS; the call spins until the reply lands in host memory -- no launch, no
+ * stream synchronisation per step.  A
  * handle joining the server restarts it (its state goes back to the planes and every
  * handle is relaunched); a 16th handle steps through lz_step_host instead.  Handles of
  * at most 64 envs without LZ_FLAG_AUTORESET (LZ_ERR_UNSUPPORTED otherwise).  The server
- * exits after LZ_RESIDENT_IDLE_US (default 1000) microseconds without a request to ANY
- * of its handles and is relaunched by the next call (a device-wide synchronize waits
+ * exits after LZ_RESIDENT_IDLE_US (default 1000; read at every launch of the server)
+ * microseconds without a request to ANY of its handles and is relaunched by the next call (a device-wide synchronize waits
  * for that exit); every other call on a served handle stops it first (all states go
  * back to the planes), as does lz_resident_stop.  Synchronous: LZ_ERR_STATE while the
  * handle's stream is being captured into a graph. */

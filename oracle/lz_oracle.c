@@ -138,6 +138,78 @@ L4_BODY(double)
 L4_BODY(float)
 
 /* =========================================================================
+ * LZ_INT_RK4 (lz_config.integrator) -- an opt-in mode of LORENZ3 / LORENZ4 that the
+ * reference does NOT have (its Lorenz envs are forward Euler, dynamic.py:70-75): the
+ * classical RK4 step in HRSyncEnv's stage order (lorenz_env_try.py:100-113):
+ *   k1 = f(s); k2 = f(s + dt/2*k1); k3 = f(s + dt/2*k2); k4 = f(s + dt*k3);
+ *   s  = s + (dt/6.0)*(((k1 + 2*k2) + 2*k3) + k4)
+ * with python-float dt/2 and dt/6.0, on the L3 / L4 right-hand sides above; LORENZ3
+ * then adds the clipped action as dynamic.py:73-75 does: s' = (s + ...) + u.  Obs,
+ * reward and done are the Euler steps'.  PARITY UNPINNED against the reference (no RK4
+ * Lorenz exists there); tests/test_oracle_golden.py pins this C code to an independent
+ * vectorised NumPy float64 RK4 of dynamic.py's RHS instead.
+ * ========================================================================= */
+#define RK4_BODY(T, CLIP)                                                            \
+  static inline void l3_rk4_##T(T* s, const T* p, T h2, T h, T h6) {                 \
+    T k1[3], k2[3], k3[3], k4[3], y[3];                                              \
+    l3_rhs_##T(s, k1, p);                                                            \
+    for (int j = 0; j < 3; ++j) y[j] = s[j] + h2 * k1[j];                            \
+    l3_rhs_##T(y, k2, p);                                                            \
+    for (int j = 0; j < 3; ++j) y[j] = s[j] + h2 * k2[j];                            \
+    l3_rhs_##T(y, k3, p);                                                            \
+    for (int j = 0; j < 3; ++j) y[j] = s[j] + h * k3[j];                             \
+    l3_rhs_##T(y, k4, p);                                                            \
+    for (int j = 0; j < 3; ++j)                                                      \
+      s[j] = s[j] + h6 * (((k1[j] + (T)2 * k2[j]) + (T)2 * k3[j]) + k4[j]);           \
+  }                                                                                  \
+  void orc_l3_step_rk4_##T(int64_t n, T* st, const T* act, T* obs, T* rew,           \
+                           const double* pd) {                                       \
+    T p[5]; for (int j = 0; j < 5; ++j) p[j] = (T)pd[j];                             \
+    const T h2 = (T)(pd[3] / 2), h = (T)pd[3], h6 = (T)(pd[3] / 6.0);                \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      T* s = st + 3 * i; T u[3], f[3];                                               \
+      for (int j = 0; j < 3; ++j) u[j] = CLIP(act[3 * i + j], -p[4], p[4]);          \
+      l3_rk4_##T(s, p, h2, h, h6);                                                   \
+      for (int j = 0; j < 3; ++j) s[j] = s[j] + u[j];        /* :73-75's + u */      \
+      l3_rhs_##T(s, f, p);                                                           \
+      T* o = obs + 6 * i;                                                            \
+      for (int j = 0; j < 3; ++j) { o[j] = s[j] - (T)0; o[3 + j] = f[j] - (T)0; }    \
+      rew[i] = -((((T)0 + (T)fabs(o[0])) + (T)fabs(o[1])) + (T)fabs(o[2]));          \
+    }                                                                                \
+  }                                                                                  \
+  static inline void l4_rk4_##T(T* s, const T* p, T h2, T h, T h6) {                 \
+    T k1[4], k2[4], k3[4], k4[4], y[4];                                              \
+    l4_rhs_##T(s, k1, p);                                                            \
+    for (int j = 0; j < 4; ++j) y[j] = s[j] + h2 * k1[j];                            \
+    l4_rhs_##T(y, k2, p);                                                            \
+    for (int j = 0; j < 4; ++j) y[j] = s[j] + h2 * k2[j];                            \
+    l4_rhs_##T(y, k3, p);                                                            \
+    for (int j = 0; j < 4; ++j) y[j] = s[j] + h * k3[j];                             \
+    l4_rhs_##T(y, k4, p);                                                            \
+    for (int j = 0; j < 4; ++j)                                                      \
+      s[j] = s[j] + h6 * (((k1[j] + (T)2 * k2[j]) + (T)2 * k3[j]) + k4[j]);           \
+  }                                                                                  \
+  void orc_l4_step_rk4_##T(int64_t n, T* st, T* obs, T* rew, uint8_t* done,          \
+                           const double* pd) {                                       \
+    T p[5]; for (int j = 0; j < 5; ++j) p[j] = (T)pd[j];                             \
+    const T h2 = (T)(pd[3] / 2), h = (T)pd[3], h6 = (T)(pd[3] / 6.0);                \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      T* m = st + 8 * i; T* s = m + 4; T fm[4], fs[4];                               \
+      l4_rk4_##T(m, p, h2, h, h6);                                                   \
+      l4_rk4_##T(s, p, h2, h, h6);                                                   \
+      l4_rhs_##T(m, fm, p); l4_rhs_##T(s, fs, p);                                    \
+      T* o = obs + 8 * i;                                                            \
+      for (int j = 0; j < 4; ++j) { o[j] = m[j] - s[j]; o[4 + j] = fm[j] - fs[j]; }  \
+      T r = -(((((T)0 + (T)fabs(o[0])) + (T)fabs(o[1])) + (T)fabs(o[2])) +           \
+              (T)fabs(o[3]));                                                        \
+      rew[i] = r;                                                                    \
+      done[i] = (r < (T)-1e6) ? 1 : 0;                                               \
+    }                                                                                \
+  }
+RK4_BODY(double, clipd)
+RK4_BODY(float, clipf)
+
+/* =========================================================================
  * PMSM -- lorenz_env_try_pmsm.py:7-187 PMSM_Sync_Env (float32 throughout)
  * p = {sigma=5.46, gamma=20, dt=0.001, f_max=50, lambda_lr=1e-3, beta1=.9,
  *      beta2=.999, eps=1e-8, err_threshold=5, max_steps=2000, term=1000}

@@ -45,15 +45,18 @@ def test_struct_layout_matches_header(nat, tmp_path):
     c = tmp_path / "probe.c"
     c.write_text(
         '#include <stdio.h>\n#include <stddef.h>\n#include "lorenz_env.h"\n'
-        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu\\n\", sizeof(lz_config),"
+        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu %zu %zu %d %d %d\\n\", sizeof(lz_config),"
         " offsetof(lz_config, params), offsetof(lz_config, t_done_step),"
-        " offsetof(lz_config, alpha), sizeof(lz_info), offsetof(lz_config, seed));return 0;}\n")
+        " offsetof(lz_config, alpha), sizeof(lz_info), offsetof(lz_config, seed),"
+        " offsetof(lz_config, reserved), offsetof(lz_config, integrator), LZ_INT_EULER, LZ_INT_RK4,"
+        " LZ_ABI_VERSION);return 0;}\n")
     exe = tmp_path / "probe"
     subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), str(c), "-o", str(exe)])
     got = [int(v) for v in subprocess.check_output([str(exe)]).split()]
     C = nat.LzConfig
     want = [ctypes.sizeof(C), C.params.offset, C.t_done_step.offset, C.alpha.offset,
-            ctypes.sizeof(nat.LzInfo), C.seed.offset]
+            ctypes.sizeof(nat.LzInfo), C.seed.offset, C.reserved.offset, C.integrator.offset,
+            nat.INT_EULER, nat.INT_RK4, nat.ABI_VERSION]
     assert got == want
 
 
@@ -84,7 +87,8 @@ def test_config_init_reference_constants(nat, orc):
 
 
 def test_abi_version_and_errors(nat):
-    assert nat.lib.lz_abi_version() == 1
+    # 2: lz_get_state / lz_set_state gained (indices, count) and lz_config the integrator
+    assert nat.lib.lz_abi_version() == 2 == nat.ABI_VERSION
     cfg = nat.LzConfig()
     assert nat.lib.lz_config_init(ctypes.byref(cfg), 99) == nat.LZ_ERR_INVALID
     assert b"unknown system" in nat.lib.lz_last_error()
@@ -98,6 +102,16 @@ def test_abi_version_and_errors(nat):
     cfg = nat.config_init(nat.LORENZ3)
     cfg.max_episode_steps = -1
     assert nat.lib.lz_create(ctypes.byref(cfg), ctypes.byref(h)) == nat.LZ_ERR_INVALID
+    # the integrator: Euler (the reference) by default, RK4 opt-in for LORENZ3 / LORENZ4
+    assert nat.config_init(nat.LORENZ3).integrator == nat.INT_EULER
+    cfg = nat.config_init(nat.LORENZ3)
+    cfg.integrator = 7
+    assert nat.lib.lz_create(ctypes.byref(cfg), ctypes.byref(h)) == nat.LZ_ERR_INVALID
+    assert b"unknown integrator" in nat.lib.lz_last_error()
+    cfg = nat.config_init(nat.PMSM)
+    cfg.integrator = nat.INT_RK4
+    assert nat.lib.lz_create(ctypes.byref(cfg), ctypes.byref(h)) == nat.LZ_ERR_UNSUPPORTED
+    assert b"RK4" in nat.lib.lz_last_error()
     # NULL handles are rejected, never dereferenced
     assert nat.lib.lz_step(None, None, None, None, None, None, None, None, None) == nat.LZ_ERR_INVALID
     assert nat.lib.lz_reset(None, None, None, None) == nat.LZ_ERR_INVALID

@@ -7,6 +7,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -26,6 +27,48 @@ def test_cpu_baseline_leg():
     assert cb["c_port"]["value"] > cb["value"]  # the C port is far cheaper per step
 
 
+def test_launcher_rank_environment():
+    """`python bench.py --gpus N` outside torch.distributed.run spawns N rank processes
+    itself: each gets RANK = LOCAL_RANK = r, WORLD_SIZE = N and a 127.0.0.1 rendezvous;
+    the spawning process touches neither torch nor the GPU (--probe-ranks makes each rank
+    print its environment and exit; no GPU needed)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    envs = bench.rank_envs(3, 29500, base={"PATH": "/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2"]
+    assert all(e["LOCAL_RANK"] == e["RANK"] and e["WORLD_SIZE"] == "3" for e in envs)
+    assert all(e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29500" for e in envs)
+    assert all(e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e["PATH"] == "/bin" for e in envs)
+    a = bench.parse(["--gpus", "4"])
+    assert a.scaling == "strong" and a.envs == 1 << 20 and a.integrator == "euler"
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-c",
+                        "import sys, runpy; sys.argv = ['bench.py', '--gpus', '2', '--probe-ranks'];"
+                        "runpy.run_path('bench.py', run_name='__main__');"
+                        "print('torch imported:', 'torch' in sys.modules)"],
+                       capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert sorted(int(d["RANK"]) for d in lines) == [0, 1]
+    assert all(d["WORLD_SIZE"] == "2" and d["MASTER_ADDR"] == "127.0.0.1" for d in lines)
+    assert len({d["MASTER_PORT"] for d in lines}) == 1
+    # sys.exit(status) ends the parent before the print: the parent never imported torch
+    assert "torch imported" not in r.stdout
+
+
+def test_launcher_propagates_a_failed_rank():
+    """A rank that fails (rank 1 exits 3 while rank 0 is still running) makes the launcher
+    terminate the other rank and exit with the failure's status, promptly."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["LZ_BENCH_PROBE_FAIL_RANK"] = "1"
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--probe-ranks"],
+                       capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert time.time() - t0 < 40  # rank 0 (sleeping 60 s) was terminated, not waited for
+
+
 @pytest.mark.gpu
 def test_bench_line_contract_steps20():
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
@@ -38,7 +81,7 @@ def test_bench_line_contract_steps20():
     d = json.loads(lines[0])
     assert d["metric"] == base["metric"] and d["unit"] == "env-steps/s"
     assert d["n_gpus"] == 1 and d["steps"] == 20 and d["warmup"] == 5
-    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["vs_baseline"] is None
+    assert d["higher_is_better"] is True and d["scaling"] == "strong" and d["vs_baseline"] is None
     assert d["dtype"] == "f32" and d["data"].startswith("synthetic")
     assert d["config"]["envs_per_gpu"] == 1 << 20 and "workload" in d["config"]
     t = d["timing"]

@@ -128,6 +128,56 @@ def test_l4_f32_vs_oracle(gl, orc):
     assert bits_equal(_np(o), oo) and bits_equal(_np(r), rr)
 
 
+@pytest.mark.parametrize("n,rollout", [(65536, False), (70001, False), (65536, True), (70001, True)])
+def test_l4_f32_vs_oracle_cfg2(gl, orc, n, rollout):
+    """cfg2's lorenz_env_transient at its size (65,536) and ragged (70,001): float32
+    LORENZ4 vs the oracle bit for bit through lz_step (2048 steps) and through one K = 2048
+    lz_rollout launch (the 256-lane kernel with the alternating obs tiles at both sizes:
+    LORENZ4 f32 switches to it from 3/4 x 256 x CUs envs), with a TimeLimit(500) whose
+    truncations are staggered by per-env step counters, auto-reset from device Philox:
+    every step's obs / reward / done bytes, every compact done list (ids, terminal obs)
+    and the final state planes."""
+    from oracle_tl import OracleTL
+
+    K, L = 2048, 500
+    be = gl.BatchedEnv("lorenz4", n, dtype="float32", seed=13, max_episode_steps=L)
+    be.reset()
+    steps0 = np.random.default_rng(13).integers(0, L, n).astype(np.int32)
+    be.set_state(gl._native.L4_STEP, torch.from_numpy(steps0))
+    ref = OracleTL(orc, "l4", np.float32, n, 13, L, steps0)
+    zero = torch.zeros((n, 3), device="cuda")
+    if rollout:
+        obs, rew, done, (didx, tobs, nd) = be.rollout(torch.zeros((K, n, 3), device="cuda"),
+                                                      capture_terminal=8 * n)
+        wi, wt = [], []
+    for k in range(K):
+        oo, rr, dd, idx, term = ref.step()
+        if rollout:
+            o, r, d = obs[k], rew[k], done[k]
+            wi.append(k * n + idx)
+            wt.append(term)
+        else:
+            o, r, d = be.step(zero)
+            nd_k = int(be.n_done_dev.item())
+            assert nd_k == idx.size, k
+            if nd_k:
+                gi, gt = be.done_list()
+                assert np.array_equal(_np(gi), idx) and bits_equal(_np(gt), term), k
+        assert bits_equal(_np(o), oo), k
+        assert bits_equal(_np(r), rr), k
+        assert np.array_equal(_np(d), dd), k
+    if rollout:
+        m = int(nd.item())
+        wi = np.concatenate(wi)
+        assert m == wi.size and m >= 4 * n
+        order = torch.argsort(didx[:m])
+        assert np.array_equal(_np(didx[:m][order]), wi)
+        assert bits_equal(_np(tobs[:m][order]), np.concatenate(wt))
+    st = np.stack([_np(be.get_state(p)) for p in range(8)], 1)
+    assert bits_equal(st, ref.st)
+    be.close()
+
+
 # ----------------------------------------------------------------- PMSM
 def _pmsm_case(gl, g, i):
     T = g["obs"].shape[1]

@@ -169,3 +169,75 @@ def test_sb3_exact_differs_from_pooled_and_matches_sb3_order(gl, pol, orc):
     # tile sums vs lz_rms_moments, so allow rounding)
     np.testing.assert_allclose(a[0], b[0], rtol=0, atol=1e-5)
     assert np.abs(a[1:] - b[1:]).max() > 1e-3
+
+
+def test_odd_k_collect_then_step_done_list(gl, pol):
+    """a collect of the SB3-exact path flips the handle's call parity once per
+    step (K flips) and runs on its own done cursor.  After an odd K (A2C's default
+    n_steps = 5) the next lz_step must start its compact done list from 0, not from the
+    count an earlier launch left in that parity slot: every step launch of the collect
+    zeroes the slot the handle's next launch reads.  Here the earlier launch marked all n
+    envs done (TimeLimit(1)); the step after the collect must report exactly its own n."""
+    from gym_lorenz.vec_normalize import DeviceRunningMeanStd
+
+    n = 4096
+    env = gl.BatchedEnv("pmsm", n, seed=2, add_noise=True, max_episode_steps=1)
+    rms = DeviceRunningMeanStd(6, env.device)
+    col = pol.FusedRolloutCollector(env, _random_policy(pol, 6, 2, seed=1), obs_rms=rms,
+                                    training=True, precision="fp32")
+    assert col.per_step_vecnorm
+    col.reset()
+    a = torch.zeros((n, 2), device=env.device)
+    env.step(a)  # every env truncates: this launch's cursor slot holds n
+    assert int(env.n_done_dev.item()) == n
+    col.collect(5)  # odd K
+    didx = torch.full((2 * n + 1,), -1, dtype=torch.int32, device=env.device)
+    tobs = torch.empty((2 * n, 6), device=env.device)
+    nd = torch.zeros((1,), dtype=torch.int32, device=env.device)
+    env.step(a, compact_out=(didx, tobs, nd))
+    assert int(nd.item()) == n
+    assert np.array_equal(np.sort(_np(didx[:n])), np.arange(n))
+    assert (_np(didx[n:]) == -1).all()
+    env.close()
+
+
+def test_policy_step_order_guard(gl, pol):
+    """lz_policy_step_f32 carries the terminal-obs carry, the collect's done
+    cursor and the RNG parity from step to step, so it refuses (LZ_ERR_STATE) a step k > 0
+    that is not the one expected next, or that follows another launch on the handle; a
+    new collect (k = 0) always starts."""
+    import ctypes
+
+    from gym_lorenz import _native as nat
+    from gym_lorenz.policy import pack_policy_f32
+    from gym_lorenz.vec_normalize import DeviceRunningMeanStd
+
+    n, K = 1000, 3
+    env = gl.BatchedEnv("pmsm", n, seed=4)
+    obs0 = env.reset().clone()
+    dev = env.device
+    rms = DeviceRunningMeanStd(6, dev)
+    blob = torch.from_numpy(pack_policy_f32(_random_policy(pol, 6, 2, seed=3), 6, 2)).to(dev)
+    bufs = dict(obs_buf=torch.empty((K, n, 6), device=dev), act_buf=torch.empty((K, n, 2), device=dev),
+                logp_buf=torch.empty((K, n), device=dev), val_buf=torch.empty((K, n), device=dev),
+                rew_buf=torch.empty((K, n), device=dev),
+                done_buf=torch.empty((K, n), dtype=torch.uint8, device=dev),
+                last_values=torch.empty((n,), device=dev))
+    last = torch.empty((n, 6), device=dev)
+    r = nat.LzPolicyRolloutArgs()
+    r.K, r.flags = K, nat.POLICY_DETERMINISTIC
+    r.blob, r.obs_in, r.obs_last = blob.data_ptr(), obs0.data_ptr(), last.data_ptr()
+    for k_, v in bufs.items():
+        setattr(r, k_, v.data_ptr())
+    r.norm_eps, r.clip_obs, r.gamma, r.act_low, r.act_high = 1e-8, 10.0, 0.99, -1.0, 1.0
+    state = ctypes.c_void_p(rms.state.data_ptr())
+    step = lambda k: nat.lib.lz_policy_step_f32(env._h, ctypes.byref(r), k, state, None)  # noqa: E731
+    assert step(1) == nat.LZ_ERR_STATE and b"out of order" in nat.lib.lz_last_error()
+    assert step(0) == nat.LZ_OK and step(1) == nat.LZ_OK
+    env.step(torch.zeros((n, 2), device=dev))  # another launch in the middle of the collect
+    assert step(2) == nat.LZ_ERR_STATE
+    for k in range(K + 1):  # a fresh collect runs through
+        assert step(k) == nat.LZ_OK, (k, nat.lib.lz_last_error())
+    assert step(1) == nat.LZ_ERR_STATE  # the collect has ended
+    torch.cuda.synchronize()
+    env.close()
