@@ -1274,6 +1274,64 @@ lz_status lz_rollout_policy_attn_stack_f32(lz_handle* h, const lz_policy_rollout
   return rollout_policy(h, r, 5, n_stack, stack_in, stack_out);
 }
 
+lz_status lz_get_launch_shape(const lz_handle* h, int32_t call, lz_launch_shape* out) {
+  if (!h || !out) return fail(LZ_ERR_INVALID, "handle/out is NULL");
+  std::memset(out, 0, sizeof *out);
+  const int64_t n = h->cfg.num_envs;
+  if (call == LZ_CALL_STEP || call == LZ_CALL_ROLLOUT) {
+    KArgs a;
+    fill_common(h, a);
+    int32_t o[5] = {0, 0, 0, 0, 0};
+    if (lz::env_launch_shape(call == LZ_CALL_STEP ? 1 : 2, sys_key(h), h->f64, a, o) != 0)
+      return fail(LZ_ERR_INVALID, "no launch shape for system %d", h->cfg.system);
+    out->kernel = o[0];
+    out->envs_per_wave = o[1];
+    out->waves = o[2];
+    out->grid = o[3];
+    out->flags = (uint32_t)o[4];
+    out->groups = o[3];
+    return LZ_OK;
+  }
+  lz::PolShape sh;
+  switch (call) {
+    case LZ_CALL_ROLLOUT_POLICY:
+      sh = lz::policy_shape(n, h->cfg.reserved[0], h->num_cus);
+      out->kernel = sh.envs_per_wave == 64 ? LZ_KERNEL_POLICY
+                    : sh.pair == 2         ? LZ_KERNEL_POLICY_PAIR_PIPE
+                    : sh.pair              ? LZ_KERNEL_POLICY_PAIR
+                                           : LZ_KERNEL_POLICY;
+      break;
+    case LZ_CALL_ROLLOUT_POLICY_F32:
+      sh = lz::f32_policy_shape(n, h->num_cus, h->cfg.reserved[0]);
+      out->kernel = sh.pair == 1 ? LZ_KERNEL_POLICY_SPLIT : LZ_KERNEL_POLICY;
+      break;
+    case LZ_CALL_POLICY_STEP_F32:
+      sh = lz::f32_policy_shape(n, h->num_cus, h->cfg.reserved[0]);
+      out->kernel = LZ_KERNEL_POLICY_STEP;
+      break;
+    case LZ_CALL_ROLLOUT_POLICY_ATTN:
+    case LZ_CALL_ROLLOUT_POLICY_ATTN_STACK:
+      sh = lz::attn_policy_shape(n, h->num_cus);
+      out->kernel = LZ_KERNEL_POLICY_ATTN;
+      break;
+    case LZ_CALL_ROLLOUT_POLICY_ATTN_F32:
+    case LZ_CALL_ROLLOUT_POLICY_ATTN_STACK_F32:
+      sh = lz::attn_f32_policy_shape(n, h->num_cus, call == LZ_CALL_ROLLOUT_POLICY_ATTN_STACK_F32);
+      out->kernel = LZ_KERNEL_POLICY_ATTN_F32;
+      break;
+    default:
+      return fail(LZ_ERR_INVALID, "unknown call %d", call);
+  }
+  out->envs_per_wave = sh.envs_per_wave;
+  // the split kernel runs 4 tiles per workgroup on 8 waves (actor + critic per tile)
+  out->waves = (call == LZ_CALL_ROLLOUT_POLICY_F32 && sh.pair == 1) ? 8 : sh.waves;
+  out->grid = sh.grid;
+  const int64_t groups = ((n + sh.envs_per_wave - 1) / sh.envs_per_wave + sh.waves - 1) / sh.waves;
+  out->groups = (int32_t)groups;
+  out->flags = groups > sh.grid ? LZ_SHAPE_GRID_STRIDE : 0u;
+  return LZ_OK;
+}
+
 int32_t lz_plane_elem_size(const lz_handle* h, int32_t plane) {
   if (!h) return 0;
   return plane_elem(h->cfg.system, h->f64, plane);

@@ -369,6 +369,9 @@ struct ResMember {      // one wave of the server
 // table: device copy of n members; one workgroup of 64 (n + 1) threads, wave n the poller
 int launch_resident_multi(const ResMember* table, int n, uint64_t idle_ticks, void* stream);
 int launch_rollout(int system, int f64, const KArgs& a, void* stream);
+// lz_get_launch_shape of lz_step (which = 1) / lz_rollout (which = 2): out[5] = kernel,
+// envs per wave, waves per workgroup, workgroups, flags
+int env_launch_shape(int which, int system, int f64, const KArgs& a, int32_t* out);
 // gather (scatter = false: buf[i] = plane[idx[i]]) / scatter (plane[idx[i]] = buf[i]) of
 // es-byte elements; indices outside [0, n) skipped / read as zero
 int launch_plane_index(bool scatter, int es, void* plane, int64_t n, const int64_t* idx, int64_t count,

@@ -939,6 +939,29 @@ static inline bool rollout_split(const KArgs& a) {
   return std::is_same<Sys, SysL3<float>>::value && a.n >= 32768;
 }
 
+// Which rollout kernel launch_rollout_d picks (lz_get_launch_shape reports it): 0 the
+// 256-lane k_rollout, 1 one-wave k_rollout, 2 the split-lane kernel; no_done = the
+// done-free instantiation.
+struct RolloutPlan {
+  int kind;
+  bool no_done;
+};
+template <class Sys>
+static RolloutPlan rollout_plan(const KArgs& a) {
+  const int64_t cus = a.num_cus > 0 ? a.num_cus : 256;
+  const int64_t one_wave_below =
+      std::is_same<Sys, SysL3<float>>::value   ? (int64_t)kBlock * cus
+      : std::is_same<Sys, SysL4<float>>::value ? (int64_t)kBlock * cus * 3 / 4
+                                               : 2 * 256 * (int64_t)kBlock;
+  bool nd = false;
+  if constexpr (never_terminates<Sys>::value && !Sys::kNoise) nd = no_done<Sys>(a) && !(a.variant & 2048);
+  if ((a.n < one_wave_below || (a.variant & (1 << 24))) && !(a.variant & (1 << 23))) {
+    if (rollout_split<Sys>(a)) return {2, nd};
+    return {1, false};
+  }
+  return {0, nd};
+}
+
 template <class Sys, typename T, int D, int DS = D>  // DS: the split-lane kernel's distance
 static void launch_rollout_d(const KArgs& a, hipStream_t s) {
   // fewer 256-env workgroups than CUs: one-wave groups (variant bit 1<<23: the 256-lane
@@ -952,17 +975,14 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
   // at 32,768-98,304 (2,209 vs 2,493 / 1,823 vs 2,038 us at 65,536): the round-2 bound.
   // LORENZ4's crossover lies lower, between 160 and 192 workgroups per 256 CUs (40,960
   // envs: 658 vs 918 us; 49,152: 870 vs 925-1,096; 57,344: 908 vs 1,007): from 3/4 x 256 x CUs.
-  const int64_t cus = a.num_cus > 0 ? a.num_cus : 256;
-  const int64_t one_wave_below =
-      std::is_same<Sys, SysL3<float>>::value   ? (int64_t)kBlock * cus
-      : std::is_same<Sys, SysL4<float>>::value ? (int64_t)kBlock * cus * 3 / 4
-                                               : 2 * 256 * (int64_t)kBlock;
-  // variant bit 1<<24: one-wave groups at any N (A/B)
-  if ((a.n < one_wave_below || (a.variant & (1 << 24))) && !(a.variant & (1 << 23))) {
-    if (rollout_split<Sys>(a)) {
+  // (rollout_plan: variant bit 1<<24 forces one-wave groups at any N, 1<<23 the 256-lane
+  // kernel, 2048 keeps the done path -- A/B)
+  const RolloutPlan plan = rollout_plan<Sys>(a);
+  if (plan.kind != 0) {
+    if (plan.kind == 2) {
       const dim3 g((unsigned)((a.n + 31) / 32));
       if constexpr (never_terminates<Sys>::value && !Sys::kNoise) {
-        if (no_done<Sys>(a) && !(a.variant & 2048)) {  // variant bit 2048: keep the done path (A/B)
+        if (plan.no_done) {
           switch ((a.variant >> 18) & 7) {  // A/B: store policy (SV; 1 = the default)
             case 1: hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true, 0>), g, dim3(64), 0, s, a); return;
             case 3: hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS, true, 3>), g, dim3(64), 0, s, a); return;
@@ -981,7 +1001,7 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
     }
   } else {
     if constexpr (never_terminates<Sys>::value && !Sys::kNoise) {
-      if (no_done<Sys>(a) && !(a.variant & 2048)) {
+      if (plan.no_done) {
         if (a.variant & (1 << 21))  // A/B: non-temporal done stores
           hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D, true, false>), dim3((unsigned)grid_for(a.n)),
                              dim3(kBlock), 0, s, a);
@@ -1076,6 +1096,50 @@ static int dispatch(int which, int system, int f64, const KArgs& a, void* stream
     case LZ_SYS_SC:
       return f64 ? launch_all<SysSC<double>, double>(which, a, s)
                  : launch_all<SysSC<float>, float>(which, a, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------ launch shapes
+// What lz_step / lz_rollout launch for these arguments (lz_get_launch_shape): kernel code,
+// envs per wave, waves per workgroup, workgroups, flags (lorenz_env.h LZ_KERNEL_* /
+// LZ_SHAPE_*) -- the same decisions launch_all / launch_rollout_d take.
+template <class Sys, typename T>
+static int env_shape_t(int which, const KArgs& a, int32_t* o) {
+  if (which == 1) {
+    const int tiles = multi_step_ok<Sys>::value ? step_tiles(a) : 1;
+    const int64_t per = (int64_t)kBlock * tiles;
+    o[0] = tiles > 1 ? LZ_KERNEL_STEP_MULTI : LZ_KERNEL_STEP;
+    o[1] = 64;
+    o[2] = kBlock / 64;
+    o[3] = (int32_t)((a.n + per - 1) / per);
+    o[4] = 0;
+    return 0;
+  }
+  const RolloutPlan p = rollout_plan<Sys>(a);
+  o[0] = p.kind == 0 ? LZ_KERNEL_ROLLOUT : p.kind == 1 ? LZ_KERNEL_ROLLOUT_WAVE : LZ_KERNEL_ROLLOUT_SPLIT;
+  o[1] = p.kind == 2 ? 32 : 64;
+  o[2] = p.kind == 0 ? kBlock / 64 : 1;
+  const int64_t per = p.kind == 0 ? kBlock : p.kind == 1 ? 64 : 32;
+  o[3] = (int32_t)((a.n + per - 1) / per);
+  o[4] = p.no_done ? LZ_SHAPE_NO_DONE : 0;
+  return 0;
+}
+
+int env_launch_shape(int which, int system, int f64, const KArgs& a, int32_t* o) {
+  switch (system) {
+    case LZ_SYS_LORENZ3: return f64 ? env_shape_t<SysL3<double>, double>(which, a, o) : env_shape_t<SysL3<float>, float>(which, a, o);
+    case LZ_SYS_LORENZ4: return f64 ? env_shape_t<SysL4<double>, double>(which, a, o) : env_shape_t<SysL4<float>, float>(which, a, o);
+    case LZ_SYS_LORENZ3 + kSysRK4:
+      return f64 ? env_shape_t<SysL3RK4<double>, double>(which, a, o) : env_shape_t<SysL3RK4<float>, float>(which, a, o);
+    case LZ_SYS_LORENZ4 + kSysRK4:
+      return f64 ? env_shape_t<SysL4RK4<double>, double>(which, a, o) : env_shape_t<SysL4RK4<float>, float>(which, a, o);
+    case LZ_SYS_PMSM: return env_shape_t<SysPMSM, float>(which, a, o);
+    case LZ_SYS_HR: return f64 ? env_shape_t<SysHR<double>, double>(which, a, o) : env_shape_t<SysHR<float>, float>(which, a, o);
+    case LZ_SYS_T1: return f64 ? env_shape_t<SysT1<double>, double>(which, a, o) : env_shape_t<SysT1<float>, float>(which, a, o);
+    case LZ_SYS_T2: return f64 ? env_shape_t<SysT2<double>, double>(which, a, o) : env_shape_t<SysT2<float>, float>(which, a, o);
+    case LZ_SYS_TP: return f64 ? env_shape_t<SysTP<double>, double>(which, a, o) : env_shape_t<SysTP<float>, float>(which, a, o);
+    case LZ_SYS_SC: return f64 ? env_shape_t<SysSC<double>, double>(which, a, o) : env_shape_t<SysSC<float>, float>(which, a, o);
   }
   return (int)hipErrorInvalidValue;
 }

@@ -37,9 +37,16 @@ template <typename T>
 __device__ __forceinline__ T ld(const void* p, int64_t i) {
   return static_cast<const T*>(p)[i];
 }
+// LZ_STATE_NT (A/B builds only, tools/build_ab.sh; default 0): state-plane stores with
+// the non-temporal hint.  The product stores them plain: the planes are re-read by the
+// next launch.
+#ifndef LZ_STATE_NT
+#define LZ_STATE_NT 0
+#endif
 template <typename T>
 __device__ __forceinline__ void st(void* p, int64_t i, T v) {
-  static_cast<T*>(p)[i] = v;
+  if constexpr (LZ_STATE_NT) __builtin_nontemporal_store(v, static_cast<T*>(p) + i);
+  else static_cast<T*>(p)[i] = v;
 }
 
 // Uniform initial-state draws (purpose RESET): value j of [lo, hi).

@@ -146,6 +146,22 @@ class LzVecNorm(ctypes.Structure):
 
 VN_TRAINING, VN_NORM_OBS, VN_NORM_REWARD, VN_DEFER = 1, 2, 4, 8
 
+
+class LzLaunchShape(ctypes.Structure):
+    _fields_ = [("kernel", ctypes.c_int32), ("envs_per_wave", ctypes.c_int32),
+                ("waves", ctypes.c_int32), ("grid", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("groups", ctypes.c_int32)]
+
+
+# lz_get_launch_shape calls / kernels / flags (lorenz_env.h)
+(CALL_STEP, CALL_ROLLOUT, CALL_ROLLOUT_POLICY, CALL_ROLLOUT_POLICY_F32, CALL_POLICY_STEP_F32,
+ CALL_ROLLOUT_POLICY_ATTN, CALL_ROLLOUT_POLICY_ATTN_STACK, CALL_ROLLOUT_POLICY_ATTN_F32,
+ CALL_ROLLOUT_POLICY_ATTN_STACK_F32) = range(9)
+KERNELS = {1: "step", 2: "step_multi", 3: "rollout", 4: "rollout_wave", 5: "rollout_split",
+           6: "policy", 7: "policy_pair", 8: "policy_pair_pipe", 9: "policy_split",
+           10: "policy_step", 11: "policy_attn", 12: "policy_attn_f32"}
+SHAPE_NO_DONE, SHAPE_GRID_STRIDE = 1, 2
+
 VP = ctypes.c_void_p
 _SIGS = {
     "lz_config_init": (ctypes.c_int, [ctypes.POINTER(LzConfig), ctypes.c_int32]),
@@ -213,6 +229,7 @@ _SIGS = {
                                          ctypes.c_int32, VP]),
     "lz_frame_stack": (ctypes.c_int, [VP, VP, VP, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                       ctypes.c_int32, ctypes.c_int32, VP]),
+    "lz_get_launch_shape": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(LzLaunchShape)]),
     "lz_last_error": (ctypes.c_char_p, []),
     "lz_abi_version": (ctypes.c_int32, []),
 }
@@ -272,6 +289,15 @@ def config_init(system):
     cfg = LzConfig()
     check(lib.lz_config_init(ctypes.byref(cfg), system))
     return cfg
+
+
+def launch_shape(handle, call):
+    """lz_get_launch_shape as a dict: kernel name, envs_per_wave, waves, grid, groups, flags."""
+    sh = LzLaunchShape()
+    check(lib.lz_get_launch_shape(handle, int(call), ctypes.byref(sh)))
+    return {"kernel": KERNELS.get(sh.kernel, sh.kernel), "envs_per_wave": sh.envs_per_wave,
+            "waves": sh.waves, "grid": sh.grid, "groups": sh.groups,
+            "no_done": bool(sh.flags & SHAPE_NO_DONE), "grid_stride": bool(sh.flags & SHAPE_GRID_STRIDE)}
 
 
 def exported_symbols():

@@ -654,6 +654,52 @@ lz_status lz_frame_stack(float* stacked, const float* obs, const uint8_t* done, 
                          int32_t n_stack, int32_t obs_dim, int32_t reset, int32_t device,
                          void* hip_stream);
 
+/* ------------------------------------------------------------------------------
+ * Launch shapes (introspection; host-only, no device work).  Which kernel instantiation
+ * and grid a call on this handle would launch -- the launchers choose by env count, CUs
+ * and system (one-wave / split-lane / 256-lane rollouts; one wave per tile, the two nets
+ * interleaved, or split over actor and critic waves for the policies), so tests can
+ * assert that they reach every branch and profiling tools can name the kernel.
+ * ------------------------------------------------------------------------------ */
+enum {
+  LZ_CALL_STEP = 0,                        /* lz_step */
+  LZ_CALL_ROLLOUT = 1,                     /* lz_rollout */
+  LZ_CALL_ROLLOUT_POLICY = 2,              /* lz_rollout_policy (bf16 MlpPolicy) */
+  LZ_CALL_ROLLOUT_POLICY_F32 = 3,          /* lz_rollout_policy_f32 */
+  LZ_CALL_POLICY_STEP_F32 = 4,             /* lz_policy_step_f32 / lz_rollout_policy_f32_vn */
+  LZ_CALL_ROLLOUT_POLICY_ATTN = 5,         /* lz_rollout_policy_attn */
+  LZ_CALL_ROLLOUT_POLICY_ATTN_STACK = 6,   /* lz_rollout_policy_attn_stack */
+  LZ_CALL_ROLLOUT_POLICY_ATTN_F32 = 7,     /* lz_rollout_policy_attn_f32 */
+  LZ_CALL_ROLLOUT_POLICY_ATTN_STACK_F32 = 8 /* lz_rollout_policy_attn_stack_f32 */
+};
+enum {
+  LZ_KERNEL_STEP = 1,             /* k_step: one 256-env tile per workgroup */
+  LZ_KERNEL_STEP_MULTI = 2,       /* k_step_multi: 2 or 4 tiles per workgroup */
+  LZ_KERNEL_ROLLOUT = 3,          /* k_rollout, 256-lane workgroups */
+  LZ_KERNEL_ROLLOUT_WAVE = 4,     /* k_rollout, one-wave workgroups */
+  LZ_KERNEL_ROLLOUT_SPLIT = 5,    /* k_rollout_split: two lanes per env */
+  LZ_KERNEL_POLICY = 6,           /* k_rollout_policy: one wave per env tile, nets in turn */
+  LZ_KERNEL_POLICY_PAIR = 7,      /* ... both nets interleaved in one instruction stream */
+  LZ_KERNEL_POLICY_PAIR_PIPE = 8, /* ... interleaved, pipelined weight loads */
+  LZ_KERNEL_POLICY_SPLIT = 9,     /* k_rollout_policy_f32_split: actor and critic waves */
+  LZ_KERNEL_POLICY_STEP = 10,     /* k_policy_step_f32 */
+  LZ_KERNEL_POLICY_ATTN = 11,     /* k_rollout_policy<..., kAttn / kAttnLn> (bf16) */
+  LZ_KERNEL_POLICY_ATTN_F32 = 12  /* k_rollout_policy_attn_f32 */
+};
+#define LZ_SHAPE_NO_DONE 1u     /* the done-free instantiation (no done can occur) */
+#define LZ_SHAPE_GRID_STRIDE 2u /* fewer workgroups than env groups: workgroups loop */
+
+typedef struct lz_launch_shape {
+  int32_t kernel;        /* LZ_KERNEL_* */
+  int32_t envs_per_wave; /* envs one wave carries (64, 32 or 16) */
+  int32_t waves;         /* waves per workgroup */
+  int32_t grid;          /* workgroups launched */
+  uint32_t flags;        /* LZ_SHAPE_* */
+  int32_t groups;        /* env groups of waves x envs_per_wave (> grid: grid-stride) */
+} lz_launch_shape;
+
+lz_status lz_get_launch_shape(const lz_handle* h, int32_t call, lz_launch_shape* out);
+
 const char* lz_last_error(void);
 int32_t lz_abi_version(void);
 

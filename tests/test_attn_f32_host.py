@@ -159,3 +159,44 @@ def test_attn_f32_pack_rejects_bad_shapes(pol):
 
     with pytest.raises(nat.LorenzEnvError):
         pol.pack_attn_policy_f32(_net(pol, 9, False, seed=1).state_dict(), 9, 2)  # obs_dim > 8
+
+
+# ------------------------------------------------------- pinned to the reference's classes
+def _attn_ref(tag):
+    from conftest import golden
+
+    g = golden("attn_ref")
+    pre = tag + "/"
+    sd = {k[len(pre):]: torch.from_numpy(v) for k, v in g.items()
+          if k.startswith(pre) and k[len(pre):] not in ("x", "features", "mean", "value")}
+    return sd, g[pre + "x"], g[pre + "features"], g[pre + "mean"], g[pre + "value"]
+
+
+@pytest.mark.parametrize("tag", ["plain", "ln"])
+def test_oracle_attn_f32_vs_reference_classes(orc, pol, tag):
+    """tests/golden/attn_ref.npz was produced by the reference's own
+    AttentionFeaturesExtractor classes (code/train.py:52-94; code/lorenz_filter/train.py:
+    55-103, residual + LayerNorm, on 24-dim VecFrameStack(4) inputs) inside SB3's policy
+    layout, in torch float32 (tests/golden/make_attn_ref.py).  The oracle the float32
+    kernels are bit-exact against (orc_attn_f32) reproduces the features, action means
+    and values within 2e-6 of the output scale; so does this package's torch
+    restatement (gym_lorenz.policy.ActorCriticAttn, loaded with the same state_dict)."""
+    sd, x, f_ref, m_ref, v_ref = _attn_ref(tag)
+    m, v, f = orc.attn_f32(sd, x, return_features=True)
+
+    def rel(a, b):
+        return float(np.abs(a - b).max() / max(1.0, np.abs(b).max()))
+
+    df, dm, dv = rel(f, f_ref), rel(m, m_ref), rel(v, v_ref)
+    print("orc_attn_f32 vs the reference's %s extractor: features %.2e, mean %.2e, value %.2e"
+          % (tag, df, dm, dv))
+    assert df < 2e-6 and dm < 2e-6 and dv < 2e-6
+    # the softmax is far from uniform on these weights (the fixture exercises attention)
+    net = pol.ActorCriticAttn(x.shape[1], 2, layer_norm=tag == "ln")
+    net.load_state_dict(sd)
+    with torch.no_grad():
+        mt, vt = net(torch.from_numpy(x))
+        xs = torch.relu(net.features_extractor.fc1(torch.from_numpy(x[:64]))).view(-1, 8, 16)
+        _, w = net.features_extractor.attention_layer(xs, xs, xs)
+    assert rel(mt.numpy(), m_ref) < 2e-6 and rel(vt.numpy(), v_ref) < 2e-6
+    assert float(w.max()) > 0.5  # some query attends mostly to one token

@@ -319,3 +319,31 @@ def test_attn_f32_vs_sb3_torch_fp32(gl, pol, ln):
           "(|mu| <= %.3g)" % ("-LN" if ln else "", dv, sv, dm, sm))
     assert dv <= 1e-5 * max(sv, 1.0)
     assert dm <= 1e-5 * max(sm, 1.0)
+
+
+@pytest.mark.parametrize("tag", ["plain", "ln"])
+def test_attn_f32_reference_class_weights_bitexact(gl, pol, orc, tag):
+    """The weights of tests/golden/attn_ref.npz -- a policy built from the reference's own
+    AttentionFeaturesExtractor classes (code/train.py:52-94, code/lorenz_filter/
+    train.py:55-103; tests/golden/make_attn_ref.py), whose outputs the oracle reproduces
+    within 2e-6 (tests/test_attn_f32_host.py) -- drive the float32 kernels on HR (plain:
+    raw obs; ln: VecFrameStack(4)): every recorded action and value equals
+    oracle.attn_f32 of the recorded input bit for bit (deterministic actions), and so do
+    the last values."""
+    from conftest import golden
+
+    g = golden("attn_ref")
+    pre = tag + "/"
+    sd = {k[len(pre):]: torch.from_numpy(v) for k, v in g.items()
+          if k.startswith(pre) and k[len(pre):] not in ("x", "features", "mean", "value")}
+    n, K, stack = 2000, 24, 4 if tag == "ln" else 1
+    env = gl.BatchedEnv("hr", n, seed=19, add_noise=True, max_episode_steps=9)
+    col = _col(pol, env, sd, bootstrap=False, deterministic=True, frame_stack=stack)
+    assert col.f32 and (col.attention_ln if tag == "ln" else col.attention)
+    col.reset()
+    b = col.collect(K)
+    _check_forward(orc, sd, b, 6 * stack, 2)
+    last = col.last_stack if tag == "ln" else b.last_obs
+    _, vl = orc.attn_f32(sd, _np(last))
+    assert bits_equal(_np(b.last_values), vl)
+    env.close()

@@ -11,11 +11,37 @@ STAGE=${1:-new}
 O=${2:-gpurun_out/r04_$STAGE}
 mkdir -p $O
 PYT="python -u -m pytest -v --timeout 170 --timeout-method thread -p no:cacheprovider"
+BQ="--no-cpu-baseline --no-drift --no-extras"
 case $STAGE in
+new2)  # the branch table (K = 3), the reference-class attention weights, cfg2 LORENZ4 f32
+  timeout -k 10 600 $PYT -m gpu --maxfail=8 tests/test_gpu_policy_branches.py \
+    "tests/test_gpu_parity.py::test_l4_f32_vs_oracle_cfg2" \
+    "tests/test_gpu_policy_attn_f32.py::test_attn_f32_reference_class_weights_bitexact" \
+    > $O/new2_tests.txt 2>&1 || exit 1
+  timeout -k 10 120 $PYT -s -m gpu "tests/test_gpu_resident.py::test_resident_does_not_block_torch" \
+    > $O/resident_latency.txt 2>&1 || exit 1
+  timeout -k 10 1000 $PYT -x -m gpu tests > $O/gpu_tests.txt 2>&1 || exit 1
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" > $O/smoke.txt 2>&1
+  ;;
+cfg3)  # cfg3's per-GPU shard (131,072) and cfg2 (65,536): where a step's time goes
+  for n in 65536 131072; do
+    timeout -k 10 200 python bench.py --envs $n $BQ > $O/bench_$n.json 2> $O/bench_$n.err || exit 1
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_$n -o run --output-format csv \
+      -- python bench.py --envs $n $BQ > $O/trace_$n.log 2>&1 || exit 1
+  done
+  AB_VARIANTS=0,2,16,8,24,3,0 timeout -k 10 300 python tools/ab_step.py 65536 131072 > $O/ab_step_variants.json || exit 1
+  for n in 131072 65536; do
+    timeout -k 10 500 python tools/ab_lib.py default ablib/libgym_lorenz_amd_state_nt.so 3 -- --envs $n $BQ \
+      > $O/ab_state_nt_$n.json 2> $O/ab_state_nt_$n.err || exit 1
+  done
+  timeout -k 10 120 tools/launch_floor > $O/launch_floor.txt 2>&1
+  ;;
 new)
   timeout -k 10 1100 $PYT -m gpu --maxfail=8 tests/test_gpu_rk4.py tests/test_gpu_vecnorm_step.py \
-    tests/test_gpu_resident.py tests/test_bench_contract.py \
-    "tests/test_gpu_parity.py::test_l4_f32_vs_oracle_cfg2" > $O/new_tests.txt 2>&1
+    tests/test_gpu_resident.py tests/test_bench_contract.py tests/test_gpu_policy_branches.py \
+    "tests/test_gpu_parity.py::test_l4_f32_vs_oracle_cfg2" \
+    "tests/test_gpu_policy_attn_f32.py::test_attn_f32_reference_class_weights_bitexact" \
+    > $O/new_tests.txt 2>&1
   ;;
 full)
   timeout -k 10 1000 $PYT -x -m gpu tests > $O/gpu_tests.txt 2>&1 || exit 1
