@@ -123,8 +123,9 @@ struct lz_handle {
   bool rs_pub_valid;    // the published planes are this launch's (a request was served)
   int rs_use_noise;     // serving injected noise
   int64_t rs_seq;       // number of the last request served (after the reply)
-  int64_t rs_posted;    // number of the last request posted (its command-line word)
-  int rs_slot;          // its word in the server's command line (= its wave)
+  int64_t rs_posted;    // number of the last request posted
+  uint64_t rs_line[lz::kRsLineWords];  // the granules of its request line as last posted
+  int rs_slot;          // its request line in the server (= its wave)
 };
 
 // Stop the resident step server serving the handle (if it runs) and wait for it: every
@@ -537,9 +538,11 @@ lz_status lz_step_host(lz_handle* h, const float* actions, const double* noise, 
 }
 
 // ---- resident step server (lz_resident_step; lz_internal.h ResBox / ResMember)
-// mailbox layout (bytes): resp int64 @128 (own cache line; the request number goes to the
-// server's command line), actions float32 [n, A] @256, noise double [n, 3] @kRsNoise, then obs | reward | done @kRsOut,
-// then the published state planes (plane p at rs_pub_off + p * kRsPubStride(n))
+// mailbox layout (bytes): resp int64 @128 (own cache line; the request itself goes to the
+// server's request line of the handle), actions float32 [n, A] @256 and noise double
+// [n, 3] @kRsNoise (the mailbox path: inputs that do not fit in the line), then obs |
+// reward | done @kRsOut, then the published state planes (plane p at rs_pub_off + p *
+// kRsPubStride(n))
 constexpr size_t kRsResp = 128, kRsAct = 256;
 constexpr size_t kRsNoise = kRsAct + 64 * 4 * 4, kRsOut = kRsNoise + 64 * 3 * 8;
 constexpr int kRsMaxEnvs = 64;
@@ -573,9 +576,9 @@ struct RsServer {
   hipEvent_t ev;
   lz::ResMember* table_host;  // pinned staging of the member table
   lz::ResMember* table_dev;
-  int64_t* cmds;         // the command line: word k = member k's last posted request
-                         // (mapped, coherent host memory, one 128-B line)
-  const int64_t* cmds_dev;
+  uint64_t* lines;       // the request lines: 64 B per member (lz_internal.h ResBox;
+                         // mapped, coherent host memory, 1 KiB)
+  const uint64_t* lines_dev;
   int khz;               // wall-clock rate (ticks per ms)
 };
 
@@ -588,6 +591,31 @@ static uint64_t rs_idle_ticks(const RsServer& sv) {
   const double us = e ? std::atof(e) : 1000.0;
   return (uint64_t)((us > 0 ? us : 1000.0) * sv.khz / 1000.0);
 }
+constexpr size_t kRsLinesBytes = 16 * lz::kRsLineWords * sizeof(uint64_t);
+static_assert(lz::kRsMaxHandles <= 16, "one request line per member in 1 KiB");
+constexpr uint64_t kRsStop = ~0ull;  // granule 0 of any line: every wave leaves
+
+static int rs_act_words(const lz_handle* h) {
+  const bool needs_act = h->cfg.system != LZ_SYS_LORENZ4 && h->cfg.system != LZ_SYS_SC;
+  return needs_act ? h->desc.action_dim : 0;
+}
+// data words of a request that travels inside its line (1 env: its actions, then its 3
+// float64 noise values as lo / hi halves), or -1 (the mailbox path)
+static int rs_inline_words(const lz_handle* h, int use_noise) {
+  if (h->cfg.num_envs != 1) return -1;
+  const int w = rs_act_words(h) + (use_noise ? 6 : 0);
+  return w <= lz::kRsLineWords ? w : -1;
+}
+static uint64_t rs_granule(int64_t seq, uint32_t data) {
+  return ((uint64_t)((uint32_t)seq & lz::kRsTagMask) << 32) | data;
+}
+// the handle's request line into its slot: every granule one aligned 8-B store (the
+// poller validates tags, so the order does not matter; granule 0 last)
+static void rs_write_line(RsServer& sv, const lz_handle* h) {
+  uint64_t* line = sv.lines + (size_t)h->rs_slot * lz::kRsLineWords;
+  for (int g = lz::kRsLineWords - 1; g >= 0; --g) __atomic_store_n(&line[g], h->rs_line[g], __ATOMIC_RELEASE);
+}
+
 static std::mutex g_rs_mu;  // trivially destructible
 static RsServer g_rs[kRsMaxDevices];
 
@@ -599,25 +627,24 @@ static lz_status rs_server_init(RsServer& sv, int device) {
   hipEvent_t ev = nullptr;
   lz::ResMember* th = nullptr;
   lz::ResMember* td = nullptr;
-  int64_t* cmds = nullptr;
-  void* cmds_dev = nullptr;
+  uint64_t* lines = nullptr;
+  void* lines_dev = nullptr;
   const size_t tb = sizeof(lz::ResMember) * lz::kRsMaxHandles;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&th), tb) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&td), tb) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&cmds), 128, hipHostMallocMapped | hipHostMallocCoherent) !=
-          hipSuccess ||
-      hipHostGetDevicePointer(&cmds_dev, cmds, 0) != hipSuccess || !cmds_dev) {
+      hipHostMalloc(reinterpret_cast<void**>(&lines), kRsLinesBytes,
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(&lines_dev, lines, 0) != hipSuccess || !lines_dev) {
     if (st) (void)hipStreamDestroy(st);
     if (ev) (void)hipEventDestroy(ev);
     if (th) (void)hipHostFree(th);
     if (td) (void)hipFree(td);
-    if (cmds) (void)hipHostFree(cmds);
+    if (lines) (void)hipHostFree(lines);
     return fail(LZ_ERR_OOM, "resident server setup failed");
   }
-  static_assert(lz::kRsMaxHandles * sizeof(int64_t) <= 128, "one command line");
-  std::memset(cmds, 0, 128);
+  std::memset(lines, 0, kRsLinesBytes);
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0)
     khz = 100000;
@@ -625,8 +652,8 @@ static lz_status rs_server_init(RsServer& sv, int device) {
   sv.ev = ev;
   sv.table_host = th;
   sv.table_dev = td;
-  sv.cmds = cmds;
-  sv.cmds_dev = static_cast<const int64_t*>(cmds_dev);
+  sv.lines = lines;
+  sv.lines_dev = static_cast<const uint64_t*>(lines_dev);
   sv.khz = khz;
   sv.n = 0;
   sv.active = false;
@@ -649,11 +676,11 @@ static void rs_server_ended(RsServer& sv) {
 
 static lz_status rs_server_stop(RsServer& sv) {
   if (!sv.active) return LZ_OK;
-  // one mailbox's stop command makes every wave leave; the word is restored after
+  // one line's stop granule makes every wave leave; the granule is restored after
   lz_handle* m0 = sv.members[0];
-  __atomic_store_n(&sv.cmds[0], (int64_t)-1, __ATOMIC_RELEASE);
+  __atomic_store_n(&sv.lines[0], kRsStop, __ATOMIC_RELEASE);
   const hipError_t e = hipStreamSynchronize(sv.stream);
-  __atomic_store_n(&sv.cmds[0], m0->rs_posted, __ATOMIC_RELEASE);
+  __atomic_store_n(&sv.lines[0], m0->rs_line[0], __ATOMIC_RELEASE);
   rs_server_ended(sv);
   if (e != hipSuccess) return fail(LZ_ERR_HIP, "resident stop: %s", hipGetErrorString(e));
   return LZ_OK;
@@ -670,7 +697,7 @@ static void resident_unload() {
   for (int d = 0; d < kRsMaxDevices; ++d) {
     RsServer& sv = g_rs[d];
     if (!sv.init || !sv.active || sv.n == 0) continue;
-    __atomic_store_n(&sv.cmds[0], (int64_t)-1, __ATOMIC_RELEASE);
+    __atomic_store_n(&sv.lines[0], kRsStop, __ATOMIC_RELEASE);
     any = true;
   }
   if (any) usleep(2000);  // a poll period is ~2 us; the waves exit on sight
@@ -687,8 +714,9 @@ static lz_status rs_server_launch(RsServer& sv) {
     r.f64 = m->f64;
     lz::ResBox& box = r.box;
     m->rs_slot = i;
-    __atomic_store_n(&sv.cmds[i], m->rs_posted, __ATOMIC_RELEASE);
-    box.cmd = sv.cmds_dev + i;
+    rs_write_line(sv, m);  // the slot's line holds this member's latest request
+    box.inline_words = rs_inline_words(m, m->rs_use_noise);
+    box.act_words = rs_act_words(m);
     box.resp = reinterpret_cast<int64_t*>(m->rs_dev + kRsResp);
     box.act = reinterpret_cast<const float*>(m->rs_dev + kRsAct);
     box.noise = reinterpret_cast<const double*>(m->rs_dev + kRsNoise);
@@ -707,7 +735,7 @@ static lz_status rs_server_launch(RsServer& sv) {
   }
   HIP_TRY(hipMemcpyAsync(sv.table_dev, sv.table_host, sizeof(lz::ResMember) * sv.n,
                          hipMemcpyHostToDevice, sv.stream));
-  const int e = lz::launch_resident_multi(sv.table_dev, sv.n, rs_idle_ticks(sv), sv.stream);
+  const int e = lz::launch_resident_multi(sv.table_dev, sv.n, sv.lines_dev, rs_idle_ticks(sv), sv.stream);
   if (e != 0) return fail(LZ_ERR_HIP, "resident launch: %s", hipGetErrorString((hipError_t)e));
   sv.active = true;
   for (int i = 0; i < sv.n; ++i) sv.members[i]->rs_active = true;
@@ -797,11 +825,20 @@ lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noi
   }
   h->rs_use_noise = use_noise;
   const int64_t seq = h->rs_seq + 1;
-  if (needs_act) std::memcpy(h->rs_pin + kRsAct, actions, (size_t)n * h->desc.action_dim * 4);
-  if (noise) std::memcpy(h->rs_pin + kRsNoise, noise, (size_t)n * 3 * 8);
+  const int iw = rs_inline_words(h, use_noise);
+  uint32_t words[lz::kRsLineWords] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (iw >= 0) {  // the inputs travel in the request line
+    const int aw = rs_act_words(h);
+    if (aw) std::memcpy(words, actions, (size_t)aw * 4);
+    if (noise) std::memcpy(words + aw, noise, 3 * 8);  // little endian: lo, hi halves
+  } else {        // the mailbox path: inputs there first, the line's command granule after
+    if (needs_act) std::memcpy(h->rs_pin + kRsAct, actions, (size_t)n * h->desc.action_dim * 4);
+    if (noise) std::memcpy(h->rs_pin + kRsNoise, noise, (size_t)n * 3 * 8);
+  }
+  for (int g = 0; g < lz::kRsLineWords; ++g) h->rs_line[g] = rs_granule(seq, words[g]);
   h->rs_posted = seq;
-  // the inputs are in the mailbox before the command word changes (release; x86 TSO)
-  __atomic_store_n(&sv.cmds[h->rs_slot], seq, __ATOMIC_RELEASE);
+  // (x86 TSO: the mailbox inputs are visible before the granules)
+  rs_write_line(sv, h);
   if (!sv.active) {
     const lz_status q = rs_server_launch(sv);
     if (q != LZ_OK) return q;

@@ -21,10 +21,24 @@ __device__ __forceinline__ V gload(const V* p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
   else return *p;
 }
+// LZ_STEP_WT (A/B builds only, tools/build_ab.sh; default 0): the streaming (NT) stores
+// as write-through `sc1` stores instead (the line leaves the XCD's L2 at once: nothing
+// left dirty at the kernel boundary, MI355X_MICROARCH.md "stores of each flavour").
+#ifndef LZ_STEP_WT
+#define LZ_STEP_WT 0
+#endif
 template <bool NT, typename V>
 __device__ __forceinline__ void gstore(V* p, V v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  if constexpr (NT && LZ_STEP_WT) {
+    if constexpr (sizeof(V) == 16)
+      asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else
+      __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if constexpr (NT) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
 }
 
 // 64-lane ballot compaction: returns this lane's slot in the compact list (or -1).

@@ -332,27 +332,39 @@ int launch_step(int system, int f64, const KArgs& a, void* stream);
 // Resident step server (lz_resident_step): ONE launch per process and device serves
 // every handle that steps through lz_resident_step -- one wave per handle (n <= 64 envs
 // each, up to kRsMaxHandles handles) plus ONE poller wave, so a DummyVecEnv of several
-// drop-in envs shares one launch on one stream (one hardware queue).  The host posts a
-// request as: inputs into the handle's mailbox (mapped, coherent host memory), then the
-// request's number into the handle's word of the server's command line (release).  The
-// poller alone reads host memory while idle -- the whole command line in one wave-wide
-// load per poll -- and hands each new request number to its member wave through LDS;
-// the member waves wait on LDS, not on PCIe (N waves polling host memory slowed every
-// request: 5.3 -> 11.4 us at 8 handles, 24.9 at 16, profiles/r03/resident).  A member
-// wave holds its handle's state in registers, serves request `next`, `next + 1`, ... each
-// exactly as one k_step launch would (step_body), writes obs | reward | done and the
-// handle's state planes (pub: the copy lz_resident_read_state returns without stopping
-// the server) into the mailbox and then *resp = the request's number (release, system
-// scope).  All waves leave together: on -1 in any command word, or after idle_ticks
-// wall-clock ticks without a new request; each member stores its state back to the
-// planes.  The host relaunches the server (with every registered handle) when a request
-// finds it gone.
+// drop-in envs shares one launch on one stream (one hardware queue).
+//
+// Requests travel in the server's REQUEST LINES: one 64-B line per member in mapped,
+// coherent host memory (kRsLineWords 8-byte granules; 16 lines = 1 KiB).  Every granule
+// is {tag = the request number's low 31 bits (bits 63..32), one 32-bit data word (bits
+// 31..0)}, written by ONE aligned 8-byte host store, so a granule is read whole or not
+// at all and needs no ordering (the handoff-granule form of the MI355X guide's hand-off
+// table).  A request whose inputs fit in 8 words -- a 1-env handle: its actions (A
+// float32 words) and injected noise (3 float64 = 6 words: PMSM / HR / TP / SC) -- travels
+// INSIDE its line: the poller reads every member's line with one wave-wide load per poll
+// (lanes 4k..4k+3 = line k, two granules each), accepts line k when all its used
+// granules carry the same new tag (a torn read shows mixed tags and is simply read again
+// at the next poll), copies the data words into LDS and hands the tag to member wave k
+// through LDS.  One PCIe read round trip per request.  Larger handles (n > 1 env) use
+// granule 0 as a command word only and their member wave reads the inputs from the
+// handle's mailbox (the round-2 path: a second round trip).  (Rounds 2-3: one command
+// word per member, payload always from the mailbox -- 6.0 us per call; a poller wave per
+// handle slowed every request as handles were added: 5.3 -> 11.4 us at 8, 24.9 at 16,
+// profiles/r03/resident.)  A member wave holds its handle's state in registers, serves
+// requests `next`, `next + 1`, ... each exactly as one k_step launch would (step_body),
+// writes obs | reward | done and the handle's state planes (pub: the copy
+// lz_resident_read_state returns without stopping the server) into the mailbox and then
+// *resp = the request's number (release, system scope).  All waves leave together: on an
+// all-ones granule 0 in any line (stop), or after idle_ticks wall-clock ticks without a
+// new request; each member stores its state back to the planes.  The host relaunches the
+// server (with every registered handle) when a request finds it gone.
 constexpr int kRsMaxHandles = 15;  // + the poller: 16 waves, one 1024-thread workgroup
+constexpr int kRsLineWords = 8;    // granules per request line (64 B)
+constexpr uint32_t kRsTagMask = 0x7fffffffu;  // tags: 31 bits (an all-ones granule = stop)
 struct ResBox {
-  const int64_t* cmd;   // host -> device: request number, -1 = stop (the server's command line)
   int64_t* resp;        // device -> host: number of the last request served
-  const float* act;     // [n, A]
-  const double* noise;  // [n, 3] (with use_noise)
+  const float* act;     // [n, A] (mailbox path)
+  const double* noise;  // [n, 3] (mailbox path, with use_noise)
   void* obs;            // T [n, O]
   void* rew;            // T [n]
   uint8_t* done;        // [n]
@@ -360,6 +372,9 @@ struct ResBox {
   int32_t pub_es[kMaxPlanes];  // their element sizes
   int64_t next;         // first request this launch serves
   int32_t use_noise;
+  int32_t inline_words; // >= 0: the request's inputs travel in its line (that many data
+                        // words: act_words actions, then 6 noise words); -1: mailbox path
+  int32_t act_words;    // action words in the line (0 for a system without actions)
 };
 struct ResMember {      // one wave of the server
   KArgs a;
@@ -367,7 +382,8 @@ struct ResMember {      // one wave of the server
   int32_t system, f64;
 };
 // table: device copy of n members; one workgroup of 64 (n + 1) threads, wave n the poller
-int launch_resident_multi(const ResMember* table, int n, uint64_t idle_ticks, void* stream);
+int launch_resident_multi(const ResMember* table, int n, const uint64_t* lines, uint64_t idle_ticks,
+                          void* stream);
 int launch_rollout(int system, int f64, const KArgs& a, void* stream);
 // lz_get_launch_shape of lz_step (which = 1) / lz_rollout (which = 2): out[5] = kernel,
 // envs per wave, waves per workgroup, workgroups, flags

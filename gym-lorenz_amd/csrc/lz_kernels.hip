@@ -1145,20 +1145,24 @@ int env_launch_shape(int which, int system, int f64, const KArgs& a, int32_t* o)
 }
 
 // ------------------------------------------------------------------ resident step server
-// lz_resident_step (lz_internal.h ResBox / ResMember): the per-env drop-in classes step
-// ONE env per env.step() call, and a launch + stream synchronisation per call costs
-// 20-27 us (profiles/r01/dropin).  This kernel stays on the GPU between calls: one wave
-// per registered handle serves that handle's requests with the same step_body as k_step
-// (state in registers, tick += 1 per request, injected noise staged through LDS), the
-// reply going straight into host memory; one poller wave watches the command line and
-// hands request numbers to the member waves through LDS.  Bounded: every wave leaves on
-// a stop command (-1 in any command word) or after idle_ticks without a new request (the
-// shared flag in LDS), so the launch ends as a whole and a relaunch includes every handle.
+// lz_resident_step (lz_internal.h ResBox / ResMember, the request lines): the per-env
+// drop-in classes step ONE env per env.step() call, and a launch + stream synchronisation
+// per call costs 20-27 us (profiles/r01/dropin).  This kernel stays on the GPU between
+// calls: one wave per registered handle serves that handle's requests with the same
+// step_body as k_step (state in registers, tick += 1 per request, injected noise staged
+// through LDS), the reply going straight into host memory; one poller wave reads every
+// member's request line and hands new requests (tag + inline inputs) to the member waves
+// through LDS.  Bounded: every wave leaves on a stop granule or after idle_ticks without
+// a new request (the shared flag in LDS), so the launch ends as a whole and a relaunch
+// includes every handle.
 struct ResShared {
   int exit_;
-  unsigned long long last;          // wall_clock64() of the latest new request / reply
-  int64_t req[kRsMaxHandles];       // the newest request number posted to each member
+  unsigned long long last;                  // wall_clock64() of the latest new request / reply
+  uint32_t req[kRsMaxHandles];              // the newest request tag handed to each member
+  uint32_t pay[kRsMaxHandles][kRsLineWords];  // its inline input words
 };
+
+__device__ __forceinline__ uint32_t rs_tag(int64_t seq) { return (uint32_t)seq & kRsTagMask; }
 
 template <class Sys, typename T>
 __device__ __forceinline__ void resident_serve(const ResMember& m, int wave, ResShared* sh, double* s_nz) {
@@ -1166,6 +1170,7 @@ __device__ __forceinline__ void resident_serve(const ResMember& m, int wave, Res
   const ResBox& box = m.box;
   const int lane = (int)(threadIdx.x & 63u);
   const bool live = lane < a.n;
+  const bool inl = box.inline_words >= 0;  // wave-uniform
   Sys sys;
   sys.setup(a);
   int32_t steps = 0;
@@ -1189,15 +1194,16 @@ __device__ __forceinline__ void resident_serve(const ResMember& m, int wave, Res
   for (int p = 0; p < kMaxPlanes; ++p) pubk.pl[p] = box.pub[p];
   int64_t next = box.next;
   for (;;) {
-    int64_t c = 0;
+    int c = 0;
     if (lane == 0) {  // LDS only: the poller reads host memory
+      const uint32_t want = rs_tag(next);
       for (;;) {
-        if (__hip_atomic_load(&sh->req[wave], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= next) {
-          c = next;
+        if (__hip_atomic_load(&sh->req[wave], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == want) {
+          c = 1;
           break;
         }
         if (__hip_atomic_load(&sh->exit_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-          c = -2;
+          c = -1;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -1207,18 +1213,29 @@ __device__ __forceinline__ void resident_serve(const ResMember& m, int wave, Res
     if (c < 0) break;
     float act[Sys::A > 0 ? Sys::A : 1];
     if (live) {
+      if (inl) {  // one env (lane 0): the inputs came in the request line, now in LDS
+        const uint32_t* w = sh->pay[wave];
 #pragma unroll
-      for (int j = 0; j < Sys::A; ++j)
-        act[j] = __hip_atomic_load(box.act + lane * Sys::A + j, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-      if (box.use_noise) {  // the three loads in flight together, then into LDS
-        double nzv[3];
+        for (int j = 0; j < Sys::A; ++j) act[j] = j < box.act_words ? __uint_as_float(w[j]) : 0.0f;
+        if (box.use_noise) {
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          nzv[j] = __hip_atomic_load(box.noise + lane * 3 + j, __ATOMIC_RELAXED,
+          for (int j = 0; j < 3; ++j)
+            s_nz[j] = __hiloint2double((int)w[box.act_words + 2 * j + 1], (int)w[box.act_words + 2 * j]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < Sys::A; ++j)
+          act[j] = __hip_atomic_load(box.act + lane * Sys::A + j, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_SYSTEM);
+        if (box.use_noise) {  // the three loads in flight together, then into LDS
+          double nzv[3];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) s_nz[lane * 3 + j] = nzv[j];
+          for (int j = 0; j < 3; ++j)
+            nzv[j] = __hip_atomic_load(box.noise + lane * 3 + j, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+          for (int j = 0; j < 3; ++j) s_nz[lane * 3 + j] = nzv[j];
+        }
       }
     }
     T o[Sys::O];
@@ -1250,30 +1267,45 @@ __device__ __forceinline__ void resident_serve(const ResMember& m, int wave, Res
   if (lane == 0) *a.tick_out = tick;
 }
 
-// The poller wave: every member's command word sits in ONE 128-B line of mapped host
-// memory (the server's command line), so one wave-wide load -- lane i reads word i, one
-// PCIe read -- sees every posted request; a changed word is handed to its member wave
-// through LDS.  (A doorbell word read first, then the command words, cost a third PCIe
-// round trip per request: 6.8 us instead of 5.3 for one handle.)
-__device__ void resident_poll(const ResMember* __restrict__ table, int n, ResShared* sh,
-                              uint64_t idle_ticks) {
+// The poller wave: member k's request line is granules 8k .. 8k+7 of `lines` (mapped host
+// memory); lane 4k + q reads granules 8k + 2q and 8k + 2q + 1 (two 8-B loads issued
+// together: one PCIe round trip per poll for every member).  Line k is accepted when
+// granule 0's tag differs from the last one handed over and every granule the member
+// uses (inline_words, at least 1) carries that tag; then the four lanes copy the data
+// words into LDS and lane 4k hands the tag over (release, workgroup scope).  An all-ones
+// granule 0 is the stop command.
+__device__ void resident_poll(const ResMember* __restrict__ table, int n, const uint64_t* lines,
+                              ResShared* sh, uint64_t idle_ticks) {
   const int lane = (int)(threadIdx.x & 63u);
-  const int64_t* cmd = lane < n ? table[lane].box.cmd : nullptr;
-  int64_t seen = INT64_MIN;  // the first pass publishes every word (a request may predate the launch)
+  const int k = lane >> 2, q = lane & 3;
+  const bool mine = k < n;
+  int ng = 1;
+  if (mine && table[k].box.inline_words > 1) ng = table[k].box.inline_words;
+  const uint64_t* src = lines + (int64_t)k * kRsLineWords + 2 * q;
+  uint32_t seen = 0xffffffffu;  // no tag: the first pass hands over every line (a request
+                                // may predate the launch)
   for (;;) {
-    bool stop = false, moved = false;
-    if (lane < n) {
-      const int64_t c = __hip_atomic_load(cmd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (c < 0) {
-        stop = true;
-      } else if (c != seen) {
-        seen = c;
-        moved = true;
-        __hip_atomic_store(&sh->req[lane], c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
+    uint64_t g0 = 0, g1 = 0;
+    if (mine) {
+      g0 = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      g1 = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    const uint32_t tag_a = (uint32_t)(g0 >> 32), tag_b = (uint32_t)(g1 >> 32);
+    const uint32_t t0 = (uint32_t)__shfl((int)tag_a, lane & ~3, 64);  // the line's granule 0
+    const bool stop = mine && q == 0 && g0 == ~0ull;
     if (__ballot(stop)) break;  // stop: every wave leaves
-    if (__ballot(moved)) {
+    const bool ok = mine && (2 * q >= ng || tag_a == t0) && (2 * q + 1 >= ng || tag_b == t0);
+    const unsigned long long okm = __ballot(ok);
+    const bool whole = ((okm >> (4 * k)) & 0xfull) == 0xfull;
+    const bool fresh = mine && whole && t0 != seen;
+    if (fresh) {
+      if (2 * q < ng) sh->pay[k][2 * q] = (uint32_t)g0;
+      if (2 * q + 1 < ng) sh->pay[k][2 * q + 1] = (uint32_t)g1;
+      seen = t0;
+    }
+    if (fresh && q == 0)
+      __hip_atomic_store(&sh->req[k], t0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (__ballot(fresh)) {
       if (lane == 0)
         __hip_atomic_fetch_max(&sh->last, (unsigned long long)wall_clock64(), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1295,7 +1327,7 @@ __device__ void resident_poll(const ResMember* __restrict__ table, int n, ResSha
 // float64 RK4 bodies do not spill) or up to 15 (16 waves: 128 VGPRs)
 template <int kWaves>
 __global__ __launch_bounds__(64 * kWaves) void k_resident_multi(
-    const ResMember* __restrict__ table, int n, uint64_t idle_ticks) {
+    const ResMember* __restrict__ table, int n, const uint64_t* lines, uint64_t idle_ticks) {
   __shared__ ResShared sh;
   __shared__ double s_nz[kRsMaxHandles][64 * 3];
   // wave-uniform to the compiler too: the member's fields are scalar loads, and the
@@ -1305,10 +1337,10 @@ __global__ __launch_bounds__(64 * kWaves) void k_resident_multi(
     sh.exit_ = 0;
     sh.last = wall_clock64();
   }
-  if ((int)threadIdx.x < n) sh.req[threadIdx.x] = table[threadIdx.x].box.next - 1;
+  if ((int)threadIdx.x < n) sh.req[threadIdx.x] = rs_tag(table[threadIdx.x].box.next - 1);
   __syncthreads();
   if (wave == n) {
-    resident_poll(table, n, &sh, idle_ticks);
+    resident_poll(table, n, lines, &sh, idle_ticks);
     return;
   }
   const ResMember& m = table[wave];
@@ -1341,14 +1373,15 @@ __global__ __launch_bounds__(64 * kWaves) void k_resident_multi(
   }
 }
 
-int launch_resident_multi(const ResMember* table, int n, uint64_t idle_ticks, void* stream) {
+int launch_resident_multi(const ResMember* table, int n, const uint64_t* lines, uint64_t idle_ticks,
+                          void* stream) {
   if (n < 1 || n > kRsMaxHandles) return (int)hipErrorInvalidValue;
   if (n + 1 <= 8)
     hipLaunchKernelGGL(k_resident_multi<8>, dim3(1), dim3(64 * (n + 1)), 0, static_cast<hipStream_t>(stream),
-                       table, n, idle_ticks);
+                       table, n, lines, idle_ticks);
   else
     hipLaunchKernelGGL(k_resident_multi<kRsMaxHandles + 1>, dim3(1), dim3(64 * (n + 1)), 0,
-                       static_cast<hipStream_t>(stream), table, n, idle_ticks);
+                       static_cast<hipStream_t>(stream), table, n, lines, idle_ticks);
   return (int)hipGetLastError();
 }
 

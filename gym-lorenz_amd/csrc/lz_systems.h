@@ -37,15 +37,19 @@ template <typename T>
 __device__ __forceinline__ T ld(const void* p, int64_t i) {
   return static_cast<const T*>(p)[i];
 }
-// LZ_STATE_NT (A/B builds only, tools/build_ab.sh; default 0): state-plane stores with
-// the non-temporal hint.  The product stores them plain: the planes are re-read by the
-// next launch.
+// LZ_STATE_NT / LZ_STATE_WT (A/B builds only, tools/build_ab.sh; default 0): state-plane
+// stores with the non-temporal hint / write-through (`sc1`, relaxed agent-scope atomic
+// store).  The product stores them plain: the planes are re-read by the next launch.
 #ifndef LZ_STATE_NT
 #define LZ_STATE_NT 0
 #endif
+#ifndef LZ_STATE_WT
+#define LZ_STATE_WT 0
+#endif
 template <typename T>
 __device__ __forceinline__ void st(void* p, int64_t i, T v) {
-  if constexpr (LZ_STATE_NT) __builtin_nontemporal_store(v, static_cast<T*>(p) + i);
+  if constexpr (LZ_STATE_WT) __hip_atomic_store(static_cast<T*>(p) + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else if constexpr (LZ_STATE_NT) __builtin_nontemporal_store(v, static_cast<T*>(p) + i);
   else static_cast<T*>(p)[i] = v;
 }
 

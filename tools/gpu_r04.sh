@@ -23,6 +23,23 @@ new2)  # the branch table (K = 3), the reference-class attention weights, cfg2 L
   timeout -k 10 1000 $PYT -x -m gpu tests > $O/gpu_tests.txt 2>&1 || exit 1
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" > $O/smoke.txt 2>&1
   ;;
+resident)  # the one-round-trip request lines: parity, then latency
+  timeout -k 10 600 $PYT -m gpu tests/test_gpu_resident.py "tests/test_gpu_rk4.py::test_rk4_resident_server_vs_oracle" \
+    -k "resident or dropin" tests/test_gpu_parity.py > $O/resident_tests.txt 2>&1 || exit 1
+  timeout -k 10 300 python tools/single_env_latency.py > $O/single_env_latency.json 2> $O/single_env_latency.err || exit 1
+  timeout -k 10 300 python tools/resident_latency.py > $O/resident_latency.json 2> $O/resident_latency.err || exit 1
+  ;;
+pmc)  # PMC traffic of the RK4 headline kernel (separate FETCH_SIZE / WRITE_SIZE passes)
+  K=_ZN2lz6k_stepINS_8SysL3RK4IfEEfLi0EEEvNS_5KArgsE
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 180 rocprofv3 --pmc $c -d $O/rk4_$c -o run --output-format csv -- python bench.py \
+      --integrator rk4 --launch eager --steps 400 --warmup 40 $BQ > $O/rk4_$c.log 2>&1 || exit 1
+  done
+  python tools/pmc_generic.py $O/rk4_FETCH_SIZE $O/rk4_WRITE_SIZE $K "SysL3RK4<float>" 1048576 68157440 \
+    $O/rk4_step_1M_pmc_summary.json || exit 1
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/rk4_trace -o run --output-format csv -- python bench.py \
+    --integrator rk4 $BQ > $O/rk4_trace.log 2>&1 || exit 1
+  ;;
 cfg3)  # cfg3's per-GPU shard (131,072) and cfg2 (65,536): where a step's time goes
   for n in 65536 131072; do
     timeout -k 10 200 python bench.py --envs $n $BQ > $O/bench_$n.json 2> $O/bench_$n.err || exit 1
@@ -30,9 +47,10 @@ cfg3)  # cfg3's per-GPU shard (131,072) and cfg2 (65,536): where a step's time g
       -- python bench.py --envs $n $BQ > $O/trace_$n.log 2>&1 || exit 1
   done
   AB_VARIANTS=0,2,16,8,24,3,0 timeout -k 10 300 python tools/ab_step.py 65536 131072 > $O/ab_step_variants.json || exit 1
-  for n in 131072 65536; do
-    timeout -k 10 500 python tools/ab_lib.py default ablib/libgym_lorenz_amd_state_nt.so 3 -- --envs $n $BQ \
-      > $O/ab_state_nt_$n.json 2> $O/ab_state_nt_$n.err || exit 1
+  for n in 131072 65536; do  # state planes nt / write-through, streamed outputs write-through, both
+    timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_state_nt.so \
+      ablib/libgym_lorenz_amd_state_wt.so ablib/libgym_lorenz_amd_out_wt.so ablib/libgym_lorenz_amd_all_wt.so \
+      -- --envs $n $BQ > $O/ab_stores_$n.json 2> $O/ab_stores_$n.err || exit 1
   done
   timeout -k 10 120 tools/launch_floor > $O/launch_floor.txt 2>&1
   ;;
