@@ -41,6 +41,29 @@ __device__ __forceinline__ void gstore(V* p, V v) {
   }
 }
 
+// The launch's tick (KArgs::tick_in).  A plain load of the uniform pointer compiles to a
+// scalar load, and the compiler's lgkmcnt(0) in front of the first use of a later
+// kernel-argument load (the action pointer) then also waits for it: one serial memory
+// round trip (the tick was written by the previous launch, possibly on another XCD)
+// before the action tile is even requested.  As a vector (relaxed atomic) load it
+// travels with the state and action loads.  tick_ready() marks the point of first use:
+// the empty asm takes the value as a VGPR operand, so the compiler neither moves it to
+// SGPRs (a v_readfirstlane, with its vmcnt wait, right behind the load) nor waits for
+// it earlier.  LZ_TICK_SCALAR=1 (A/B builds, tools/build_ab.sh) restores the scalar load.
+#ifndef LZ_TICK_SCALAR
+#define LZ_TICK_SCALAR 0
+#endif
+__device__ __forceinline__ uint64_t load_tick(const uint64_t* p) {
+  if constexpr (LZ_TICK_SCALAR) return *p;
+  else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t tick_ready(uint64_t t) {
+  if constexpr (LZ_TICK_SCALAR) return t;
+  uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32);
+  asm volatile("" : "+v"(lo), "+v"(hi));
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // 64-lane ballot compaction: returns this lane's slot in the compact list (or -1).
 // Must be reached by every lane of the wave.
 __device__ __forceinline__ int32_t wave_compact(bool flag, int32_t* counter) {

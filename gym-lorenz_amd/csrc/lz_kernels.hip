@@ -252,11 +252,12 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
   const int nb = (int)((a.n - base) < SB ? (a.n - base) : SB);
   const bool live = tid < nb;
   const bool vec = a.vec_ok != 0;
-  const uint64_t tick = *a.tick_in;
-  if (blockIdx.x == 0 && tid == 0) {
-    *a.counter_next = 0;
-    *a.tick_out = tick + a.tick_adv;
-  }
+  // the action pointer with the first batch of kernel-argument loads (otherwise the
+  // compiler issues its s_load after the first lgkmcnt wait: a second round trip before
+  // the action tile is requested)
+  const float* ga_early = static_cast<const float*>(a.act);
+  if constexpr (Sys::kUsesAction) asm volatile("" ::"s"(ga_early));
+  if (blockIdx.x == 0 && tid == 0) *a.counter_next = 0;
   if constexpr (kVN) {  // the statistics before this step, for the normalise pass
     if (blockIdx.x == 0 && (v.flags & LZ_VN_TRAINING) && !(v.flags & LZ_VN_DEFER)) {
       if (tid < 2 * Sys::O + 1) v.old[tid] = v.obs_state[tid];
@@ -272,9 +273,10 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
     if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
     if constexpr (kVN) ret_in = v.returns[i];
   }
+  uint64_t tick = load_tick(a.tick_in);  // in flight with the state and action loads
   float act[Sys::A];
   if constexpr (Sys::kUsesAction) {
-    const float* ga = static_cast<const float*>(a.act);
+    const float* ga = ga_early;
     if constexpr (kLds) {
       stage_in<NT, float, Sys::A, SB>(s_act, ga + base * Sys::A, nb, tid, vec);
       wg_barrier<kFullBar>();
@@ -287,12 +289,14 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
       for (int j = 0; j < Sys::A; ++j) act[j] = gload<NT>(ga + i * Sys::A + j);
     }
   }
+  tick = tick_ready(tick);
   T o[Sys::O];
   T rew = (T)0;
   bool did_reset;
   double rn = 0.0;  // kVN: the updated VecNormalize.returns[i] (before the done reset)
   const uint8_t dflag =
       step_body<Sys, T, false>(sys, steps, a, i, live, act, tick, 0, o, rew, did_reset);
+  if (blockIdx.x == 0 && tid == 0) *a.tick_out = tick + a.tick_adv;  // tick waited for here
   __shared__ double s_ret[kVN ? SB : 1];
   if constexpr (kVN) {  // VecNormalize.returns: r*gamma + reward, moments, then [done] = 0
     if (live) {
@@ -371,11 +375,8 @@ __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
   __shared__ __attribute__((aligned(16))) T s_obs[E][SB * Sys::O];
   const int tid = (int)threadIdx.x;
   const bool vec = a.vec_ok != 0;
-  const uint64_t tick = *a.tick_in;
-  if (blockIdx.x == 0 && tid == 0) {
-    *a.counter_next = 0;
-    *a.tick_out = tick + a.tick_adv;
-  }
+  uint64_t tick = load_tick(a.tick_in);
+  if (blockIdx.x == 0 && tid == 0) *a.counter_next = 0;
   Sys sys[E];
   int32_t steps[E];
   float act[E][2];
@@ -399,6 +400,7 @@ __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
       }
     }
   }
+  tick = tick_ready(tick);
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int64_t base = ((int64_t)blockIdx.x * E + e) * SB;
@@ -423,6 +425,7 @@ __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
     wg_barrier<false>();
     stage_out<true, T, Sys::O, SB>(static_cast<T*>(a.obs) + base * Sys::O, s_obs[e], nb, tid, vec);
   }
+  if (blockIdx.x == 0 && tid == 0) *a.tick_out = tick + a.tick_adv;
 }
 
 // Tiles per workgroup of k_step_multi: variant bits 14-15 (16384 x {1, 2, 3}) force 1

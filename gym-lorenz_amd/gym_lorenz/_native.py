@@ -280,6 +280,12 @@ for _name, (_res, _args) in _SIGS.items():
     _f.argtypes = _args
 
 
+# The same library through a second CDLL object whose functions carry no argtypes: the
+# per-env drop-in classes' hot call (envs/_single.py) passes prebuilt ctypes arguments
+# and skips the per-call argtypes conversion.  Not for general use.
+lib_fast = ctypes.CDLL(LIB_PATH)
+
+
 def check(status):
     if status != LZ_OK:
         raise LorenzEnvError(status, lib.lz_last_error().decode(errors="replace"))

@@ -35,7 +35,7 @@ pmc)  # PMC traffic of the RK4 headline kernel (separate FETCH_SIZE / WRITE_SIZE
     timeout -k 10 180 rocprofv3 --pmc $c -d $O/rk4_$c -o run --output-format csv -- python bench.py \
       --integrator rk4 --launch eager --steps 400 --warmup 40 $BQ > $O/rk4_$c.log 2>&1 || exit 1
   done
-  python tools/pmc_generic.py $O/rk4_FETCH_SIZE $O/rk4_WRITE_SIZE $K "SysL3RK4<float>" 1048576 68157440 \
+  python tools/pmc_generic.py $O/rk4_FETCH_SIZE $O/rk4_WRITE_SIZE $K "k_step<lz::SysL3RK4<float>" 1048576 68157440 \
     $O/rk4_step_1M_pmc_summary.json || exit 1
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/rk4_trace -o run --output-format csv -- python bench.py \
     --integrator rk4 $BQ > $O/rk4_trace.log 2>&1 || exit 1
@@ -53,6 +53,21 @@ cfg3)  # cfg3's per-GPU shard (131,072) and cfg2 (65,536): where a step's time g
       -- --envs $n $BQ > $O/ab_stores_$n.json 2> $O/ab_stores_$n.err || exit 1
   done
   timeout -k 10 120 tools/launch_floor > $O/launch_floor.txt 2>&1
+  ;;
+tick)  # the tick as a vector load + one kernel-argument round trip (vs HEAD's k_step)
+  timeout -k 10 600 $PYT -m gpu --maxfail=4 tests/test_gpu_parity.py tests/test_gpu_vecnorm_step.py \
+    "tests/test_gpu_rk4.py::test_l3_rk4_step_vs_oracle" > $O/tick_tests.txt 2>&1 || exit 1
+  for n in 131072 65536 1048576; do
+    timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_base.so \
+      ablib/libgym_lorenz_amd_statent.so -- --envs $n $BQ > $O/ab_tick_$n.json 2> $O/ab_tick_$n.err || exit 1
+  done
+  for r in 1 2; do
+    for nv in 65536:0 65536:3 65536:2 131072:0 131072:16 131072:3; do
+      timeout -k 10 200 python bench.py --envs ${nv%%:*} --variant ${nv##*:} $BQ \
+        > $O/var_${nv%%:*}_${nv##*:}_$r.json 2>> $O/var.err || exit 1
+    done
+  done
+  timeout -k 10 300 python tools/single_env_latency.py > $O/single_env_latency.json 2> $O/single_env_latency.err || exit 1
   ;;
 new)
   timeout -k 10 1100 $PYT -m gpu --maxfail=8 tests/test_gpu_rk4.py tests/test_gpu_vecnorm_step.py \
