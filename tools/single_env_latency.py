@@ -26,8 +26,10 @@ def timed(env, act, steps):
 
 def main():
     out = {}
-    for flag, label in (("0", "lz_step_host"), ("1", "lz_resident_step")):
+    for flag, cstep, label in (("0", "1", "lz_step_host"), ("1", "1", "lz_resident_step"),
+                               ("1", "0", "lz_resident_step, ctypes call (LZ_STEPPER=0)")):
         os.environ["LZ_RESIDENT"] = flag
+        os.environ["LZ_STEPPER"] = cstep
         res = {}
         np.random.seed(0)
         e = gl.make("lorenz_dynamic-v0")
