@@ -99,7 +99,8 @@ __device__ __forceinline__ void make_noise(const Sys& sys, const KArgs& a, int64
 // rollout) -- same arithmetic, but it takes no slot in the compact done list.
 // kNoDone: the launch can produce no done at all (a never-terminating system and no
 // step counter, see no_done()): the step alone, no done bookkeeping.
-template <class Sys, typename T, bool kRollout, bool kKeepTerm = false, bool kNoDone = false>
+template <class Sys, typename T, bool kRollout, bool kKeepTerm = false, bool kNoDone = false,
+          bool kInject = !kRollout>
 __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KArgs& a, int64_t i,
                                              bool live, const float* act, uint64_t tick, int k,
                                              T* o, T& rew, bool& did_reset,
@@ -120,7 +121,7 @@ __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KAr
     bool use_nz = false;
     if constexpr (Sys::kNoise) {
       if (a.flags & LZ_FLAG_ADD_NOISE) {
-        make_noise<Sys, T, !kRollout>(sys, a, i, tick, nz);
+        make_noise<Sys, T, kInject>(sys, a, i, tick, nz);
         use_nz = true;
       }
     }

@@ -252,10 +252,12 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
   const int nb = (int)((a.n - base) < SB ? (a.n - base) : SB);
   const bool live = tid < nb;
   const bool vec = a.vec_ok != 0;
-  // the action pointer with the first batch of kernel-argument loads (otherwise the
-  // compiler issues its s_load after the first lgkmcnt wait: a second round trip before
-  // the action tile is requested)
+  // the pointers the step dereferences, with the first batch of kernel-argument loads:
+  // otherwise the compiler issues their s_loads late and waits for each (the action
+  // pointer's after the first lgkmcnt wait, the terminal-obs pointer's right after the
+  // action barrier) -- serial kernel-argument round trips on the step's critical path
   const float* ga_early = static_cast<const float*>(a.act);
+  asm volatile("" ::"s"(a.term_obs), "s"(a.obs), "s"(a.rew), "s"(a.done));
   if constexpr (Sys::kUsesAction) asm volatile("" ::"s"(ga_early));
   if (blockIdx.x == 0 && tid == 0) *a.counter_next = 0;
   if constexpr (kVN) {  // the statistics before this step, for the normalise pass
@@ -368,39 +370,77 @@ __global__ __launch_bounds__(step_block<VB>()) void k_step_vn(KArgs a, VArgs v) 
 // in k_step, one LDS buffer per tile (no reuse hazard between tiles).  Same step_body,
 // same per-env arithmetic: bit-identical to k_step.
 typedef float f2m __attribute__((ext_vector_type(2)));
+// Load layout of k_step_multi per system (measured, profiles/r04/kargs/): "flat" issues
+// every tile's loads straight-line -- each lane loads (index clamped to the last env; a
+// dead lane's values are never stored), the step counter unconditionally (plane 0 stands
+// in when there is none, the value then unused), a scheduling barrier between tiles -- so
+// the compiler's wait at tile 0's step covers tile 0's loads only, and the tick is a
+// scalar load (HR f32 1M: 18.19 -> 17.35 us).  PMSM keeps round 3's layout (loads under
+// the lane condition, the vector tick of k_step): flat measured 23.66 -> 26.14 us there.
+template <class Sys>
+struct multi_flat_loads {
+  static constexpr bool value = false;
+};
+template <>
+struct multi_flat_loads<SysHR<float>> {
+  static constexpr bool value = true;
+};
+
 template <class Sys, typename T, int E, bool kDoneT = false>
 __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
   static_assert(Sys::A == 2 && Sys::kUsesAction, "k_step_multi: two-action systems");
   constexpr int SB = kBlock;
+  constexpr bool kFlat = multi_flat_loads<Sys>::value;
   __shared__ __attribute__((aligned(16))) T s_obs[E][SB * Sys::O];
   const int tid = (int)threadIdx.x;
   const bool vec = a.vec_ok != 0;
-  uint64_t tick = load_tick(a.tick_in);
-  if (blockIdx.x == 0 && tid == 0) *a.counter_next = 0;
   Sys sys[E];
   int32_t steps[E];
   float act[E][2];
   const float* ga = static_cast<const float*>(a.act);
+  uint64_t tick;
+  if constexpr (kFlat) {
+    tick = *a.tick_in;
+    if (blockIdx.x == 0 && tid == 0) {
+      *a.counter_next = 0;
+      *a.tick_out = tick + a.tick_adv;
+    }
 #pragma unroll
-  for (int e = 0; e < E; ++e) {  // every tile's loads, in tile order
-    const int64_t i = ((int64_t)blockIdx.x * E + e) * SB + tid;
-    sys[e].setup(a);
-    steps[e] = 0;
-    act[e][0] = act[e][1] = 0.0f;
-    if (i < a.n) {
-      sys[e].load(a, i);
-      if (a.count_steps) steps[e] = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
-      if (vec) {
-        const f2m v2 = __builtin_nontemporal_load(reinterpret_cast<const f2m*>(ga) + i);
-        act[e][0] = v2[0];
-        act[e][1] = v2[1];
-      } else {
-        act[e][0] = __builtin_nontemporal_load(ga + 2 * i);
-        act[e][1] = __builtin_nontemporal_load(ga + 2 * i + 1);
+    for (int e = 0; e < E; ++e) {
+      const int64_t i = ((int64_t)blockIdx.x * E + e) * SB + tid;
+      const int64_t ic = i < a.n ? i : a.n - 1;
+      sys[e].setup(a);
+      sys[e].load(a, ic);
+      const int32_t* sp = static_cast<const int32_t*>(a.count_steps ? a.pl[Sys::kStepPlane] : a.pl[0]);
+      steps[e] = sp[ic];
+      act[e][0] = __builtin_nontemporal_load(ga + 2 * ic);  // (merged into one 8-B load)
+      act[e][1] = __builtin_nontemporal_load(ga + 2 * ic + 1);
+      __builtin_amdgcn_sched_barrier(0);  // tile e's loads stay ahead of tile e+1's
+    }
+  } else {
+    tick = load_tick(a.tick_in);
+    if (blockIdx.x == 0 && tid == 0) *a.counter_next = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {  // every tile's loads, in tile order
+      const int64_t i = ((int64_t)blockIdx.x * E + e) * SB + tid;
+      sys[e].setup(a);
+      steps[e] = 0;
+      act[e][0] = act[e][1] = 0.0f;
+      if (i < a.n) {
+        sys[e].load(a, i);
+        if (a.count_steps) steps[e] = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
+        if (vec) {
+          const f2m v2 = __builtin_nontemporal_load(reinterpret_cast<const f2m*>(ga) + i);
+          act[e][0] = v2[0];
+          act[e][1] = v2[1];
+        } else {
+          act[e][0] = __builtin_nontemporal_load(ga + 2 * i);
+          act[e][1] = __builtin_nontemporal_load(ga + 2 * i + 1);
+        }
       }
     }
+    tick = tick_ready(tick);
   }
-  tick = tick_ready(tick);
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int64_t base = ((int64_t)blockIdx.x * E + e) * SB;
@@ -411,8 +451,9 @@ __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
     T o[Sys::O];
     T rew = (T)0;
     bool did_reset;
-    const uint8_t dflag =
-        step_body<Sys, T, false>(sys[e], steps[e], a, i, live, act[e], tick, 0, o, rew, did_reset);
+    // noise is never injected here (step_tiles sends injected-noise launches to k_step)
+    const uint8_t dflag = step_body<Sys, T, false, false, false, !kFlat>(sys[e], steps[e], a, i, live, act[e],
+                                                                         tick, 0, o, rew, did_reset);
     if (live) {
       sys[e].store(a, i);
       if (did_reset) sys[e].store_autoreset_extra(a, i);
@@ -425,7 +466,9 @@ __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
     wg_barrier<false>();
     stage_out<true, T, Sys::O, SB>(static_cast<T*>(a.obs) + base * Sys::O, s_obs[e], nb, tid, vec);
   }
-  if (blockIdx.x == 0 && tid == 0) *a.tick_out = tick + a.tick_adv;
+  if constexpr (!kFlat) {
+    if (blockIdx.x == 0 && tid == 0) *a.tick_out = tick + a.tick_adv;
+  }
 }
 
 // Tiles per workgroup of k_step_multi: variant bits 14-15 (16384 x {1, 2, 3}) force 1
@@ -455,6 +498,7 @@ inline int step_tiles_auto(int64_t n, int num_cus) {
   return (4 * groups > 3 * full && groups <= full) ? 4 : 1;
 }
 inline int step_tiles(const KArgs& a) {
+  if (a.noise) return 1;  // injected noise: k_step (k_step_multi draws its noise on device)
   switch ((a.variant >> 14) & 3) {
     case 1: return 1;
     case 2: return 2;

@@ -70,13 +70,21 @@ tick)  # the tick as a vector load + one kernel-argument round trip (vs HEAD's k
   timeout -k 10 300 python tools/single_env_latency.py > $O/single_env_latency.json 2> $O/single_env_latency.err || exit 1
   ;;
 kargs)  # one kernel-argument batch in k_step; straight-line multi-tile loads (vs HEAD = tick)
-  timeout -k 10 90 tools/vram_poll 20000 > $O/vram_poll.txt 2>&1 || exit 1
   timeout -k 10 600 $PYT -m gpu --maxfail=4 tests/test_gpu_step_multi.py tests/test_gpu_parity.py \
     tests/test_gpu_noise.py "tests/test_gpu_rk4.py::test_l3_rk4_step_vs_oracle" tests/test_gpu_resident.py \
     > $O/kargs_tests.txt 2>&1 || exit 1
   timeout -k 10 300 python tools/single_env_latency.py > $O/single_env_latency.json 2> $O/single_env_latency.err || exit 1
   for cfg in "--envs 131072" "--envs 65536" "--system pmsm --envs 1048576" "--system hr --envs 1048576" \
              "--envs 1048576" "--system pmsm --envs 262144"; do
+    tag=$(echo $cfg | tr -d ' -')
+    timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_tick.so \
+      -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
+  done
+  ;;
+rt)  # the resident round trip taken apart; the per-system multi-tile load layouts
+  timeout -k 10 120 tools/rt_probe 20000 > $O/rt_probe.txt 2>&1 || exit 1
+  timeout -k 10 600 $PYT -m gpu --maxfail=4 tests/test_gpu_step_multi.py > $O/multi_tests.txt 2>&1 || exit 1
+  for cfg in "--system pmsm --envs 1048576" "--system hr --envs 1048576"; do
     tag=$(echo $cfg | tr -d ' -')
     timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_tick.so \
       -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
