@@ -64,6 +64,8 @@ def parse(argv=None):
                         "vecnorm = VecNormalize(VecEnv).step fused (lz_step_vecnorm + "
                         "lz_vecnorm_apply), 1 GPU")
     p.add_argument("--K", type=int, default=2048, help="rollout length (--mode rollout)")
+    p.add_argument("--add-noise", type=int, choices=[0, 1], default=None,
+                   help=argparse.SUPPRESS)  # A/B: the process-noise flag (default: the config's)
     p.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                    help="--mode policy --policy mlp: fp32 = SB3's float32 forward "
                         "(lz_rollout_policy_f32), bf16 = the bf16-MFMA kernel")
@@ -998,6 +1000,8 @@ def main():
     kw = {"add_noise": True, "alpha": 0.5} if args.system == "pmsm" else {}
     if args.integrator == "rk4" and args.system in ("lorenz3", "lorenz4"):
         kw["integrator"] = "rk4"
+    if args.add_noise is not None:
+        kw["add_noise"] = bool(args.add_noise)
     env = gl.BatchedEnv(args.system, n, dtype="float32", seed=0, global_env_offset=start,
                         autoreset=True, device=local, max_episode_steps=args.max_episode_steps,
                         variant=args.variant, **kw)

@@ -126,6 +126,9 @@ struct lz_handle {
   int64_t rs_posted;    // number of the last request posted
   uint64_t rs_line[lz::kRsLineWords];  // the granules of its request line as last posted
   int rs_slot;          // its request line in the server (= its wave)
+  // one env: the reply arrives as tagged granules (lz_internal.h ResBox::reply); the data
+  // words of the last accepted reply (the published state for lz_resident_read_state)
+  uint32_t rs_rep[lz::kRsReplyWords];
 };
 
 // Stop the resident step server serving the handle (if it runs) and wait for it: every
@@ -555,9 +558,38 @@ static size_t rs_done_off(const lz_handle* h) {
 }
 static size_t rs_pub_stride(const lz_handle* h) { return align16((size_t)h->cfg.num_envs * 8); }
 static size_t rs_pub_off(const lz_handle* h) { return rs_done_off(h) + align16((size_t)h->cfg.num_envs); }
-static size_t rs_bytes(const lz_handle* h) {
-  return rs_pub_off(h) + (size_t)h->desc.n_planes * rs_pub_stride(h);
+static size_t rs_reply_off(const lz_handle* h) {
+  return (rs_pub_off(h) + (size_t)h->desc.n_planes * rs_pub_stride(h) + 63) & ~(size_t)63;
 }
+static size_t rs_bytes(const lz_handle* h) { return rs_reply_off(h) + lz::kRsReplyWords * 8; }
+
+// Word layout of a one-env handle's tagged reply (ResBox::rep_*): the 8-byte items first
+// (float64 planes, then float64 obs and reward), then the 4-byte ones (float32 / int32
+// planes, float32 obs and reward), then the done byte as a word.  Returns the word count.
+struct RsReplyLayout {
+  int32_t obs, rew, done, pub[lz::kMaxPlanes];
+};
+static int rs_reply_layout(const lz_handle* h, RsReplyLayout& L) {
+  int c = 0;
+  const int O = h->desc.obs_dim;
+  for (int p = 0; p < lz::kMaxPlanes; ++p) L.pub[p] = -1;
+  for (int pass = 8; pass >= 4; pass -= 4) {
+    for (int p = 0; p < h->desc.n_planes; ++p)
+      if (plane_elem(h->cfg.system, h->f64, p) == pass) {
+        L.pub[p] = c;
+        c += pass / 4;
+      }
+    if ((h->f64 ? 8 : 4) == pass) {
+      L.obs = c;
+      c += O * pass / 4;
+      L.rew = c;
+      c += pass / 4;
+    }
+  }
+  L.done = c++;
+  return c;
+}
+static bool rs_reply_mode(const lz_handle* h) { return h->cfg.num_envs == 1; }
 
 static volatile int64_t* rs_word(const lz_handle* h, size_t off) {
   return reinterpret_cast<volatile int64_t*>(h->rs_pin + off);
@@ -729,6 +761,16 @@ static lz_status rs_server_launch(RsServer& sv) {
     }
     box.next = m->rs_seq + 1;  // the requester's pending request, the others' next one
     box.use_noise = m->rs_use_noise;
+    for (int p = 0; p < lz::kMaxPlanes; ++p) box.rep_pub[p] = -1;
+    if (rs_reply_mode(m)) {
+      RsReplyLayout L;
+      box.rep_words = rs_reply_layout(m, L);
+      box.rep_obs = L.obs;
+      box.rep_rew = L.rew;
+      box.rep_done = L.done;
+      for (int p = 0; p < lz::kMaxPlanes; ++p) box.rep_pub[p] = L.pub[p];
+      box.reply = reinterpret_cast<uint64_t*>(m->rs_dev + rs_reply_off(m));
+    }
     // after everything already queued on the member's stream (reset, set_state, ...)
     HIP_TRY(hipEventRecord(sv.ev, m->stream));
     HIP_TRY(hipStreamWaitEvent(sv.stream, sv.ev, 0));
@@ -844,13 +886,30 @@ lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noi
     if (q != LZ_OK) return q;
   }
   volatile int64_t* resp = rs_word(h, kRsResp);
+  const bool rep_mode = rs_reply_mode(h);
+  RsReplyLayout L;
+  const int rw = rep_mode ? rs_reply_layout(h, L) : 0;
+  const uint64_t* rep = reinterpret_cast<const uint64_t*>(h->rs_pin + rs_reply_off(h));
+  const uint32_t tag = (uint32_t)seq & lz::kRsTagMask;
+  uint32_t rwords[lz::kRsReplyWords];
+  // the reply is in: the mailbox's resp word, or every tagged granule (each an atomic 8-B
+  // read; any granule still from an earlier request fails the check and is read again)
+  auto served = [&]() -> bool {
+    if (!rep_mode) return __atomic_load_n(const_cast<int64_t*>(resp), __ATOMIC_ACQUIRE) == seq;
+    for (int g = rw - 1; g >= 0; --g) {
+      const uint64_t v = __atomic_load_n(&rep[g], __ATOMIC_ACQUIRE);
+      if ((uint32_t)(v >> 32) != tag) return false;
+      rwords[g] = (uint32_t)v;
+    }
+    return true;
+  };
   for (uint32_t spin = 1;; ++spin) {
-    if (__atomic_load_n(const_cast<int64_t*>(resp), __ATOMIC_ACQUIRE) == seq) break;
+    if (served()) break;
     if ((spin & 4095u) == 0) {
       // the server may have exited (idle) before it saw this request
       const hipError_t q = hipStreamQuery(sv.stream);
       if (q == hipErrorNotReady) continue;
-      if (__atomic_load_n(const_cast<int64_t*>(resp), __ATOMIC_ACQUIRE) == seq) break;
+      if (served()) break;
       rs_server_ended(sv);
       if (q != hipSuccess) return fail(LZ_ERR_HIP, "resident server: %s", hipGetErrorString(q));
       const lz_status r = rs_server_launch(sv);
@@ -860,6 +919,14 @@ lz_status lz_resident_step(lz_handle* h, const float* actions, const double* noi
   }
   h->rs_seq = seq;
   h->rs_pub_valid = true;
+  if (rep_mode) {
+    std::memcpy(h->rs_rep, rwords, (size_t)rw * 4);
+    lk.unlock();
+    std::memcpy(obs_out, rwords + L.obs, (size_t)h->desc.obs_dim * es);
+    std::memcpy(rew_out, rwords + L.rew, es);
+    *done_out = (uint8_t)rwords[L.done];
+    return LZ_OK;
+  }
   lk.unlock();
   std::memcpy(obs_out, h->rs_pin + kRsOut, (size_t)n * h->desc.obs_dim * es);
   std::memcpy(rew_out, h->rs_pin + rs_rew_off(h), (size_t)n * es);
@@ -882,7 +949,13 @@ lz_status lz_resident_read_state(lz_handle* h, int32_t plane, void* host_dst) {
   {
     std::lock_guard<std::mutex> lk(g_rs_mu);
     if (h->rs_active && h->rs_pub_valid) {  // the server's copy after its last request
-      std::memcpy(host_dst, h->rs_pin + rs_pub_off(h) + (size_t)plane * rs_pub_stride(h), bytes);
+      if (rs_reply_mode(h)) {  // ... carried by that request's reply
+        RsReplyLayout L;
+        rs_reply_layout(h, L);
+        std::memcpy(host_dst, h->rs_rep + L.pub[plane], bytes);
+      } else {
+        std::memcpy(host_dst, h->rs_pin + rs_pub_off(h) + (size_t)plane * rs_pub_stride(h), bytes);
+      }
       return LZ_OK;
     }
   }

@@ -361,8 +361,9 @@ int launch_step(int system, int f64, const KArgs& a, void* stream);
 constexpr int kRsMaxHandles = 15;  // + the poller: 16 waves, one 1024-thread workgroup
 constexpr int kRsLineWords = 8;    // granules per request line (64 B)
 constexpr uint32_t kRsTagMask = 0x7fffffffu;  // tags: 31 bits (an all-ones granule = stop)
+constexpr int kRsReplyWords = 64;  // tagged reply granules of a one-env handle (one per lane)
 struct ResBox {
-  int64_t* resp;        // device -> host: number of the last request served
+  int64_t* resp;        // device -> host: number of the last request served (mailbox path)
   const float* act;     // [n, A] (mailbox path)
   const double* noise;  // [n, 3] (mailbox path, with use_noise)
   void* obs;            // T [n, O]
@@ -375,6 +376,15 @@ struct ResBox {
   int32_t inline_words; // >= 0: the request's inputs travel in its line (that many data
                         // words: act_words actions, then 6 noise words); -1: mailbox path
   int32_t act_words;    // action words in the line (0 for a system without actions)
+  // The reply of a one-env handle (inline_words >= 0): rep_words 8-byte granules
+  // {tag = request number (31 bits) << 32 | data word}, written by one wave-wide store (lane g
+  // granule g) with no ordering among them -- the host accepts the reply when every granule
+  // carries the request's tag.  Data words: obs at rep_obs, reward at rep_rew, the done byte
+  // at rep_done, published plane p at rep_pub[p] (8-byte values at even offsets); nullptr
+  // reply: the mailbox path (obs / rew / done / pub, then resp)
+  uint64_t* reply;
+  int32_t rep_words, rep_obs, rep_rew, rep_done;
+  int32_t rep_pub[kMaxPlanes];
 };
 struct ResMember {      // one wave of the server
   KArgs a;

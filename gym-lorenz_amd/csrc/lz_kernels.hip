@@ -1207,6 +1207,7 @@ struct ResShared {
   unsigned long long last;                  // wall_clock64() of the latest new request / reply
   uint32_t req[kRsMaxHandles];              // the newest request tag handed to each member
   uint32_t pay[kRsMaxHandles][kRsLineWords];  // its inline input words
+  uint64_t rep[kRsMaxHandles][kRsReplyWords / 2];  // a one-env member's reply words (as 2 x 32 b)
 };
 
 __device__ __forceinline__ uint32_t rs_tag(int64_t seq) { return (uint32_t)seq & kRsTagMask; }
@@ -1229,6 +1230,11 @@ __device__ __forceinline__ void resident_serve(const ResMember& m, int wave, Res
       const int es = box.pub_es[p];
       if (es == 8) static_cast<uint64_t*>(box.pub[p])[lane] = static_cast<const uint64_t*>(a.pl[p])[lane];
       else if (es == 4) static_cast<uint32_t*>(box.pub[p])[lane] = static_cast<const uint32_t*>(a.pl[p])[lane];
+      if (box.reply && es) {  // and the reply's plane words (planes a step does not store)
+        uint32_t* w = reinterpret_cast<uint32_t*>(sh->rep[wave]) + box.rep_pub[p];
+        w[0] = static_cast<const uint32_t*>(a.pl[p])[0];
+        if (es == 8) w[1] = static_cast<const uint32_t*>(a.pl[p])[1];
+      }
     }
   }
   uint64_t tick = *a.tick_in;
@@ -1239,6 +1245,10 @@ __device__ __forceinline__ void resident_serve(const ResMember& m, int wave, Res
   KArgs pubk = a;  // sys.store into the published planes
 #pragma unroll
   for (int p = 0; p < kMaxPlanes; ++p) pubk.pl[p] = box.pub[p];
+  KArgs pubr = a;  // ... or into the reply's words in LDS (one env, index 0)
+#pragma unroll
+  for (int p = 0; p < kMaxPlanes; ++p)
+    pubr.pl[p] = box.rep_pub[p] >= 0 ? reinterpret_cast<uint32_t*>(sh->rep[wave]) + box.rep_pub[p] : nullptr;
   int64_t next = box.next;
   for (;;) {
     int c = 0;
@@ -1290,21 +1300,38 @@ __device__ __forceinline__ void resident_serve(const ResMember& m, int wave, Res
     bool did_reset;
     const uint8_t d = step_body<Sys, T, false>(sys, steps, b, lane, live, act, tick, 0, o, rew,
                                                did_reset);
-    if (live) {
+    if (box.reply) {  // one env: the reply as tagged granules (ResBox), one store per lane
+      uint32_t* w = reinterpret_cast<uint32_t*>(sh->rep[wave]);
+      if (live) {  // lane 0 lays the words out in LDS (the planes through the LDS copy)
 #pragma unroll
-      for (int j = 0; j < Sys::O; ++j) static_cast<T*>(box.obs)[lane * Sys::O + j] = o[j];
-      static_cast<T*>(box.rew)[lane] = rew;
-      box.done[lane] = d;
-      sys.store(pubk, lane);
-      if (a.count_steps) static_cast<int32_t*>(pubk.pl[Sys::kStepPlane])[lane] = steps;
+        for (int j = 0; j < Sys::O; ++j) reinterpret_cast<T*>(w + box.rep_obs)[j] = o[j];
+        *reinterpret_cast<T*>(w + box.rep_rew) = rew;
+        w[box.rep_done] = d;
+        sys.store(pubr, 0);
+        if (a.count_steps) *static_cast<int32_t*>(pubr.pl[Sys::kStepPlane]) = steps;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < box.rep_words)
+        __hip_atomic_store(box.reply + lane, ((uint64_t)rs_tag(next) << 32) | w[lane], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      if (live) {
+#pragma unroll
+        for (int j = 0; j < Sys::O; ++j) static_cast<T*>(box.obs)[lane * Sys::O + j] = o[j];
+        static_cast<T*>(box.rew)[lane] = rew;
+        box.done[lane] = d;
+        sys.store(pubk, lane);
+        if (a.count_steps) static_cast<int32_t*>(pubk.pl[Sys::kStepPlane])[lane] = steps;
+      }
+      // the outputs of the whole wave reach host memory before the reply (release)
+      if (lane == 0) __hip_atomic_store(box.resp, next, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     tick += 1;
-    // the outputs of the whole wave reach host memory before the reply (release)
-    if (lane == 0) {
-      __hip_atomic_store(box.resp, next, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0)
       __hip_atomic_fetch_max(&sh->last, (unsigned long long)wall_clock64(), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
     ++next;
   }
   if (live) {
