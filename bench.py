@@ -247,11 +247,13 @@ def step_tiles(system, n, f64=False, num_cus=256, variant=0):
 
 
 def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=0,
-                integrator="euler"):
+                integrator="euler", noise=None):
     """Mangled name of the dominant kernel (lz_kernels.hip launch_all / launch_rollout_d).
     no_done: a rollout launch that cannot produce a done (LORENZ3 without a TimeLimit)
     runs the done-free instantiation (kNoDone = true).  integrator "rk4": SysL3RK4 /
-    SysL4RK4 (lz_systems.h), which take the generic launcher bounds."""
+    SysL4RK4 (lz_systems.h), which take the generic launcher bounds.  noise: the launch
+    draws process noise (default: PMSM, as this bench configures it) -- the one-wave
+    rollout then runs with a noise-producer wave (k_rollout kNP)."""
     tag = SYSTEM_INFO[system][1]
     if f64:
         tag = tag.replace("IfEEf", "IdEEd")
@@ -276,6 +278,9 @@ def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=
     if n < one_wave_below:
         if system == "lorenz3" and not f64 and not rk4 and n >= 32768:
             return "_ZN2lz15k_rollout_splitINS_%sLi2ELi%dE%sLi1EEEvNS_5KArgsE" % (sysname, D, b)
+        if (system == "pmsm" if noise is None else noise) and system in ("pmsm", "hr") \
+                and variant & (1 << 25):  # opt-in noise-producer wave
+            return "_ZN2lz12k_rollout_npINS_%sLi%dEEEvNS_5KArgsE" % (sysname, D)
         return "_ZN2lz9k_rolloutINS_%sLi64ELi%dE%sLb1EEEvNS_5KArgsE" % (sysname, D, b)
     return "_ZN2lz9k_rolloutINS_%sLi256ELi%dE%sLb1EEEvNS_5KArgsE" % (sysname, D, b)
 
@@ -1075,7 +1080,8 @@ def main():
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
             "kernel": kernel_name(args.system, args.mode, n, no_done=args.max_episode_steps == 0,
                                   num_cus=torch.cuda.get_device_properties(device).multi_processor_count,
-                                  variant=args.variant, integrator=kw.get("integrator", "euler")),
+                                  variant=args.variant, integrator=kw.get("integrator", "euler"),
+                                  noise=bool(env.config.flags & nat.FLAG_ADD_NOISE)),
             "avg_launch_us": launch_s * 1e6,
             "bytes_per_env_step": bytes_step,
             "note": "achieved = algorithmic bytes per launch (bytes_per_env_step x envs_per_gpu"

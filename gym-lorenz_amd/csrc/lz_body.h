@@ -100,11 +100,12 @@ __device__ __forceinline__ void make_noise(const Sys& sys, const KArgs& a, int64
 // kNoDone: the launch can produce no done at all (a never-terminating system and no
 // step counter, see no_done()): the step alone, no done bookkeeping.
 template <class Sys, typename T, bool kRollout, bool kKeepTerm = false, bool kNoDone = false,
-          bool kInject = !kRollout>
+          bool kInject = !kRollout, bool kZPre = false>
 __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KArgs& a, int64_t i,
                                              bool live, const float* act, uint64_t tick, int k,
                                              T* o, T& rew, bool& did_reset,
-                                             T* o_term = nullptr, bool lead = true) {
+                                             T* o_term = nullptr, bool lead = true,
+                                             const float* zpre = nullptr) {
   uint8_t dflag = 0;
   did_reset = false;
   if constexpr (kNoDone) {
@@ -121,7 +122,13 @@ __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KAr
     bool use_nz = false;
     if constexpr (Sys::kNoise) {
       if (a.flags & LZ_FLAG_ADD_NOISE) {
-        make_noise<Sys, T, kInject>(sys, a, i, tick, nz);
+        if constexpr (kZPre) {  // the normals drawn ahead by a producer wave (k_rollout kNP):
+          // zpre[0], zpre[64], zpre[128] -- the same normal3(seed, gid, tick) values
+          float z[3] = {zpre[0], zpre[64], zpre[128]};
+          sys.noise_from_normals(z, nz);
+        } else {
+          make_noise<Sys, T, kInject>(sys, a, i, tick, nz);
+        }
         use_nz = true;
       }
     }

@@ -613,10 +613,14 @@ __device__ __forceinline__ void ladder_wait(int k) {
   }
 }
 
-template <class Sys, typename T, int B, bool FULL, int D, bool kNoDone, bool kDoneT>
+constexpr int kZSlots = 4;  // steps of normals a producer wave may draw ahead (k_rollout kNP)
+constexpr uint32_t kZSpinCap = 1u << 24;  // polls of one flag before a wave gives up (~1 s)
+template <class Sys, typename T, int B, bool FULL, int D, bool kNoDone, bool kDoneT, bool kNP = false>
 __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any_reset,
                                              const KArgs& a, int64_t base, int tid, int nb,
-                                             uint64_t tick, float* s_act, T* s_obs) {
+                                             uint64_t tick, float* s_act, T* s_obs,
+                                             const float* s_z = nullptr, int* zflag = nullptr) {
+  static_assert(!kNP || (FULL && B == 64), "the noise producer pairs with full one-wave groups");
   using CO = Chunk<Sys::O * (int)sizeof(T)>;
   using co_t = typename CO::t;
   const int64_t i = base + tid;
@@ -716,9 +720,22 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
     T o[Sys::O];
     T rew = (T)0;
     bool did_reset;
-    const uint8_t dflag = step_body<Sys, T, true, false, kNoDone>(sys, steps, a, i, live, act,
-                                                                  tick + (uint64_t)k, k, o, rew,
-                                                                  did_reset);
+    const float* zp = nullptr;
+    if constexpr (kNP) {  // step k's normals: wait for the producer wave (LDS flag, relaxed:
+      // LDS operations of a wave execute in order, the signal fences keep the compiler's)
+      for (uint32_t spin = 0; spin < kZSpinCap &&  // (a cap: every wave leaves, whatever happens)
+                              __hip_atomic_load(&zflag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= k;
+           ++spin)
+        __builtin_amdgcn_s_sleep(1);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      zp = s_z + (k % kZSlots) * 3 * B + tid;
+    }
+    const uint8_t dflag = step_body<Sys, T, true, false, kNoDone, false, kNP>(
+        sys, steps, a, i, live, act, tick + (uint64_t)k, k, o, rew, did_reset, nullptr, true, zp);
+    if constexpr (kNP) {  // slot k % kZSlots is free again
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (tid == 0) __hip_atomic_store(&zflag[1], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     any_reset = any_reset || did_reset;
     T* gobs = static_cast<T*>(a.obs) + (off + base) * Sys::O;
     if constexpr (kDirect) {
@@ -762,6 +779,39 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
 // 128-B line, merged in the L2 with the other wave's half; +5.6% mean over three
 // allocations at 262,144 envs, K = 2048, profiles/r03/done_stores/); variant bit 21 keeps
 // the non-temporal stores (A/B)
+// kNP (one-wave groups of a system with process noise, noise on; opt-in, variant bit
+// 1<<25): a second wave per group draws the normals -- Philox + Box-Muller, ~1/5 of a
+// PMSM / HR step (noise off: HR 32,768 x 2048 1,829 -> 1,461 us), and independent of the
+// state -- up to kZSlots steps ahead into an LDS ring; the stepping wave reads them
+// instead of drawing (bit-identical: the same normal3(seed, gid, tick) values).  The
+// intent was a shorter dependent chain per stepping wave and work for the idle SIMDs of
+// a small-N launch; measured, the pair is SLOWER (HR +42% at 32,768, +74% at 65,536; PMSM
+// +4%, profiles/r04/np/), so the one-wave kernel draws its own by default.  Flags in LDS: zflag[0] = steps drawn, zflag[1] = steps consumed.  Only full
+// groups pair (the last, ragged group's producer leaves at once and its stepping wave
+// draws itself; a finished wave no longer holds up s_barrier).
+template <class Sys>
+__device__ __forceinline__ void noise_producer(const KArgs& a, int64_t base, int lane, uint64_t tick,
+                                               float* s_z, int* zflag) {
+  const uint64_t gid = (uint64_t)(a.gid0 + base + lane);
+  for (int k = 0; k < a.K; ++k) {
+    if (k >= kZSlots) {  // the stepping wave is done with step k - kZSlots's slot
+      for (uint32_t spin = 0;
+           spin < kZSpinCap && __hip_atomic_load(&zflag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= k - kZSlots;
+           ++spin)
+        __builtin_amdgcn_s_sleep(1);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    float z[3];
+    normal3(a.seed, gid, tick + (uint64_t)k, z);
+    float* slot = s_z + (k % kZSlots) * 3 * 64 + lane;
+    slot[0] = z[0];
+    slot[64] = z[1];
+    slot[128] = z[2];
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (lane == 0) __hip_atomic_store(&zflag[0], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
 template <class Sys, typename T, int B, int D, bool kNoDone = false, bool kDoneT = true>
 __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
   // DMA ring (a placeholder for systems that take no action)
@@ -789,6 +839,53 @@ __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
     rollout_loop<Sys, T, B, true, D, kNoDone, kDoneT>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
   else
     rollout_loop<Sys, T, B, false, D, kNoDone, kDoneT>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
+  if (live) {
+    sys.store(a, i);
+    if (any_reset) sys.store_autoreset_extra(a, i);
+    if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
+  }
+}
+
+// one-wave groups + a noise-producer wave (kNP above): 128 threads per 64 envs, wave 1
+// the producer; wave 0 is k_rollout<Sys, T, 64, D>'s wave with the normals read from LDS
+template <class Sys, typename T, int D>
+__global__ __launch_bounds__(128) void k_rollout_np(KArgs a) {
+  constexpr int B = 64;
+  __shared__ __attribute__((aligned(16))) float s_act[dma_slots<D>() * act_slot_floats<Sys::A, B>()];
+  __shared__ __attribute__((aligned(16))) T s_obs[B * Sys::O];
+  __shared__ float s_z[kZSlots * 3 * B];
+  __shared__ int zflag[2];
+  static_assert(Sys::kUsesAction && Sys::kNoise, "k_rollout_np: noisy systems with actions");
+  const int tid = (int)threadIdx.x;
+  if (tid == 0) zflag[0] = zflag[1] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * B;
+  const int nb = (int)((a.n - base) < B ? (a.n - base) : B);
+  const bool full = nb == B && a.vec_ok;
+  if (tid >= B) {  // the producer wave (none for the last, ragged group)
+    if (full) noise_producer<Sys>(a, base, tid - B, *a.tick_in, s_z, zflag);
+    return;
+  }
+  const int64_t i = base + tid;
+  const bool live = tid < nb;
+  const uint64_t tick = *a.tick_in;
+  if (blockIdx.x == 0 && tid == 0) {
+    *a.counter_next = 0;
+    *a.tick_out = tick + a.tick_adv;
+  }
+  Sys sys;
+  sys.setup(a);
+  int32_t steps = 0;
+  bool any_reset = false;
+  if (live) {
+    sys.load(a, i);
+    if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
+  }
+  if (full)
+    rollout_loop<Sys, T, B, true, D, false, true, true>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs,
+                                                        s_z, zflag);
+  else
+    rollout_loop<Sys, T, B, false, D, false, true>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
   if (live) {
     sys.store(a, i);
     if (any_reset) sys.store_autoreset_extra(a, i);
@@ -992,6 +1089,7 @@ static inline bool rollout_split(const KArgs& a) {
 struct RolloutPlan {
   int kind;
   bool no_done;
+  bool np;  // one-wave groups with a noise-producer wave (k_rollout kNP)
 };
 template <class Sys>
 static RolloutPlan rollout_plan(const KArgs& a) {
@@ -1003,10 +1101,14 @@ static RolloutPlan rollout_plan(const KArgs& a) {
   bool nd = false;
   if constexpr (never_terminates<Sys>::value && !Sys::kNoise) nd = no_done<Sys>(a) && !(a.variant & 2048);
   if ((a.n < one_wave_below || (a.variant & (1 << 24))) && !(a.variant & (1 << 23))) {
-    if (rollout_split<Sys>(a)) return {2, nd};
-    return {1, false};
+    if (rollout_split<Sys>(a)) return {2, nd, false};
+    // variant bit 1<<25: with a noise-producer wave (k_rollout_np; A/B, measured slower:
+    // HR f32 32,768 x 2048 1,840 -> 2,610 us, 65,536 1,823 -> 3,175; PMSM 2,190 -> 2,274 /
+    // 2,111 -> 2,191, profiles/r04/np/)
+    const bool np = Sys::kNoise && Sys::kUsesAction && (a.flags & LZ_FLAG_ADD_NOISE) && (a.variant & (1 << 25));
+    return {1, false, np};
   }
-  return {0, nd};
+  return {0, nd, false};
 }
 
 template <class Sys, typename T, int D, int DS = D>  // DS: the split-lane kernel's distance
@@ -1042,6 +1144,11 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
         }
       }
       hipLaunchKernelGGL((k_rollout_split<Sys, T, 2, DS>), g, dim3(64), 0, s, a);
+    } else if constexpr (Sys::kNoise && Sys::kUsesAction) {
+      if (plan.np)
+        hipLaunchKernelGGL((k_rollout_np<Sys, T, D>), dim3((unsigned)((a.n + 63) / 64)), dim3(128), 0, s, a);
+      else
+        hipLaunchKernelGGL((k_rollout<Sys, T, 64, D>), dim3((unsigned)((a.n + 63) / 64)), dim3(64), 0, s, a);
     } else {
       hipLaunchKernelGGL((k_rollout<Sys, T, 64, D>), dim3((unsigned)((a.n + 63) / 64)), dim3(64),
                          0, s, a);
@@ -1166,7 +1273,7 @@ static int env_shape_t(int which, const KArgs& a, int32_t* o) {
   const RolloutPlan p = rollout_plan<Sys>(a);
   o[0] = p.kind == 0 ? LZ_KERNEL_ROLLOUT : p.kind == 1 ? LZ_KERNEL_ROLLOUT_WAVE : LZ_KERNEL_ROLLOUT_SPLIT;
   o[1] = p.kind == 2 ? 32 : 64;
-  o[2] = p.kind == 0 ? kBlock / 64 : 1;
+  o[2] = p.kind == 0 ? kBlock / 64 : p.np ? 2 : 1;
   const int64_t per = p.kind == 0 ? kBlock : p.kind == 1 ? 64 : 32;
   o[3] = (int32_t)((a.n + per - 1) / per);
   o[4] = p.no_done ? LZ_SHAPE_NO_DONE : 0;

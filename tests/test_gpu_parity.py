@@ -453,6 +453,44 @@ def test_rollout_equals_steps(gl, system, dtype, n):
     assert nd == int((_np(done) != 0).sum())
 
 
+@pytest.mark.parametrize("system,dtype,n,K", [("pmsm", "float32", 32768, 300), ("hr", "float32", 65536, 200),
+                                              ("hr", "float64", 4160, 100), ("pmsm", "float32", 4097, 100)])
+def test_rollout_noise_producer_equals_steps(gl, system, dtype, n, K):
+    """One-wave rollout of a system with process noise, with the opt-in noise-producer wave
+    (variant bit 1<<25: a second wave per group draws the normals ahead into an LDS ring,
+    k_rollout_np, lz_kernels.hip -- reported as 2 waves per group) and without it (the
+    default): each equals K lz_step calls (which draw their own) bit for bit: obs, reward,
+    done, the compact done list and the final state; ragged sizes run the last group
+    without a producer."""
+    from gym_lorenz import _native as nat
+
+    for variant in (0, 1 << 25):
+        a_be = gl.BatchedEnv(system, n, dtype=dtype, seed=9, max_episode_steps=37, add_noise=True, variant=variant)
+        b_be = gl.BatchedEnv(system, n, dtype=dtype, seed=9, max_episode_steps=37, add_noise=True)
+        sh = nat.launch_shape(a_be._h, nat.CALL_ROLLOUT)
+        assert sh["kernel"] == "rollout_wave" and sh["waves"] == (2 if variant else 1), sh
+        a_be.reset()
+        b_be.reset()
+        A = torch.from_numpy(np.random.default_rng(5).uniform(-1.2, 1.2, (K, n, a_be.action_dim))
+                             .astype(np.float32)).cuda()
+        obs, rew, done, (didx, tobs, nd) = a_be.rollout(A, capture_terminal=K * n)
+        want_idx = []
+        for k in range(K):
+            o, r, d = b_be.step(A[k])
+            assert bits_equal(_np(obs[k]), _np(o)), (variant, k)
+            assert bits_equal(_np(rew[k]), _np(r)), (variant, k)
+            assert np.array_equal(_np(done[k]), _np(d)), (variant, k)
+            want_idx.append(k * n + np.nonzero(_np(d))[0])
+        m = int(nd.item())
+        wi = np.concatenate(want_idx)
+        assert m == wi.size and m > 0
+        assert np.array_equal(np.sort(_np(didx[:m])), wi)
+        for p in range(a_be.info.n_planes):
+            assert bits_equal(_np(a_be.get_state(p)), _np(b_be.get_state(p))), (variant, p)
+        a_be.close()
+        b_be.close()
+
+
 @pytest.mark.parametrize("system,dtype", [("lorenz3", "float32"), ("pmsm", "float32"),
                                           ("lorenz4", "float64"), ("hr", "float32")])
 @pytest.mark.parametrize("n", [2016, 1000])

@@ -90,6 +90,21 @@ rt)  # the resident round trip taken apart; the per-system multi-tile load layou
       -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
   done
   ;;
+noise)  # how much of the PMSM / HR env rollout at cfg5's 32,768 envs is the process noise
+  for sys in pmsm hr; do for nz in 1 0; do for n in 32768 65536; do
+    timeout -k 10 200 python bench.py --system $sys --mode rollout --K 2048 --envs $n --steps 4096 --warmup 2048 \
+      --add-noise $nz $BQ > $O/${sys}_${n}_noise$nz.json 2>> $O/noise.err || exit 1
+  done; done; done
+  ;;
+np)  # the noise-producer wave of the one-wave PMSM / HR rollout: parity, then A/B
+  timeout -k 10 600 $PYT -m gpu --maxfail=3 "tests/test_gpu_parity.py::test_rollout_noise_producer_equals_steps" \
+    "tests/test_gpu_parity.py::test_rollout_equals_steps" tests/test_gpu_cfg5.py tests/test_gpu_noise.py \
+    "tests/test_gpu_policy_branches.py::test_env_rollout_branch_reported" > $O/np_tests.txt 2>&1 || exit 1
+  for r in 1 2; do for sys in pmsm hr; do for n in 32768 65536; do for v in 0 33554432; do
+    timeout -k 10 200 python bench.py --system $sys --mode rollout --K 2048 --envs $n --steps 4096 --warmup 2048 \
+      --add-noise 1 --variant $v $BQ > $O/${sys}_${n}_v${v}_$r.json 2>> $O/np.err || exit 1
+  done; done; done; done
+  ;;
 new)
   timeout -k 10 1100 $PYT -m gpu --maxfail=8 tests/test_gpu_rk4.py tests/test_gpu_vecnorm_step.py \
     tests/test_gpu_resident.py tests/test_bench_contract.py tests/test_gpu_policy_branches.py \
