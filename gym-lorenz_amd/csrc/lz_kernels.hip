@@ -385,10 +385,15 @@ template <>
 struct multi_flat_loads<SysHR<float>> {
   static constexpr bool value = true;
 };
+template <>
+struct multi_flat_loads<SysL3<float>> {
+  static constexpr bool value = true;
+};
 
 template <class Sys, typename T, int E, bool kDoneT = false>
 __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
-  static_assert(Sys::A == 2 && Sys::kUsesAction, "k_step_multi: two-action systems");
+  static_assert(Sys::kUsesAction && (Sys::A == 2 || multi_flat_loads<Sys>::value),
+                "k_step_multi: systems with actions (round 3's loads: two actions)");
   constexpr int SB = kBlock;
   constexpr bool kFlat = multi_flat_loads<Sys>::value;
   __shared__ __attribute__((aligned(16))) T s_obs[E][SB * Sys::O];
@@ -396,7 +401,7 @@ __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
   const bool vec = a.vec_ok != 0;
   Sys sys[E];
   int32_t steps[E];
-  float act[E][2];
+  float act[E][Sys::A];
   const float* ga = static_cast<const float*>(a.act);
   uint64_t tick;
   if constexpr (kFlat) {
@@ -413,11 +418,12 @@ __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
       sys[e].load(a, ic);
       const int32_t* sp = static_cast<const int32_t*>(a.count_steps ? a.pl[Sys::kStepPlane] : a.pl[0]);
       steps[e] = sp[ic];
-      act[e][0] = __builtin_nontemporal_load(ga + 2 * ic);  // (merged into one 8-B load)
-      act[e][1] = __builtin_nontemporal_load(ga + 2 * ic + 1);
+#pragma unroll
+      for (int j = 0; j < Sys::A; ++j)  // (merged into one 8-B / 12-B load)
+        act[e][j] = __builtin_nontemporal_load(ga + Sys::A * ic + j);
       __builtin_amdgcn_sched_barrier(0);  // tile e's loads stay ahead of tile e+1's
     }
-  } else {
+  } else if constexpr (Sys::A == 2) {
     tick = load_tick(a.tick_in);
     if (blockIdx.x == 0 && tid == 0) *a.counter_next = 0;
 #pragma unroll
@@ -485,6 +491,10 @@ template <>
 struct multi_step_ok<SysHR<float>> {
   static constexpr bool value = true;
 };
+template <>
+struct multi_step_ok<SysL3<float>> {  // opt-in only (variant bits 14-15; auto = k_step)
+  static constexpr bool value = true;
+};
 // Four tiles per workgroup only where that grid is ONE full generation of the chip (4
 // waves per SIMD, 109 VGPRs: 4 workgroups of 1,024 envs per CU, more than 3/4 of them
 // used): then k_step's 2-3 generations (HR 1M: 4,096 workgroups at 6 waves per SIMD =
@@ -497,13 +507,16 @@ inline int step_tiles_auto(int64_t n, int num_cus) {
   const int64_t groups = (n + 4 * kBlock - 1) / (4 * kBlock), full = 4 * (int64_t)num_cus;
   return (4 * groups > 3 * full && groups <= full) ? 4 : 1;
 }
+template <class Sys>
 inline int step_tiles(const KArgs& a) {
   if (a.noise) return 1;  // injected noise: k_step (k_step_multi draws its noise on device)
   switch ((a.variant >> 14) & 3) {
     case 1: return 1;
     case 2: return 2;
     case 3: return 4;
-    default: return step_tiles_auto(a.n, a.num_cus > 0 ? a.num_cus : 256);
+    default:
+      if constexpr (std::is_same<Sys, SysL3<float>>::value) return 1;
+      else return step_tiles_auto(a.n, a.num_cus > 0 ? a.num_cus : 256);
   }
 }
 
@@ -1179,7 +1192,7 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
 template <class Sys, typename T, bool kVariants = false>
 static int launch_all(int which, const KArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)grid_for(a.n)), block(kBlock);
-  const int tiles = which == 1 && multi_step_ok<Sys>::value ? step_tiles(a) : 1;
+  const int tiles = which == 1 && multi_step_ok<Sys>::value ? step_tiles<Sys>(a) : 1;
   if (which == 0)
     hipLaunchKernelGGL((k_reset<Sys, T>), grid, block, 0, s, a);
   else if (tiles > 1) {
@@ -1261,7 +1274,7 @@ static int dispatch(int which, int system, int f64, const KArgs& a, void* stream
 template <class Sys, typename T>
 static int env_shape_t(int which, const KArgs& a, int32_t* o) {
   if (which == 1) {
-    const int tiles = multi_step_ok<Sys>::value ? step_tiles(a) : 1;
+    const int tiles = multi_step_ok<Sys>::value ? step_tiles<Sys>(a) : 1;
     const int64_t per = (int64_t)kBlock * tiles;
     o[0] = tiles > 1 ? LZ_KERNEL_STEP_MULTI : LZ_KERNEL_STEP;
     o[1] = 64;

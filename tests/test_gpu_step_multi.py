@@ -43,7 +43,8 @@ def _run(gl, system, n, variant, A, kw, noise=None):
 
 
 CASES = [("pmsm", {"add_noise": True}), ("pmsm", {"add_noise": False, "alpha": 0.3}),
-         ("hr", {"add_noise": True}), ("hr", {"add_noise": True, "add_filter": True})]
+         ("hr", {"add_noise": True}), ("hr", {"add_noise": True, "add_filter": True}),
+         ("lorenz3", {})]  # LORENZ3 f32: multi-tile only when forced (A/B), 3 actions
 
 
 @pytest.mark.parametrize("system,kw", CASES, ids=[c[0] + str(i) for i, c in enumerate(CASES)])
@@ -52,7 +53,8 @@ def test_step_multi_equals_step(gl, system, kw, n):
     """n = 1613: 6.3 tiles (E = 4: the second workgroup's trailing tiles are empty, the
     last live one ragged); 2048: whole groups; 70,000: 274 groups, ragged."""
     K = 20
-    A = torch.from_numpy(np.random.default_rng(5).uniform(-1.3, 1.3, (K, n, 2))
+    na = 3 if system == "lorenz3" else 2
+    A = torch.from_numpy(np.random.default_rng(5).uniform(-1.3, 1.3, (K, n, na))
                          .astype(np.float32)).cuda()
     ref_out, ref_st = _run(gl, system, n, E1, A, kw)
     assert sum(len(x[3]) for x in ref_out) > 0  # truncations happened inside the window

@@ -105,6 +105,12 @@ np)  # the noise-producer wave of the one-wave PMSM / HR rollout: parity, then A
       --add-noise 1 --variant $v $BQ > $O/${sys}_${n}_v${v}_$r.json 2>> $O/np.err || exit 1
   done; done; done; done
   ;;
+l3multi)  # LORENZ3 f32 multi-tile step (E = 2 / 4, straight-line loads) vs k_step
+  timeout -k 10 600 $PYT -m gpu --maxfail=3 tests/test_gpu_step_multi.py > $O/l3multi_tests.txt 2>&1 || exit 1
+  for r in 1 2; do for n in 1048576 131072 2097152 4194304; do for v in 0 32768 49152; do
+    timeout -k 10 200 python bench.py --envs $n --variant $v $BQ > $O/l3_${n}_v${v}_$r.json 2>> $O/l3multi.err || exit 1
+  done; done; done
+  ;;
 new)
   timeout -k 10 1100 $PYT -m gpu --maxfail=8 tests/test_gpu_rk4.py tests/test_gpu_vecnorm_step.py \
     tests/test_gpu_resident.py tests/test_bench_contract.py tests/test_gpu_policy_branches.py \
