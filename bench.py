@@ -235,15 +235,13 @@ SYSTEM_INFO = {  # system -> (reference env, mangled k_step / k_rollout names, a
 
 def step_tiles(system, n, f64=False, num_cus=256, variant=0):
     """Tiles per workgroup of the step launch: lz_kernels.hip step_tiles (variant bits
-    14-15 force 1 / 2 / 4) and step_tiles_auto (PMSM / HR float32: 4 where that grid is
-    one full chip generation, else 1)."""
+    14-15 force 1 / 2 / 4) and step_tiles_auto (LORENZ3 / PMSM / HR float32: 4 where that
+    grid is one full chip generation, else 1)."""
     if system not in ("pmsm", "hr", "lorenz3") or f64:
         return 1
     forced = (variant >> 14) & 3
     if forced:
         return {1: 1, 2: 2, 3: 4}[forced]
-    if system == "lorenz3":  # k_step_multi for LORENZ3 f32 only when forced (A/B)
-        return 1
     groups, full = -(-n // 1024), 4 * num_cus
     return 4 if 4 * groups > 3 * full and groups <= full else 1
 

@@ -491,8 +491,12 @@ template <>
 struct multi_step_ok<SysHR<float>> {
   static constexpr bool value = true;
 };
+// LORENZ3 f32 (straight-line loads, 3 actions as one 12-B load): at 1,048,576 envs E = 4
+// (one chip generation, 4 waves per SIMD) 11.31-11.41 -> 11.09-11.12 us per step; E = 2
+// 12.8 us; at 131,072 / 2M / 4M k_step wins (profiles/r04/l3multi/) -- the same window
+// rule as PMSM / HR
 template <>
-struct multi_step_ok<SysL3<float>> {  // opt-in only (variant bits 14-15; auto = k_step)
+struct multi_step_ok<SysL3<float>> {
   static constexpr bool value = true;
 };
 // Four tiles per workgroup only where that grid is ONE full generation of the chip (4
@@ -514,9 +518,7 @@ inline int step_tiles(const KArgs& a) {
     case 1: return 1;
     case 2: return 2;
     case 3: return 4;
-    default:
-      if constexpr (std::is_same<Sys, SysL3<float>>::value) return 1;
-      else return step_tiles_auto(a.n, a.num_cus > 0 ? a.num_cus : 256);
+    default: return step_tiles_auto(a.n, a.num_cus > 0 ? a.num_cus : 256);
   }
 }
 

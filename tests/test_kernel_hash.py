@@ -56,4 +56,7 @@ def test_bench_kernel_names_exist():
     assert "k_rolloutINS_5SysL4IfEEfLi64E" in bench.kernel_name("lorenz4", "rollout", 40960)
     assert "k_rolloutINS_5SysL4IfEEfLi256E" in bench.kernel_name("lorenz4", "rollout", 49152)
     assert bench.step_tiles("pmsm", 262144) == 1 and bench.step_tiles("hr", 1 << 20) == 4
-    assert bench.step_tiles("hr", 1 << 21) == 1 and bench.step_tiles("lorenz3", 1 << 20) == 1
+    assert bench.step_tiles("hr", 1 << 21) == 1 and bench.step_tiles("lorenz3", 1 << 20) == 4
+    assert bench.step_tiles("lorenz3", 131072) == 1 and bench.step_tiles("lorenz3", 1 << 21) == 1
+    assert bench.step_tiles("lorenz3", 1 << 20, f64=True) == 1
+    assert "k_step_multiINS_5SysL3IfEEfLi4E" in bench.kernel_name("lorenz3", "step", 1 << 20)
