@@ -64,6 +64,8 @@ def parse(argv=None):
                         "vecnorm = VecNormalize(VecEnv).step fused (lz_step_vecnorm + "
                         "lz_vecnorm_apply), 1 GPU")
     p.add_argument("--K", type=int, default=2048, help="rollout length (--mode rollout)")
+    p.add_argument("--dtype", choices=["float32", "float64"], default="float32",
+                   help=argparse.SUPPRESS)  # A/B: the env arithmetic of the main line
     p.add_argument("--add-noise", type=int, choices=[0, 1], default=None,
                    help=argparse.SUPPRESS)  # A/B: the process-noise flag (default: the config's)
     p.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
@@ -233,11 +235,11 @@ SYSTEM_INFO = {  # system -> (reference env, mangled k_step / k_rollout names, a
 }
 
 
-def step_tiles(system, n, f64=False, num_cus=256, variant=0):
+def step_tiles(system, n, f64=False, num_cus=256, variant=0, integrator="euler"):
     """Tiles per workgroup of the step launch: lz_kernels.hip step_tiles (variant bits
     14-15 force 1 / 2 / 4) and step_tiles_auto (LORENZ3 / PMSM / HR float32: 4 where that
     grid is one full chip generation, else 1)."""
-    if system not in ("pmsm", "hr", "lorenz3") or f64:
+    if system not in ("pmsm", "hr", "lorenz3") or f64 or integrator == "rk4":
         return 1
     forced = (variant >> 14) & 3
     if forced:
@@ -263,7 +265,7 @@ def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=
     name = tag[: tag.index("I")] if "I" in tag else tag[: tag.index("E")]
     sysname = str(len(name)) + tag
     if mode != "rollout":
-        tiles = step_tiles(system, n, f64, num_cus, variant)
+        tiles = step_tiles(system, n, f64, num_cus, variant, integrator)
         if tiles > 1:  # k_step_multi<Sys, T, E, kDoneT = false>
             return "_ZN2lz12k_step_multiINS_%sLi%dELb0EEEvNS_5KArgsE" % (sysname, tiles)
         return "_ZN2lz6k_stepINS_%sLi0EEEvNS_5KArgsE" % sysname
@@ -1007,7 +1009,7 @@ def main():
         kw["integrator"] = "rk4"
     if args.add_noise is not None:
         kw["add_noise"] = bool(args.add_noise)
-    env = gl.BatchedEnv(args.system, n, dtype="float32", seed=0, global_env_offset=start,
+    env = gl.BatchedEnv(args.system, n, dtype=args.dtype, seed=0, global_env_offset=start,
                         autoreset=True, device=local, max_episode_steps=args.max_episode_steps,
                         variant=args.variant, **kw)
     if args.mode == "policy":
@@ -1064,7 +1066,7 @@ def main():
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f64" if args.dtype == "float64" else "f32",
         "data": "synthetic: initial states from on-device Philox keyed by global env id "
                 "(reference distributions); actions ~ U(-%g,%g) f32 pre-generated on device"
                 % (arange, arange),
@@ -1078,7 +1080,8 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": kernel_name(args.system, args.mode, n, no_done=args.max_episode_steps == 0,
+            "kernel": kernel_name(args.system, args.mode, n, f64=args.dtype == "float64",
+                                  no_done=args.max_episode_steps == 0,
                                   num_cus=torch.cuda.get_device_properties(device).multi_processor_count,
                                   variant=args.variant, integrator=kw.get("integrator", "euler"),
                                   noise=bool(env.config.flags & nat.FLAG_ADD_NOISE)),

@@ -111,6 +111,10 @@ l3multi)  # LORENZ3 f32 multi-tile step (E = 2 / 4, straight-line loads) vs k_st
     timeout -k 10 200 python bench.py --envs $n --variant $v $BQ > $O/l3_${n}_v${v}_$r.json 2>> $O/l3multi.err || exit 1
   done; done; done
   ;;
+f64ab)  # the fp64 extra line's k_step across the round's step-prologue changes
+  timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_tick.so ablib/libgym_lorenz_amd_base.so \
+    -- --dtype float64 $BQ > $O/ab_f64_1M.json 2> $O/ab_f64_1M.err || exit 1
+  ;;
 new)
   timeout -k 10 1100 $PYT -m gpu --maxfail=8 tests/test_gpu_rk4.py tests/test_gpu_vecnorm_step.py \
     tests/test_gpu_resident.py tests/test_bench_contract.py tests/test_gpu_policy_branches.py \
