@@ -103,6 +103,9 @@ __global__ __launch_bounds__(kBlock) void k_reset(KArgs a) {
 }
 
 // ------------------------------------------------------------------ step
+#ifndef LZ_F64_PROLOGUE  // float64 steps keep round 3's prologue (step_tile)
+#define LZ_F64_PROLOGUE 1
+#endif
 // V (tuning variant, lz_config.reserved[0], default 0): bit 0 = plain (temporal)
 // act/obs/rew/done accesses instead of non-temporal, bit 1 = lanes access their own
 // act/obs rows directly instead of LDS staging, bit 2 = __syncthreads() instead of the
@@ -256,10 +259,23 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
   // otherwise the compiler issues their s_loads late and waits for each (the action
   // pointer's after the first lgkmcnt wait, the terminal-obs pointer's right after the
   // action barrier) -- serial kernel-argument round trips on the step's critical path
+  // (float64 keeps round 3's prologue -- the tick as a scalar load at entry, no forced
+  // argument batch: with the float32 prologue the float64 LORENZ3 step measured 18.34 ->
+  // 19.84 us at 1M, profiles/r04/tick/ab_f64_1M.json; LZ_F64_PROLOGUE=0 for the A/B)
+  constexpr bool kOldProlog = LZ_F64_PROLOGUE && sizeof(T) == 8;
   const float* ga_early = static_cast<const float*>(a.act);
-  asm volatile("" ::"s"(a.term_obs), "s"(a.obs), "s"(a.rew), "s"(a.done));
-  if constexpr (Sys::kUsesAction) asm volatile("" ::"s"(ga_early));
-  if (blockIdx.x == 0 && tid == 0) *a.counter_next = 0;
+  uint64_t tick0 = 0;
+  if constexpr (kOldProlog) {
+    tick0 = *a.tick_in;
+    if (blockIdx.x == 0 && tid == 0) {
+      *a.counter_next = 0;
+      *a.tick_out = tick0 + a.tick_adv;
+    }
+  } else {
+    asm volatile("" ::"s"(a.term_obs), "s"(a.obs), "s"(a.rew), "s"(a.done));
+    if constexpr (Sys::kUsesAction) asm volatile("" ::"s"(ga_early));
+    if (blockIdx.x == 0 && tid == 0) *a.counter_next = 0;
+  }
   if constexpr (kVN) {  // the statistics before this step, for the normalise pass
     if (blockIdx.x == 0 && (v.flags & LZ_VN_TRAINING) && !(v.flags & LZ_VN_DEFER)) {
       if (tid < 2 * Sys::O + 1) v.old[tid] = v.obs_state[tid];
@@ -275,7 +291,7 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
     if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
     if constexpr (kVN) ret_in = v.returns[i];
   }
-  uint64_t tick = load_tick(a.tick_in);  // in flight with the state and action loads
+  uint64_t tick = kOldProlog ? tick0 : load_tick(a.tick_in);  // in flight with the state and action loads
   float act[Sys::A];
   if constexpr (Sys::kUsesAction) {
     const float* ga = ga_early;
@@ -291,14 +307,15 @@ __device__ __forceinline__ void step_tile(const KArgs& a, const VArgs& v) {
       for (int j = 0; j < Sys::A; ++j) act[j] = gload<NT>(ga + i * Sys::A + j);
     }
   }
-  tick = tick_ready(tick);
+  if constexpr (!kOldProlog) tick = tick_ready(tick);
   T o[Sys::O];
   T rew = (T)0;
   bool did_reset;
   double rn = 0.0;  // kVN: the updated VecNormalize.returns[i] (before the done reset)
   const uint8_t dflag =
       step_body<Sys, T, false>(sys, steps, a, i, live, act, tick, 0, o, rew, did_reset);
-  if (blockIdx.x == 0 && tid == 0) *a.tick_out = tick + a.tick_adv;  // tick waited for here
+  if constexpr (!kOldProlog)
+    if (blockIdx.x == 0 && tid == 0) *a.tick_out = tick + a.tick_adv;  // tick waited for here
   __shared__ double s_ret[kVN ? SB : 1];
   if constexpr (kVN) {  // VecNormalize.returns: r*gamma + reward, moments, then [done] = 0
     if (live) {

@@ -115,6 +115,20 @@ f64ab)  # the fp64 extra line's k_step across the round's step-prologue changes
   timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_tick.so ablib/libgym_lorenz_amd_base.so \
     -- --dtype float64 $BQ > $O/ab_f64_1M.json 2> $O/ab_f64_1M.err || exit 1
   ;;
+f64b)  # float64 back on round 3's step prologue (vs the float32 one), then the bench line
+  timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_f64new.so ablib/libgym_lorenz_amd_base.so \
+    -- --dtype float64 $BQ > $O/ab_f64_1M.json 2> $O/ab_f64_1M.err || exit 1
+  timeout -k 10 600 $PYT -m gpu --maxfail=3 tests/test_gpu_parity.py tests/test_gpu_step_multi.py \
+    > $O/f64b_tests.txt 2>&1 || exit 1
+  timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 1
+  ;;
+scalartick)  # the scalar tick load (with the one-batch kernel arguments) vs the vector one
+  for cfg in "--dtype float64" "--envs 131072" "--integrator rk4" "--envs 2097152"; do
+    tag=$(echo $cfg | tr -d ' -')
+    timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_scalartick.so ablib/libgym_lorenz_amd_base.so \
+      -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
+  done
+  ;;
 new)
   timeout -k 10 1100 $PYT -m gpu --maxfail=8 tests/test_gpu_rk4.py tests/test_gpu_vecnorm_step.py \
     tests/test_gpu_resident.py tests/test_bench_contract.py tests/test_gpu_policy_branches.py \

@@ -26,6 +26,8 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/head.trace -o run --out
 E="--launch eager"
 one lz_step_1M _ZN2lz12k_step_multiINS_5SysL3IfEEfLi4ELb0EEEvNS_5KArgsE "k_step_multi<lz::SysL3<float>, float, 4" \
   1048576 68157440 $E --steps 400 --warmup 40 || exit 1
+one f64_step_1M _ZN2lz6k_stepINS_5SysL3IdEEdLi0EEEvNS_5KArgsE "k_step<lz::SysL3<double>, double, 0>" 1048576 \
+  122683392 --dtype float64 $E --steps 400 --warmup 40 || exit 1
 one rk4_step_1M _ZN2lz6k_stepINS_8SysL3RK4IfEEfLi0EEEvNS_5KArgsE "k_step<lz::SysL3RK4<float>" 1048576 68157440 \
   --integrator rk4 $E --steps 400 --warmup 40 || exit 1
 one cfg2_l3_65k _ZN2lz6k_stepINS_5SysL3IfEEfLi0EEEvNS_5KArgsE "k_step<lz::SysL3<float>, float, 0>" 65536 4259840 \
