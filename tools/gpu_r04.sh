@@ -122,6 +122,14 @@ f64b)  # float64 back on round 3's step prologue (vs the float32 one), then the 
     > $O/f64b_tests.txt 2>&1 || exit 1
   timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 1
   ;;
+l3window)  # LORENZ3 multi-tile: temporal done stores at 1M; the window edges (k_step forced = 16384)
+  for r in 1 2; do
+    for nv in 1048576:0 1048576:4194304 917504:0 917504:16384 786432:0 786432:49152 851968:0 851968:16384; do
+      timeout -k 10 200 python bench.py --envs ${nv%%:*} --variant ${nv##*:} $BQ \
+        > $O/w_${nv%%:*}_${nv##*:}_$r.json 2>> $O/w.err || exit 1
+    done
+  done
+  ;;
 scalartick)  # the scalar tick load (with the one-batch kernel arguments) vs the vector one
   for cfg in "--dtype float64" "--envs 131072" "--integrator rk4" "--envs 2097152"; do
     tag=$(echo $cfg | tr -d ' -')
