@@ -245,6 +245,8 @@ def step_tiles(system, n, f64=False, num_cus=256, variant=0, integrator="euler")
     if forced:
         return {1: 1, 2: 2, 3: 4}[forced]
     groups, full = -(-n // 1024), 4 * num_cus
+    if system == "lorenz3":  # step_tiles_auto_l3: balanced grids only (3 or 4 groups per CU)
+        return 4 if groups in (3 * num_cus, 4 * num_cus) else 1
     return 4 if 4 * groups > 3 * full and groups <= full else 1
 
 

@@ -510,8 +510,8 @@ struct multi_step_ok<SysHR<float>> {
 };
 // LORENZ3 f32 (straight-line loads, 3 actions as one 12-B load): at 1,048,576 envs E = 4
 // (one chip generation, 4 waves per SIMD) 11.31-11.41 -> 11.09-11.12 us per step; E = 2
-// 12.8 us; at 131,072 / 2M / 4M k_step wins (profiles/r04/l3multi/) -- the same window
-// rule as PMSM / HR
+// 12.8 us; at 131,072 / 2M / 4M k_step wins (profiles/r04/l3multi/); only on balanced
+// grids (step_tiles_auto_l3)
 template <>
 struct multi_step_ok<SysL3<float>> {
   static constexpr bool value = true;
@@ -528,6 +528,14 @@ inline int step_tiles_auto(int64_t n, int num_cus) {
   const int64_t groups = (n + 4 * kBlock - 1) / (4 * kBlock), full = 4 * (int64_t)num_cus;
   return (4 * groups > 3 * full && groups <= full) ? 4 : 1;
 }
+// LORENZ3 f32: four tiles only on a balanced grid -- 3 or 4 workgroups of 1,024 envs on
+// every CU.  Measured (profiles/r04/l3window/): 1,048,576 envs 11.36 -> 11.11 us, 786,432
+// (forced) 8.93 -> 8.58; but 851,968 (3.25 per CU) 9.29 -> 11.26 and 917,504 9.54 ->
+// 11.69 -- the CUs holding a fourth workgroup set the time, as at 1M.
+inline int step_tiles_auto_l3(int64_t n, int num_cus) {
+  const int64_t groups = (n + 4 * kBlock - 1) / (4 * kBlock);
+  return (groups == 3 * (int64_t)num_cus || groups == 4 * (int64_t)num_cus) ? 4 : 1;
+}
 template <class Sys>
 inline int step_tiles(const KArgs& a) {
   if (a.noise) return 1;  // injected noise: k_step (k_step_multi draws its noise on device)
@@ -535,7 +543,11 @@ inline int step_tiles(const KArgs& a) {
     case 1: return 1;
     case 2: return 2;
     case 3: return 4;
-    default: return step_tiles_auto(a.n, a.num_cus > 0 ? a.num_cus : 256);
+    default:
+      if constexpr (std::is_same<Sys, SysL3<float>>::value)
+        return step_tiles_auto_l3(a.n, a.num_cus > 0 ? a.num_cus : 256);
+      else
+        return step_tiles_auto(a.n, a.num_cus > 0 ? a.num_cus : 256);
   }
 }
 
