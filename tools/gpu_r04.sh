@@ -130,6 +130,23 @@ l3window)  # LORENZ3 multi-tile: temporal done stores at 1M; the window edges (k
     done
   done
   ;;
+phwindow)  # PMSM / HR multi-tile window edges: E = 4 (49152) vs k_step (16384)
+  for r in 1 2; do for sys in pmsm hr; do for n in 786432 851968 917504; do for v in 16384 49152; do
+    timeout -k 10 200 python bench.py --system $sys --envs $n --variant $v --steps 1000 --warmup 100 $BQ \
+      > $O/w_${sys}_${n}_${v}_$r.json 2>> $O/w.err || exit 1
+  done; done; done; done
+  ;;
+hrflat)  # HR's flag planes read without a branch: parity, then A/B vs HEAD's kernels
+  timeout -k 10 900 $PYT -m gpu --maxfail=3 tests/test_gpu_step_multi.py tests/test_gpu_parity.py \
+    tests/test_gpu_noise.py tests/test_gpu_wrappers.py tests/test_gpu_policy_attn_f32.py tests/test_gpu_resident.py \
+    > $O/hrflat_tests.txt 2>&1 || exit 1
+  for cfg in "--system hr --envs 1048576" "--system hr --envs 2097152" "--system hr --envs 262144" \
+             "--system hr --mode rollout --K 2048 --envs 32768 --steps 4096 --warmup 2048"; do
+    tag=$(echo $cfg | tr -d ' -')
+    timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_head.so \
+      -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
+  done
+  ;;
 scalartick)  # the scalar tick load (with the one-batch kernel arguments) vs the vector one
   for cfg in "--dtype float64" "--envs 131072" "--integrator rk4" "--envs 2097152"; do
     tag=$(echo $cfg | tr -d ' -')
