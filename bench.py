@@ -237,17 +237,16 @@ SYSTEM_INFO = {  # system -> (reference env, mangled k_step / k_rollout names, a
 
 def step_tiles(system, n, f64=False, num_cus=256, variant=0, integrator="euler"):
     """Tiles per workgroup of the step launch: lz_kernels.hip step_tiles (variant bits
-    14-15 force 1 / 2 / 4) and step_tiles_auto (LORENZ3 / PMSM / HR float32: 4 where that
-    grid is one full chip generation, else 1)."""
+    14-15 force 1 / 2 / 4) and step_tiles_balanced (LORENZ3 / PMSM / HR float32: 4 where
+    that grid puts exactly 4 -- LORENZ3 / PMSM: or 3 -- workgroups on every CU, else 1)."""
     if system not in ("pmsm", "hr", "lorenz3") or f64 or integrator == "rk4":
         return 1
     forced = (variant >> 14) & 3
     if forced:
         return {1: 1, 2: 2, 3: 4}[forced]
-    groups, full = -(-n // 1024), 4 * num_cus
-    if system == "lorenz3":  # step_tiles_auto_l3: balanced grids only (3 or 4 groups per CU)
-        return 4 if groups in (3 * num_cus, 4 * num_cus) else 1
-    return 4 if 4 * groups > 3 * full and groups <= full else 1
+    # step_tiles_balanced: exactly 4 (LORENZ3 / PMSM: or 3) workgroups of 1,024 envs per CU
+    groups = -(-n // 1024)
+    return 4 if groups == 4 * num_cus or (system != "hr" and groups == 3 * num_cus) else 1
 
 
 def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=0,

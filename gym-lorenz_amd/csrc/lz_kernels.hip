@@ -495,7 +495,7 @@ __global__ __launch_bounds__(kBlock) void k_step_multi(KArgs a) {
 }
 
 // Tiles per workgroup of k_step_multi: variant bits 14-15 (16384 x {1, 2, 3}) force 1
-// (k_step), 2 or 4; 0 = the measured default, step_tiles_auto.
+// (k_step), 2 or 4; 0 = the measured default, step_tiles_balanced.
 template <class Sys>
 struct multi_step_ok {
   static constexpr bool value = false;
@@ -511,12 +511,12 @@ struct multi_step_ok<SysHR<float>> {
 // LORENZ3 f32 (straight-line loads, 3 actions as one 12-B load): at 1,048,576 envs E = 4
 // (one chip generation, 4 waves per SIMD) 11.31-11.41 -> 11.09-11.12 us per step; E = 2
 // 12.8 us; at 131,072 / 2M / 4M k_step wins (profiles/r04/l3multi/); only on balanced
-// grids (step_tiles_auto_l3)
+// grids (step_tiles_balanced)
 template <>
 struct multi_step_ok<SysL3<float>> {
   static constexpr bool value = true;
 };
-// Four tiles per workgroup only where that grid is ONE full generation of the chip (4
+// Round 3: four tiles per workgroup only where that grid is ONE full generation of the chip (4
 // waves per SIMD, 109 VGPRs: 4 workgroups of 1,024 envs per CU, more than 3/4 of them
 // used): then k_step's 2-3 generations (HR 1M: 4,096 workgroups at 6 waves per SIMD =
 // 2.67) and their partial last one go away.  Elsewhere one wave running its tiles in
@@ -524,17 +524,16 @@ struct multi_step_ok<SysL3<float>> {
 // ~1.6 us dependent chain of ~400 instructions): PMSM 262,144 6.9 -> 11.3 us, HR 2M
 // 32 -> 35.6 us.  Measured (profiles/r03/multi_step/): HR 1M 17.0 -> 15.8 us, PMSM 1M
 // 24.6 -> 23.5, PMSM 786,432 19.0 -> 18.1; 917,504 a tie.
-inline int step_tiles_auto(int64_t n, int num_cus) {
-  const int64_t groups = (n + 4 * kBlock - 1) / (4 * kBlock), full = 4 * (int64_t)num_cus;
-  return (4 * groups > 3 * full && groups <= full) ? 4 : 1;
-}
-// LORENZ3 f32: four tiles only on a balanced grid -- 3 or 4 workgroups of 1,024 envs on
-// every CU.  Measured (profiles/r04/l3window/): 1,048,576 envs 11.36 -> 11.11 us, 786,432
-// (forced) 8.93 -> 8.58; but 851,968 (3.25 per CU) 9.29 -> 11.26 and 917,504 9.54 ->
-// 11.69 -- the CUs holding a fourth workgroup set the time, as at 1M.
-inline int step_tiles_auto_l3(int64_t n, int num_cus) {
+// Round 4: four tiles only on a balanced grid -- exactly 4 (or, LORENZ3 / PMSM, 3)
+// workgroups of 1,024 envs on every CU; elsewhere the CUs holding one more workgroup set
+// the time.  Measured (profiles/r04/l3window/, profiles/r04/hrflat/ window runs), k_step
+// -> E = 4 in us: LORENZ3 1,048,576 11.36 -> 11.11, 786,432 8.93 -> 8.58, 851,968 9.29 ->
+// 11.26, 917,504 9.54 -> 11.69; PMSM 786,432 19.46 -> 18.16, 851,968 21.20 -> 21.49,
+// 917,504 22.83 -> 22.61; HR 786,432 14.89 -> 15.38, 851,968 15.75 -> 16.90, 917,504
+// 16.73 -> 17.39 (HR 1M: +3.5-4.8%, above).
+inline int step_tiles_balanced(int64_t n, int num_cus, bool three) {
   const int64_t groups = (n + 4 * kBlock - 1) / (4 * kBlock);
-  return (groups == 3 * (int64_t)num_cus || groups == 4 * (int64_t)num_cus) ? 4 : 1;
+  return (groups == 4 * (int64_t)num_cus || (three && groups == 3 * (int64_t)num_cus)) ? 4 : 1;
 }
 template <class Sys>
 inline int step_tiles(const KArgs& a) {
@@ -544,10 +543,7 @@ inline int step_tiles(const KArgs& a) {
     case 2: return 2;
     case 3: return 4;
     default:
-      if constexpr (std::is_same<Sys, SysL3<float>>::value)
-        return step_tiles_auto_l3(a.n, a.num_cus > 0 ? a.num_cus : 256);
-      else
-        return step_tiles_auto(a.n, a.num_cus > 0 ? a.num_cus : 256);
+      return step_tiles_balanced(a.n, a.num_cus > 0 ? a.num_cus : 256, !std::is_same<Sys, SysHR<float>>::value);
   }
 }
 

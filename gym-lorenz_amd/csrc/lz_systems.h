@@ -503,8 +503,15 @@ struct SysHR {
   __device__ void load(const KArgs& a, int64_t i) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) { m[j] = ld<T>(a.pl[j], i); s[j] = ld<T>(a.pl[3 + j], i); }
-    if (a.flags & LZ_FLAG_ADD_NOISE) sigma = ld<T>(a.pl[6], i);
-    if (a.flags & LZ_FLAG_ADD_FILTER) { fa0 = ld<float>(a.pl[7], i); fa1 = ld<float>(a.pl[8], i); }
+    // sigma / the filter planes are read unconditionally -- from plane 0's own element
+    // (already being fetched: no extra traffic) when the flag is off, the value then
+    // unused -- so the loads carry no branch: a branch between them makes the compiler's
+    // wait counts conservative (k_step_multi's tiles waited for each other's loads)
+    const bool nz = (a.flags & LZ_FLAG_ADD_NOISE) != 0, fl = (a.flags & LZ_FLAG_ADD_FILTER) != 0;
+    constexpr int64_t kW = sizeof(T) / 4;  // float words per T: plane 0's element i as floats
+    sigma = ld<T>(nz ? a.pl[6] : a.pl[0], i);
+    fa0 = ld<float>(fl ? a.pl[7] : a.pl[0], fl ? i : i * kW);
+    fa1 = ld<float>(fl ? a.pl[8] : a.pl[0], fl ? i : i * kW);
   }
   __device__ void store(const KArgs& a, int64_t i) const {
 #pragma unroll

@@ -60,4 +60,6 @@ def test_bench_kernel_names_exist():
     assert bench.step_tiles("lorenz3", 131072) == 1 and bench.step_tiles("lorenz3", 1 << 21) == 1
     assert bench.step_tiles("lorenz3", 1 << 20, f64=True) == 1
     assert bench.step_tiles("lorenz3", 786432) == 4 and bench.step_tiles("lorenz3", 851968) == 1
+    assert bench.step_tiles("pmsm", 786432) == 4 and bench.step_tiles("pmsm", 917504) == 1
+    assert bench.step_tiles("hr", 786432) == 1 and bench.step_tiles("pmsm", 1 << 20) == 4
     assert "k_step_multiINS_5SysL3IfEEfLi4E" in bench.kernel_name("lorenz3", "step", 1 << 20)
