@@ -147,6 +147,15 @@ hrflat)  # HR's flag planes read without a branch: parity, then A/B vs HEAD's ke
       -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
   done
   ;;
+pmc_hr)  # HR's multi-tile step after the branch-free flag-plane loads
+  K=_ZN2lz12k_step_multiINS_5SysHRIfEEfLi4ELb0EEEvNS_5KArgsE
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 180 rocprofv3 --pmc $c -d $O/hr_$c -o run --output-format csv -- python bench.py \
+      --system hr --envs 1048576 --launch eager --steps 256 --warmup 64 $BQ > $O/hr_$c.log 2>&1 || exit 1
+  done
+  python tools/pmc_generic.py $O/hr_FETCH_SIZE $O/hr_WRITE_SIZE $K "k_step_multi<lz::SysHR<float>, float, 4" 1048576 \
+    89128960 $O/hr_multi_1M_pmc_summary.json || exit 1
+  ;;
 scalartick)  # the scalar tick load (with the one-batch kernel arguments) vs the vector one
   for cfg in "--dtype float64" "--envs 131072" "--integrator rk4" "--envs 2097152"; do
     tag=$(echo $cfg | tr -d ' -')
