@@ -598,7 +598,8 @@ def fp64_line(args, gl, nat, torch, dist, device, n):
     launch_s = tm["ev_ms"] / 1e3 / tm["launches"]
     achieved = bytes_step * n / launch_s / 1e9
     env.close()
-    return {
+    kname = kernel_name("lorenz3", "step", n, f64=True)
+    line = {
         "metric": METRIC + " (fp64: the reference's arithmetic, bit-exact)",
         "value": n * tm["steps"] * tm["windows"] / tm["elapsed"], "unit": "env-steps/s",
         "steps": tm["steps"], "ms_per_step": tm["elapsed"] * 1e3 / (tm["steps"] * tm["windows"]),
@@ -608,10 +609,14 @@ def fp64_line(args, gl, nat, torch, dist, device, n):
                    "launch": describe_launches(tm, False)},
         "timing": tm["timing"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": kernel_name("lorenz3", "step", n, f64=True),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": kname,
                      "avg_launch_us": launch_s * 1e6, "bytes_per_env_step": bytes_step},
     }
+    traffic = load_traffic(kname, n)
+    if traffic is not None:
+        line["roofline"]["traffic"] = traffic["bytes_per_launch"]
+        line["roofline"]["traffic_source"] = traffic["source"]
+    return line
 
 
 # FLOP per env-step of the RK4 mode (lz_systems.h SysL3RK4 / SysL4RK4): 4 RHS evaluations
