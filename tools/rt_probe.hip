@@ -134,6 +134,22 @@ int main(int argc, char** argv) {
                 lost ? "LOST " : "ok ", bad ? "STALE-OBS" : "", lat.size(), n, (t1 - t0) / (double)lat.size(),
                 lat[lat.size() / 2], lat[lat.size() * 99 / 100]);
   }
+  {  // host-side per-call costs inside lz_resident_step's steady state
+    hipStream_t hs;
+    CK(hipStreamCreateWithFlags(&hs, hipStreamNonBlocking));
+    const int R = 200000;
+    double t0 = now_us();
+    for (int i = 0; i < R; ++i) (void)hipSetDevice(0);
+    double t1 = now_us();
+    hipStreamCaptureStatus cs;
+    for (int i = 0; i < R; ++i) (void)hipStreamIsCapturing(hs, &cs);
+    double t2 = now_us();
+    for (int i = 0; i < R; ++i) (void)hipStreamQuery(hs);
+    double t3 = now_us();
+    std::printf("host calls: hipSetDevice %.1f ns, hipStreamIsCapturing %.1f ns, hipStreamQuery %.1f ns\n",
+                (t1 - t0) * 1e3 / R, (t2 - t1) * 1e3 / R, (t3 - t2) * 1e3 / R);
+    CK(hipStreamDestroy(hs));
+  }
   CK(hipStreamDestroy(s));
   return 0;
 }
