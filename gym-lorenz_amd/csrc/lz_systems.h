@@ -301,6 +301,9 @@ struct SysL4RK4 : SysL4<T> {
 //         beta2=.999, eps=1e-8, err_threshold=5, max_steps=2000, term=1000
 // planes: state1(3), state2(3), lambda, m_t, v_t, adam_step(i32), step(i32)
 // ===========================================================================
+#ifndef LZ_PMSM_NO_BIAS_LOAD
+#define LZ_PMSM_NO_BIAS_LOAD 0
+#endif
 struct SysPMSM {
   using T = float;
   static constexpr int A = 2, O = 6, NI = 6;
@@ -394,6 +397,10 @@ struct SysPMSM {
     y = __uint_as_float((uint32_t)(v >> 32));
   }
   __device__ void bias_pair(const KArgs& a, float& bm, float& bv) const {
+#if LZ_PMSM_NO_BIAS_LOAD  // A/B only (tools/build_ab.sh): what the table load costs -- WRONG results
+    bm = bv = 1.0f;
+    return;
+#endif
     for (;;) {
       const int32_t k0 = __builtin_amdgcn_readfirstlane(adam);
       float m = 1.0f, v = 1.0f;

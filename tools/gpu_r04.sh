@@ -156,6 +156,14 @@ pmc_hr)  # HR's multi-tile step after the branch-free flag-plane loads
   python tools/pmc_generic.py $O/hr_FETCH_SIZE $O/hr_WRITE_SIZE $K "k_step_multi<lz::SysHR<float>, float, 4" 1048576 \
     89128960 $O/hr_multi_1M_pmc_summary.json || exit 1
   ;;
+nobias)  # what PMSM's per-step Adam bias-table load costs (A/B lib gives WRONG results)
+  for cfg in "--system pmsm --mode rollout --K 2048 --envs 32768 --steps 4096 --warmup 2048" \
+             "--system pmsm --envs 262144" "--system pmsm --envs 1048576"; do
+    tag=$(echo $cfg | tr -d ' -')
+    timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_nobias.so \
+      -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
+  done
+  ;;
 scalartick)  # the scalar tick load (with the one-batch kernel arguments) vs the vector one
   for cfg in "--dtype float64" "--envs 131072" "--integrator rk4" "--envs 2097152"; do
     tag=$(echo $cfg | tr -d ' -')
