@@ -301,6 +301,9 @@ struct SysL4RK4 : SysL4<T> {
 //         beta2=.999, eps=1e-8, err_threshold=5, max_steps=2000, term=1000
 // planes: state1(3), state2(3), lambda, m_t, v_t, adam_step(i32), step(i32)
 // ===========================================================================
+#ifndef LZ_PMSM_BIAS_FAST  // 0: the waterfall alone (A/B)
+#define LZ_PMSM_BIAS_FAST 1
+#endif
 #ifndef LZ_PMSM_NO_BIAS_LOAD
 #define LZ_PMSM_NO_BIAS_LOAD 0
 #endif
@@ -400,6 +403,19 @@ struct SysPMSM {
 #if LZ_PMSM_NO_BIAS_LOAD  // A/B only (tools/build_ab.sh): what the table load costs -- WRONG results
     bm = bv = 1.0f;
     return;
+#endif
+#if LZ_PMSM_BIAS_FAST
+    {  // the wave's first lane's step, loaded without a branch (index clamped, 1.0 selected
+       // past the table); the waterfall below only when the wave's steps differ
+      const int32_t k0 = __builtin_amdgcn_readfirstlane(adam);
+      const int32_t kc = __builtin_amdgcn_readfirstlane(k0 < a.bc_len ? k0 : a.bc_len - 1);
+      float m, v;
+      sload2(a.bc + 2 * (int64_t)(kc > 0 ? kc : 0), m, v);
+      const bool in = k0 < a.bc_len;
+      bm = in ? m : 1.0f;
+      bv = in ? v : 1.0f;
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(adam != k0) == 0, 1)) return;
+    }
 #endif
     for (;;) {
       const int32_t k0 = __builtin_amdgcn_readfirstlane(adam);

@@ -164,6 +164,40 @@ nobias)  # what PMSM's per-step Adam bias-table load costs (A/B lib gives WRONG 
       -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
   done
   ;;
+bias)  # PMSM fused rollout: the Adam bias pair carried by the action DMA ring (vs HEAD)
+  timeout -k 10 900 $PYT -m gpu --maxfail=4 tests/test_gpu_parity.py tests/test_gpu_cfg5.py tests/test_gpu_noise.py \
+    tests/test_gpu_step_multi.py tests/test_gpu_policy_branches.py > $O/bias_tests.txt 2>&1 || exit 1
+  for cfg in "--system pmsm --mode rollout --K 2048 --envs 32768 --steps 4096 --warmup 2048" \
+             "--system pmsm --mode rollout --K 2048 --envs 262144 --steps 4096 --warmup 2048"; do
+    tag=$(echo $cfg | tr -d ' -')
+    timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_head.so \
+      -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
+  done
+  ;;
+div)  # PMSM: the Adam bias correction through the tabulated reciprocals (vs HEAD's divisions)
+  timeout -k 10 900 $PYT -m gpu --maxfail=4 tests/test_gpu_parity.py tests/test_gpu_cfg5.py tests/test_gpu_noise.py \
+    tests/test_gpu_step_multi.py tests/test_gpu_policy_branches.py tests/test_gpu_vecnorm_step.py \
+    > $O/div_tests.txt 2>&1 || exit 1
+  for cfg in "--system pmsm --mode rollout --K 2048 --envs 32768 --steps 4096 --warmup 2048" \
+             "--system pmsm --envs 262144" "--system pmsm --envs 1048576" \
+             "--mode vecnorm --system pmsm --envs 262144 --steps 512 --warmup 64"; do
+    tag=$(echo $cfg | tr -d ' -')
+    timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_head.so \
+      -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
+  done
+  ;;
+fast)  # PMSM: the bias pair for the wave's first lane without a branch (waterfall only on mixed k)
+  timeout -k 10 900 $PYT -m gpu --maxfail=4 tests/test_gpu_pmsm_adam_mixed.py tests/test_gpu_parity.py \
+    tests/test_gpu_cfg5.py tests/test_gpu_noise.py tests/test_gpu_step_multi.py tests/test_gpu_policy_branches.py \
+    tests/test_gpu_vecnorm_step.py tests/test_gpu_state_index.py > $O/fast_tests.txt 2>&1 || exit 1
+  for cfg in "--system pmsm --mode rollout --K 2048 --envs 32768 --steps 4096 --warmup 2048" \
+             "--system pmsm --envs 262144" "--system pmsm --envs 1048576" \
+             "--mode vecnorm --system pmsm --envs 262144 --steps 512 --warmup 64"; do
+    tag=$(echo $cfg | tr -d ' -')
+    timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_head.so \
+      -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
+  done
+  ;;
 scalartick)  # the scalar tick load (with the one-batch kernel arguments) vs the vector one
   for cfg in "--dtype float64" "--envs 131072" "--integrator rk4" "--envs 2097152"; do
     tag=$(echo $cfg | tr -d ' -')
