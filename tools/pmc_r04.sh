@@ -8,7 +8,9 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=${1:-gpurun_out/r04_pmc_final}
+ONLY=${ONLY:-}  # space-separated pass names (e.g. "pmsm_262k vn"): re-measure just those
 mkdir -p $O
+want() { [ -z "$ONLY" ] || [[ " $ONLY " == *" $1 "* ]]; }
 pass() {  # pass <name> <counter> bench args...
   local name=$1 c=$2; shift 2
   timeout -k 10 180 rocprofv3 --pmc $c -d $O/$name.$c -o run --output-format csv -- python bench.py "$@" \
@@ -16,13 +18,14 @@ pass() {  # pass <name> <counter> bench args...
 }
 one() {  # one <name> <mangled> <match> <envs> <alg_bytes> bench args...
   local name=$1 mangled=$2 match=$3 envs=$4 alg=$5; shift 5
+  want $name || return 0
   pass $name FETCH_SIZE "$@" || return 1
   pass $name WRITE_SIZE "$@" || return 1
   python tools/pmc_generic.py $O/$name.FETCH_SIZE $O/$name.WRITE_SIZE "$mangled" "$match" $envs $alg \
     $O/${name}_pmc_summary.json | tee -a $O/summary.jsonl
 }
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/head.trace -o run --output-format csv -- python bench.py \
-  --no-cpu-baseline --no-extras > $O/head.trace.log 2>&1 || exit 1
+want head && { timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/head.trace -o run --output-format csv -- python bench.py \
+  --no-cpu-baseline --no-extras > $O/head.trace.log 2>&1 || exit 1; }
 E="--launch eager"
 one lz_step_1M _ZN2lz12k_step_multiINS_5SysL3IfEEfLi4ELb0EEEvNS_5KArgsE "k_step_multi<lz::SysL3<float>, float, 4" \
   1048576 68157440 $E --steps 400 --warmup 40 || exit 1
@@ -42,6 +45,7 @@ one pmsm_multi_1M _ZN2lz12k_step_multiINS_7SysPMSMEfLi4ELb0EEEvNS_5KArgsE "k_ste
   1048576 131072000 --system pmsm --envs 1048576 --steps 256 --warmup 64 $E || exit 1
 one hr_multi_1M _ZN2lz12k_step_multiINS_5SysHRIfEEfLi4ELb0EEEvNS_5KArgsE "k_step_multi<lz::SysHR<float>, float, 4" \
   1048576 89128960 --system hr --envs 1048576 --steps 256 --warmup 64 $E || exit 1
+want vn || exit 0
 VN="--mode vecnorm --system pmsm --envs 262144 --steps 512 --warmup 64"
 pass vn FETCH_SIZE $VN || exit 1
 pass vn WRITE_SIZE $VN || exit 1
