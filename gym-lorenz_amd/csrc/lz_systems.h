@@ -301,8 +301,8 @@ struct SysL4RK4 : SysL4<T> {
 //         beta2=.999, eps=1e-8, err_threshold=5, max_steps=2000, term=1000
 // planes: state1(3), state2(3), lambda, m_t, v_t, adam_step(i32), step(i32)
 // ===========================================================================
-#ifndef LZ_PMSM_BIAS_FAST  // 0: the waterfall alone (A/B)
-#define LZ_PMSM_BIAS_FAST 1
+#ifndef LZ_PMSM_BIAS_FAST  // 2: early constant-space load; 1: in-place asm load; 0: waterfall alone (A/B)
+#define LZ_PMSM_BIAS_FAST 2
 #endif
 #ifndef LZ_PMSM_NO_BIAS_LOAD
 #define LZ_PMSM_NO_BIAS_LOAD 0
@@ -399,12 +399,39 @@ struct SysPMSM {
     x = __uint_as_float((uint32_t)v);
     y = __uint_as_float((uint32_t)(v >> 32));
   }
-  __device__ void bias_pair(const KArgs& a, float& bm, float& bv) const {
+  // LZ_PMSM_BIAS_FAST 2: the pair for the wave's first lane's next step, loaded at the top
+  // of step() through a constant-address-space pointer -- a scalar load the compiler issues
+  // there and waits for (lgkmcnt) only at the first use, after the two RHS evaluations, so
+  // its latency overlaps them (the table is never written while a kernel runs).
+  struct BiasPre {
+    float m, v;
+    int32_t k;
+  };
+  __device__ BiasPre bias_pre(const KArgs& a) const {
+    BiasPre p{1.0f, 1.0f, 0};
+#if LZ_PMSM_BIAS_FAST == 2 && !LZ_PMSM_NO_BIAS_LOAD
+    typedef const __attribute__((address_space(4))) uint64_t cu64;
+    p.k = __builtin_amdgcn_readfirstlane(adam) + 1;  // this step's Adam k (:121)
+    const int32_t kc = p.k < a.bc_len ? p.k : a.bc_len - 1;
+    const uint64_t t = ((cu64*)a.bc)[kc > 0 ? kc : 0];
+    p.m = __uint_as_float((uint32_t)t);
+    p.v = __uint_as_float((uint32_t)(t >> 32));
+#endif
+    return p;
+  }
+  __device__ void bias_pair(const KArgs& a, float& bm, float& bv, const BiasPre& pre) const {
 #if LZ_PMSM_NO_BIAS_LOAD  // A/B only (tools/build_ab.sh): what the table load costs -- WRONG results
     bm = bv = 1.0f;
     return;
 #endif
-#if LZ_PMSM_BIAS_FAST
+#if LZ_PMSM_BIAS_FAST == 2
+    {  // the early pair (bias_pre); the waterfall below only when the wave's steps differ
+      const bool in = pre.k < a.bc_len;
+      bm = in ? pre.m : 1.0f;
+      bv = in ? pre.v : 1.0f;
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(adam != pre.k) == 0, 1)) return;
+    }
+#elif LZ_PMSM_BIAS_FAST
     {  // the wave's first lane's step, loaded without a branch (index clamped, 1.0 selected
        // past the table); the waterfall below only when the wave's steps differ
       const int32_t k0 = __builtin_amdgcn_readfirstlane(adam);
@@ -431,6 +458,7 @@ struct SysPMSM {
   // step(): :76-184
   __device__ bool step(const float* act, bool use_nz, const double* nz, float* o, float& rew,
                        const KArgs& a) {
+    const BiasPre pre = bias_pre(a);
     const float a1 = clip_nz(act[0], -1.0f, 1.0f) * fmax;  // :81-82
     const float a2 = clip_nz(act[1], -1.0f, 1.0f) * fmax;
     float d1[3], d2[3];
@@ -449,7 +477,7 @@ struct SysPMSM {
     mt = b1 * mt + c1 * grad;                              // :124
     vt = b2 * vt + c2 * (grad * grad);                     // :127 (glibc powf(g,2) in ref)
     float bcm, bcv;
-    bias_pair(a, bcm, bcv);
+    bias_pair(a, bcm, bcv, pre);
     const float mh = mt / bcm;                             // :130 (1-b1**k) -> f32
     const float vh = vt / bcv;                             // :131
     lam = lam - (lr * mh) / (sqrtf(vh) + eps);             // :135

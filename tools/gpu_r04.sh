@@ -198,6 +198,19 @@ fast)  # PMSM: the bias pair for the wave's first lane without a branch (waterfa
       -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
   done
   ;;
+fast2)  # PMSM: the bias pair loaded at the top of step() through a constant-space pointer (vs HEAD)
+  timeout -k 10 900 $PYT -m gpu --maxfail=4 tests/test_gpu_pmsm_adam_mixed.py tests/test_gpu_parity.py \
+    tests/test_gpu_cfg5.py tests/test_gpu_noise.py tests/test_gpu_step_multi.py tests/test_gpu_policy_branches.py \
+    tests/test_gpu_vecnorm_step.py tests/test_gpu_state_index.py > $O/fast2_tests.txt 2>&1 || exit 1
+  for cfg in "--system pmsm --mode rollout --K 2048 --envs 32768 --steps 4096 --warmup 2048" \
+             "--system pmsm --mode rollout --K 2048 --envs 262144 --steps 4096 --warmup 2048" \
+             "--system pmsm --envs 262144" "--system pmsm --envs 1048576" \
+             "--mode vecnorm --system pmsm --envs 262144 --steps 512 --warmup 64"; do
+    tag=$(echo $cfg | tr -d ' -')
+    timeout -k 10 600 python tools/ab_libs.py 3 default ablib/libgym_lorenz_amd_fast1.so \
+      -- $cfg $BQ > $O/ab_$tag.json 2> $O/ab_$tag.err || exit 1
+  done
+  ;;
 scalartick)  # the scalar tick load (with the one-batch kernel arguments) vs the vector one
   for cfg in "--dtype float64" "--envs 131072" "--integrator rk4" "--envs 2097152"; do
     tag=$(echo $cfg | tr -d ' -')
