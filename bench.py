@@ -692,6 +692,31 @@ def scaling_line(args, gl, nat, torch, dist, device, world, rank):
     }
 
 
+XGMI_LINKS = 7  # point-to-point xGMI links per MI355X (MI355X_MICROARCH.md)
+
+
+def gather_accounting(world, nbytes, steps, seconds):
+    """Bytes and rates of `steps` gathers of `nbytes` per rank into rank 0.  Rank 0's own
+    shard never leaves its HBM, so (world - 1) x nbytes cross xGMI per gather; each peer
+    sends its shard over its own point-to-point link into rank 0 (a full mesh of 8), so
+    the per-link figure divides by the min(world - 1, 7) links rank 0 receives on."""
+    xgmi = (world - 1) * nbytes
+    links = max(1, min(world - 1, XGMI_LINKS))
+    return {"us_per_step": seconds * 1e6 / steps, "bytes_per_step_xgmi": xgmi,
+            "bytes_per_step_rank0_local": nbytes,
+            "GB_per_s": xgmi * steps / seconds / 1e9,
+            "links": links, "GB_per_s_per_link": xgmi * steps / seconds / 1e9 / links}
+
+
+def check_devices(gpus, backend, device_count):
+    """RCCL runs one rank per GPU: more ranks than visible GPUs would share cards (rank r
+    takes cuda:(r mod count)) and report a 'strong' number that is not one -- refuse."""
+    if backend == "nccl" and gpus > 1 and gpus > device_count:
+        raise SystemExit("bench.py: --gpus %d but only %d GPU(s) visible; the nccl (RCCL) backend "
+                         "needs one GPU per rank (LZ_BENCH_BACKEND=gloo rehearses ranks sharing a "
+                         "GPU)" % (gpus, device_count))
+
+
 def gather_line(args, gl, nat, torch, dist, device, world, rank, total, n, start, backend,
                 steps=200):
     """N > 1: north_star's optional learner gather -- every step, lz_step on each rank's
@@ -743,11 +768,11 @@ def gather_line(args, gl, nat, torch, dist, device, world, rank, total, n, start
         "metric": "env-steps/s with the per-step gather of obs | reward | done to rank 0",
         "value": total * steps / t_both, "unit": "env-steps/s", "n_gpus": world, "steps": steps,
         "ms_per_step": t_both * 1e3 / steps, "dtype": "f32",
-        "gather": {"us_per_step": t_gather * 1e6 / steps, "bytes_per_step": world * nbytes,
-                   "GB_per_s": world * nbytes * steps / t_gather / 1e9,
+        "gather": dict(gather_accounting(world, nbytes, steps, t_gather), **{
                    "backend": "RCCL (xGMI)" if not host else "%s on host copies (rehearsal)" % backend,
                    "collective": "one torch.distributed.gather of each rank's packed obs|reward|done "
-                                 "(%d B) into rank 0" % nbytes},
+                                 "(%d B) into rank 0; GB_per_s counts the (world - 1) shards that "
+                                 "cross xGMI" % nbytes}),
         "config": {"workload": "dynamic.py env step (lz_step, fp32) + gather to rank 0, %d envs "
                                "total, %d per GPU" % (total, n),
                    "envs_total": total, "envs_per_gpu": n},
@@ -990,6 +1015,7 @@ def main():
     # LZ_BENCH_BACKEND=gloo + ranks sharing a GPU: rehearsal of the multi-rank path on a
     # 1-GPU box (the driver's 8-GPU runs use the default: RCCL, one GPU per rank)
     backend = os.environ.get("LZ_BENCH_BACKEND", "nccl")
+    check_devices(world, backend, torch.cuda.device_count())
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)

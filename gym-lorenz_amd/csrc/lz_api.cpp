@@ -589,7 +589,16 @@ static int rs_reply_layout(const lz_handle* h, RsReplyLayout& L) {
   L.done = c++;
   return c;
 }
-static bool rs_reply_mode(const lz_handle* h) { return h->cfg.num_envs == 1; }
+// Every system today fits (worst case 12 float64 planes + 8 float64 obs + reward + done =
+// 43 words); a layout that would not fit the reply's kRsReplyWords granules (the host's
+// rwords[] and ResShared::rep) takes the mailbox path instead of overflowing them.
+static_assert(lz::kMaxPlanes * 2 + 2 * lz::kVnMaxObs + 3 <= lz::kRsReplyWords,
+              "the tagged reply of a one-env handle must fit kRsReplyWords granules");
+static bool rs_reply_mode(const lz_handle* h) {
+  if (h->cfg.num_envs != 1) return false;
+  RsReplyLayout L;
+  return rs_reply_layout(h, L) <= lz::kRsReplyWords;
+}
 
 static volatile int64_t* rs_word(const lz_handle* h, size_t off) {
   return reinterpret_cast<volatile int64_t*>(h->rs_pin + off);
@@ -1388,11 +1397,15 @@ lz_status lz_get_launch_shape(const lz_handle* h, int32_t call, lz_launch_shape*
   if (!h || !out) return fail(LZ_ERR_INVALID, "handle/out is NULL");
   std::memset(out, 0, sizeof *out);
   const int64_t n = h->cfg.num_envs;
-  if (call == LZ_CALL_STEP || call == LZ_CALL_ROLLOUT) {
+  if (call == LZ_CALL_STEP || call == LZ_CALL_STEP_NOISE || call == LZ_CALL_ROLLOUT) {
     KArgs a;
     fill_common(h, a);
+    // lz_step's noise argument (only its presence matters to the launcher): fill_common
+    // leaves it NULL, the device-drawn case; LZ_CALL_STEP_NOISE asks for the injected one
+    static const double kNoiseTag = 0.0;
+    if (call == LZ_CALL_STEP_NOISE) a.noise = &kNoiseTag;
     int32_t o[5] = {0, 0, 0, 0, 0};
-    if (lz::env_launch_shape(call == LZ_CALL_STEP ? 1 : 2, sys_key(h), h->f64, a, o) != 0)
+    if (lz::env_launch_shape(call == LZ_CALL_ROLLOUT ? 2 : 1, sys_key(h), h->f64, a, o) != 0)
       return fail(LZ_ERR_INVALID, "no launch shape for system %d", h->cfg.system);
     out->kernel = o[0];
     out->envs_per_wave = o[1];

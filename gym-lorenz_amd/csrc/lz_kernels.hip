@@ -722,6 +722,7 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   // running source of the DMA issued at step k (step min(k + D, K - 1)): advanced by
   // one step per step until it reaches the last (no per-step 64-bit multiply)
   const float* dsrc = dma_src(D < a.K ? D : a.K - 1);
+  uint32_t zcap = 0;  // kNP: the producer timed out once -- stop waiting for it (sticky)
   // kLadder: one of the first D steps (its wait count depends on k); later steps all
   // wait with the steady-state count -- peeled so the hot loop carries no ladder
   auto run_step = [&](int k, auto ladder) __attribute__((always_inline)) {
@@ -763,12 +764,22 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
     const float* zp = nullptr;
     if constexpr (kNP) {  // step k's normals: wait for the producer wave (LDS flag, relaxed:
       // LDS operations of a wave execute in order, the signal fences keep the compiler's)
-      for (uint32_t spin = 0; spin < kZSpinCap &&  // (a cap: every wave leaves, whatever happens)
-                              __hip_atomic_load(&zflag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= k;
-           ++spin)
+      uint32_t spin = zcap;
+      while (spin < kZSpinCap &&  // (a cap: every wave leaves, whatever happens)
+             __hip_atomic_load(&zflag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= k) {
         __builtin_amdgcn_s_sleep(1);
+        ++spin;
+      }
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      zp = s_z + (k % kZSlots) * 3 * B + tid;
+      float* zs = const_cast<float*>(s_z) + (k % kZSlots) * 3 * B + tid;  // (LDS ring)
+      if (spin >= kZSpinCap) {  // the producer never delivered: poison this step's normals
+        // and every later step's (NaN obs / reward: a wrong result is visible, never silently
+        // stale); the producer leaves on its own cap and is not waited for again
+        zcap = kZSpinCap;
+        zs[0] = zs[B] = zs[2 * B] = __builtin_nanf("");
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      }
+      zp = zs;
     }
     const uint8_t dflag = step_body<Sys, T, true, false, kNoDone, false, kNP>(
         sys, steps, a, i, live, act, tick + (uint64_t)k, k, o, rew, did_reset, nullptr, true, zp);
@@ -835,11 +846,14 @@ __device__ __forceinline__ void noise_producer(const KArgs& a, int64_t base, int
   const uint64_t gid = (uint64_t)(a.gid0 + base + lane);
   for (int k = 0; k < a.K; ++k) {
     if (k >= kZSlots) {  // the stepping wave is done with step k - kZSlots's slot
-      for (uint32_t spin = 0;
-           spin < kZSpinCap && __hip_atomic_load(&zflag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= k - kZSlots;
-           ++spin)
+      uint32_t spin = 0;
+      while (spin < kZSpinCap &&
+             __hip_atomic_load(&zflag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= k - kZSlots) {
         __builtin_amdgcn_s_sleep(1);
+        ++spin;
+      }
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (spin >= kZSpinCap) return;  // never overwrite a slot still in use: stop drawing
     }
     float z[3];
     normal3(a.seed, gid, tick + (uint64_t)k, z);
@@ -1502,6 +1516,10 @@ __device__ void resident_poll(const ResMember* __restrict__ table, int n, const 
   const bool mine = k < n;
   int ng = 1;
   if (mine && table[k].box.inline_words > 1) ng = table[k].box.inline_words;
+  // a member on the mailbox path (inline_words < 0) reads its inputs from host memory
+  // after the LDS hand-off: the poller orders the host's mailbox stores before that hand-off
+  // with one system-scope acquire per accepted request
+  const bool mailbox = mine && table[k].box.inline_words < 0;
   const uint64_t* src = lines + (int64_t)k * kRsLineWords + 2 * q;
   uint32_t seen = 0xffffffffu;  // no tag: the first pass hands over every line (a request
                                 // may predate the launch)
@@ -1519,6 +1537,7 @@ __device__ void resident_poll(const ResMember* __restrict__ table, int n, const 
     const unsigned long long okm = __ballot(ok);
     const bool whole = ((okm >> (4 * k)) & 0xfull) == 0xfull;
     const bool fresh = mine && whole && t0 != seen;
+    if (__ballot(fresh && mailbox)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (fresh) {
       if (2 * q < ng) sh->pay[k][2 * q] = (uint32_t)g0;
       if (2 * q + 1 < ng) sh->pay[k][2 * q + 1] = (uint32_t)g1;

@@ -151,9 +151,19 @@ static PyObject* Stepper_step(Stepper* s, PyObject* const* args, Py_ssize_t narg
   return t;
 }
 
+/* The handle is destroyed by its owner (SingleEnvCore.close -> lz_destroy): forget its
+ * address, so a later step passes NULL and the library answers LZ_ERR_INVALID instead of
+ * touching freed memory. */
+static PyObject* Stepper_close(Stepper* s, PyObject* unused) {
+  (void)unused;
+  s->h = NULL;
+  Py_RETURN_NONE;
+}
+
 static PyMethodDef Stepper_methods[] = {
     {"step", (PyCFunction)(void (*)(void))Stepper_step, METH_FASTCALL,
      "step(action, noise=None) -> (obs, reward, done) or an lz_status int"},
+    {"close", (PyCFunction)Stepper_close, METH_NOARGS, "forget the handle (steps then fail cleanly)"},
     {NULL, NULL, 0, NULL}};
 
 static PyTypeObject StepperType = {

@@ -156,7 +156,7 @@ class LzLaunchShape(ctypes.Structure):
 # lz_get_launch_shape calls / kernels / flags (lorenz_env.h)
 (CALL_STEP, CALL_ROLLOUT, CALL_ROLLOUT_POLICY, CALL_ROLLOUT_POLICY_F32, CALL_POLICY_STEP_F32,
  CALL_ROLLOUT_POLICY_ATTN, CALL_ROLLOUT_POLICY_ATTN_STACK, CALL_ROLLOUT_POLICY_ATTN_F32,
- CALL_ROLLOUT_POLICY_ATTN_STACK_F32) = range(9)
+ CALL_ROLLOUT_POLICY_ATTN_STACK_F32, CALL_STEP_NOISE) = range(10)
 KERNELS = {1: "step", 2: "step_multi", 3: "rollout", 4: "rollout_wave", 5: "rollout_split",
            6: "policy", 7: "policy_pair", 8: "policy_pair_pipe", 9: "policy_split",
            10: "policy_step", 11: "policy_attn", 12: "policy_attn_f32"}

@@ -143,6 +143,13 @@ class SingleEnvCore:
             self.be.set_state(first + j, torch.tensor([v], dtype=self.be.plane_dtype(first + j)))
 
     def close(self):
+        # the fast paths hold the raw handle address: drop it before lz_destroy frees the
+        # handle, so a step after close() gets LZ_ERR_INVALID (a NULL handle), not freed memory
+        if self._stepper is not None:
+            self._stepper.close()
+            self._stepper = None
+        self._args = (None,) + self._args[1:]
+        self._args_nz = (None,) + self._args_nz[1:]
         self.be.close()
 
 

@@ -662,7 +662,7 @@ lz_status lz_frame_stack(float* stacked, const float* obs, const uint8_t* done, 
  * assert that they reach every branch and profiling tools can name the kernel.
  * ------------------------------------------------------------------------------ */
 enum {
-  LZ_CALL_STEP = 0,                        /* lz_step */
+  LZ_CALL_STEP = 0,                        /* lz_step, noise drawn on the device (noise NULL) */
   LZ_CALL_ROLLOUT = 1,                     /* lz_rollout */
   LZ_CALL_ROLLOUT_POLICY = 2,              /* lz_rollout_policy (bf16 MlpPolicy) */
   LZ_CALL_ROLLOUT_POLICY_F32 = 3,          /* lz_rollout_policy_f32 */
@@ -670,7 +670,9 @@ enum {
   LZ_CALL_ROLLOUT_POLICY_ATTN = 5,         /* lz_rollout_policy_attn */
   LZ_CALL_ROLLOUT_POLICY_ATTN_STACK = 6,   /* lz_rollout_policy_attn_stack */
   LZ_CALL_ROLLOUT_POLICY_ATTN_F32 = 7,     /* lz_rollout_policy_attn_f32 */
-  LZ_CALL_ROLLOUT_POLICY_ATTN_STACK_F32 = 8 /* lz_rollout_policy_attn_stack_f32 */
+  LZ_CALL_ROLLOUT_POLICY_ATTN_STACK_F32 = 8, /* lz_rollout_policy_attn_stack_f32 */
+  LZ_CALL_STEP_NOISE = 9                   /* lz_step with caller-supplied noise (always
+                                              k_step: the multi-tile kernel draws on device) */
 };
 enum {
   LZ_KERNEL_STEP = 1,             /* k_step: one 256-env tile per workgroup */

@@ -69,6 +69,49 @@ def test_launcher_propagates_a_failed_rank():
     assert time.time() - t0 < 40  # rank 0 (sleeping 60 s) was terminated, not waited for
 
 
+def test_gather_accounting_counts_xgmi_bytes_only():
+    """rank 0's own shard never crosses xGMI -- the gather line
+    counts (world - 1) shards, and per link over the min(world - 1, 7) links into rank 0."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    nb, steps, secs = 1_000_000, 100, 0.5
+    g = bench.gather_accounting(8, nb, steps, secs)
+    assert g["bytes_per_step_xgmi"] == 7 * nb and g["bytes_per_step_rank0_local"] == nb
+    assert g["links"] == 7
+    assert abs(g["GB_per_s"] - 7 * nb * steps / secs / 1e9) < 1e-12
+    assert abs(g["GB_per_s_per_link"] - nb * steps / secs / 1e9) < 1e-12
+    assert abs(g["us_per_step"] - secs * 1e6 / steps) < 1e-9
+    g2 = bench.gather_accounting(2, nb, steps, secs)
+    assert g2["bytes_per_step_xgmi"] == nb and g2["links"] == 1
+    assert g2["GB_per_s_per_link"] == g2["GB_per_s"]
+    g4 = bench.gather_accounting(4, nb, steps, secs)
+    assert g4["links"] == 3 and g4["bytes_per_step_xgmi"] == 3 * nb
+
+
+def test_refuses_more_rccl_ranks_than_gpus():
+    """`--gpus N` with the nccl (RCCL) backend and fewer than N visible GPUs exits non-zero
+    with a clear message (ranks would share cards and report a false 'strong' number);
+    gloo rehearsals and one-rank runs are not refused."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    with pytest.raises(SystemExit) as ei:
+        bench.check_devices(8, "nccl", 1)
+    assert "only 1 GPU" in str(ei.value.code)
+    bench.check_devices(8, "nccl", 8)
+    bench.check_devices(2, "gloo", 1)
+    bench.check_devices(1, "nccl", 1)
+    # end to end on this GPU-less host: both spawned ranks refuse, the launcher fails
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK",
+                                                             "LZ_BENCH_BACKEND")}
+    env["HIP_VISIBLE_DEVICES"] = ""  # no GPU visible even on a GPU box
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode != 0 and "GPU(s) visible" in r.stderr, (r.returncode, r.stderr[-2000:])
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
 @pytest.mark.gpu
 def test_bench_line_contract_steps20():
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))

@@ -241,6 +241,24 @@ def test_dropin_resident_matches_step_host(gl, monkeypatch):
         assert bits_equal(np.asarray(p), np.asarray(q))
 
 
+@pytest.mark.parametrize("stepper", ["1", "0"])
+@pytest.mark.parametrize("noise", [False, True])
+def test_dropin_step_after_close_raises(gl, monkeypatch, stepper, noise):
+    """the drop-in's fast paths (C stepper, prebuilt ctypes args) drop the
+    handle on close(): a later step() raises LorenzEnvError(LZ_ERR_INVALID) instead of
+    reaching the freed handle."""
+    from gym_lorenz import _native as nat
+
+    monkeypatch.setenv("LZ_STEPPER", stepper)
+    env = gl.make("lorenz_pmsm-v0", alpha=0.5, add_noise=noise)
+    env.reset(seed=3)
+    env.step(np.zeros(2, np.float32))
+    env.close()
+    with pytest.raises(nat.LorenzEnvError) as ei:
+        env.unwrapped.step(np.zeros(2, np.float32))
+    assert ei.value.status == nat.LZ_ERR_INVALID
+
+
 @pytest.mark.parametrize("close", [False, True])
 def test_process_exit_with_live_server(close):
     """A script that exits while the server is resident (no close(): the atexit hook

@@ -101,12 +101,16 @@ def _planes(be, p0, k):
     return np.stack([_np(be.get_state(p0 + j)) for j in range(k)], 1)
 
 
-def test_hr_1m_default_multi_vs_oracle(gl, orc):
-    """The HR bench line's size (1,048,576 envs: the default launch IS k_step_multi with
-    4 tiles per workgroup): 6 float32 steps with injected noise, the whole batch bit for
-    bit against the oracle's DEV restatement."""
+def test_hr_1m_injected_noise_vs_oracle(gl, orc):
+    """HR at 1,048,576 envs with INJECTED noise: step_tiles sends every injected-noise
+    launch to k_step (k_step_multi draws its noise on the device; that default launch is
+    covered in test_gpu_default_launch.py) -- asserted through LZ_CALL_STEP_NOISE.  6
+    float32 steps, the whole batch bit for bit against the oracle's DEV restatement."""
+    from gym_lorenz import _native as nat
+
     n, T = 1 << 20, 6
     be = gl.BatchedEnv("hr", n, dtype="float32", seed=5, add_noise=True, autoreset=False)
+    assert nat.launch_shape(be._h, nat.CALL_STEP_NOISE)["kernel"] == "step"
     be.reset()
     init = orc.reset_draw("hr", np.float32, n, 0, 5, 0, add_noise=True)
     st = np.ascontiguousarray(init[:, :6])
@@ -124,11 +128,15 @@ def test_hr_1m_default_multi_vs_oracle(gl, orc):
     be.close()
 
 
-def test_pmsm_1m_default_multi_vs_oracle(gl, orc):
-    """PMSM at 1,048,576 envs (default launch: k_step_multi, 4 tiles): 6 steps with
-    injected noise, obs / state / lambda path bit for bit vs the oracle's DEV mode."""
+def test_pmsm_1m_injected_noise_vs_oracle(gl, orc):
+    """PMSM at 1,048,576 envs with INJECTED noise (k_step, asserted; the device-noise
+    default k_step_multi is test_gpu_default_launch.py's): 6 steps, obs / state / lambda
+    path bit for bit vs the oracle's DEV mode."""
+    from gym_lorenz import _native as nat
+
     n, T = 1 << 20, 6
     be = gl.BatchedEnv("pmsm", n, seed=6, add_noise=True, autoreset=False)
+    assert nat.launch_shape(be._h, nat.CALL_STEP_NOISE)["kernel"] == "step"
     be.reset()
     S = orc.PmsmState(n)
     S.st[:] = orc.reset_draw("pmsm", np.float32, n, 0, 6, 0)

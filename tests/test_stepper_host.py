@@ -87,3 +87,24 @@ def test_no_action_system():
     f = Fake(0, 8, np.float32)  # LORENZ4 / singlecontrol: no action read
     obs, rew, done = f.stepper().step([])
     assert obs.shape == (8,) and rew == 0.0 and done == 1
+
+
+def test_close_forgets_handle():
+    """after Stepper.close() (SingleEnvCore.close, before lz_destroy) a step
+    passes a NULL handle -- the library's clean LZ_ERR_INVALID -- never the freed address."""
+    f = Fake(2, 6, np.float64)
+    s = f.stepper()
+    s.step([0.0, 1.0])
+    assert f.seen[-1][0] == 0x1234
+    s.close()
+    s.step([0.0, 1.0])
+    assert f.seen[-1][0] is None  # ctypes hands a NULL c_void_p over as None
+
+
+def test_real_library_null_handle_is_invalid():
+    """The real entry points answer a NULL handle with LZ_ERR_INVALID (no GPU touched)."""
+    from gym_lorenz import _native as nat
+
+    for name in ("lz_resident_step", "lz_step_host"):
+        st = getattr(nat.lib, name)(None, None, None, None, None, None)
+        assert st == nat.LZ_ERR_INVALID, name
