@@ -68,7 +68,7 @@ def parse(argv=None):
                    help=argparse.SUPPRESS)  # A/B: the env arithmetic of the main line
     p.add_argument("--add-noise", type=int, choices=[0, 1], default=None,
                    help=argparse.SUPPRESS)  # A/B: the process-noise flag (default: the config's)
-    p.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+    p.add_argument("--precision", choices=["fp32", "bf16", "i8x4"], default="fp32",
                    help="--mode policy --policy mlp: fp32 = SB3's float32 forward "
                         "(lz_rollout_policy_f32), bf16 = the bf16-MFMA kernel")
     p.add_argument("--vecnorm-update", choices=["step", "rollout"], default="step",
@@ -436,11 +436,14 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
     net = (ActorCriticAttn(stack * O, A, seed=0, layer_norm=ln) if attn
            else ActorCriticMlp(O, A, seed=0))
     rms = None if attn else DeviceRunningMeanStd(O, device)
-    f32 = args.precision == "fp32"
+    f32 = args.precision in ("fp32", "i8x4")
+    i8 = args.precision == "i8x4"
+    if i8 and not attn:
+        raise SystemExit("--precision i8x4 runs the attention policies (--policy attn / attn_ln)")
     per_step = f32 and not attn and args.vecnorm_update == "step"
     col = FusedRolloutCollector(env, net.state_dict(), gamma=0.99, gae_lambda=0.95, obs_rms=rms,
                                 clip_obs=10.0, training=True, bootstrap=True, frame_stack=stack,
-                                precision="fp32" if f32 else "bf16",
+                                precision=args.precision,
                                 vecnorm_update=("step" if per_step else "rollout")
                                 if f32 and not attn else None)
     assert col.per_step_vecnorm == per_step
@@ -501,8 +504,12 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "f32 MFMA (f32 accumulate), f32 env" if f32 else "bf16 MFMA (fp32 accumulate), f32 env",
-        "precision_note": ("float32 end to end, bit-exact vs the C oracle (SB3's own precision)"
+        "dtype": ("f32 MFMA extractor + exact int8 MFMA (4-digit fixed point) nets, f32 env" if i8 else
+                  "f32 MFMA (f32 accumulate), f32 env" if f32 else "bf16 MFMA (fp32 accumulate), f32 env"),
+        "precision_note": ("opt-in i8x4: the nets' wide layers as exact fixed-point products, float32-"
+                           "level accuracy, bit-exact vs the C oracle (orc_attn_i8x4); frac = useful "
+                           "FLOP against the f32 MFMA peak, like the fp32 line" if i8 else
+                           "float32 end to end, bit-exact vs the C oracle (SB3's own precision)"
                            if f32 else "bf16 operands (opt-in, ~1e-2 off SB3's float32)"),
         "data": "synthetic: on-device Philox initial states and Gaussian action samples; "
                 "SB3-initialised (orthogonal) random policy weights",
@@ -510,13 +517,15 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
             "workload": ("%s with code/lorenz_filter/train.py's PPO actor-critic on "
                          "VecFrameStack(4) (attention + residual + LayerNorm extractor, pi/vf "
                          "[128,128] Tanh): %d-step fused rollout (lz_rollout_policy_attn_stack" +
-                         ("_f32, float32 as SB3" if f32 else ", bf16 MFMA") + ": "
+                         ("_f32 + LZ_POLICY_I8X4, exact int8 nets" if i8 else "_f32, float32 as SB3"
+                          if f32 else ", bf16 MFMA") + ": "
                          "frame stack + extractor + nets + sample + clip + env step + bootstrap), "
                          "GAE (lz_gae); %d envs total, %d per GPU" if ln else
                          "%s with code/train.py's PPO actor-critic (AttentionFeaturesExtractor "
                          "fc1 + 4-head self-attention over 8 tokens + post_fc 64, then pi/vf "
                          "[128,128] Tanh) in the loop: %d-step fused rollout "
-                         "(lz_rollout_policy_attn" + ("_f32, float32 as SB3" if f32 else ", bf16 MFMA")
+                         "(lz_rollout_policy_attn" + ("_f32 + LZ_POLICY_I8X4, exact int8 nets" if i8 else
+                                                      "_f32, float32 as SB3" if f32 else ", bf16 MFMA")
                          + ": extractor + nets + DiagGaussian sample + clip "
                          "+ env step + truncation bootstrap), GAE (lz_gae); %d envs total, %d per "
                          "GPU" if attn else
@@ -535,7 +544,7 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
                             "%d envs total, %d per GPU"))
                         % (SYSTEM_INFO[args.system][0], K, total, n),
             "system": args.system, "envs_total": total, "envs_per_gpu": n, "mode": "policy",
-            "policy": args.policy, "precision": "fp32" if f32 else "bf16",
+            "policy": args.policy, "precision": args.precision,
             "vecnorm_update": None if attn else ("step (SB3 order)" if per_step
                                                  else "rollout (pooled, opt-in)"),
             "K": K, "parallelism": "env shard x%d (no collective on step; obs_rms moments "
@@ -544,9 +553,9 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         "roofline": {
             "bound": "mfma", "achieved": achieved, "peak": peak,
             "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-            "kernel": ("_ZN2lz25k_rollout_policy_attn_f32INS_%sLb1ELi4ELi8EEEvNS_5KArgsENS_5PArgsE"
+            "kernel": (("_ZN2lz25k_rollout_policy_attn_f32INS_%sLb1ELi4ELi8ELb" + "01"[i8] + "EEEvNS_5KArgsENS_5PArgsE")
                        if ln and f32 else
-                       "_ZN2lz25k_rollout_policy_attn_f32INS_%sLb0ELi1ELi8EEEvNS_5KArgsENS_5PArgsE"
+                       ("_ZN2lz25k_rollout_policy_attn_f32INS_%sLb0ELi1ELi8ELb" + "01"[i8] + "EEEvNS_5KArgsENS_5PArgsE")
                        if attn and f32 else
                        "_ZN2lz16k_rollout_policyINS_%sLi4ELi32ELi4ELi4EEEvNS_5KArgsENS_5PArgsE"
                        if ln else

@@ -1168,6 +1168,8 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
     if (sys != LZ_SYS_LORENZ3 && sys != LZ_SYS_PMSM && sys != LZ_SYS_HR)
       return fail(LZ_ERR_UNSUPPORTED, "the float32 attention rollout runs LORENZ3 / PMSM / HR");
   }
+  if ((r->flags & LZ_POLICY_I8X4) && arch < 4)
+    return fail(LZ_ERR_UNSUPPORTED, "LZ_POLICY_I8X4 runs the attention float32 rollouts only");
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_rollout_policy before the first lz_reset");
   if (h->f64) return fail(LZ_ERR_UNSUPPORTED, "the policy rollout runs float32 handles only");
   if (sys_key(h) != h->cfg.system)
@@ -1262,6 +1264,8 @@ lz_status lz_policy_step_f32(lz_handle* h, const lz_policy_rollout_args* r, int3
                              double* obs_rms_state, double* moments_out) {
   if (!h || !r) return fail(LZ_ERR_INVALID, "handle/args is NULL");
   RESIDENT_QUIESCE(h);
+  if (r->flags & LZ_POLICY_I8X4)
+    return fail(LZ_ERR_UNSUPPORTED, "LZ_POLICY_I8X4 runs the attention float32 rollouts only");
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_policy_step_f32 before the first lz_reset");
   if (h->f64) return fail(LZ_ERR_UNSUPPORTED, "the policy rollout runs float32 handles only");
   if (sys_key(h) != h->cfg.system)

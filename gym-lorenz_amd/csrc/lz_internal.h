@@ -238,6 +238,20 @@ constexpr int kAFLogStd = kAFExt + 2 * kAFNet;
 constexpr int kAFTanh = kAFLogStd + 64;
 constexpr int kAFBlobBytes = kAFLogStd + kAFConst;          // 261,568 B (device)
 constexpr int kAFLdsBytes = kAFExt + kAFConst + kAFNet;     // 159,168 B (LDS)
+// The opt-in "i8x4" nets (lz_attn_policy_pack_i8x4, LZ_POLICY_I8X4): the same blob, the
+// same extractor, the same offsets -- the two wide layers' float32 weights replaced by
+// their four int8 digits (4 B per weight either way, v_mfma_i32_16x16x64_i8 A operands)
+// and two int16 tables of per-row shifts after the head bias.  Layer 1 tile t, digit i:
+// lane (G, m) 16 B, byte 4f + r = digit i of W1[16t + m][16f + 4G + r]; layer 2 tile t,
+// k-block kb, digit i: byte 4f + r = digit i of W2[16t + m][64kb + 16f + 4G + r].
+// Shift of unit u: 24 - q_u (layer 1, the input's q subtracted in the kernel) and
+// 24 - q_u - 28 (layer 2; its inputs are tanh outputs at q = 28).
+constexpr int kAXN1 = kAFN1;                                // [8][4][64][16 B]
+constexpr int kAXN2 = kAFN2;                                // [8][2][4][64][16 B]
+static_assert(kAXN2 == kAXN1 + 8 * 4 * 64 * 16 && kAFNB1 == kAXN2 + 8 * 2 * 4 * 64 * 16, "i8x4 layout");
+constexpr int kAXSh1 = kAFNHB + 16;                         // int16 [128]
+constexpr int kAXSh2 = kAXSh1 + 128 * 2;                    // int16 [128]
+static_assert(kAXSh2 + 128 * 2 <= kAFNet, "i8x4 net slot");
 
 struct PArgs {
   const uint8_t* blob;     // device copy of the packed policy

@@ -404,6 +404,68 @@ void pack_attn_f32(uint8_t* b, const lz_attn_policy* p, const float* ln_w, const
   }
 }
 
+// The opt-in i8x4 nets (lz_internal.h kAX*): float32 -> V = rint(v 2^q), |V| <= 2^28, as
+// four balanced int8 digits (U = V + 0x808080: bytes 0..2 of U ^ 0x80, then U >> 24); q of
+// a weight row = 28 - e of its largest |w| = f 2^e.  oracle/lz_oracle.c orc_i8x_* restates
+// this independently (tests/test_i8x4_host.py).
+int i8x_q(float m) {
+  int e = 0;
+  (void)std::frexp(m, &e);
+  return 28 - e;
+}
+void i8x_digits(float v, int q, int8_t* d) {
+  const int32_t V = (int32_t)std::nearbyint(std::ldexp(v, q));
+  const int32_t U = (int32_t)((uint32_t)V + 0x808080u);
+  d[0] = (int8_t)((U & 0xff) ^ 0x80);
+  d[1] = (int8_t)(((U >> 8) & 0xff) ^ 0x80);
+  d[2] = (int8_t)(((U >> 16) & 0xff) ^ 0x80);
+  d[3] = (int8_t)(U >> 24);
+}
+int i8x_row_q(const float* w, int K) {
+  float m = 0.0f;
+  for (int k = 0; k < K; ++k) m = std::fmax(m, std::fabs(w[k]));
+  return i8x_q(m);
+}
+
+// pack_attn_f32's blob with the pi / vf nets' two wide layers as digits + row shifts
+void pack_attn_i8x4(uint8_t* b, const lz_attn_policy* p, const float* ln_w, const float* ln_b) {
+  using lz::kPolHidden;
+  pack_attn_f32(b, p, ln_w, ln_b);
+  const float* W1[2] = {p->pi_w1, p->vf_w1};
+  const float* W2[2] = {p->pi_w2, p->vf_w2};
+  for (int n = 0; n < 2; ++n) {
+    uint8_t* net = b + (n == 0 ? lz::kAFPi : lz::kAFVf);
+    int8_t* g1 = reinterpret_cast<int8_t*>(net + lz::kAXN1);
+    int8_t* g2 = reinterpret_cast<int8_t*>(net + lz::kAXN2);
+    int16_t* s1 = reinterpret_cast<int16_t*>(net + lz::kAXSh1);
+    int16_t* s2 = reinterpret_cast<int16_t*>(net + lz::kAXSh2);
+    int q1[kPolHidden], q2[kPolHidden];
+    for (int u = 0; u < kPolHidden; ++u) {
+      q1[u] = i8x_row_q(W1[n] + u * lz::kAttFeat, lz::kAttFeat);
+      q2[u] = i8x_row_q(W2[n] + u * kPolHidden, kPolHidden);
+      s1[u] = (int16_t)(24 - q1[u]);
+      s2[u] = (int16_t)(24 - q2[u] - 28);
+    }
+    int8_t d[4];
+    for (int lane = 0; lane < 64; ++lane) {
+      const int m = lane & 15, G = lane >> 4;
+      for (int t = 0; t < 8; ++t) {
+        const int u = 16 * t + m;
+        for (int f = 0; f < 4; ++f)
+          for (int r = 0; r < 4; ++r) {
+            const int j = 4 * f + r;
+            i8x_digits(W1[n][u * lz::kAttFeat + 16 * f + 4 * G + r], q1[u], d);
+            for (int i = 0; i < 4; ++i) g1[((t * 4 + i) * 64 + lane) * 16 + j] = d[i];
+            for (int kb = 0; kb < 2; ++kb) {
+              i8x_digits(W2[n][u * kPolHidden + 64 * kb + 16 * f + 4 * G + r], q2[u], d);
+              for (int i = 0; i < 4; ++i) g2[(((t * 2 + kb) * 4 + i) * 64 + lane) * 16 + j] = d[i];
+            }
+          }
+      }
+    }
+  }
+}
+
 void pack_gauss(float* ls, int act_dim, const float* log_std) {
   // [log_std(4)][scale(4)][2 scale^2 (4)][log scale (4)]: torch Normal's
   // scale = exp(log_std), var = scale**2 (the kernel divides by 2 * var), log(scale)
@@ -599,6 +661,30 @@ static lz_status pack_attn_f32_checked(const lz_attn_policy* p, const float* ln_
 
 lz_status lz_attn_policy_pack_f32(const lz_attn_policy* p, void* host_blob, int64_t cap) {
   return pack_attn_f32_checked(p, nullptr, nullptr, host_blob, cap, lz::kPolMaxObs);
+}
+
+static lz_status pack_attn_i8x4_checked(const lz_attn_policy* p, const float* ln_w, const float* ln_b,
+                                        void* host_blob, int64_t cap, int max_in) {
+  const lz_status st = pack_attn_f32_checked(p, ln_w, ln_b, host_blob, cap, max_in);
+  if (st != LZ_OK) return st;
+  const float* w[4] = {p->pi_w1, p->vf_w1, p->pi_w2, p->vf_w2};
+  for (int j = 0; j < 4; ++j) {
+    const int cnt = lz::kPolHidden * (j < 2 ? lz::kAttFeat : lz::kPolHidden);
+    for (int k = 0; k < cnt; ++k)
+      if (!std::isfinite(w[j][k])) return pfail(LZ_ERR_INVALID, "i8x4: the nets' weights must be finite");
+  }
+  pack_attn_i8x4(static_cast<uint8_t*>(host_blob), p, ln_w, ln_b);
+  return LZ_OK;
+}
+
+lz_status lz_attn_policy_pack_i8x4(const lz_attn_policy* p, void* host_blob, int64_t cap) {
+  return pack_attn_i8x4_checked(p, nullptr, nullptr, host_blob, cap, lz::kPolMaxObs);
+}
+
+lz_status lz_attn_ln_policy_pack_i8x4(const lz_attn_ln_policy* p, void* host_blob, int64_t cap) {
+  if (!p) return pfail(LZ_ERR_INVALID, "policy is NULL");
+  if (!p->ln_w || !p->ln_b) return pfail(LZ_ERR_INVALID, "layer_norm weight / bias is NULL");
+  return pack_attn_i8x4_checked(&p->attn, p->ln_w, p->ln_b, host_blob, cap, lz::kAFMaxIn);
 }
 
 lz_status lz_attn_ln_policy_pack_f32(const lz_attn_ln_policy* p, void* host_blob, int64_t cap) {

@@ -1736,6 +1736,144 @@ __device__ __forceinline__ void attn16_net(const uint8_t* net, const f32x4* feat
   for (int j = 0; j < NH; ++j) head[j] = group_sum4(acc[j]) + bh[j];
 }
 
+// ---------------------------------------------------------------------------------------
+// attn16_net with the opt-in i8x4 wide layers (kAX* net slot, LZ_POLICY_I8X4; oracle:
+// lz_oracle.c orc_attn_i8x4).  Each float32 input / weight is V = rint(v 2^q), |V| <=
+// 2^28, as four balanced int8 digits (U = V + 0x808080: bytes 0..2 of U ^ 0x80, byte 3);
+// a 16-unit tile's dot products are the 10 digit pairs (i, j), i + j >= 3, on
+// v_mfma_i32_16x16x64_i8 into four int32 accumulators (levels 6..3) -- exact, so their
+// order is free -- then hi = L6 * 256 + L5 (< 2^24), lo = L4 * 256 + L3 and
+// y = ldexp(fmaf(float(hi), 2^16, float(lo)), shift) + bias.  The B operand of k-block
+// digit i is lane (G, env) 16 B with byte 4f + r = digit i of input 16f + 4G + r of the
+// block (the A operand's byte of the same k: the k order inside the instruction does not
+// matter for an exact sum); the 16x16 accumulator's register r of lane (G, env) is unit
+// 16t + 4G + r -- the f32 path's layout, so the inputs of layer 2 are layer 1's registers.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+// the digits of the 4 values of v at scale 2^q: d[i] byte r = digit i of v[r]
+__device__ __forceinline__ void i8x_digits4(const f32x4& v, int q, uint32_t* d) {
+  uint32_t U[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    U[r] = (uint32_t)(int32_t)__builtin_rintf(__builtin_ldexpf(v[r], q)) + 0x808080u;
+  const uint32_t t0 = __builtin_amdgcn_perm(U[1], U[0], 0x05010400u);  // U0.b0 U1.b0 U0.b1 U1.b1
+  const uint32_t t1 = __builtin_amdgcn_perm(U[1], U[0], 0x07030602u);  // U0.b2 U1.b2 U0.b3 U1.b3
+  const uint32_t t2 = __builtin_amdgcn_perm(U[3], U[2], 0x05010400u);
+  const uint32_t t3 = __builtin_amdgcn_perm(U[3], U[2], 0x07030602u);
+  d[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u) ^ 0x80808080u;
+  d[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u) ^ 0x80808080u;
+  d[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u) ^ 0x80808080u;
+  d[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+}
+
+// one 16-unit tile over KB k-blocks: w(kb, i) the weight digits, x[kb][i] the inputs'
+// -> the four level accumulators
+template <int KB, class WF>
+__device__ __forceinline__ void i8x_tile(WF w, const i32x4 (*x)[4], i32x4* L) {
+  const i32x4 z = {0, 0, 0, 0};
+  L[0] = L[1] = L[2] = L[3] = z;  // levels 6, 5, 4, 3
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const i32x4 w3 = w(kb, 3), w2 = w(kb, 2), w1 = w(kb, 1), w0 = w(kb, 0);
+    L[0] = mfma_i8(w3, x[kb][3], L[0]);
+    L[1] = mfma_i8(w3, x[kb][2], L[1]);
+    L[1] = mfma_i8(w2, x[kb][3], L[1]);
+    L[2] = mfma_i8(w3, x[kb][1], L[2]);
+    L[2] = mfma_i8(w2, x[kb][2], L[2]);
+    L[2] = mfma_i8(w1, x[kb][3], L[2]);
+    L[3] = mfma_i8(w3, x[kb][0], L[3]);
+    L[3] = mfma_i8(w2, x[kb][1], L[3]);
+    L[3] = mfma_i8(w1, x[kb][2], L[3]);
+    L[3] = mfma_i8(w0, x[kb][3], L[3]);
+  }
+}
+
+__device__ __forceinline__ float i8x_recombine(int l6, int l5, int l4, int l3, int sh) {
+  const int hi = l6 * 256 + l5, lo = l4 * 256 + l3;
+  return __builtin_ldexpf(fmaf((float)hi, 65536.0f, (float)lo), sh);
+}
+
+template <int NH>
+__device__ __forceinline__ void attn16_net_i8(const uint8_t* net, const f32x4* feat, int lane,
+                                              float* head, const float* ttab) {
+  asm volatile("" ::: "memory");
+  const int G = lane >> 4;
+  // the env's feature scale: its largest feature (ReLU outputs >= 0; a NaN propagates)
+  float m = feat[0][0];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) m = __builtin_elementwise_maximum(m, feat[f][r]);
+  m = __builtin_elementwise_maximum(m, __shfl_xor(m, 16, 64));
+  m = __builtin_elementwise_maximum(m, __shfl_xor(m, 32, 64));
+  const bool bad = !(m <= 3.40282347e38f);
+  const int qa = 28 - __builtin_amdgcn_frexp_expf(m);
+  i32x4 xf[1][4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    uint32_t d[4];
+    i8x_digits4(feat[f], qa, d);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xf[0][i][f] = (int)d[i];
+  }
+  const i32x4* w1 = reinterpret_cast<const i32x4*>(net + kAXN1) + lane;
+  const f32x4* b1 = reinterpret_cast<const f32x4*>(net + kAFNB1) + G;
+  const int16_t* s1 = reinterpret_cast<const int16_t*>(net + kAXSh1) + 4 * G;
+  i32x4 xa[2][4];  // layer 2's inputs: k-block kb = tiles 4kb .. 4kb + 3
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    asm volatile("" ::: "memory");
+    i32x4 L[4];
+    i8x_tile<1>([&](int, int i) { return w1[(t * 4 + i) * 64]; }, xf, L);
+    const f32x4 bb = b1[4 * t];
+    f32x4 a;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float y = i8x_recombine(L[0][r], L[1][r], L[2][r], L[3][r], s1[16 * t + r] - qa) + bb[r];
+      a[r] = tanh_tab(bad ? __builtin_nanf("") : y, ttab);
+    }
+    uint32_t d[4];
+    i8x_digits4(a, 28, d);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xa[t >> 2][i][t & 3] = (int)d[i];
+  }
+  const i32x4* w2 = reinterpret_cast<const i32x4*>(net + kAXN2) + lane;
+  const f32x4* b2 = reinterpret_cast<const f32x4*>(net + kAFNB2) + G;
+  const int16_t* s2 = reinterpret_cast<const int16_t*>(net + kAXSh2) + 4 * G;
+  const f32x4* wh = reinterpret_cast<const f32x4*>(net + kAFNH) + G;
+  const float* bh = reinterpret_cast<const float*>(net + kAFNHB);
+  float acc[NH];
+#pragma unroll
+  for (int j = 0; j < NH; ++j) acc[j] = 0.0f;  // first step fmaf(w, v, +0)
+#pragma unroll 1
+  for (int t = 0; t < 8; ++t) {
+    asm volatile("" ::: "memory");
+    i32x4 L[4];
+    i8x_tile<2>([&](int kb, int i) { return w2[((t * 2 + kb) * 4 + i) * 64]; }, xa, L);
+    const f32x4 bb = b2[4 * t];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float y = i8x_recombine(L[0][r], L[1][r], L[2][r], L[3][r], s2[16 * t + r]) + bb[r];
+      const float v = tanh_tab(bad ? __builtin_nanf("") : y, ttab);
+#pragma unroll
+      for (int j = 0; j < NH; ++j) acc[j] = fmaf(wh[j * 32 + 4 * t][r], v, acc[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NH; ++j) head[j] = group_sum4(acc[j]) + bh[j];
+}
+
+template <int NH, bool kI8>
+__device__ __forceinline__ void attn16_net_sel(const uint8_t* net, const f32x4* feat, int lane,
+                                               float* head, const float* ttab) {
+  if constexpr (kI8) attn16_net_i8<NH>(net, feat, lane, head, ttab);
+  else attn16_net<NH>(net, feat, lane, head, ttab);
+}
+
 typedef __attribute__((address_space(3))) void* las_p;
 // 1 KiB per wave instruction from global (L2-resident weights: default cache policy)
 // into LDS at M0 + 16 lane; issued from inline asm, so hipcc neither sees nor waits for
@@ -1749,7 +1887,7 @@ __device__ __forceinline__ void dma16_keep(const void* g, uint32_t m0) {
                : "memory");
 }
 
-template <class Sys, bool kLn, int S, int W>
+template <class Sys, bool kLn, int S, int W, bool kI8 = false>
 __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PArgs p) {
   constexpr int E = 16;
   constexpr int O = Sys::O, A = Sys::A;
@@ -1927,7 +2065,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
       for (int j = 0; j < A; ++j) act_c[j] = 0.0f;
       if (active) {
         float mean[A];
-        attn16_net<A>(s_net, F, lane, mean, ttab);
+        attn16_net_sel<A, kI8>(s_net, F, lane, mean, ttab);
         if (valid) {
           float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
           if (!det) {
@@ -2007,11 +2145,11 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
       // [4] V(this step's input); the previous step's truncation bootstrap
       if (active) {
         float v[1];
-        attn16_net<1>(s_net, F, lane, v, ttab);
+        attn16_net_sel<1, kI8>(s_net, F, lane, v, ttab);
         if (own) p.val[off] = v[0];
         if (any_pb) {
           float vt[1];
-          attn16_net<1>(s_net, Ft, lane, vt, ttab);
+          attn16_net_sel<1, kI8>(s_net, Ft, lane, vt, ttab);
           if (own && pb) rew_buf[off - a.n] = prew + gamma * vt[0];
         }
       }
@@ -2033,7 +2171,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
       }
       attn16_extract<KS, kLn>(s_ext, xs, lane, F);
       float vl[1];
-      attn16_net<1>(s_net, F, lane, vl, ttab);
+      attn16_net_sel<1, kI8>(s_net, F, lane, vl, ttab);
       if (any_pb) {
         float xt[KS];
         if constexpr (kLn) {
@@ -2045,7 +2183,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
         }
         attn16_extract<KS, kLn>(s_ext, xt, lane, F);
         float vt[1];
-        attn16_net<1>(s_net, F, lane, vt, ttab);
+        attn16_net_sel<1, kI8>(s_net, F, lane, vt, ttab);
         if (own && pb) rew_buf[(int64_t)(a.K - 1) * a.n + i] = prew + gamma * vt[0];
       }
       if (own) {
@@ -2379,8 +2517,12 @@ template <class Sys>
 static int launch_pol_attn_f32(int ln, int n_stack, const KArgs& a, const PArgs& p, const PolShape& sh,
                                hipStream_t s) {
   const dim3 grid((unsigned)sh.grid), block(sh.waves * 64);
+  const bool i8 = (p.pflags & LZ_POLICY_I8X4) != 0;
 #define LZ_ATTN_F32(LN, S_)                                                                        \
-  if (sh.waves == 8) hipLaunchKernelGGL((k_rollout_policy_attn_f32<Sys, LN, S_, 8>), grid, block, 0, s, a, p); \
+  if (i8) {                                                                                        \
+    if (sh.waves == 8) hipLaunchKernelGGL((k_rollout_policy_attn_f32<Sys, LN, S_, 8, true>), grid, block, 0, s, a, p); \
+    else hipLaunchKernelGGL((k_rollout_policy_attn_f32<Sys, LN, S_, 4, true>), grid, block, 0, s, a, p); \
+  } else if (sh.waves == 8) hipLaunchKernelGGL((k_rollout_policy_attn_f32<Sys, LN, S_, 8>), grid, block, 0, s, a, p); \
   else hipLaunchKernelGGL((k_rollout_policy_attn_f32<Sys, LN, S_, 4>), grid, block, 0, s, a, p);
   if (!ln) { LZ_ATTN_F32(false, 1) }
   else if (n_stack == 4) { LZ_ATTN_F32(true, 4) }

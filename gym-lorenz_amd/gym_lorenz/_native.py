@@ -78,7 +78,7 @@ class LzInfo(ctypes.Structure):
     ]
 
 
-POLICY_DETERMINISTIC, POLICY_BOOTSTRAP = 1, 2
+POLICY_DETERMINISTIC, POLICY_BOOTSTRAP, POLICY_I8X4 = 1, 2, 4
 POLICY_HIDDEN = 128
 
 
@@ -220,6 +220,8 @@ _SIGS = {
     "lz_attn_policy_f32_blob_bytes": (ctypes.c_int64, []),
     "lz_attn_policy_pack_f32": (ctypes.c_int, [ctypes.POINTER(LzAttnPolicy), VP, ctypes.c_int64]),
     "lz_attn_ln_policy_pack_f32": (ctypes.c_int, [ctypes.POINTER(LzAttnLnPolicy), VP, ctypes.c_int64]),
+    "lz_attn_policy_pack_i8x4": (ctypes.c_int, [ctypes.POINTER(LzAttnPolicy), VP, ctypes.c_int64]),
+    "lz_attn_ln_policy_pack_i8x4": (ctypes.c_int, [ctypes.POINTER(LzAttnLnPolicy), VP, ctypes.c_int64]),
     "lz_rollout_policy_attn_f32": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
     "lz_rollout_policy_attn_stack_f32": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs),
                                                         ctypes.c_int32, VP, VP]),

@@ -435,6 +435,25 @@ def pack_attn_ln_policy_f32(state_dict, in_dim, act_dim, features_dim=64):
     return blob
 
 
+def pack_attn_policy_i8x4(state_dict, obs_dim, act_dim, features_dim=64):
+    """lz_attn_policy_pack_i8x4: code/train.py's attention actor-critic with the nets' two
+    wide layers as exact 4-digit int8 fixed-point products (precision="i8x4"; the float32
+    blob's size and layout otherwise) -> uint8 numpy blob (host; needs no GPU)."""
+    p, _keep = _attn_struct(state_dict, obs_dim, act_dim, features_dim, False)
+    blob = np.zeros(int(nat.lib.lz_attn_policy_f32_blob_bytes()), np.uint8)
+    nat.check(nat.lib.lz_attn_policy_pack_i8x4(ctypes.byref(p), blob.ctypes.data, blob.size))
+    return blob
+
+
+def pack_attn_ln_policy_i8x4(state_dict, in_dim, act_dim, features_dim=64):
+    """lz_attn_ln_policy_pack_i8x4: code/lorenz_filter/train.py's residual + LayerNorm
+    policy, precision="i8x4" (in_dim = the stacked observation width)."""
+    p, _keep = _attn_struct(state_dict, in_dim, act_dim, features_dim, True)
+    blob = np.zeros(int(nat.lib.lz_attn_policy_f32_blob_bytes()), np.uint8)
+    nat.check(nat.lib.lz_attn_ln_policy_pack_i8x4(ctypes.byref(p), blob.ctypes.data, blob.size))
+    return blob
+
+
 def pack_attn_policy(state_dict, obs_dim, act_dim, features_dim=64):
     """lz_attn_policy_pack: SB3 state_dict of code/train.py's attention actor-critic ->
     uint8 numpy blob (host; needs no GPU)."""
@@ -532,8 +551,12 @@ class FusedRolloutCollector:
     precision:     policy arithmetic: "fp32" (default; SB3's float32 forward --
                    lz_rollout_policy_f32, and for the attention actor-critics of
                    code/train.py / code/lorenz_filter/train.py lz_rollout_policy_attn_f32 /
-                   _attn_stack_f32) or "bf16" (bf16 MFMA operands, fp32 accumulation:
-                   lz_rollout_policy / _attn / _attn_stack, ~2.5-5x faster, ~1e-2 off SB3).
+                   _attn_stack_f32), "i8x4" (attention actor-critics only: the same
+                   kernels with the pi / vf nets' wide layers as exact 4-digit int8
+                   fixed-point products on the int8 MFMA -- float32-level accuracy,
+                   bit-exact vs orc_attn_i8x4, not bit-equal to "fp32") or "bf16" (bf16 MFMA
+                   operands, fp32 accumulation: lz_rollout_policy / _attn / _attn_stack,
+                   ~2.5-5x faster, ~1e-2 off SB3).
     """
 
     def __init__(self, backend, state_dict=None, gamma=0.99, gae_lambda=0.95, obs_rms=None,
@@ -551,13 +574,14 @@ class FusedRolloutCollector:
         self.capture_terminal = int(capture_terminal)
         self.group = group
         self.act_low, self.act_high = action_bounds(backend.system_name)
-        if precision not in (None, "fp32", "bf16"):
-            raise ValueError("precision must be 'fp32' or 'bf16'")
+        if precision not in (None, "fp32", "bf16", "i8x4"):
+            raise ValueError("precision must be 'fp32', 'i8x4' or 'bf16'")
         self.precision = precision
         if vecnorm_update not in (None, "step", "rollout"):
             raise ValueError("vecnorm_update must be 'step' or 'rollout'")
         self.vecnorm_update = vecnorm_update
         self.f32 = False
+        self.i8x4 = False
         self.blob = None
         self.attention = False
         self.attention_ln = False
@@ -584,13 +608,19 @@ class FusedRolloutCollector:
             raise ValueError("frame_stack > 1 runs code/lorenz_filter/train.py's policy "
                              "(the residual + LayerNorm attention extractor)")
         self.f32 = self.precision != "bf16"
+        self.i8x4 = self.precision == "i8x4"
+        if self.i8x4 and not (self.attention or self.attention_ln):
+            raise ValueError("precision='i8x4' runs the attention actor-critics (code/train.py, "
+                             "code/lorenz_filter/train.py)")
         if self.attention_ln:
             if self.obs_rms is not None:
                 raise ValueError("the LayerNorm attention rollout takes raw observations")
-            blob = (pack_attn_ln_policy_f32 if self.f32 else pack_attn_ln_policy)(
+            blob = (pack_attn_ln_policy_i8x4 if self.i8x4 else
+                    pack_attn_ln_policy_f32 if self.f32 else pack_attn_ln_policy)(
                 state_dict, self.frame_stack * self.O, self.A)
         elif self.attention:
-            blob = (pack_attn_policy_f32 if self.f32 else pack_attn_policy)(state_dict, self.O, self.A)
+            blob = (pack_attn_policy_i8x4 if self.i8x4 else
+                    pack_attn_policy_f32 if self.f32 else pack_attn_policy)(state_dict, self.O, self.A)
         else:
             blob = (pack_policy_f32 if self.f32 else pack_policy)(state_dict, self.O, self.A)
         if self.vecnorm_update == "step" and (not self.f32 or self.attention or self.attention_ln):
@@ -658,7 +688,8 @@ class FusedRolloutCollector:
         r = nat.LzPolicyRolloutArgs()
         r.K = int(K)
         r.flags = ((nat.POLICY_DETERMINISTIC if self.deterministic else 0)
-                   | (nat.POLICY_BOOTSTRAP if self.bootstrap else 0))
+                   | (nat.POLICY_BOOTSTRAP if self.bootstrap else 0)
+                   | (nat.POLICY_I8X4 if self.i8x4 else 0))
         r.blob, r.obs_in, r.obs_last = _p(self.blob), _p(self.last_obs), _p(obs_last)
         r.obs_norm = _p(self.obs_rms.state) if self.obs_rms is not None and not per_step else None
         r.norm_eps, r.clip_obs, r.gamma = self.norm_eps, self.clip_obs, self.gamma

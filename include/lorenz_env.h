@@ -311,6 +311,8 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
 #define LZ_POLICY_HIDDEN 128
 #define LZ_POLICY_DETERMINISTIC 1u /* action = mean (SB3 predict(deterministic=True)) */
 #define LZ_POLICY_BOOTSTRAP 2u     /* reward += gamma * V(terminal obs) when truncated */
+#define LZ_POLICY_I8X4 4u          /* the blob is an lz_attn*_policy_pack_i8x4 blob (attention
+                                      f32 rollouts only; see there) */
 
 /* Float32 weights in torch nn.Linear layout ([out, in], row-major), host memory.
  * Names are the SB3 ActorCriticPolicy state_dict keys. */
@@ -504,6 +506,20 @@ lz_status lz_attn_ln_policy_pack_f32(const lz_attn_ln_policy* p, void* host_blob
  * pi / vf nets into it by LDS-DMA twice per step; a truncated step's bootstrap value is
  * added to its reward by the next step's launch segment (same result). */
 lz_status lz_rollout_policy_attn_f32(lz_handle* h, const lz_policy_rollout_args* r);
+/* Opt-in precision "i8x4" of the same actor-critics (same blob size, same rollout entry
+ * points with LZ_POLICY_I8X4 in lz_policy_rollout_args.flags): the two wide layers of
+ * each pi / vf net (64 -> 128, 128 -> 128: three quarters of the policy's multiplies) run
+ * as EXACT fixed-point dot products on the int8 MFMA (v_mfma_i32_16x16x64_i8): every
+ * float32 input and weight is the int32 V = rint(v 2^q), |V| <= 2^28 (q per weight row
+ * from its largest |w|; per env from its largest feature; 28 for tanh outputs), split into
+ * four balanced int8 digits; the 10 digit products of weight >= 2^-24 of the leading one
+ * are summed exactly in int32 (no order, no rounding), then recombined and rounded to
+ * float32 once (+ the bias).  Error vs the exact dot product: that of float32's own fmaf
+ * chain (tests/test_i8x4_host.py); bit-exact vs the C oracle (orc_attn_i8x4).  A NaN / inf
+ * feature makes all of that env's outputs NaN.  The packers refuse non-finite net weights.
+ * The extractor, softmax, heads and everything else are the float32 path's. */
+lz_status lz_attn_policy_pack_i8x4(const lz_attn_policy* p, void* host_blob, int64_t cap);
+lz_status lz_attn_ln_policy_pack_i8x4(const lz_attn_ln_policy* p, void* host_blob, int64_t cap);
 lz_status lz_rollout_policy_attn_stack_f32(lz_handle* h, const lz_policy_rollout_args* r,
                                            int32_t n_stack, const float* stack_in,
                                            float* stack_out);

@@ -991,3 +991,133 @@ void orc_attn_f32(int64_t n, int in_dim, int A, const float* x, const float* fc1
     attn_net_one(1, feat, vf_w1, vf_b1, vf_w2, vf_b2, val_w, val_b, value + i);
   }
 }
+
+/* ---- f3 opt-in precision "i8x4" (lz_attn_policy_pack_i8x4 / lz_attn_ln_policy_pack_i8x4,
+ * gym-lorenz_amd/csrc/lz_policy.hip attn16_net<kI8>): the two wide layers of each pi / vf
+ * net (64 -> 128 and 128 -> 128) as EXACT fixed-point dot products on the int8 MFMA
+ * (v_mfma_i32_16x16x64_i8, 16 x the f32 MFMA's multiply rate), everything else as in
+ * orc_attn_f32.  Restated here, operation for operation:
+ *   fixed point:  V = (int32)rintf(ldexpf(v, q)), |V| <= 2^28 -- q = 28 for the layer-2
+ *                 inputs (tanh outputs, |v| <= 1); q = 28 - e, m = fract * 2^e (frexpf) of
+ *                 the env's largest feature for the layer-1 inputs (ReLU outputs >= 0); per
+ *                 weight row q_r = 28 - e_r of the row's largest |w|;
+ *   digits:       U = V + 0x808080, d_k = (int8)(byte k of U ^ 0x80) for k < 3 and d_3 =
+ *                 (int8)(U >> 24): V = sum_k d_k 2^(8k), |d_3| <= 16 (balanced digits);
+ *   products:     the 10 digit pairs (i, j) with i + j >= 3 (weight digit i, input digit
+ *                 j), summed per level s = i + j in int32 (exact: no order, no rounding):
+ *                 L6 .. L3; the dropped levels (i + j <= 2) weigh < 2^-24 of the leading;
+ *   recombine:    hi = L6 * 256 + L5 (< 2^24: exact in float), lo = L4 * 256 + L3 (int32),
+ *                 y = ldexpf(fmaf((float)hi, 65536, (float)lo), 24 - q_r - q) + bias;
+ *   non-finite:   a NaN / inf feature makes every output of the env NaN (the weights are
+ *                 finite: the packer refuses others).
+ * Precision: the products are exact and one rounding (plus lo's) ends each sum -- closer
+ * to the exact dot product than float32's k-ordered fmaf chain. */
+static inline int32_t i8x_fixed(float v, int q) { return (int32_t)rintf(ldexpf(v, q)); }
+
+static inline void i8x_digits(int32_t V, int8_t d[4]) {
+  const int32_t U = (int32_t)((uint32_t)V + 0x808080u);
+  d[0] = (int8_t)((U & 0xff) ^ 0x80);
+  d[1] = (int8_t)(((U >> 8) & 0xff) ^ 0x80);
+  d[2] = (int8_t)(((U >> 16) & 0xff) ^ 0x80);
+  d[3] = (int8_t)(U >> 24);
+}
+
+/* q of a weight row / of an input vector with largest magnitude m: 28 - e, m = f 2^e */
+static inline int i8x_q(float m) {
+  int e = 0;
+  (void)frexpf(m, &e);
+  return 28 - e;
+}
+
+int32_t orc_i8x_row_q(const float* w, int32_t K) {
+  float m = 0.0f;
+  for (int k = 0; k < K; ++k) m = fmaxf(m, fabsf(w[k]));
+  return i8x_q(m);
+}
+
+/* digits of n values at one q: d [n][4] (for tests) */
+void orc_i8x_digits(int64_t n, const float* v, int32_t q, int8_t* d) {
+  for (int64_t i = 0; i < n; ++i) i8x_digits(i8x_fixed(v[i], q), d + 4 * i);
+}
+
+/* sum_k W_k V_k over K digit rows, recombined and scaled by 2^sh (no bias) */
+float orc_i8x_dot(int32_t K, const int8_t* wd, const int8_t* vd, int32_t sh) {
+  int32_t L[7] = {0, 0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < K; ++k)
+    for (int i = 0; i < 4; ++i)
+      for (int j = 3 - i; j < 4; ++j) L[i + j] += (int32_t)wd[4 * k + i] * (int32_t)vd[4 * k + j];
+  const int32_t hi = L[6] * 256 + L[5];
+  const int32_t lo = L[4] * 256 + L[3];
+  return ldexpf(fmaf((float)hi, 65536.0f, (float)lo), sh);
+}
+
+/* a wide layer's weight digits and row q's, made once per call */
+typedef struct {
+  int8_t d1[128 * 64 * 4], d2[128 * 128 * 4];
+  int32_t q1[128], q2[128];
+} i8x_net;
+
+static void i8x_prep(i8x_net* t, const float* w1, const float* w2) {
+  for (int u = 0; u < 128; ++u) {
+    t->q1[u] = orc_i8x_row_q(w1 + u * 64, 64);
+    for (int k = 0; k < 64; ++k) i8x_digits(i8x_fixed(w1[u * 64 + k], t->q1[u]), t->d1 + 4 * (u * 64 + k));
+    t->q2[u] = orc_i8x_row_q(w2 + u * 128, 128);
+    for (int k = 0; k < 128; ++k)
+      i8x_digits(i8x_fixed(w2[u * 128 + k], t->q2[u]), t->d2 + 4 * (u * 128 + k));
+  }
+}
+
+static void attn_net_one_i8x(int R, const float* feat, const i8x_net* t, const float* b1, const float* b2,
+                             const float* w3, const float* b3, float* out) {
+  float m = 0.0f;
+  for (int f = 0; f < 64; ++f) m = (m != m || feat[f] != feat[f]) ? NAN : fmaxf(m, feat[f]);
+  if (!(m <= 3.40282347e38f)) {
+    for (int r = 0; r < R; ++r) out[r] = NAN;
+    return;
+  }
+  const int qa = i8x_q(m);
+  int8_t fd[64 * 4], ad[128 * 4];
+  for (int f = 0; f < 64; ++f) i8x_digits(i8x_fixed(feat[f], qa), fd + 4 * f);
+  float a2[128];
+  for (int u = 0; u < 128; ++u) {
+    const float y = orc_i8x_dot(64, t->d1 + 4 * 64 * u, fd, 24 - t->q1[u] - qa) + b1[u];
+    i8x_digits(i8x_fixed(orc_tanh_tab(y), 28), ad + 4 * u);
+  }
+  for (int u = 0; u < 128; ++u)
+    a2[u] = orc_tanh_tab(orc_i8x_dot(128, t->d2 + 4 * 128 * u, ad, 24 - t->q2[u] - 28) + b2[u]);
+  for (int r = 0; r < R; ++r) {
+    float part[4];
+    for (int G = 0; G < 4; ++G) {
+      float acc = 0.0f;
+      for (int tt = 0; tt < 8; ++tt)
+        for (int c = 0; c < 4; ++c) {
+          const int k = 16 * tt + 4 * G + c;
+          acc = fmaf(w3[r * 128 + k], a2[k], acc);
+        }
+      part[G] = acc;
+    }
+    out[r] = ((part[0] + part[1]) + (part[2] + part[3])) + b3[r];
+  }
+}
+
+/* orc_attn_f32 with the i8x4 nets (the extractor is orc_attn_f32's) */
+void orc_attn_i8x4(int64_t n, int in_dim, int A, const float* x, const float* fc1_w, const float* fc1_b,
+                   const float* in_w, const float* in_b, const float* out_w, const float* out_b,
+                   const float* post_w, const float* post_b, const float* ln_w, const float* ln_b,
+                   const float* pi_w1, const float* pi_b1, const float* pi_w2, const float* pi_b2,
+                   const float* vf_w1, const float* vf_b1, const float* vf_w2, const float* vf_b2,
+                   const float* act_w, const float* act_b, const float* val_w, const float* val_b,
+                   float* mean, float* value, float* feat_out) {
+  const orc_attn_ext e = {fc1_w, fc1_b, in_w, in_b, out_w, out_b, post_w, post_b, ln_w, ln_b};
+  static i8x_net pi, vf;  /* (not reentrant: test infrastructure) */
+  i8x_prep(&pi, pi_w1, pi_w2);
+  i8x_prep(&vf, vf_w1, vf_w2);
+  for (int64_t i = 0; i < n; ++i) {
+    float feat[64];
+    attn_ext_one(&e, in_dim, x + i * in_dim, feat);
+    if (feat_out)
+      for (int f = 0; f < 64; ++f) feat_out[i * 64 + f] = feat[f];
+    attn_net_one_i8x(A, feat, &pi, pi_b1, pi_b2, act_w, act_b, mean + i * A);
+    attn_net_one_i8x(1, feat, &vf, vf_b1, vf_b2, val_w, val_b, value + i);
+  }
+}
