@@ -82,6 +82,13 @@ def parse(argv=None):
                         "with the AttentionFeaturesExtractor (no VecNormalize, as there); "
                         "attn_ln = code/lorenz_filter/train.py's residual + LayerNorm extractor "
                         "on VecFrameStack(4)")
+    p.add_argument("--ic-flush-mib", type=int, default=0,
+                   help="A/B only (profiles/r05/ic/): after every lz_step copy a buffer of this many "
+                        "MiB on the step's stream, so two uses of a state line are more than the "
+                        "256 MiB Infinity Cache apart; the step kernel's own time comes from "
+                        "rocprofv3 --kernel-trace (this line's value includes the copies)")
+    p.add_argument("--ic-flush-kind", choices=["copy", "read"], default="copy",
+                   help="--ic-flush-mib: copy the buffer (reads + writes) or only read it (a sum)")
     p.add_argument("--variant", type=int, default=0,
                    help="step-kernel tuning variant (lz_config.reserved[0]; A/B only, e.g. "
                         "16384 / 32768 / 49152 force 1 / 2 / 4 tiles per PMSM / HR workgroup)")
@@ -814,6 +821,13 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
     didx, tobs = P(env.done_idx), P(env.term_obs)
     lz_step, lz_rollout = nat.lib.lz_step, nat.lib.lz_rollout
     counter = [0]
+    flush = getattr(args, "ic_flush_mib", 0)
+    if flush:  # A/B only: evict the Infinity Cache between steps (see --ic-flush-mib)
+        fsrc = torch.ones((flush << 18,), device=device)
+        fdst = torch.empty_like(fsrc) if args.ic_flush_kind == "copy" else None
+        fsum = torch.empty((), device=device)
+        if args.ic_flush_kind == "read":  # the same bytes read as the copy moves in total
+            fsrc = torch.ones((flush << 19,), device=device)
 
     def one():
         a, o, r_, d = slots[counter[0] % R]
@@ -824,6 +838,10 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
             st = lz_step(h, a, None, o, r_, d, didx, tobs, None)
         if st:
             nat.check(st)
+        if flush and args.ic_flush_kind == "copy":
+            fdst.copy_(fsrc)
+        elif flush:
+            torch.sum(fsrc, dim=0, out=fsum)
 
     stream = torch.cuda.Stream(device)
     graph = None

@@ -251,7 +251,12 @@ constexpr int kAXN2 = kAFN2;                                // [8][2][4][64][16 
 static_assert(kAXN2 == kAXN1 + 8 * 4 * 64 * 16 && kAFNB1 == kAXN2 + 8 * 2 * 4 * 64 * 16, "i8x4 layout");
 constexpr int kAXSh1 = kAFNHB + 16;                         // int16 [128]
 constexpr int kAXSh2 = kAXSh1 + 128 * 2;                    // int16 [128]
-static_assert(kAXSh2 + 128 * 2 <= kAFNet, "i8x4 net slot");
+// post_attention_fc in i8x4 too: its float32 weights at kAFPostW become digits ([4 tiles]
+// [2 k-blocks][4 digits][64][16 B], byte 4f + r of lane (G, m) = digit of post_w[16u + m]
+// [64kb + 16f + 4G + r]); the 64 row shifts (24 - q, int16) ride in the pi slot's spare bytes
+// at kAXPostSh and are copied into LDS once per launch (the slot itself is overwritten).
+constexpr int kAXPostSh = kAXSh2 + 128 * 2;                 // int16 [64], pi slot only
+static_assert(kAXPostSh + 64 * 2 <= kAFNet, "i8x4 net slot");
 
 struct PArgs {
   const uint8_t* blob;     // device copy of the packed policy

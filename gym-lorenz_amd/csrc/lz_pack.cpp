@@ -433,6 +433,27 @@ void pack_attn_i8x4(uint8_t* b, const lz_attn_policy* p, const float* ln_w, cons
   pack_attn_f32(b, p, ln_w, ln_b);
   const float* W1[2] = {p->pi_w1, p->vf_w1};
   const float* W2[2] = {p->pi_w2, p->vf_w2};
+  {  // post_attention_fc [64, 128]: digits over kAFPostW, row shifts in the pi slot
+    int8_t* gp = reinterpret_cast<int8_t*>(b + lz::kAFPostW);
+    int16_t* sp = reinterpret_cast<int16_t*>(b + lz::kAFPi + lz::kAXPostSh);
+    int qp[lz::kAttFeat];
+    for (int f = 0; f < lz::kAttFeat; ++f) {
+      qp[f] = i8x_row_q(p->post_w + f * kPolHidden, kPolHidden);
+      sp[f] = (int16_t)(24 - qp[f]);
+    }
+    int8_t d[4];
+    for (int lane = 0; lane < 64; ++lane) {
+      const int m = lane & 15, G = lane >> 4;
+      for (int u = 0; u < 4; ++u)
+        for (int kb = 0; kb < 2; ++kb)
+          for (int f = 0; f < 4; ++f)
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * u + m;
+              i8x_digits(p->post_w[row * kPolHidden + 64 * kb + 16 * f + 4 * G + r], qp[row], d);
+              for (int i = 0; i < 4; ++i) gp[(((u * 2 + kb) * 4 + i) * 64 + lane) * 16 + 4 * f + r] = d[i];
+            }
+    }
+  }
   for (int n = 0; n < 2; ++n) {
     uint8_t* net = b + (n == 0 ? lz::kAFPi : lz::kAFVf);
     int8_t* g1 = reinterpret_cast<int8_t*>(net + lz::kAXN1);
@@ -667,11 +688,12 @@ static lz_status pack_attn_i8x4_checked(const lz_attn_policy* p, const float* ln
                                         void* host_blob, int64_t cap, int max_in) {
   const lz_status st = pack_attn_f32_checked(p, ln_w, ln_b, host_blob, cap, max_in);
   if (st != LZ_OK) return st;
-  const float* w[4] = {p->pi_w1, p->vf_w1, p->pi_w2, p->vf_w2};
-  for (int j = 0; j < 4; ++j) {
-    const int cnt = lz::kPolHidden * (j < 2 ? lz::kAttFeat : lz::kPolHidden);
+  const float* w[5] = {p->pi_w1, p->vf_w1, p->post_w, p->pi_w2, p->vf_w2};
+  for (int j = 0; j < 5; ++j) {
+    const int cnt = lz::kPolHidden * (j < 3 ? lz::kAttFeat : lz::kPolHidden);
     for (int k = 0; k < cnt; ++k)
-      if (!std::isfinite(w[j][k])) return pfail(LZ_ERR_INVALID, "i8x4: the nets' weights must be finite");
+      if (!std::isfinite(w[j][k]))
+        return pfail(LZ_ERR_INVALID, "i8x4: the nets' and post_attention_fc's weights must be finite");
   }
   pack_attn_i8x4(static_cast<uint8_t*>(host_blob), p, ln_w, ln_b);
   return LZ_OK;

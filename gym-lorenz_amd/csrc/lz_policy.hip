@@ -1555,11 +1555,60 @@ __device__ __forceinline__ float group_sum4(float v) {
   return v + __shfl_xor(v, 32, 64);
 }
 
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+// the digits of the 4 values of v at scale 2^q: d[i] byte r = digit i of v[r]
+__device__ __forceinline__ void i8x_digits4(const f32x4& v, int q, uint32_t* d) {
+  uint32_t U[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    U[r] = (uint32_t)(int32_t)__builtin_rintf(__builtin_ldexpf(v[r], q)) + 0x808080u;
+  const uint32_t t0 = __builtin_amdgcn_perm(U[1], U[0], 0x05010400u);  // U0.b0 U1.b0 U0.b1 U1.b1
+  const uint32_t t1 = __builtin_amdgcn_perm(U[1], U[0], 0x07030602u);  // U0.b2 U1.b2 U0.b3 U1.b3
+  const uint32_t t2 = __builtin_amdgcn_perm(U[3], U[2], 0x05010400u);
+  const uint32_t t3 = __builtin_amdgcn_perm(U[3], U[2], 0x07030602u);
+  d[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u) ^ 0x80808080u;
+  d[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u) ^ 0x80808080u;
+  d[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u) ^ 0x80808080u;
+  d[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+}
+
+// one 16-unit tile over KB k-blocks: w(kb, i) the weight digits, x[kb][i] the inputs'
+// -> the four level accumulators
+template <int KB, class WF>
+__device__ __forceinline__ void i8x_tile(WF w, const i32x4 (*x)[4], i32x4* L) {
+  const i32x4 z = {0, 0, 0, 0};
+  L[0] = L[1] = L[2] = L[3] = z;  // levels 6, 5, 4, 3
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const i32x4 w3 = w(kb, 3), w2 = w(kb, 2), w1 = w(kb, 1), w0 = w(kb, 0);
+    L[0] = mfma_i8(w3, x[kb][3], L[0]);
+    L[1] = mfma_i8(w3, x[kb][2], L[1]);
+    L[1] = mfma_i8(w2, x[kb][3], L[1]);
+    L[2] = mfma_i8(w3, x[kb][1], L[2]);
+    L[2] = mfma_i8(w2, x[kb][2], L[2]);
+    L[2] = mfma_i8(w1, x[kb][3], L[2]);
+    L[3] = mfma_i8(w3, x[kb][0], L[3]);
+    L[3] = mfma_i8(w2, x[kb][1], L[3]);
+    L[3] = mfma_i8(w1, x[kb][2], L[3]);
+    L[3] = mfma_i8(w0, x[kb][3], L[3]);
+  }
+}
+
+__device__ __forceinline__ float i8x_recombine(int l6, int l5, int l4, int l3, int sh) {
+  const int hi = l6 * 256 + l5, lo = l4 * 256 + l3;
+  return __builtin_ldexpf(fmaf((float)hi, 65536.0f, (float)lo), sh);
+}
+
 // the 64 features (4 tiles) of one input; xs[s] = this lane group's fc1 input of k-step
 // s (input 4s + G)
-template <int KS, bool kLn>
+template <int KS, bool kLn, bool kI8 = false>
 __device__ __forceinline__ void attn16_extract(const uint8_t* ext, const float* xs, int lane,
-                                               f32x4* feat) {
+                                               f32x4* feat, const int16_t* psh = nullptr) {
   asm volatile("" ::: "memory");
   const int G = lane >> 4;
   constexpr int KQ = (KS + 3) / 4;
@@ -1607,14 +1656,19 @@ __device__ __forceinline__ void attn16_extract(const uint8_t* ext, const float* 
   const f32x4 bet = reinterpret_cast<const f32x4*>(ext + kAFBet)[G];
   const f32x4* wp = reinterpret_cast<const f32x4*>(ext + kAFPostW) + lane;
   f32x4 post[4];
+  f32x4 uall[kI8 ? kAttTokens : 1];  // kI8: every token's attention outputs (dims 4G..4G+3)
+  if constexpr (!kI8) {  // (kI8: the bias is read after the token loop: fewer live registers)
 #pragma unroll
-  for (int u = 0; u < 4; ++u) post[u] = reinterpret_cast<const f32x4*>(ext + kAFPostB)[4 * u + G];
+    for (int u = 0; u < 4; ++u) post[u] = reinterpret_cast<const f32x4*>(ext + kAFPostB)[4 * u + G];
+  }
 #pragma unroll
   for (int i = 0; i < kAttTokens; ++i) {
     asm volatile("" ::: "memory");  // one query token's weights in flight at a time
     f32x4 pw[4];  // token i's post_fc weights, issued ahead of the attention math
+    if constexpr (!kI8) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) pw[u] = wp[(u * 8 + i) * 64];
+      for (int u = 0; u < 4; ++u) pw[u] = wp[(u * 8 + i) * 64];
+    }
     const f32x4 tk = token(i);
     f32x4 q = bq;
 #pragma unroll
@@ -1667,11 +1721,52 @@ __device__ __forceinline__ void attn16_extract(const uint8_t* ext, const float* 
 #pragma unroll
       for (int d = 0; d < 4; ++d) u[d] = y[d];
     }
+    if constexpr (kI8) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) uall[i][d] = u[d];
+    } else {
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) post[uu] = mfma16(pw[uu][s], u[s], post[uu]);
+      }
+    }
+  }
+  if constexpr (kI8) {
+    // post_attention_fc as i8x4 products (lz_oracle.c i8x_post): the env's 128 attention
+    // outputs at the scale of their largest magnitude, k-block kb = tokens 4kb .. 4kb + 3
+    // (byte 4f + r of lane group G = dim 4G + r of token 4kb + f)
+    float m = 0.0f;
+#pragma unroll
+    for (int i = 0; i < kAttTokens; ++i)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) m = __builtin_elementwise_maximum(m, fabsf(uall[i][d]));
+    m = __builtin_elementwise_maximum(m, __shfl_xor(m, 16, 64));
+    m = __builtin_elementwise_maximum(m, __shfl_xor(m, 32, 64));
+    const bool bad = !(m <= 3.40282347e38f);
+    const int qu = 28 - __builtin_amdgcn_frexp_expf(m);
+    i32x4 xu[2][4];
+#pragma unroll
+    for (int i = 0; i < kAttTokens; ++i) {
+      uint32_t d[4];
+      i8x_digits4(uall[i], qu, d);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xu[i >> 2][q][i & 3] = (int)d[q];
+    }
+    const i32x4* w8 = reinterpret_cast<const i32x4*>(ext + kAFPostW) + lane;
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu) {
+      i32x4 L[4];
+      i8x_tile<2>([&](int kb, int q) { return w8[((uu * 2 + kb) * 4 + q) * 64]; }, xu, L);
+      post[uu] = reinterpret_cast<const f32x4*>(ext + kAFPostB)[4 * uu + G];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) post[uu] = mfma16(pw[uu][s], u[s], post[uu]);
+      for (int r = 0; r < 4; ++r) {
+        const float y = i8x_recombine(L[0][r], L[1][r], L[2][r], L[3][r], psh[16 * uu + 4 * G + r] - qu) +
+                        post[uu][r];
+        feat[uu][r] = relu_f(bad ? __builtin_nanf("") : y);
+      }
     }
+    return;
   }
 #pragma unroll
   for (int uu = 0; uu < 4; ++uu) {
@@ -1748,61 +1843,16 @@ __device__ __forceinline__ void attn16_net(const uint8_t* net, const f32x4* feat
 // block (the A operand's byte of the same k: the k order inside the instruction does not
 // matter for an exact sum); the 16x16 accumulator's register r of lane (G, env) is unit
 // 16t + 4G + r -- the f32 path's layout, so the inputs of layer 2 are layer 1's registers.
-typedef int i32x4 __attribute__((ext_vector_type(4)));
+// the 64 features of a tile's envs as i8x4 digits at the env's scale (its largest
+// feature; ReLU outputs >= 0, a NaN propagates): computed once per extraction and shared
+// by the pi and vf nets.  x[i] byte 4f + r = digit i of feature 16f + 4G + r.
+struct I8Feat {
+  i32x4 x[4];
+  int qa;
+  bool bad;  // a NaN / inf feature: every output of the env is NaN
+};
 
-__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
-  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
-}
-
-// the digits of the 4 values of v at scale 2^q: d[i] byte r = digit i of v[r]
-__device__ __forceinline__ void i8x_digits4(const f32x4& v, int q, uint32_t* d) {
-  uint32_t U[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    U[r] = (uint32_t)(int32_t)__builtin_rintf(__builtin_ldexpf(v[r], q)) + 0x808080u;
-  const uint32_t t0 = __builtin_amdgcn_perm(U[1], U[0], 0x05010400u);  // U0.b0 U1.b0 U0.b1 U1.b1
-  const uint32_t t1 = __builtin_amdgcn_perm(U[1], U[0], 0x07030602u);  // U0.b2 U1.b2 U0.b3 U1.b3
-  const uint32_t t2 = __builtin_amdgcn_perm(U[3], U[2], 0x05010400u);
-  const uint32_t t3 = __builtin_amdgcn_perm(U[3], U[2], 0x07030602u);
-  d[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u) ^ 0x80808080u;
-  d[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u) ^ 0x80808080u;
-  d[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u) ^ 0x80808080u;
-  d[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
-}
-
-// one 16-unit tile over KB k-blocks: w(kb, i) the weight digits, x[kb][i] the inputs'
-// -> the four level accumulators
-template <int KB, class WF>
-__device__ __forceinline__ void i8x_tile(WF w, const i32x4 (*x)[4], i32x4* L) {
-  const i32x4 z = {0, 0, 0, 0};
-  L[0] = L[1] = L[2] = L[3] = z;  // levels 6, 5, 4, 3
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    const i32x4 w3 = w(kb, 3), w2 = w(kb, 2), w1 = w(kb, 1), w0 = w(kb, 0);
-    L[0] = mfma_i8(w3, x[kb][3], L[0]);
-    L[1] = mfma_i8(w3, x[kb][2], L[1]);
-    L[1] = mfma_i8(w2, x[kb][3], L[1]);
-    L[2] = mfma_i8(w3, x[kb][1], L[2]);
-    L[2] = mfma_i8(w2, x[kb][2], L[2]);
-    L[2] = mfma_i8(w1, x[kb][3], L[2]);
-    L[3] = mfma_i8(w3, x[kb][0], L[3]);
-    L[3] = mfma_i8(w2, x[kb][1], L[3]);
-    L[3] = mfma_i8(w1, x[kb][2], L[3]);
-    L[3] = mfma_i8(w0, x[kb][3], L[3]);
-  }
-}
-
-__device__ __forceinline__ float i8x_recombine(int l6, int l5, int l4, int l3, int sh) {
-  const int hi = l6 * 256 + l5, lo = l4 * 256 + l3;
-  return __builtin_ldexpf(fmaf((float)hi, 65536.0f, (float)lo), sh);
-}
-
-template <int NH>
-__device__ __forceinline__ void attn16_net_i8(const uint8_t* net, const f32x4* feat, int lane,
-                                              float* head, const float* ttab) {
-  asm volatile("" ::: "memory");
-  const int G = lane >> 4;
-  // the env's feature scale: its largest feature (ReLU outputs >= 0; a NaN propagates)
+__device__ __forceinline__ I8Feat i8x_feat(const f32x4* feat) {
   float m = feat[0][0];
 #pragma unroll
   for (int f = 0; f < 4; ++f)
@@ -1810,16 +1860,27 @@ __device__ __forceinline__ void attn16_net_i8(const uint8_t* net, const f32x4* f
     for (int r = 0; r < 4; ++r) m = __builtin_elementwise_maximum(m, feat[f][r]);
   m = __builtin_elementwise_maximum(m, __shfl_xor(m, 16, 64));
   m = __builtin_elementwise_maximum(m, __shfl_xor(m, 32, 64));
-  const bool bad = !(m <= 3.40282347e38f);
-  const int qa = 28 - __builtin_amdgcn_frexp_expf(m);
-  i32x4 xf[1][4];
+  I8Feat fi;
+  fi.bad = !(m <= 3.40282347e38f);
+  fi.qa = 28 - __builtin_amdgcn_frexp_expf(m);
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
     uint32_t d[4];
-    i8x_digits4(feat[f], qa, d);
+    i8x_digits4(feat[f], fi.qa, d);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xf[0][i][f] = (int)d[i];
+    for (int i = 0; i < 4; ++i) fi.x[i][f] = (int)d[i];
   }
+  return fi;
+}
+
+template <int NH>
+__device__ __forceinline__ void attn16_net_i8(const uint8_t* net, const I8Feat& fi, int lane,
+                                              float* head, const float* ttab) {
+  asm volatile("" ::: "memory");
+  const int G = lane >> 4;
+  const bool bad = fi.bad;
+  const int qa = fi.qa;
+  const i32x4(*xf)[4] = reinterpret_cast<const i32x4(*)[4]>(fi.x);
   const i32x4* w1 = reinterpret_cast<const i32x4*>(net + kAXN1) + lane;
   const f32x4* b1 = reinterpret_cast<const f32x4*>(net + kAFNB1) + G;
   const int16_t* s1 = reinterpret_cast<const int16_t*>(net + kAXSh1) + 4 * G;
@@ -1849,18 +1910,33 @@ __device__ __forceinline__ void attn16_net_i8(const uint8_t* net, const f32x4* f
   float acc[NH];
 #pragma unroll
   for (int j = 0; j < NH; ++j) acc[j] = 0.0f;  // first step fmaf(w, v, +0)
+  // software-pipelined: tile t + 1's MFMAs are issued before tile t's recombination /
+  // tanh / head work, so the matrix pipe runs under that VALU work
+  auto tile2 = [&](int t, i32x4* L) __attribute__((always_inline)) {
+    i8x_tile<2>([&](int kb, int i) { return w2[((t * 2 + kb) * 4 + i) * 64]; }, xa, L);
+  };
+#ifndef LZ_I8_PIPE
+#define LZ_I8_PIPE 1
+#endif
+  i32x4 Lc[4];
+  if (LZ_I8_PIPE) tile2(0, Lc);
 #pragma unroll 1
   for (int t = 0; t < 8; ++t) {
     asm volatile("" ::: "memory");
-    i32x4 L[4];
-    i8x_tile<2>([&](int kb, int i) { return w2[((t * 2 + kb) * 4 + i) * 64]; }, xa, L);
+    i32x4 Ln[4];
+    if (!LZ_I8_PIPE) tile2(t, Lc);
+    if (LZ_I8_PIPE && t + 1 < 8) tile2(t + 1, Ln);
     const f32x4 bb = b2[4 * t];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float y = i8x_recombine(L[0][r], L[1][r], L[2][r], L[3][r], s2[16 * t + r]) + bb[r];
+      const float y = i8x_recombine(Lc[0][r], Lc[1][r], Lc[2][r], Lc[3][r], s2[16 * t + r]) + bb[r];
       const float v = tanh_tab(bad ? __builtin_nanf("") : y, ttab);
 #pragma unroll
       for (int j = 0; j < NH; ++j) acc[j] = fmaf(wh[j * 32 + 4 * t][r], v, acc[j]);
+    }
+    if (LZ_I8_PIPE) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Lc[q] = Ln[q];
     }
   }
 #pragma unroll
@@ -1868,9 +1944,9 @@ __device__ __forceinline__ void attn16_net_i8(const uint8_t* net, const f32x4* f
 }
 
 template <int NH, bool kI8>
-__device__ __forceinline__ void attn16_net_sel(const uint8_t* net, const f32x4* feat, int lane,
-                                               float* head, const float* ttab) {
-  if constexpr (kI8) attn16_net_i8<NH>(net, feat, lane, head, ttab);
+__device__ __forceinline__ void attn16_net_sel(const uint8_t* net, const f32x4* feat, const I8Feat& fi,
+                                               int lane, float* head, const float* ttab) {
+  if constexpr (kI8) attn16_net_i8<NH>(net, fi, lane, head, ttab);
   else attn16_net<NH>(net, feat, lane, head, ttab);
 }
 
@@ -1897,6 +1973,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
   constexpr int SZ = SO - O;  // the stack's older frames
   __shared__ __attribute__((aligned(16))) uint8_t s_lds[kAFLdsBytes];
   __shared__ double s_norm[2 * kPolMaxObs];
+  __shared__ __attribute__((aligned(16))) int16_t s_psh[kI8 ? kAttFeat : 8];  // kI8: post_fc row shifts
   const int tid = (int)threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, G = lane >> 4, col = lane & 15;
   {
@@ -1906,6 +1983,10 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
     const f4v* sc = reinterpret_cast<const f4v*>(p.blob + kAFLogStd);
     f4v* dc = reinterpret_cast<f4v*>(s_lds + kAFExt);
     for (int v = tid; v < kAFConst / 16; v += W * 64) dc[v] = sc[v];
+    if constexpr (kI8) {
+      if (tid < kAttFeat * 2 / 16)
+        reinterpret_cast<f4v*>(s_psh)[tid] = reinterpret_cast<const f4v*>(p.blob + kAFPi + kAXPostSh)[tid];
+    }
   }
   if (tid < O) {
     s_norm[tid] = p.norm ? p.norm[tid] : 0.0;
@@ -2037,6 +2118,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
       const bool pb = pend;
       const bool any_pb = __ballot(pb) != 0ull;
       f32x4 F[4], Ft[4];
+      I8Feat FI, FIt;  // kI8: F / Ft as digits (unused otherwise)
       if (active) {
         float xs[KS];
         if constexpr (kLn) {
@@ -2055,7 +2137,8 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
           }
           inputs(x, xs);
         }
-        attn16_extract<KS, kLn>(s_ext, xs, lane, F);
+        attn16_extract<KS, kLn, kI8>(s_ext, xs, lane, F, s_psh);
+        if constexpr (kI8) FI = i8x_feat(F);
       }
       __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA pieces have landed
       __syncthreads();
@@ -2065,7 +2148,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
       for (int j = 0; j < A; ++j) act_c[j] = 0.0f;
       if (active) {
         float mean[A];
-        attn16_net_sel<A, kI8>(s_net, F, lane, mean, ttab);
+        attn16_net_sel<A, kI8>(s_net, F, FI, lane, mean, ttab);
         if (valid) {
           float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
           if (!det) {
@@ -2101,7 +2184,8 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
             normalize<O>(pt, x, norm, mu, sd, p.clip);
             inputs(x, xt);
           }
-          attn16_extract<KS, kLn>(s_ext, xt, lane, Ft);
+          attn16_extract<KS, kLn, kI8>(s_ext, xt, lane, Ft, s_psh);
+          if constexpr (kI8) FIt = i8x_feat(Ft);
         }
         if constexpr (kLn) {  // the deferred zeroing, now that the bootstrap has its input
 #pragma unroll
@@ -2145,11 +2229,11 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
       // [4] V(this step's input); the previous step's truncation bootstrap
       if (active) {
         float v[1];
-        attn16_net_sel<1, kI8>(s_net, F, lane, v, ttab);
+        attn16_net_sel<1, kI8>(s_net, F, FI, lane, v, ttab);
         if (own) p.val[off] = v[0];
         if (any_pb) {
           float vt[1];
-          attn16_net_sel<1, kI8>(s_net, Ft, lane, vt, ttab);
+          attn16_net_sel<1, kI8>(s_net, Ft, FIt, lane, vt, ttab);
           if (own && pb) rew_buf[off - a.n] = prew + gamma * vt[0];
         }
       }
@@ -2161,6 +2245,7 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
       const bool pb = pend;
       const bool any_pb = __ballot(pb) != 0ull;
       f32x4 F[4];
+      I8Feat FI;
       float xs[KS];
       if constexpr (kLn) {
         cur_stack(st, zf, xs);
@@ -2169,9 +2254,10 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
         normalize<O>(o, x, norm, mu, sd, p.clip);
         inputs(x, xs);
       }
-      attn16_extract<KS, kLn>(s_ext, xs, lane, F);
+      attn16_extract<KS, kLn, kI8>(s_ext, xs, lane, F, s_psh);
+        if constexpr (kI8) FI = i8x_feat(F);
       float vl[1];
-      attn16_net_sel<1, kI8>(s_net, F, lane, vl, ttab);
+      attn16_net_sel<1, kI8>(s_net, F, FI, lane, vl, ttab);
       if (any_pb) {
         float xt[KS];
         if constexpr (kLn) {
@@ -2181,9 +2267,10 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
           normalize<O>(pt, x, norm, mu, sd, p.clip);
           inputs(x, xt);
         }
-        attn16_extract<KS, kLn>(s_ext, xt, lane, F);
+        attn16_extract<KS, kLn, kI8>(s_ext, xt, lane, F, s_psh);
+        if constexpr (kI8) FI = i8x_feat(F);
         float vt[1];
-        attn16_net_sel<1, kI8>(s_net, F, lane, vt, ttab);
+        attn16_net_sel<1, kI8>(s_net, F, FI, lane, vt, ttab);
         if (own && pb) rew_buf[(int64_t)(a.K - 1) * a.n + i] = prew + gamma * vt[0];
       }
       if (own) {

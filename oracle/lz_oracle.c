@@ -853,7 +853,12 @@ float orc_exp_f32(float x) {
 
 typedef struct {
   const float *fc1_w, *fc1_b, *in_w, *in_b, *out_w, *out_b, *post_w, *post_b, *ln_w, *ln_b;
+  const void* post8;  /* non-NULL: post_attention_fc as i8x4 products (orc_attn_i8x4) */
 } orc_attn_ext;
+
+/* post_attention_fc of the i8x4 extractor: the 128 attention outputs of all 8 tokens ->
+ * the 64 features (defined with the i8x4 section below) */
+static void i8x_post(const void* post8, const float* uall, const float* post_b, float* feat);
 
 /* acc + sum_{s < 4} sum_{G < 4} w[4G + s] * v[4G + s]: one 16-dim k order (4 k-steps) */
 static inline float dot16(float acc, const float* w, const float* v) {
@@ -896,7 +901,7 @@ static void attn_ext_one(const orc_attn_ext* e, int in_dim, const float* x, floa
       kk[T][o] = dot16(e->in_b[16 + o], e->in_w + (16 + o) * 16, tok + 16 * T);
       vv[T][o] = dot16(e->in_b[32 + o], e->in_w + (32 + o) * 16, tok + 16 * T);
     }
-  float post[64];
+  float post[64], uall[128];
   for (int f = 0; f < 64; ++f) post[f] = e->post_b[f];
   for (int i = 0; i < 8; ++i) {
     float q[16], att[16], y[16], u[16];
@@ -936,7 +941,13 @@ static void attn_ext_one(const orc_attn_ext* e, int in_dim, const float* x, floa
     } else {
       for (int d = 0; d < 16; ++d) u[d] = y[d];
     }
-    for (int f = 0; f < 64; ++f) post[f] = dot16(post[f], e->post_w + f * 128 + 16 * i, u);
+    for (int d = 0; d < 16; ++d) uall[16 * i + d] = u[d];
+    if (!e->post8)
+      for (int f = 0; f < 64; ++f) post[f] = dot16(post[f], e->post_w + f * 128 + 16 * i, u);
+  }
+  if (e->post8) {
+    i8x_post(e->post8, uall, e->post_b, feat);
+    return;
   }
   for (int f = 0; f < 64; ++f) feat[f] = post[f] < 0.0f ? 0.0f : post[f];
 }
@@ -981,7 +992,7 @@ void orc_attn_f32(int64_t n, int in_dim, int A, const float* x, const float* fc1
                   const float* vf_w1, const float* vf_b1, const float* vf_w2, const float* vf_b2,
                   const float* act_w, const float* act_b, const float* val_w, const float* val_b,
                   float* mean, float* value, float* feat_out) {
-  const orc_attn_ext e = {fc1_w, fc1_b, in_w, in_b, out_w, out_b, post_w, post_b, ln_w, ln_b};
+  const orc_attn_ext e = {fc1_w, fc1_b, in_w, in_b, out_w, out_b, post_w, post_b, ln_w, ln_b, NULL};
   for (int64_t i = 0; i < n; ++i) {
     float feat[64];
     attn_ext_one(&e, in_dim, x + i * in_dim, feat);
@@ -1100,7 +1111,32 @@ static void attn_net_one_i8x(int R, const float* feat, const i8x_net* t, const f
   }
 }
 
-/* orc_attn_f32 with the i8x4 nets (the extractor is orc_attn_f32's) */
+/* post_attention_fc in i8x4: the env's 128 attention outputs (any sign) at the scale of
+ * their largest magnitude, the 64 rows at theirs; a NaN / inf output -> NaN features */
+typedef struct {
+  int8_t d[64 * 128 * 4];
+  int32_t q[64];
+} i8x_postw;
+
+static void i8x_post(const void* post8, const float* uall, const float* post_b, float* feat) {
+  const i8x_postw* pw = (const i8x_postw*)post8;
+  float m = 0.0f;
+  for (int k = 0; k < 128; ++k)
+    m = (m != m || uall[k] != uall[k]) ? NAN : fmaxf(m, fabsf(uall[k]));
+  if (!(m <= 3.40282347e38f)) {
+    for (int f = 0; f < 64; ++f) feat[f] = NAN;
+    return;
+  }
+  const int qu = i8x_q(m);
+  int8_t ud[128 * 4];
+  for (int k = 0; k < 128; ++k) i8x_digits(i8x_fixed(uall[k], qu), ud + 4 * k);
+  for (int f = 0; f < 64; ++f) {
+    const float y = orc_i8x_dot(128, pw->d + 4 * 128 * f, ud, 24 - pw->q[f] - qu) + post_b[f];
+    feat[f] = y < 0.0f ? 0.0f : y;
+  }
+}
+
+/* orc_attn_f32 with the i8x4 nets and post_attention_fc */
 void orc_attn_i8x4(int64_t n, int in_dim, int A, const float* x, const float* fc1_w, const float* fc1_b,
                    const float* in_w, const float* in_b, const float* out_w, const float* out_b,
                    const float* post_w, const float* post_b, const float* ln_w, const float* ln_b,
@@ -1108,10 +1144,15 @@ void orc_attn_i8x4(int64_t n, int in_dim, int A, const float* x, const float* fc
                    const float* vf_w1, const float* vf_b1, const float* vf_w2, const float* vf_b2,
                    const float* act_w, const float* act_b, const float* val_w, const float* val_b,
                    float* mean, float* value, float* feat_out) {
-  const orc_attn_ext e = {fc1_w, fc1_b, in_w, in_b, out_w, out_b, post_w, post_b, ln_w, ln_b};
   static i8x_net pi, vf;  /* (not reentrant: test infrastructure) */
+  static i8x_postw pw;
   i8x_prep(&pi, pi_w1, pi_w2);
   i8x_prep(&vf, vf_w1, vf_w2);
+  for (int f = 0; f < 64; ++f) {
+    pw.q[f] = orc_i8x_row_q(post_w + f * 128, 128);
+    for (int k = 0; k < 128; ++k) i8x_digits(i8x_fixed(post_w[f * 128 + k], pw.q[f]), pw.d + 4 * (f * 128 + k));
+  }
+  const orc_attn_ext e = {fc1_w, fc1_b, in_w, in_b, out_w, out_b, post_w, post_b, ln_w, ln_b, &pw};
   for (int64_t i = 0; i < n; ++i) {
     float feat[64];
     attn_ext_one(&e, in_dim, x + i * in_dim, feat);

@@ -93,10 +93,21 @@ def test_i8x4_env_part_and_forward_bitexact(gl, pol, orc, system, n, K, kw):
     _check_forward(orc, sd, b, O, A, rows)
     _, vl = orc.attn_f32(sd, _np(b.last_obs), precision="i8x4")
     assert bits_equal(_np(b.last_values), vl)
-    # not the float32 path's bits (a different arithmetic), but within its accuracy
-    m32, _ = orc.attn_f32(sd, _np(b.observations).reshape(-1, O)[:2000])
-    d = np.abs(_np(b.actions).reshape(-1, A)[:2000] - m32).max()
-    assert 0 < d <= 1e-5 * max(1.0, np.abs(m32).max())
+    # not the float32 path's bits (a different arithmetic) but its accuracy: both against
+    # the same net in float64 (LORENZ3's raw +-30 obs through 0.2-scale random weights make
+    # float32 itself ~1e-5 off there)
+    x = _np(b.observations).reshape(-1, O)[:2000]
+    net = pol.ActorCriticAttn(O, A)
+    net.load_state_dict(sd)
+    with torch.no_grad():
+        m64 = net.double()(torch.from_numpy(x).double())[0].numpy()
+    m32, _ = orc.attn_f32(sd, x)
+    sc = max(1.0, np.abs(m64).max())
+    e8 = np.abs(_np(b.actions).reshape(-1, A)[:2000] - m64).max() / sc
+    e32 = np.abs(m32 - m64).max() / sc
+    print("i8x4 vs float64 %.2e, float32 vs float64 %.2e" % (e8, e32))
+    assert not np.array_equal(_np(b.actions).reshape(-1, A)[:2000], m32)
+    assert e8 <= 1.5 * e32 + 1e-6
 
 
 def test_i8x4_vecnormalize_frozen_bitexact(gl, pol, orc):

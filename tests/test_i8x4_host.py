@@ -141,6 +141,8 @@ def pol():
 PI, VF = 54400, 54400 + 102400          # lz_internal.h kAFPi / kAFVf
 N1, N2, NB1, NB2, NH, NHB = 0, 32768, 98304, 98816, 99328, 101376
 SH1, SH2 = NHB + 16, NHB + 16 + 256     # kAXSh1 / kAXSh2
+POSTSH = SH2 + 256                      # kAXPostSh (pi slot)
+POSTW, POSTB = 21376, 54144             # kAFPostW / kAFPostB (extractor)
 
 
 def _lane_bytes(blob, off, n_ops):
@@ -225,19 +227,39 @@ def test_packed_blob_dataflow_equals_oracle(orc, pol, ln):
     ve = _net_from_blob(orc, blob, VF, feat, 1)[:, 0]
     assert np.array_equal(me.view(np.uint32), m.view(np.uint32))
     assert np.array_equal(ve.view(np.uint32), v.view(np.uint32))
-    # the float32 blob differs only in the wide layers' encodings and the shift tables
+    # post_attention_fc's digits (kAFPostW) and row shifts (the pi slot's kAXPostSh): byte
+    # 4f + r of lane (G, m), A operand (tile u, k-block kb, digit i) = digit i of
+    # post_w[16u + m][64kb + 16f + 4G + r] at its row's q
+    post_w = sd["features_extractor.post_attention_fc.0.weight"].numpy()
+    ops = _lane_bytes(blob, POSTW, 32)
+    psh = np.frombuffer(blob[PI + POSTSH: PI + POSTSH + 128].tobytes(), np.int16)
+    for row in range(64):
+        q = orc.i8x_row_q(post_w[row])
+        assert psh[row] == 24 - q
+        dg = orc.i8x_digits(post_w[row], q)
+        u, mm = row // 16, row % 16
+        for G in range(4):
+            for kb in range(2):
+                ks = [64 * kb + 16 * f + 4 * G + r for f in range(4) for r in range(4)]
+                for i in range(4):
+                    assert np.array_equal(ops[(u * 2 + kb) * 4 + i, 16 * G + mm], dg[ks, i]), (row, G, kb, i)
+    # the float32 blob differs only in those encodings and the shift tables
     b32 = (pol.pack_attn_ln_policy_f32 if ln else pol.pack_attn_policy_f32)(sd, in_dim, 2)
     same = np.ones(blob.size, bool)
+    same[POSTW: POSTB] = False
+    same[PI + POSTSH: PI + POSTSH + 128] = False
     for base in (PI, VF):
         same[base + N1: base + NB1] = False
         same[base + SH1: base + SH2 + 256] = False
     assert np.array_equal(blob[same], b32[same])
 
 
-def test_pack_refuses_nonfinite_net_weights(pol):
+@pytest.mark.parametrize("key", ["mlp_extractor.value_net.2.weight",
+                                 "features_extractor.post_attention_fc.0.weight"])
+def test_pack_refuses_nonfinite_weights(pol, key):
     from gym_lorenz import _native as nat
 
     sd = pol.ActorCriticAttn(6, 2, seed=1).state_dict()
-    sd["mlp_extractor.value_net.2.weight"][3, 7] = float("inf")
+    sd[key][3, 7] = float("inf")
     with pytest.raises(nat.LorenzEnvError):
         pol.pack_attn_policy_i8x4(sd, 6, 2)

@@ -10,8 +10,12 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=$ROOT/gym-lorenz_amd
 mkdir -p $ROOT/ablib $PKG/build_ab
 FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -fPIC -Wall -I$ROOT/include -I$PKG/csrc"
-/opt/rocm/bin/hipcc $FLAGS "$@" -c $PKG/csrc/lz_kernels.hip -o $PKG/build_ab/lz_kernels_$NAME.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/ablib/libgym_lorenz_amd_$NAME.so \
-  $PKG/build_ab/lz_kernels_$NAME.o $PKG/build/lz_rms.o $PKG/build/lz_policy.o $PKG/build/lz_wrappers.o \
-  $PKG/build/lz_api.o $PKG/build/lz_pack.o
+# AB_SRC=lz_policy recompiles the policy kernels instead (the other objects from build/)
+SRC=${AB_SRC:-lz_kernels}
+/opt/rocm/bin/hipcc $FLAGS "$@" -c $PKG/csrc/$SRC.hip -o $PKG/build_ab/${SRC}_$NAME.o
+OBJS=""
+for o in lz_kernels lz_rms lz_policy lz_wrappers lz_api lz_pack; do
+  if [ $o = $SRC ]; then OBJS="$OBJS $PKG/build_ab/${SRC}_$NAME.o"; else OBJS="$OBJS $PKG/build/$o.o"; fi
+done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/ablib/libgym_lorenz_amd_$NAME.so $OBJS
 echo $ROOT/ablib/libgym_lorenz_amd_$NAME.so

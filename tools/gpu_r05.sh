@@ -18,11 +18,10 @@ new)
     tests/test_gpu_resident.py tests/test_gpu_policy_branches.py > $O/new_tests.txt 2>&1 || exit 1
   LZ_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 > $O/bench_gpus2_gloo.json 2> $O/bench_gpus2_gloo.err
   ;;
-ic)  # the headline state's reuse distance: warm (bench) vs cold (384 MiB copy between steps)
-  KN="k_step_multi<lz::SysL3<float>, float, 4"
-  for r in 1 2 3; do for m in warm cold; do
-    timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/${m}_$r -o run --output-format csv \
-      -- python tools/ic_flush.py $m 20 > $O/${m}_$r.json 2> $O/${m}_$r.err || exit 1
+ic)  # the headline state's reuse distance: bench.py as is (warm) vs a 2 x 192 MiB copy after every step (cold)
+  for r in 1 2; do for m in 0 192; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/f${m}_$r -o run --output-format csv \
+      -- python bench.py --ic-flush-mib $m --steps 2000 --warmup 100 $BQ > $O/f${m}_$r.json 2> $O/f${m}_$r.err || exit 1
   done; done
   ;;
 diag)  # graph replays of lz_step: eager, k_step graph, then the default (k_step_multi) graph
@@ -37,6 +36,47 @@ i8)  # the default bench path first, then the i8x4 attention policies: parity, t
   for r in 1 2; do for pr in fp32 i8x4; do for po in attn attn_ln; do
     timeout -k 10 300 python bench.py $PB --policy $po --precision $pr > $O/${po}_${pr}_$r.json 2>> $O/bench.err || exit 1
   done; done; done
+  ;;
+pmc_i8)  # SQ issue / co-execution counters of the attention rollout: fp32 vs i8x4
+  for pr in fp32 i8x4; do
+    bash tools/policy_pmc.sh r05_attn_$pr --policy attn --precision $pr --system hr --envs 32768 --K 2048 --steps 4096 $BQ || exit 1
+  done
+  ;;
+r2)  # i8x4 after the shared feature digits + pipelined layer 2: parity, A/B, counters; IC read-only flush
+  timeout -k 10 900 $PYT -m gpu --maxfail=6 tests/test_gpu_policy_i8x4.py > $O/i8_tests.txt 2>&1 || exit 1
+  PB="--mode policy --system hr --envs 32768 --K 2048 --steps 4096 $BQ"
+  for r in 1 2; do for pr in fp32 i8x4; do for po in attn attn_ln; do
+    timeout -k 10 300 python bench.py $PB --policy $po --precision $pr > $O/${po}_${pr}_$r.json 2>> $O/bench.err || exit 1
+  done; done; done
+  for r in 1 2; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/read192_$r -o run --output-format csv \
+      -- python bench.py --ic-flush-mib 192 --ic-flush-kind read --steps 2000 --warmup 100 $BQ > $O/read192_$r.json 2> $O/read192_$r.err || exit 1
+  done
+  bash tools/policy_pmc.sh r05_attn_i8x4 --policy attn --precision i8x4 --system hr --envs 32768 --K 2048 --steps 4096 $BQ || exit 1
+  bash tools/policy_pmc.sh r05_attn_fp32 --policy attn --precision fp32 --system hr --envs 32768 --K 2048 --steps 4096 $BQ || exit 1
+  ;;
+r3)  # IC read-only flush; SQ counters of the attention rollout (fp32 vs i8x4)
+  for r in 1 2; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/read192_$r -o run --output-format csv \
+      -- python bench.py --ic-flush-mib 192 --ic-flush-kind read --steps 2000 --warmup 100 $BQ > $O/read192_$r.json 2> $O/read192_$r.err || exit 1
+  done
+  bash tools/policy_pmc.sh r05_attn_i8x4 --policy attn --precision i8x4 --system hr --envs 32768 --K 2048 --steps 4096 $BQ || exit 1
+  bash tools/policy_pmc.sh r05_attn_fp32 --policy attn --precision fp32 --system hr --envs 32768 --K 2048 --steps 4096 $BQ || exit 1
+  ;;
+r4)  # i8x4 with post_attention_fc on the int8 MFMA: parity, A/B vs fp32 and vs the r2 build; IC read flush; counters
+  timeout -k 10 900 $PYT -m gpu --maxfail=6 tests/test_gpu_policy_i8x4.py > $O/i8_tests.txt 2>&1 || exit 1
+  PB="--mode policy --system hr --envs 32768 --K 2048 --steps 4096 $BQ"
+  for r in 1 2; do for pr in fp32 i8x4; do for po in attn attn_ln; do
+    timeout -k 10 300 python bench.py $PB --policy $po --precision $pr > $O/${po}_${pr}_$r.json 2>> $O/bench.err || exit 1
+  done; done; done
+  timeout -k 10 900 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_i8nopipe.so -- $PB --policy attn \
+    --precision i8x4 > $O/ab_i8_nopipe.json 2> $O/ab_i8_nopipe.err || exit 1
+  for r in 1 2; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/read192_$r -o run --output-format csv \
+      -- python bench.py --ic-flush-mib 192 --ic-flush-kind read --steps 2000 --warmup 100 $BQ > $O/read192_$r.json 2> $O/read192_$r.err || exit 1
+  done
+  bash tools/policy_pmc.sh r05_attn_i8x4 --policy attn --precision i8x4 --system hr --envs 32768 --K 2048 --steps 4096 $BQ || exit 1
+  bash tools/policy_pmc.sh r05_attn_fp32 --policy attn --precision fp32 --system hr --envs 32768 --K 2048 --steps 4096 $BQ || exit 1
   ;;
 full)
   timeout -k 10 1000 $PYT -x -m gpu tests > $O/gpu_tests.txt 2>&1 || exit 1
