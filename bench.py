@@ -291,8 +291,13 @@ def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=
         if (system == "pmsm" if noise is None else noise) and system in ("pmsm", "hr") \
                 and variant & (1 << 25):  # opt-in noise-producer wave
             return "_ZN2lz12k_rollout_npINS_%sLi%dEEEvNS_5KArgsE" % (sysname, D)
-        return "_ZN2lz9k_rolloutINS_%sLi64ELi%dE%sLb1EEEvNS_5KArgsE" % (sysname, D, b)
-    return "_ZN2lz9k_rolloutINS_%sLi256ELi%dE%sLb1EEEvNS_5KArgsE" % (sysname, D, b)
+    # k_rollout<Sys, T, B, D, kNoDone, kDoneT = true, kZN>: kZN (variant bit 1<<26) = the next
+    # step's normals drawn during this step, noisy systems only
+    zn = "Lb%dE" % int(bool(variant & (1 << 26)) and system in ("pmsm", "hr")
+                       and bool(system == "pmsm" if noise is None else noise))
+    if n < one_wave_below:
+        return "_ZN2lz9k_rolloutINS_%sLi64ELi%dE%sLb1E%sEEvNS_5KArgsE" % (sysname, D, b, zn)
+    return "_ZN2lz9k_rolloutINS_%sLi256ELi%dE%sLb1E%sEEvNS_5KArgsE" % (sysname, D, b, zn)
 
 
 def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
@@ -445,8 +450,9 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
     rms = None if attn else DeviceRunningMeanStd(O, device)
     f32 = args.precision in ("fp32", "i8x4")
     i8 = args.precision == "i8x4"
-    if i8 and not attn:
-        raise SystemExit("--precision i8x4 runs the attention policies (--policy attn / attn_ln)")
+    if i8 and not attn and args.vecnorm_update == "step":
+        raise SystemExit("--precision i8x4 --policy mlp runs the fused rollout: add --vecnorm-update "
+                         "rollout (the per-step VecNormalize collect is float32 only)")
     per_step = f32 and not attn and args.vecnorm_update == "step"
     col = FusedRolloutCollector(env, net.state_dict(), gamma=0.99, gae_lambda=0.95, obs_rms=rms,
                                 clip_obs=10.0, training=True, bootstrap=True, frame_stack=stack,
@@ -498,6 +504,7 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
     fl = attn_policy_flops(stack * O, A) if attn else policy_flops(O, A)
     achieved = fl * n * K / launch_s / 1e12
     peak = MFMA_F32_PEAK_TFLOPS if f32 else MFMA_BF16_PEAK_TFLOPS
+    num_cus = torch.cuda.get_device_properties(device).multi_processor_count
     mangled = {"pmsm": "7SysPMSME", "lorenz3": "5SysL3IfEE", "lorenz4": "5SysL4IfEE",
                "hr": "5SysHRIfEE"}[args.system]
     return {
@@ -514,7 +521,8 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         "dtype": ("f32 MFMA extractor + exact int8 MFMA (4-digit fixed point) nets, f32 env" if i8 else
                   "f32 MFMA (f32 accumulate), f32 env" if f32 else "bf16 MFMA (fp32 accumulate), f32 env"),
         "precision_note": ("opt-in i8x4: the nets' wide layers as exact fixed-point products, float32-"
-                           "level accuracy, bit-exact vs the C oracle (orc_attn_i8x4); frac = useful "
+                           "level accuracy, bit-exact vs the C oracle (orc_attn_i8x4 / orc_mlp_i8x4); "
+                           "frac = useful "
                            "FLOP against the f32 MFMA peak, like the fp32 line" if i8 else
                            "float32 end to end, bit-exact vs the C oracle (SB3's own precision)"
                            if f32 else "bf16 operands (opt-in, ~1e-2 off SB3's float32)"),
@@ -543,8 +551,9 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
                             "+ clip + env step + float64 tile moments, then the obs_rms update; "
                             "truncation bootstraps valued with their step's statistics), GAE "
                             "(lz_gae); %d envs total, %d per GPU" if per_step else
-                            "%d-step fused rollout (lz_rollout_policy" + ("_f32, float32 as SB3" if f32 else
-                                                                          ", bf16 MFMA")
+                            "%d-step fused rollout (lz_rollout_policy" + (
+                                "_f32 + LZ_POLICY_I8X4, layer 2 as exact int8 products" if i8 else
+                                "_f32, float32 as SB3" if f32 else ", bf16 MFMA")
                             + ": policy forward + DiagGaussian "
                             "sample + clip + env step + truncation bootstrap + VecNormalize obs with "
                             "the rollout-start statistics), pooled obs_rms update, GAE (lz_gae); "
@@ -570,7 +579,9 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
                        if attn else
                        "_ZN2lz17k_policy_step_f32INS_%sLi8EEEvNS_5KArgsENS_5PArgsENS_9PStepArgsE"
                        if per_step else
-                       "_ZN2lz16k_rollout_policyINS_%sLi8ELi32ELi5ELi1EEEvNS_5KArgsENS_5PArgsE"
+                       (("_ZN2lz16k_rollout_policyINS_%sLi8ELi32ELi" + "56"[i8] + "ELi1EEEvNS_5KArgsENS_5PArgsE")
+                        if n >= 8 * 32 * num_cus else
+                        ("_ZN2lz26k_rollout_policy_f32_splitINS_%sLb" + "01"[i8] + "EEEvNS_5KArgsENS_5PArgsE"))
                        if f32 else "_ZN2lz16k_rollout_policyINS_%sLi8EEEvNS_5KArgsENS_5PArgsE")
                       % mangled,
             "avg_launch_us": launch_s * 1e6, "flop_per_env_step": fl,
@@ -1163,6 +1174,16 @@ def main():
         out["roofline"]["flop_per_env_step"] = RK4_FLOP[args.system]
     headline = args.system == "lorenz3" and not rollout and "integrator" not in kw
     env.close()
+    if rank == 0 and world == 1 and headline and args.dtype == "float32" and not args.no_extras:
+        cs = cold_state_probe(gl, nat, torch, device, n)
+        cs["frac_cold_scaled"] = out["roofline"]["frac"] * cs["us_per_launch_warm"] / cs["us_per_launch_cold"]
+        out["roofline"]["cold_state"] = cs
+        out["roofline"]["memory_level_note"] = (
+            "the state the step reads was written by the previous step ~68 MB of traffic earlier, "
+            "so in this loop it is served from the 256 MiB Infinity Cache, not DRAM "
+            "(profiles/r05/ic/): with the state evicted before every step the same launch takes "
+            "cold_over_warm x as long; frac_cold_scaled = frac x warm / cold is the fraction of "
+            "8 TB/s the kernel reaches when every byte comes from DRAM")
     extras = []
     if rank == 0 and world == 1 and headline and not args.no_drift:
         out["fp32_drift"] = fp32_drift(gl, torch, device)
@@ -1185,6 +1206,70 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def cold_state_probe(gl, nat, torch, device, n, reps=96, flush_mib=384):
+    """Which memory level the headline's state reads come from.  The
+    12 MB of LORENZ3 state is written by step k and read by step k + 1 with ~68 MB of other
+    traffic between, so the Infinity Cache (256 MiB, MI355X_MICROARCH.md "Infinity Cache")
+    can serve those reads, and FETCH_SIZE counts such hits as traffic.  Here the same
+    handle / ring / kernel is timed per launch (HIP events around each lz_step on its
+    stream, a spin kernel queued first so the GPU never waits for Python) in two loops:
+    `warm` = back-to-back steps as in the bench; `cold` = a read of `flush_mib` MiB (a sum)
+    before every step, so nothing of the state survives in the Infinity Cache.  Returns
+    the two per-launch times and the HBM fraction of the cold one."""
+    import ctypes
+
+    env = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=0, autoreset=True, device=device.index)
+    env.reset()
+    R, A, O = 16, env.action_dim, env.obs_dim
+    acts = torch.rand((R, n, A), device=device) * 2 - 1
+    obs = torch.empty((R, n, O), device=device)
+    rew = torch.empty((R, n), device=device)
+    done = torch.empty((R, n), dtype=torch.uint8, device=device)
+    big = torch.ones((flush_mib << 18,), device=device)
+    out = torch.empty((), device=device)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    slots = [(P(acts[r]), P(obs[r]), P(rew[r]), P(done[r])) for r in range(R)]
+    didx, tobs = P(env.done_idx), P(env.term_obs)
+    stream = torch.cuda.Stream(device)
+    nat.check(nat.lib.lz_set_stream(env._h, ctypes.c_void_p(stream.cuda_stream)))
+    k = [0]
+
+    def step():
+        a, o, r_, d = slots[k[0] % R]
+        k[0] += 1
+        nat.check(nat.lib.lz_step(env._h, a, None, o, r_, d, didx, tobs, None))
+
+    res = {}
+    with torch.cuda.stream(stream):
+        for _ in range(8):
+            step()
+        torch.cuda.synchronize(device)
+        for mode in ("warm", "cold", "warm2", "cold2"):
+            evs = []
+            torch.cuda._sleep(int(5e7))  # the queue fills while the GPU spins
+            for _ in range(reps):
+                if mode.startswith("cold"):
+                    torch.sum(big, dim=0, out=out)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                step()
+                e1.record(stream)
+                evs.append((e0, e1))
+            torch.cuda.synchronize(device)
+            ts = sorted(e0.elapsed_time(e1) * 1e3 for e0, e1 in evs[4:])
+            res.setdefault(mode.rstrip("2"), []).append(ts[len(ts) // 2])
+    env.close()
+    del big
+    torch.cuda.empty_cache()
+    warm, cold = min(res["warm"]), min(res["cold"])
+    alg = env.bytes_per_env_step * n
+    return {"us_per_launch_warm": warm, "us_per_launch_cold": cold, "cold_over_warm": cold / warm,
+            "frac_cold": alg / (cold * 1e-6) / 1e9 / HBM_PEAK_GBS,
+            "method": "per-launch HIP events (median of %d, best of 2 loops), the same 1M LORENZ3 "
+                      "handle and 16-slot ring; cold = a %d MiB read (torch.sum) before every step "
+                      "evicts the state from the 256 MiB Infinity Cache" % (reps - 4, flush_mib)}
 
 
 def load_traffic(kernel, n):

@@ -1168,8 +1168,13 @@ static lz_status rollout_policy(lz_handle* h, const lz_policy_rollout_args* r, i
     if (sys != LZ_SYS_LORENZ3 && sys != LZ_SYS_PMSM && sys != LZ_SYS_HR)
       return fail(LZ_ERR_UNSUPPORTED, "the float32 attention rollout runs LORENZ3 / PMSM / HR");
   }
-  if ((r->flags & LZ_POLICY_I8X4) && arch < 4)
-    return fail(LZ_ERR_UNSUPPORTED, "LZ_POLICY_I8X4 runs the attention float32 rollouts only");
+  if ((r->flags & LZ_POLICY_I8X4) && arch < 3)
+    return fail(LZ_ERR_UNSUPPORTED, "LZ_POLICY_I8X4 runs the float32 (attention / MlpPolicy) rollouts only");
+  if ((r->flags & LZ_POLICY_I8X4) && arch == 3) {
+    const int sys = h->cfg.system;
+    if (sys != LZ_SYS_LORENZ3 && sys != LZ_SYS_LORENZ4 && sys != LZ_SYS_PMSM && sys != LZ_SYS_HR)
+      return fail(LZ_ERR_UNSUPPORTED, "the i8x4 MlpPolicy rollout runs LORENZ3 / LORENZ4 / PMSM / HR");
+  }
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_rollout_policy before the first lz_reset");
   if (h->f64) return fail(LZ_ERR_UNSUPPORTED, "the policy rollout runs float32 handles only");
   if (sys_key(h) != h->cfg.system)
@@ -1265,7 +1270,7 @@ lz_status lz_policy_step_f32(lz_handle* h, const lz_policy_rollout_args* r, int3
   if (!h || !r) return fail(LZ_ERR_INVALID, "handle/args is NULL");
   RESIDENT_QUIESCE(h);
   if (r->flags & LZ_POLICY_I8X4)
-    return fail(LZ_ERR_UNSUPPORTED, "LZ_POLICY_I8X4 runs the attention float32 rollouts only");
+    return fail(LZ_ERR_UNSUPPORTED, "LZ_POLICY_I8X4 runs the float32 rollouts only, not the per-step collect");
   if (!h->was_reset) return fail(LZ_ERR_STATE, "lz_policy_step_f32 before the first lz_reset");
   if (h->f64) return fail(LZ_ERR_UNSUPPORTED, "the policy rollout runs float32 handles only");
   if (sys_key(h) != h->cfg.system)

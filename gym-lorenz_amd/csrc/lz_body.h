@@ -99,8 +99,14 @@ __device__ __forceinline__ void make_noise(const Sys& sys, const KArgs& a, int64
 // rollout) -- same arithmetic, but it takes no slot in the compact done list.
 // kNoDone: the launch can produce no done at all (a never-terminating system and no
 // step counter, see no_done()): the step alone, no done bookkeeping.
+// kZMode (noisy systems, device noise): 0 draws this step's normals here; 1 reads them
+// from a producer wave's LDS ring (zpre[0], zpre[64], zpre[128]); 2 (software-pipelined,
+// k_rollout kZN) reads them from the caller's registers zpre[0..2] and draws the NEXT
+// step's normals (tick + 1) into the same registers here, in the basic block of sys.step,
+// so the scheduler interleaves that independent Philox + Box-Muller chain with the
+// integrator's.  The normals are keyed by (seed, env id, tick) only: bit-identical.
 template <class Sys, typename T, bool kRollout, bool kKeepTerm = false, bool kNoDone = false,
-          bool kInject = !kRollout, bool kZPre = false>
+          bool kInject = !kRollout, int kZMode = 0>
 __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KArgs& a, int64_t i,
                                              bool live, const float* act, uint64_t tick, int k,
                                              T* o, T& rew, bool& did_reset,
@@ -122,9 +128,13 @@ __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KAr
     bool use_nz = false;
     if constexpr (Sys::kNoise) {
       if (a.flags & LZ_FLAG_ADD_NOISE) {
-        if constexpr (kZPre) {  // the normals drawn ahead by a producer wave (k_rollout kNP):
+        if constexpr (kZMode == 1) {  // the normals drawn ahead by a producer wave (k_rollout kNP):
           // zpre[0], zpre[64], zpre[128] -- the same normal3(seed, gid, tick) values
           float z[3] = {zpre[0], zpre[64], zpre[128]};
+          sys.noise_from_normals(z, nz);
+        } else if constexpr (kZMode == 2) {  // this step's from registers; draw the next step's
+          float z[3] = {zpre[0], zpre[1], zpre[2]};
+          normal3(a.seed, (uint64_t)(a.gid0 + i), tick + 1, const_cast<float*>(zpre));
           sys.noise_from_normals(z, nz);
         } else {
           make_noise<Sys, T, kInject>(sys, a, i, tick, nz);

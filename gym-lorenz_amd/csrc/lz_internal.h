@@ -182,10 +182,15 @@ constexpr int kF32B1 = kF32W2 + 4 * 16 * 64 * 4 * 4;
 constexpr int kF32B2 = kF32B1 + 4 * 2 * 16 * 4;
 constexpr int kF32H = kF32B2 + 4 * 2 * 16 * 4;
 constexpr int kF32HB = kF32H + 4 * 2 * 64 * 4;
-constexpr int kF32Net = kF32HB + 64;                 // 72768 B
+// opt-in i8x4 (lz_policy_pack_i8x4, LZ_POLICY_I8X4): layer 2's weights at kF32W2 as digits
+// ([4 out tiles][4 k-blocks][4 digits][64 lanes][16 B], byte j of lane (m, h) = digit of
+// W2[32T + m][32kb + row(j, h)]) and its row shifts 24 - q - 28 here, int16 in the
+// accumulator order [4 tiles][2 halves][16] (unused by the float32 kernels)
+constexpr int kF32Sh2 = kF32HB + 64;
+constexpr int kF32Net = kF32Sh2 + 4 * 2 * 16 * 2;    // 73024 B
 constexpr int kF32LogStd = 2 * kF32Net;
 constexpr int kF32Tanh = kF32LogStd + 64;           // tanh table: 72 segments x 8 floats
-constexpr int kF32BlobBytes = kF32Tanh + 72 * 32;   // 147904 B (resident in LDS)
+constexpr int kF32BlobBytes = kF32Tanh + 72 * 32;   // 148416 B (resident in LDS)
 
 // The attention actor-critics at SB3's precision (float32 operands and accumulation;
 // lz_attn_policy_pack_f32 / lz_attn_ln_policy_pack_f32 -> k_rollout_policy_attn_f32).

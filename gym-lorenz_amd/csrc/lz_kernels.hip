@@ -655,7 +655,8 @@ __device__ __forceinline__ void ladder_wait(int k) {
 
 constexpr int kZSlots = 4;  // steps of normals a producer wave may draw ahead (k_rollout kNP)
 constexpr uint32_t kZSpinCap = 1u << 24;  // polls of one flag before a wave gives up (~1 s)
-template <class Sys, typename T, int B, bool FULL, int D, bool kNoDone, bool kDoneT, bool kNP = false>
+template <class Sys, typename T, int B, bool FULL, int D, bool kNoDone, bool kDoneT, bool kNP = false,
+          bool kZN = false>
 __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any_reset,
                                              const KArgs& a, int64_t base, int tid, int nb,
                                              uint64_t tick, float* s_act, T* s_obs,
@@ -723,6 +724,11 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   // one step per step until it reaches the last (no per-step 64-bit multiply)
   const float* dsrc = dma_src(D < a.K ? D : a.K - 1);
   uint32_t zcap = 0;  // kNP: the producer timed out once -- stop waiting for it (sticky)
+  // kZN: step k's normals, drawn during step k - 1 (step 0's here); see step_body kZMode 2
+  float zn[3] = {0.0f, 0.0f, 0.0f};
+  if constexpr (kZN) {
+    if (live && (a.flags & LZ_FLAG_ADD_NOISE)) normal3(a.seed, (uint64_t)(a.gid0 + i), tick, zn);
+  }
   // kLadder: one of the first D steps (its wait count depends on k); later steps all
   // wait with the steady-state count -- peeled so the hot loop carries no ladder
   auto run_step = [&](int k, auto ladder) __attribute__((always_inline)) {
@@ -781,7 +787,8 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
       }
       zp = zs;
     }
-    const uint8_t dflag = step_body<Sys, T, true, false, kNoDone, false, kNP>(
+    if constexpr (kZN) zp = zn;
+    const uint8_t dflag = step_body<Sys, T, true, false, kNoDone, false, kNP ? 1 : kZN ? 2 : 0>(
         sys, steps, a, i, live, act, tick + (uint64_t)k, k, o, rew, did_reset, nullptr, true, zp);
     if constexpr (kNP) {  // slot k % kZSlots is free again
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -866,7 +873,7 @@ __device__ __forceinline__ void noise_producer(const KArgs& a, int64_t base, int
   }
 }
 
-template <class Sys, typename T, int B, int D, bool kNoDone = false, bool kDoneT = true>
+template <class Sys, typename T, int B, int D, bool kNoDone = false, bool kDoneT = true, bool kZN = false>
 __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
   // DMA ring (a placeholder for systems that take no action)
   __shared__ __attribute__((aligned(16))) float s_act[Sys::kUsesAction ? dma_slots<D>() * act_slot_floats<Sys::A, B>() : 4];
@@ -890,9 +897,11 @@ __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
     if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
   }
   if (nb == B && a.vec_ok)
-    rollout_loop<Sys, T, B, true, D, kNoDone, kDoneT>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
+    rollout_loop<Sys, T, B, true, D, kNoDone, kDoneT, false, kZN>(sys, steps, any_reset, a, base, tid, nb, tick,
+                                                                  s_act, s_obs);
   else
-    rollout_loop<Sys, T, B, false, D, kNoDone, kDoneT>(sys, steps, any_reset, a, base, tid, nb, tick, s_act, s_obs);
+    rollout_loop<Sys, T, B, false, D, kNoDone, kDoneT, false, kZN>(sys, steps, any_reset, a, base, tid, nb, tick,
+                                                                   s_act, s_obs);
   if (live) {
     sys.store(a, i);
     if (any_reset) sys.store_autoreset_extra(a, i);
@@ -1201,6 +1210,9 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
     } else if constexpr (Sys::kNoise && Sys::kUsesAction) {
       if (plan.np)
         hipLaunchKernelGGL((k_rollout_np<Sys, T, D>), dim3((unsigned)((a.n + 63) / 64)), dim3(128), 0, s, a);
+      else if (a.variant & (1 << 26))  // A/B: the next step's normals drawn during this step (kZN)
+        hipLaunchKernelGGL((k_rollout<Sys, T, 64, D, false, true, true>), dim3((unsigned)((a.n + 63) / 64)),
+                           dim3(64), 0, s, a);
       else
         hipLaunchKernelGGL((k_rollout<Sys, T, 64, D>), dim3((unsigned)((a.n + 63) / 64)), dim3(64), 0, s, a);
     } else {
@@ -1216,6 +1228,13 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
         else
           hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D, true>), dim3((unsigned)grid_for(a.n)),
                              dim3(kBlock), 0, s, a);
+        return;
+      }
+    }
+    if constexpr (Sys::kNoise && Sys::kUsesAction) {
+      if (a.variant & (1 << 26)) {  // A/B: kZN, as above
+        hipLaunchKernelGGL((k_rollout<Sys, T, kBlock, D, false, true, true>), dim3((unsigned)grid_for(a.n)),
+                           dim3(kBlock), 0, s, a);
         return;
       }
     }

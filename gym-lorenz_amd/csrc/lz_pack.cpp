@@ -568,7 +568,41 @@ lz_status lz_policy_pack_hidden(const lz_mlp_policy* p, int32_t hidden, void* ho
 
 int64_t lz_policy_f32_blob_bytes(void) { return lz::kF32BlobBytes; }
 
+// layer 2 of a packed float32 MlpPolicy net (pack_net_f32) as i8x4 digits + row shifts
+static void pack_net_i8x4(uint8_t* net, const float* w2) {
+  using lz::kPolHidden;
+  int8_t* g2 = reinterpret_cast<int8_t*>(net + lz::kF32W2);
+  int16_t* sh = reinterpret_cast<int16_t*>(net + lz::kF32Sh2);
+  int q[kPolHidden];
+  for (int u = 0; u < kPolHidden; ++u) q[u] = i8x_row_q(w2 + u * kPolHidden, kPolHidden);
+  int8_t d[4];
+  for (int lane = 0; lane < 64; ++lane) {
+    const int m = lane & 31, h = lane >> 5;
+    for (int T = 0; T < 4; ++T) {
+      const int u = 32 * T + m;
+      for (int kb = 0; kb < 4; ++kb)
+        for (int j = 0; j < 16; ++j) {
+          i8x_digits(w2[u * kPolHidden + 32 * kb + row_of(j, h)], q[u], d);
+          for (int i = 0; i < 4; ++i) g2[(((T * 4 + kb) * 4 + i) * 64 + lane) * 16 + j] = d[i];
+        }
+    }
+  }
+  for (int T = 0; T < 4; ++T)
+    for (int h = 0; h < 2; ++h)
+      for (int g = 0; g < 16; ++g) sh[(2 * T + h) * 16 + g] = (int16_t)(24 - q[32 * T + row_of(g, h)] - 28);
+}
+
+static lz_status pack_mlp_f32(const lz_mlp_policy* p, int32_t hidden, void* host_blob, int64_t cap, bool i8);
+
 lz_status lz_policy_pack_f32(const lz_mlp_policy* p, int32_t hidden, void* host_blob, int64_t cap) {
+  return pack_mlp_f32(p, hidden, host_blob, cap, false);
+}
+
+lz_status lz_policy_pack_i8x4(const lz_mlp_policy* p, int32_t hidden, void* host_blob, int64_t cap) {
+  return pack_mlp_f32(p, hidden, host_blob, cap, true);
+}
+
+static lz_status pack_mlp_f32(const lz_mlp_policy* p, int32_t hidden, void* host_blob, int64_t cap, bool i8) {
   if (!p || !host_blob) return pfail(LZ_ERR_INVALID, "policy/blob is NULL");
   if (cap < lz::kF32BlobBytes) return pfail(LZ_ERR_INVALID, "blob capacity too small");
   if (hidden < 1 || hidden > lz::kPolHidden) return pfail(LZ_ERR_UNSUPPORTED, "hidden width must be 1..128");
@@ -603,8 +637,17 @@ lz_status lz_policy_pack_f32(const lz_mlp_policy* p, int32_t hidden, void* host_
   const float* uw = pad(p->val_w, 1, hidden, 1, H);
   uint8_t* b = static_cast<uint8_t*>(host_blob);
   std::memset(b, 0, lz::kF32BlobBytes);
+  if (i8) {
+    for (const float* w : {pw2, vw2})
+      for (int k = 0; k < H * H; ++k)
+        if (!std::isfinite(w[k])) return pfail(LZ_ERR_INVALID, "i8x4: layer 2 weights must be finite");
+  }
   pack_net_f32(b, O, A, pw1, pb1, pw2, pb2, aw, p->act_b);
   pack_net_f32(b + lz::kF32Net, O, 1, vw1, vb1, vw2, vb2, uw, p->val_b);
+  if (i8) {
+    pack_net_i8x4(b, pw2);
+    pack_net_i8x4(b + lz::kF32Net, vw2);
+  }
   pack_gauss(reinterpret_cast<float*>(b + lz::kF32LogStd), A, p->log_std);
   // c_j 8^-j: the kernel's Horner runs in u = 8 t (tanh_tab)
   float* tt = reinterpret_cast<float*>(b + lz::kF32Tanh);

@@ -770,10 +770,117 @@ __device__ __forceinline__ void mlp_f32_tail(const uint8_t* w2p, const uint8_t* 
   }
 }
 
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+// the digits of the 4 values of v at scale 2^q: d[i] byte r = digit i of v[r] (the i8x4
+// fixed point of lz_attn_policy_pack_i8x4: V = rint(v 2^q), U = V + 0x808080, digits
+// 0-2 = bytes 0-2 of U minus 128, digit 3 = U >> 24), four bytes per v_perm
+__device__ __forceinline__ void i8x_digits4(const f32x4& v, int q, uint32_t* d) {
+  uint32_t U[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    U[r] = (uint32_t)(int32_t)__builtin_rintf(__builtin_ldexpf(v[r], q)) + 0x808080u;
+  const uint32_t t0 = __builtin_amdgcn_perm(U[1], U[0], 0x05010400u);  // U0.b0 U1.b0 U0.b1 U1.b1
+  const uint32_t t1 = __builtin_amdgcn_perm(U[1], U[0], 0x07030602u);  // U0.b2 U1.b2 U0.b3 U1.b3
+  const uint32_t t2 = __builtin_amdgcn_perm(U[3], U[2], 0x05010400u);
+  const uint32_t t3 = __builtin_amdgcn_perm(U[3], U[2], 0x07030602u);
+  d[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u) ^ 0x80808080u;
+  d[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u) ^ 0x80808080u;
+  d[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u) ^ 0x80808080u;
+  d[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+}
+
+__device__ __forceinline__ float i8x_recombine(int l6, int l5, int l4, int l3, int sh) {
+  const int hi = l6 * 256 + l5, lo = l4 * 256 + l3;
+  return __builtin_ldexpf(fmaf((float)hi, 65536.0f, (float)lo), sh);
+}
+
+__device__ __forceinline__ i32x16 mfma_i8_32(i32x4 a, i32x4 b, i32x16 c) {
+  return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+}
+
+// mlp_f32_tail with layer 2 as exact i8x4 fixed-point products (LZ_POLICY_I8X4,
+// lz_policy_pack_i8x4; oracle orc_mlp_i8x4).  Layer 1's tanh outputs at scale 2^28 are
+// the B operand of v_mfma_i32_32x32x32_i8 as they sit: k-block kb = layer-1 tile kb, byte
+// j of lane (env, h) = its register j (unit 32 kb + row(j, h)); the packer lays W2 out to
+// match ([T][kb][digit][64 lanes][16 B]).  The 10 digit products of levels 6..3 per
+// k-block accumulate in int32 (exact, order-free); y = ldexp(fma(float(L6 256 + L5),
+// 2^16, float(L4 256 + L3)), 24 - q_row - 28) + b2, then tanh_tab and the heads exactly as
+// the float32 tail.  The int8 MFMA issues beside the VALU (the float32 one shares it).
+// An env with a NaN among its layer-1 outputs gets NaN heads (the digits cannot carry it).
+template <int NH>
+__device__ __forceinline__ void mlp_i8_tail(const uint8_t* net, const f32x16* a1, int lane, float* head,
+                                            const float* ttab) {
+  const int h = lane >> 5;
+  const i32x4* w2 = reinterpret_cast<const i32x4*>(net + kF32W2) + lane;
+  const f32x16* b2 = reinterpret_cast<const f32x16*>(net + kF32B2) + h;
+  const int16_t* sh2 = reinterpret_cast<const int16_t*>(net + kF32Sh2) + h * 16;
+  const float* wh = reinterpret_cast<const float*>(net + kF32H) + h * 64;
+  const float* bh = reinterpret_cast<const float*>(net + kF32HB);
+  i32x4 xd[4][4];  // [k-block][digit]
+  float chk = 0.0f;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x4 v = {a1[kb][4 * e], a1[kb][4 * e + 1], a1[kb][4 * e + 2], a1[kb][4 * e + 3]};
+      chk += (v[0] + v[1]) + (v[2] + v[3]);
+      uint32_t d[4];
+      i8x_digits4(v, 28, d);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xd[kb][i][e] = (int)d[i];
+    }
+  }
+  const bool bad = __builtin_isnan(chk + __shfl_xor(chk, 32, 64));
+  float acc[NH];
+#pragma unroll
+  for (int j = 0; j < NH; ++j) acc[j] = 0.0f;
+#pragma unroll 1
+  for (int t = 0; t < 4; ++t) {
+    const i32x16 z = {};
+    i32x16 L6 = z, L5 = z, L4 = z, L3 = z;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      asm volatile("" ::: "memory");
+      const i32x4* wp = w2 + (t * 4 + kb) * 4 * 64;
+      const i32x4 w0 = wp[0], w1 = wp[64], w2d = wp[128], w3 = wp[192];
+      L6 = mfma_i8_32(w3, xd[kb][3], L6);
+      L5 = mfma_i8_32(w3, xd[kb][2], L5);
+      L5 = mfma_i8_32(w2d, xd[kb][3], L5);
+      L4 = mfma_i8_32(w3, xd[kb][1], L4);
+      L4 = mfma_i8_32(w2d, xd[kb][2], L4);
+      L4 = mfma_i8_32(w1, xd[kb][3], L4);
+      L3 = mfma_i8_32(w3, xd[kb][0], L3);
+      L3 = mfma_i8_32(w2d, xd[kb][1], L3);
+      L3 = mfma_i8_32(w1, xd[kb][2], L3);
+      L3 = mfma_i8_32(w0, xd[kb][3], L3);
+    }
+    const f32x16 bias = b2[2 * t];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const float y = i8x_recombine(L6[g], L5[g], L4[g], L3[g], sh2[t * 32 + g]) + bias[g];
+      const float v = tanh_tab(y, ttab);
+#pragma unroll
+      for (int j = 0; j < NH; ++j) {
+        const float w = wh[j * 128 + t * 16 + g];
+        acc[j] = fmaf(w, v, acc[j]);
+      }
+      if ((g & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NH; ++j) {
+    const float o = __shfl_xor(acc[j], 32, 64);
+    const float r = (acc[j] + o) + bh[j];
+    head[j] = bad ? __builtin_nanf("") : r;
+  }
+}
+
 // One net on the wave's 32-env tile.  xs[s] = this lane's layer-1 input for k-step s
 // (obs[2s + h] of env lane & 31).  Returns the NH head rows in head[] on every lane
-// (both halves hold the same values).
-template <int KS1, int NH>
+// (both halves hold the same values).  kI8: layer 2 as mlp_i8_tail.
+template <int KS1, int NH, bool kI8 = false>
 __device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int lane, float* head,
                                         const float* ttab) {
   asm volatile("" ::: "memory");
@@ -793,7 +900,8 @@ __device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int
     }
     a1[t] = c;
   }
-  mlp_f32_tail<NH>(net + kF32W2, net + kF32B2, net + kF32H, net + kF32HB, a1, lane, head, ttab);
+  if constexpr (kI8) mlp_i8_tail<NH>(net, a1, lane, head, ttab);
+  else mlp_f32_tail<NH>(net + kF32W2, net + kF32B2, net + kF32H, net + kF32HB, a1, lane, head, ttab);
 }
 
 // this lane's layer-1 inputs from the env-owning lane (half 0) of its env
@@ -813,7 +921,8 @@ __device__ __forceinline__ void f32_inputs(const float* x, int lane, float* xs) 
 // code/train.py's attention actor-critic, code/lorenz_filter/train.py's residual +
 // LayerNorm attention actor-critic on VecFrameStack observations.
 constexpr int kMlpSerial = 0, kMlpPair = 1, kMlpPairPipe = 2, kAttn = 3, kAttnLn = 4,
-              kMlpF32 = 5;
+              kMlpF32 = 5, kMlpI8 = 6;  // kMlpI8: kMlpF32 with layer 2 as mlp_i8_tail
+constexpr bool mlp_f32_kind(int k) { return k == kMlpF32 || k == kMlpI8; }
 
 // V(x) alone (truncation bootstrap, last values): the value net, after the shared
 // attention extractor for kPair == kAttn
@@ -824,10 +933,10 @@ __device__ __forceinline__ void value_fwd(const uint8_t* blob, const uint8_t* vf
     bf16x8 f[4];
     attn_extract(blob, obs_frag<O>(x, use), lane, f);
     out[0] = attn_net(blob + kAttVf, f, lane)[0];
-  } else if constexpr (kPair == kMlpF32) {
+  } else if constexpr (mlp_f32_kind(kPair)) {
     float xs[(O + 1) / 2];
     f32_inputs<O, (O + 1) / 2>(x, lane, xs);
-    mlp_f32<(O + 1) / 2, 1>(vf_net, xs, lane, out,
+    mlp_f32<(O + 1) / 2, 1, kPair == kMlpI8>(vf_net, xs, lane, out,
                             reinterpret_cast<const float*>(blob + kF32Tanh));
   } else {
     net_fwd<E, O, 1>(vf_net, x, use, lane, out);
@@ -844,8 +953,8 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   static_assert(kPair == kMlpSerial || E == 32, "the paired / attention kernels run 32-env tiles");
   constexpr int kBlob = kPair == kAttnLn ? kLnBlobBytes
                         : kPair == kAttn ? kAttBlobBytes
-                        : kPair == kMlpF32 ? kF32BlobBytes : kPolBlobBytes;
-  constexpr bool kRegMom = kPair == kMlpF32;  // obs moments in registers, not LDS
+                        : mlp_f32_kind(kPair) ? kF32BlobBytes : kPolBlobBytes;
+  constexpr bool kRegMom = mlp_f32_kind(kPair);  // obs moments in registers, not LDS
   constexpr int O = Sys::O, A = Sys::A;
   constexpr int SO = S * O, KS = (SO + 15) / 16;  // kAttnLn: stacked dims, fc1 k-steps
   static_assert(kPair == kAttnLn || S == 1, "frame stacking is the kAttnLn path");
@@ -876,14 +985,14 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   __syncthreads();
   const uint8_t* pi_net = s_blob + (kPair == kAttnLn ? kLnPi : kPair == kAttn ? kAttPi : 0);
   const uint8_t* vf_net =
-      s_blob + (kPair == kAttnLn ? kLnVf : kPair == kAttn ? kAttVf : kPair == kMlpF32 ? kF32Net : kPolNet);
+      s_blob + (kPair == kAttnLn ? kLnVf : kPair == kAttn ? kAttVf : mlp_f32_kind(kPair) ? kF32Net : kPolNet);
   // torch.distributions.Normal constants, computed by the packer: scale = exp(log_std),
   // 2 * scale**2, log(scale) (LDS, wave-uniform broadcast reads)
   const float* g_scale =
       reinterpret_cast<const float*>(
           s_blob + (kPair == kAttnLn   ? kLnLogStd
                     : kPair == kAttn   ? kAttLogStd
-                    : kPair == kMlpF32 ? kF32LogStd : kPolLogStd)) + 4;
+                    : mlp_f32_kind(kPair) ? kF32LogStd : kPolLogStd)) + 4;
   const float* g_var2 = g_scale + 4;
   const float* g_lscale = g_scale + 8;
   const bool norm = p.norm != nullptr;
@@ -968,13 +1077,14 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
 #pragma unroll
         for (int j = 0; j < A; ++j) mean[j] = hp[j];
         val[0] = hv[0];
-      } else if constexpr (kPair == kMlpF32) {
+      } else if constexpr (mlp_f32_kind(kPair)) {
+        constexpr bool kI8 = kPair == kMlpI8;
         float xs[(O + 1) / 2];
         f32_inputs<O, (O + 1) / 2>(x, lane, xs);
         const float* ttab = reinterpret_cast<const float*>(s_blob + kF32Tanh);
-        mlp_f32<(O + 1) / 2, A>(pi_net, xs, lane, mean, ttab);
+        mlp_f32<(O + 1) / 2, A, kI8>(pi_net, xs, lane, mean, ttab);
         __builtin_amdgcn_sched_barrier(0);  // the two nets one after the other
-        mlp_f32<(O + 1) / 2, 1>(vf_net, xs, lane, val, ttab);
+        mlp_f32<(O + 1) / 2, 1, kI8>(vf_net, xs, lane, val, ttab);
       } else if constexpr (kPair == kMlpPair || kPair == kMlpPairPipe) {
         f32x16 hp, hv;
         if constexpr (kPair == kMlpPairPipe)
@@ -1136,8 +1246,9 @@ __device__ __forceinline__ void lds_barrier() {
 // writes step k's next obs, terminal obs, reward and done code between barriers M_k and
 // B_k; the critic reads them between B_k and M_{k+1}, then evaluates V(x_{k+1}) (and
 // step k's bootstraps) while the actor runs step k + 1.
-template <class Sys>
+template <class Sys, bool kI8 = false>
 __global__ __launch_bounds__(512) void k_rollout_policy_f32_split(KArgs a, PArgs p) {
+  constexpr int kKind = kI8 ? kMlpI8 : kMlpF32;
   constexpr int O = Sys::O, A = Sys::A, KS1 = (O + 1) / 2, T = 4;  // T tiles per workgroup
   static_assert(O <= kPolMaxObs && A <= kPolMaxAct, "policy tile shape");
   __shared__ __attribute__((aligned(64))) uint8_t s_blob[kF32BlobBytes];
@@ -1213,7 +1324,7 @@ __global__ __launch_bounds__(512) void k_rollout_policy_f32_split(KArgs a, PArgs
         }
         float xs[KS1], mean[A];
         f32_inputs<O, KS1>(x, lane, xs);
-        mlp_f32<KS1, A>(pi_net, xs, lane, mean, ttab);
+        mlp_f32<KS1, A, kI8>(pi_net, xs, lane, mean, ttab);
         float act_c[A];
         if (live) {
           float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1293,7 +1404,7 @@ __global__ __launch_bounds__(512) void k_rollout_policy_f32_split(KArgs a, PArgs
           if (__ballot(bt) != 0ull) {
             float xt[O], vt[1];
             normalize<O>(ot, xt, norm, mu, sd, p.clip);
-            value_fwd<32, O, kMlpF32>(s_blob, vf_net, xt, bt, lane, vt);
+            value_fwd<32, O, kKind>(s_blob, vf_net, xt, bt, lane, vt);
             if (bt) rew = rew + gamma * vt[0];
           }
         }
@@ -1306,7 +1417,7 @@ __global__ __launch_bounds__(512) void k_rollout_policy_f32_split(KArgs a, PArgs
         float x[O], xs[KS1], val[1];
         normalize<O>(o, x, norm, mu, sd, p.clip);
         f32_inputs<O, KS1>(x, lane, xs);
-        mlp_f32<KS1, 1>(vf_net, xs, lane, val, ttab);
+        mlp_f32<KS1, 1, kI8>(vf_net, xs, lane, val, ttab);
         if (live) p.val[(int64_t)k * a.n + i] = val[0];
         lds_barrier();  // B_k
       }
@@ -1314,7 +1425,7 @@ __global__ __launch_bounds__(512) void k_rollout_policy_f32_split(KArgs a, PArgs
       settle(a.K - 1);
       float x[O], vl[1];
       normalize<O>(o, x, norm, mu, sd, p.clip);
-      value_fwd<32, O, kMlpF32>(s_blob, vf_net, x, live, lane, vl);
+      value_fwd<32, O, kKind>(s_blob, vf_net, x, live, lane, vl);
       if (live) p.last_val[i] = vl[0];
     }
   }
@@ -1555,26 +1666,9 @@ __device__ __forceinline__ float group_sum4(float v) {
   return v + __shfl_xor(v, 32, 64);
 }
 
-typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
   return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
-}
-
-// the digits of the 4 values of v at scale 2^q: d[i] byte r = digit i of v[r]
-__device__ __forceinline__ void i8x_digits4(const f32x4& v, int q, uint32_t* d) {
-  uint32_t U[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    U[r] = (uint32_t)(int32_t)__builtin_rintf(__builtin_ldexpf(v[r], q)) + 0x808080u;
-  const uint32_t t0 = __builtin_amdgcn_perm(U[1], U[0], 0x05010400u);  // U0.b0 U1.b0 U0.b1 U1.b1
-  const uint32_t t1 = __builtin_amdgcn_perm(U[1], U[0], 0x07030602u);  // U0.b2 U1.b2 U0.b3 U1.b3
-  const uint32_t t2 = __builtin_amdgcn_perm(U[3], U[2], 0x05010400u);
-  const uint32_t t3 = __builtin_amdgcn_perm(U[3], U[2], 0x07030602u);
-  d[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u) ^ 0x80808080u;
-  d[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u) ^ 0x80808080u;
-  d[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u) ^ 0x80808080u;
-  d[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
 }
 
 // one 16-unit tile over KB k-blocks: w(kb, i) the weight digits, x[kb][i] the inputs'
@@ -1597,11 +1691,6 @@ __device__ __forceinline__ void i8x_tile(WF w, const i32x4 (*x)[4], i32x4* L) {
     L[3] = mfma_i8(w1, x[kb][2], L[3]);
     L[3] = mfma_i8(w0, x[kb][3], L[3]);
   }
-}
-
-__device__ __forceinline__ float i8x_recombine(int l6, int l5, int l4, int l3, int sh) {
-  const int hi = l6 * 256 + l5, lo = l4 * 256 + l3;
-  return __builtin_ldexpf(fmaf((float)hi, 65536.0f, (float)lo), sh);
 }
 
 // the 64 features (4 tiles) of one input; xs[s] = this lane group's fc1 input of k-step
@@ -2450,17 +2539,30 @@ static int launch_pol(const KArgs& a, const PArgs& p, const PolShape& sh, hipStr
   return (int)hipGetLastError();
 }
 
-template <class Sys>
-static int launch_pol_f32(const KArgs& a, const PArgs& p, const PolShape& sh, hipStream_t s) {
+template <class Sys, bool kI8>
+static void launch_pol_f32_k(const KArgs& a, const PArgs& p, const PolShape& sh, hipStream_t s) {
+  constexpr int kKind = kI8 ? kMlpI8 : kMlpF32;
   if (sh.pair == 1)
-    hipLaunchKernelGGL((k_rollout_policy_f32_split<Sys>), dim3((unsigned)sh.grid), dim3(8 * 64), 0, s, a,
-                       p);
+    hipLaunchKernelGGL((k_rollout_policy_f32_split<Sys, kI8>), dim3((unsigned)sh.grid), dim3(8 * 64), 0, s,
+                       a, p);
   else if (sh.waves == 4)
-    hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, kMlpF32>), dim3((unsigned)sh.grid), dim3(4 * 64), 0, s,
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 4, 32, kKind>), dim3((unsigned)sh.grid), dim3(4 * 64), 0, s,
                        a, p);
   else
-    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 32, kMlpF32>), dim3((unsigned)sh.grid), dim3(8 * 64), 0, s,
+    hipLaunchKernelGGL((k_rollout_policy<Sys, 8, 32, kKind>), dim3((unsigned)sh.grid), dim3(8 * 64), 0, s,
                        a, p);
+}
+
+// kI8: LZ_POLICY_I8X4 is built for the four systems of the reference's training scripts
+// (LORENZ3 / LORENZ4 / PMSM / HR); the others refuse it
+template <class Sys, bool kHasI8 = false>
+static int launch_pol_f32(const KArgs& a, const PArgs& p, const PolShape& sh, hipStream_t s) {
+  if (p.pflags & LZ_POLICY_I8X4) {
+    if constexpr (kHasI8) launch_pol_f32_k<Sys, true>(a, p, sh, s);
+    else return (int)hipErrorInvalidValue;
+  } else {
+    launch_pol_f32_k<Sys, false>(a, p, sh, s);
+  }
   return (int)hipGetLastError();
 }
 
@@ -2488,10 +2590,10 @@ int launch_rollout_policy_f32(int system, const KArgs& a, const PArgs& p, const 
                               void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (system) {
-    case LZ_SYS_LORENZ3: return launch_pol_f32<SysL3<float>>(a, p, grid, s);
-    case LZ_SYS_LORENZ4: return launch_pol_f32<SysL4<float>>(a, p, grid, s);
-    case LZ_SYS_PMSM: return launch_pol_f32<SysPMSM>(a, p, grid, s);
-    case LZ_SYS_HR: return launch_pol_f32<SysHR<float>>(a, p, grid, s);
+    case LZ_SYS_LORENZ3: return launch_pol_f32<SysL3<float>, true>(a, p, grid, s);
+    case LZ_SYS_LORENZ4: return launch_pol_f32<SysL4<float>, true>(a, p, grid, s);
+    case LZ_SYS_PMSM: return launch_pol_f32<SysPMSM, true>(a, p, grid, s);
+    case LZ_SYS_HR: return launch_pol_f32<SysHR<float>, true>(a, p, grid, s);
     case LZ_SYS_T1: return launch_pol_f32<SysT1<float>>(a, p, grid, s);
     case LZ_SYS_T2: return launch_pol_f32<SysT2<float>>(a, p, grid, s);
     case LZ_SYS_TP: return launch_pol_f32<SysTP<float>>(a, p, grid, s);

@@ -221,6 +221,8 @@ _SIGS = {
     "lz_attn_policy_pack_f32": (ctypes.c_int, [ctypes.POINTER(LzAttnPolicy), VP, ctypes.c_int64]),
     "lz_attn_ln_policy_pack_f32": (ctypes.c_int, [ctypes.POINTER(LzAttnLnPolicy), VP, ctypes.c_int64]),
     "lz_attn_policy_pack_i8x4": (ctypes.c_int, [ctypes.POINTER(LzAttnPolicy), VP, ctypes.c_int64]),
+    "lz_policy_pack_i8x4": (ctypes.c_int, [ctypes.POINTER(LzMlpPolicy), ctypes.c_int32, VP,
+                                           ctypes.c_int64]),
     "lz_attn_ln_policy_pack_i8x4": (ctypes.c_int, [ctypes.POINTER(LzAttnLnPolicy), VP, ctypes.c_int64]),
     "lz_rollout_policy_attn_f32": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
     "lz_rollout_policy_attn_stack_f32": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs),

@@ -379,6 +379,15 @@ def pack_policy_f32(state_dict, obs_dim, act_dim):
     return blob
 
 
+def pack_policy_i8x4(state_dict, obs_dim, act_dim):
+    """lz_policy_pack_i8x4: the float32 MlpPolicy blob with each net's layer 2 as exact
+    4-digit int8 fixed-point products (precision="i8x4"; oracle orc_mlp_i8x4)."""
+    p, H, _keep = _mlp_policy_struct(state_dict, obs_dim, act_dim)
+    blob = np.zeros(int(nat.lib.lz_policy_f32_blob_bytes()), np.uint8)
+    nat.check(nat.lib.lz_policy_pack_i8x4(ctypes.byref(p), H, blob.ctypes.data, blob.size))
+    return blob
+
+
 def pack_policy(state_dict, obs_dim, act_dim):
     """lz_policy_pack / lz_policy_pack_hidden: SB3 state_dict (net_arch pi=[H,H]
     vf=[H,H], H <= 128) -> uint8 numpy blob of the bf16 kernel (host; needs no GPU)."""
@@ -551,10 +560,12 @@ class FusedRolloutCollector:
     precision:     policy arithmetic: "fp32" (default; SB3's float32 forward --
                    lz_rollout_policy_f32, and for the attention actor-critics of
                    code/train.py / code/lorenz_filter/train.py lz_rollout_policy_attn_f32 /
-                   _attn_stack_f32), "i8x4" (attention actor-critics only: the same
-                   kernels with the pi / vf nets' wide layers as exact 4-digit int8
-                   fixed-point products on the int8 MFMA -- float32-level accuracy,
-                   bit-exact vs orc_attn_i8x4, not bit-equal to "fp32") or "bf16" (bf16 MFMA
+                   _attn_stack_f32), "i8x4" (the same float32 kernels with the pi / vf
+                   nets' wide layers as exact 4-digit int8 fixed-point products on the
+                   int8 MFMA -- float32-level accuracy, bit-exact vs orc_attn_i8x4 /
+                   orc_mlp_i8x4, not bit-equal to "fp32"; the MlpPolicy one without the
+                   per-step VecNormalize collect, and for LORENZ3 / LORENZ4 / PMSM / HR)
+                   or "bf16" (bf16 MFMA
                    operands, fp32 accumulation: lz_rollout_policy / _attn / _attn_stack,
                    ~2.5-5x faster, ~1e-2 off SB3).
     """
@@ -610,8 +621,11 @@ class FusedRolloutCollector:
         self.f32 = self.precision != "bf16"
         self.i8x4 = self.precision == "i8x4"
         if self.i8x4 and not (self.attention or self.attention_ln):
-            raise ValueError("precision='i8x4' runs the attention actor-critics (code/train.py, "
-                             "code/lorenz_filter/train.py)")
+            if self.env.system_name not in ("lorenz3", "lorenz4", "pmsm", "hr"):
+                raise ValueError("the i8x4 MlpPolicy runs LORENZ3 / LORENZ4 / PMSM / HR")
+            if self.obs_rms is not None and self.training and self.vecnorm_update != "rollout":
+                raise ValueError("precision='i8x4' with a training VecNormalize needs "
+                                 "vecnorm_update='rollout' (the per-step collect is float32)")
         if self.attention_ln:
             if self.obs_rms is not None:
                 raise ValueError("the LayerNorm attention rollout takes raw observations")
@@ -622,7 +636,8 @@ class FusedRolloutCollector:
             blob = (pack_attn_policy_i8x4 if self.i8x4 else
                     pack_attn_policy_f32 if self.f32 else pack_attn_policy)(state_dict, self.O, self.A)
         else:
-            blob = (pack_policy_f32 if self.f32 else pack_policy)(state_dict, self.O, self.A)
+            blob = (pack_policy_i8x4 if self.i8x4 else
+                    pack_policy_f32 if self.f32 else pack_policy)(state_dict, self.O, self.A)
         if self.vecnorm_update == "step" and (not self.f32 or self.attention or self.attention_ln):
             raise ValueError("vecnorm_update='step' runs the float32 MlpPolicy kernel")
         self.blob = torch.from_numpy(blob).to(self.device)

@@ -311,8 +311,8 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
 #define LZ_POLICY_HIDDEN 128
 #define LZ_POLICY_DETERMINISTIC 1u /* action = mean (SB3 predict(deterministic=True)) */
 #define LZ_POLICY_BOOTSTRAP 2u     /* reward += gamma * V(terminal obs) when truncated */
-#define LZ_POLICY_I8X4 4u          /* the blob is an lz_attn*_policy_pack_i8x4 blob (attention
-                                      f32 rollouts only; see there) */
+#define LZ_POLICY_I8X4 4u          /* the blob is an lz_*policy_pack_i8x4 blob (the float32
+                                      attention / MlpPolicy rollouts; see there) */
 
 /* Float32 weights in torch nn.Linear layout ([out, in], row-major), host memory.
  * Names are the SB3 ActorCriticPolicy state_dict keys. */
@@ -519,6 +519,11 @@ lz_status lz_rollout_policy_attn_f32(lz_handle* h, const lz_policy_rollout_args*
  * feature makes all of that env's outputs NaN.  The packers refuse non-finite net weights.
  * The extractor, softmax, heads and everything else are the float32 path's. */
 lz_status lz_attn_policy_pack_i8x4(const lz_attn_policy* p, void* host_blob, int64_t cap);
+/* The same opt-in precision for the float32 MlpPolicy (lz_rollout_policy_f32 with
+ * LZ_POLICY_I8X4; not the per-step VecNormalize collect, lz_policy_step_f32): layer 2 of
+ * each net (128 -> 128) on v_mfma_i32_32x32x32_i8 as above, layer 1 and the heads as the
+ * float32 path; systems LORENZ3 / LORENZ4 / PMSM / HR.  Oracle: orc_mlp_i8x4. */
+lz_status lz_policy_pack_i8x4(const lz_mlp_policy* p, int32_t hidden, void* host_blob, int64_t cap);
 lz_status lz_attn_ln_policy_pack_i8x4(const lz_attn_ln_policy* p, void* host_blob, int64_t cap);
 lz_status lz_rollout_policy_attn_stack_f32(lz_handle* h, const lz_policy_rollout_args* r,
                                            int32_t n_stack, const float* stack_in,

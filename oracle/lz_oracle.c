@@ -1162,3 +1162,72 @@ void orc_attn_i8x4(int64_t n, int in_dim, int A, const float* x, const float* fc
     attn_net_one_i8x(1, feat, &vf, vf_b1, vf_b2, val_w, val_b, value + i);
   }
 }
+
+/* orc_mlp_f32 with layer 2 as exact i8x4 products (lz_policy_pack_i8x4, LZ_POLICY_I8X4;
+ * lz_policy.hip mlp_i8_tail): layer 1, tanh_tab and the heads as mlp_f32_one; layer 2's
+ * inputs (tanh outputs, |a| <= 1) at q = 28, its 128 (zero-padded) rows at their own q;
+ * y[u] = orc_i8x_dot(row u, a, 24 - q2[u] - 28) + b2[u] -> tanh_tab.  A NaN among an env's
+ * layer-1 outputs makes that env's outputs NaN. */
+static void mlp_i8x_one(int O, int H, int R, const float* x, const float* w1, const float* b1,
+                        const int8_t* d2, const int32_t* q2, const float* b2, const float* w3,
+                        const float* b3, float* out) {
+  float a1[128], a2[128];
+  int nan = 0;
+  for (int u = 0; u < 128; ++u) {
+    float acc = u < H ? b1[u] : 0.0f;
+    for (int s = 0; s < (O + 1) / 2; ++s)
+      for (int h = 0; h < 2; ++h) {
+        const int k = 2 * s + h;
+        const float w = (u < H && k < O) ? w1[u * O + k] : 0.0f;
+        acc = fmaf(w, k < O ? x[k] : 0.0f, acc);
+      }
+    a1[u] = orc_tanh_tab(acc);
+    nan |= a1[u] != a1[u];
+  }
+  if (nan) {
+    for (int r = 0; r < R; ++r) out[r] = NAN;
+    return;
+  }
+  int8_t ad[128 * 4];
+  for (int k = 0; k < 128; ++k) i8x_digits(i8x_fixed(a1[k], 28), ad + 4 * k);
+  for (int u = 0; u < 128; ++u)
+    a2[u] = orc_tanh_tab(orc_i8x_dot(128, d2 + 4 * 128 * u, ad, 24 - q2[u] - 28) + (u < H ? b2[u] : 0.0f));
+  for (int r = 0; r < R; ++r) {
+    float part[2];
+    for (int h = 0; h < 2; ++h) {
+      float acc = 0.0f;
+      for (int t = 0; t < 4; ++t)
+        for (int g = 0; g < 16; ++g) {
+          const int k = 32 * t + pol_row(g, h);
+          acc = fmaf(k < H ? w3[r * H + k] : 0.0f, a2[k], acc);
+        }
+      part[h] = acc;
+    }
+    out[r] = (part[0] + part[1]) + b3[r];
+  }
+}
+
+/* the 128 x 128 zero-padded layer-2 digits and row q's of an [H, H] weight */
+static void i8x_prep_w2(int H, const float* w2, int8_t* d2, int32_t* q2) {
+  float row[128];
+  for (int u = 0; u < 128; ++u) {
+    for (int k = 0; k < 128; ++k) row[k] = (u < H && k < H) ? w2[u * H + k] : 0.0f;
+    q2[u] = orc_i8x_row_q(row, 128);
+    for (int k = 0; k < 128; ++k) i8x_digits(i8x_fixed(row[k], q2[u]), d2 + 4 * (u * 128 + k));
+  }
+}
+
+void orc_mlp_i8x4(int64_t n, int O, int A, int H, const float* x, const float* pi_w1,
+                  const float* pi_b1, const float* pi_w2, const float* pi_b2, const float* vf_w1,
+                  const float* vf_b1, const float* vf_w2, const float* vf_b2, const float* act_w,
+                  const float* act_b, const float* val_w, const float* val_b, float* mean,
+                  float* value) {
+  static int8_t pd[128 * 128 * 4], vd[128 * 128 * 4];  /* (not reentrant: test infrastructure) */
+  int32_t pq[128], vq[128];
+  i8x_prep_w2(H, pi_w2, pd, pq);
+  i8x_prep_w2(H, vf_w2, vd, vq);
+  for (int64_t i = 0; i < n; ++i) {
+    mlp_i8x_one(O, H, A, x + i * O, pi_w1, pi_b1, pd, pq, pi_b2, act_w, act_b, mean + i * A);
+    mlp_i8x_one(O, H, 1, x + i * O, vf_w1, vf_b1, vd, vq, vf_b2, val_w, val_b, value + i);
+  }
+}

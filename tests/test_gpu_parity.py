@@ -454,21 +454,26 @@ def test_rollout_equals_steps(gl, system, dtype, n):
 
 
 @pytest.mark.parametrize("system,dtype,n,K", [("pmsm", "float32", 32768, 300), ("hr", "float32", 65536, 200),
-                                              ("hr", "float64", 4160, 100), ("pmsm", "float32", 4097, 100)])
+                                              ("hr", "float64", 4160, 100), ("pmsm", "float32", 4097, 100),
+                                              ("pmsm", "float32", 140001, 40)])
 def test_rollout_noise_producer_equals_steps(gl, system, dtype, n, K):
-    """One-wave rollout of a system with process noise, with the opt-in noise-producer wave
-    (variant bit 1<<25: a second wave per group draws the normals ahead into an LDS ring,
-    k_rollout_np, lz_kernels.hip -- reported as 2 waves per group) and without it (the
-    default): each equals K lz_step calls (which draw their own) bit for bit: obs, reward,
-    done, the compact done list and the final state; ragged sizes run the last group
-    without a producer."""
+    """Rollout of a system with process noise: the default (each step draws its normals),
+    the opt-in noise-producer wave (variant bit 1<<25, one-wave groups only: a second wave
+    per group draws the normals ahead into an LDS ring, k_rollout_np, lz_kernels.hip --
+    reported as 2 waves per group) and the software-pipelined draws (variant bit 1<<26,
+    kZN: the next step's normals drawn in registers during this step) each equal K lz_step
+    calls (which draw their own) bit for bit: obs, reward, done, the compact done list and
+    the final state; ragged sizes run the last group without a producer; 140,001 envs run
+    the 256-lane kernel."""
     from gym_lorenz import _native as nat
 
-    for variant in (0, 1 << 25):
+    one_wave = n < 131072
+    for variant in ((0, 1 << 25, 1 << 26) if one_wave else (0, 1 << 26)):
         a_be = gl.BatchedEnv(system, n, dtype=dtype, seed=9, max_episode_steps=37, add_noise=True, variant=variant)
         b_be = gl.BatchedEnv(system, n, dtype=dtype, seed=9, max_episode_steps=37, add_noise=True)
         sh = nat.launch_shape(a_be._h, nat.CALL_ROLLOUT)
-        assert sh["kernel"] == "rollout_wave" and sh["waves"] == (2 if variant else 1), sh
+        assert sh["kernel"] == ("rollout_wave" if one_wave else "rollout"), sh
+        assert sh["waves"] == (2 if variant == 1 << 25 else 1 if one_wave else 4), sh
         a_be.reset()
         b_be.reset()
         A = torch.from_numpy(np.random.default_rng(5).uniform(-1.2, 1.2, (K, n, a_be.action_dim))

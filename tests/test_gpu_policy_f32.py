@@ -30,7 +30,7 @@ from test_policy_f32_host import GOLD, normalize_obs, oracle_closed_loop
 
 pytestmark = pytest.mark.gpu
 
-F32_LOGSTD = 2 * 72768  # lz_internal.h kF32LogStd
+F32_LOGSTD = 2 * 73024  # lz_internal.h kF32LogStd
 
 
 @pytest.fixture(scope="module")

@@ -247,11 +247,10 @@ def test_i8x4_flag_refused_elsewhere(gl, pol):
     from gym_lorenz import _native as nat
 
     env = gl.BatchedEnv("hr", 100, seed=1)
-    sd = _random_attn(pol, 6, 2, seed=5)
-    with pytest.raises(ValueError):  # the MlpPolicy has no i8x4 kernel
-        pol.FusedRolloutCollector(env, pol.ActorCriticMlp(6, 2).state_dict(), precision="i8x4")
-    col = pol.FusedRolloutCollector(env, sd, precision="i8x4")
+    mlp = pol.ActorCriticMlp(6, 2).state_dict()
+    col = pol.FusedRolloutCollector(env, mlp, precision="bf16")
     col.reset()
-    col.attention = False  # route the flagged args to the MlpPolicy kernel: refused
+    col.i8x4 = True  # the flag on the bf16 MlpPolicy kernel: refused before any launch
     with pytest.raises(nat.LorenzEnvError):
         col.collect(2)
+    env.close()

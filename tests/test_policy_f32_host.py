@@ -89,7 +89,7 @@ def _emulate_f32(blob, x, A, orc):
     W1, W2 = 0, 4 * 64 * 16
     B1 = W2 + 4 * 16 * 64 * 16
     B2, H, HB = B1 + 512, B1 + 1024, B1 + 1024 + 2048
-    NET = HB + 64
+    NET = HB + 64 + 256  # kF32Sh2's int16[128] (the i8x4 row shifts) end each net
     f = blob.view(np.float32)
     O = x.shape[1]
     KS1 = (O + 1) // 2

@@ -78,11 +78,33 @@ r4)  # i8x4 with post_attention_fc on the int8 MFMA: parity, A/B vs fp32 and vs 
   bash tools/policy_pmc.sh r05_attn_i8x4 --policy attn --precision i8x4 --system hr --envs 32768 --K 2048 --steps 4096 $BQ || exit 1
   bash tools/policy_pmc.sh r05_attn_fp32 --policy attn --precision fp32 --system hr --envs 32768 --K 2048 --steps 4096 $BQ || exit 1
   ;;
+mlp)  # i8x4 MlpPolicy: parity, then fp32 vs i8x4 at cfg5's 32,768 envs (split kernel) and at 1M (8 / 4 waves)
+  timeout -k 10 900 $PYT -m gpu --maxfail=5 tests/test_gpu_policy_mlp_i8x4.py tests/test_gpu_policy_f32.py \
+    "tests/test_gpu_policy_i8x4.py::test_i8x4_flag_refused_elsewhere" > $O/mlp_tests.txt 2>&1 || exit 1
+  PB="--mode policy --system pmsm --vecnorm-update rollout $BQ"
+  for r in 1 2; do for p in fp32 i8x4; do
+    timeout -k 10 200 python bench.py $PB --envs 32768 --K 2048 --steps 4096 --precision $p > $O/mlp32k_${p}_$r.json 2>> $O/bench.err || exit 1
+    timeout -k 10 200 python bench.py $PB --envs 1048576 --K 64 --steps 256 --precision $p > $O/mlp1m_${p}_$r.json 2>> $O/bench.err || exit 1
+    LZ_POL_F32_WAVES=4 timeout -k 10 200 python bench.py $PB --envs 1048576 --K 64 --steps 256 --precision $p > $O/mlp1m_w4_${p}_$r.json 2>> $O/bench.err || exit 1
+  done; done
+  ;;
+zn)  # software-pipelined noise draws in the PMSM / HR rollouts (variant 1<<26): parity, then A/B
+  timeout -k 10 600 $PYT -m gpu --maxfail=3 "tests/test_gpu_parity.py::test_rollout_noise_producer_equals_steps" \
+    > $O/zn_tests.txt 2>&1 || exit 1
+  for r in 1 2 3; do for sys in pmsm hr; do for n in 32768 4097 65536; do for v in 0 67108864; do
+    timeout -k 10 200 python bench.py --system $sys --mode rollout --K 2048 --envs $n --steps 4096 --warmup 2048 \
+      --add-noise 1 --variant $v $BQ > $O/${sys}_${n}_v${v}_$r.json 2>> $O/zn.err || exit 1
+  done; done; done; done
+  ;;
 full)
   timeout -k 10 1000 $PYT -x -m gpu tests > $O/gpu_tests.txt 2>&1 || exit 1
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" > $O/smoke.txt 2>&1
   ;;
 bench)
+  timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 1
+  timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $O/bench_steps20.json 2> $O/bench_steps20.err || exit 1
+  ;;
+bench_all)
   timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 1
   timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $O/bench_steps20.json 2> $O/bench_steps20.err || exit 1
   LZ_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 > $O/bench_gpus2_gloo.json 2> $O/bench_gpus2_gloo.err
