@@ -804,62 +804,68 @@ __device__ __forceinline__ i32x16 mfma_i8_32(i32x4 a, i32x4 b, i32x16 c) {
 // lz_policy_pack_i8x4; oracle orc_mlp_i8x4).  Layer 1's tanh outputs at scale 2^28 are
 // the B operand of v_mfma_i32_32x32x32_i8 as they sit: k-block kb = layer-1 tile kb, byte
 // j of lane (env, h) = its register j (unit 32 kb + row(j, h)); the packer lays W2 out to
-// match ([T][kb][digit][64 lanes][16 B]).  The 10 digit products of levels 6..3 per
-// k-block accumulate in int32 (exact, order-free); y = ldexp(fma(float(L6 256 + L5),
-// 2^16, float(L4 256 + L3)), 24 - q_row - 28) + b2, then tanh_tab and the heads exactly as
-// the float32 tail.  The int8 MFMA issues beside the VALU (the float32 one shares it).
-// An env with a NaN among its layer-1 outputs gets NaN heads (the digits cannot carry it).
+// match ([T][kb][digit][64 lanes][16 B]).  xd[kb][i] = digit i of tile kb (made by
+// mlp_f32 right after each tile's tanh, so the float activations never all live at once).
+// The 10 digit products of levels 6..3 accumulate in int32 (exact, order-free) in two
+// passes per output tile -- levels 6 + 5 (-> hi = L6 256 + L5), then 4 + 3 (-> lo) -- so
+// two 16-register accumulators are live instead of four (the 512-lane kernels' 256-VGPR
+// budget; the weight digits of w3 / w2 are read twice);
+// y = ldexp(fma(float(hi), 2^16, float(lo)), 24 - q_row - 28) + b2, then tanh_tab and the
+// heads exactly as the float32 tail.  The int8 MFMA issues beside the VALU (the float32
+// one shares it).  An env with a NaN among its layer-1 outputs (bad) gets NaN heads.
 template <int NH>
-__device__ __forceinline__ void mlp_i8_tail(const uint8_t* net, const f32x16* a1, int lane, float* head,
-                                            const float* ttab) {
+__device__ __forceinline__ void mlp_i8_tail(const uint8_t* net, const i32x4 (*xd)[4], bool bad, int lane,
+                                            float* head, const float* ttab) {
   const int h = lane >> 5;
   const i32x4* w2 = reinterpret_cast<const i32x4*>(net + kF32W2) + lane;
   const f32x16* b2 = reinterpret_cast<const f32x16*>(net + kF32B2) + h;
   const int16_t* sh2 = reinterpret_cast<const int16_t*>(net + kF32Sh2) + h * 16;
   const float* wh = reinterpret_cast<const float*>(net + kF32H) + h * 64;
   const float* bh = reinterpret_cast<const float*>(net + kF32HB);
-  i32x4 xd[4][4];  // [k-block][digit]
-  float chk = 0.0f;
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const f32x4 v = {a1[kb][4 * e], a1[kb][4 * e + 1], a1[kb][4 * e + 2], a1[kb][4 * e + 3]};
-      chk += (v[0] + v[1]) + (v[2] + v[3]);
-      uint32_t d[4];
-      i8x_digits4(v, 28, d);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) xd[kb][i][e] = (int)d[i];
-    }
-  }
-  const bool bad = __builtin_isnan(chk + __shfl_xor(chk, 32, 64));
   float acc[NH];
 #pragma unroll
   for (int j = 0; j < NH; ++j) acc[j] = 0.0f;
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll 1
   for (int t = 0; t < 4; ++t) {
+    __builtin_amdgcn_sched_barrier(0);
     const i32x16 z = {};
-    i32x16 L6 = z, L5 = z, L4 = z, L3 = z;
+    const i32x4* wt = w2 + t * 4 * 4 * 64;
+    // hi = L6 256 + L5 and lo = L4 256 + L3 accumulated directly: the first pass sums the
+    // levels 6 and 4 over the k-blocks, both accumulators are shifted left 8 bits, the
+    // second adds levels 5 and 3 (exact: |hi| < 2^24, |lo| < 2^31)
+    i32x16 Hi = z, Lo = z;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       asm volatile("" ::: "memory");
-      const i32x4* wp = w2 + (t * 4 + kb) * 4 * 64;
-      const i32x4 w0 = wp[0], w1 = wp[64], w2d = wp[128], w3 = wp[192];
-      L6 = mfma_i8_32(w3, xd[kb][3], L6);
-      L5 = mfma_i8_32(w3, xd[kb][2], L5);
-      L5 = mfma_i8_32(w2d, xd[kb][3], L5);
-      L4 = mfma_i8_32(w3, xd[kb][1], L4);
-      L4 = mfma_i8_32(w2d, xd[kb][2], L4);
-      L4 = mfma_i8_32(w1, xd[kb][3], L4);
-      L3 = mfma_i8_32(w3, xd[kb][0], L3);
-      L3 = mfma_i8_32(w2d, xd[kb][1], L3);
-      L3 = mfma_i8_32(w1, xd[kb][2], L3);
-      L3 = mfma_i8_32(w0, xd[kb][3], L3);
+      const i32x4* wp = wt + kb * 4 * 64;
+      const i32x4 w1 = wp[64], w2d = wp[128], w3 = wp[192];
+      Hi = mfma_i8_32(w3, xd[kb][3], Hi);
+      Lo = mfma_i8_32(w3, xd[kb][1], Lo);
+      Lo = mfma_i8_32(w2d, xd[kb][2], Lo);
+      Lo = mfma_i8_32(w1, xd[kb][3], Lo);
     }
-    const f32x16 bias = b2[2 * t];
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
-      const float y = i8x_recombine(L6[g], L5[g], L4[g], L3[g], sh2[t * 32 + g]) + bias[g];
+      Hi[g] <<= 8;
+      Lo[g] <<= 8;
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      asm volatile("" ::: "memory");
+      const i32x4* wp = wt + kb * 4 * 64;
+      const i32x4 w0 = wp[0], w1 = wp[64], w2d = wp[128], w3 = wp[192];
+      Hi = mfma_i8_32(w3, xd[kb][2], Hi);
+      Hi = mfma_i8_32(w2d, xd[kb][3], Hi);
+      Lo = mfma_i8_32(w3, xd[kb][0], Lo);
+      Lo = mfma_i8_32(w2d, xd[kb][1], Lo);
+      Lo = mfma_i8_32(w1, xd[kb][2], Lo);
+      Lo = mfma_i8_32(w0, xd[kb][3], Lo);
+    }
+    const float* bias = reinterpret_cast<const float*>(b2 + 2 * t);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const float y = __builtin_ldexpf(fmaf((float)Hi[g], 65536.0f, (float)Lo[g]), sh2[t * 32 + g]) + bias[g];
       const float v = tanh_tab(y, ttab);
 #pragma unroll
       for (int j = 0; j < NH; ++j) {
@@ -879,7 +885,8 @@ __device__ __forceinline__ void mlp_i8_tail(const uint8_t* net, const f32x16* a1
 
 // One net on the wave's 32-env tile.  xs[s] = this lane's layer-1 input for k-step s
 // (obs[2s + h] of env lane & 31).  Returns the NH head rows in head[] on every lane
-// (both halves hold the same values).  kI8: layer 2 as mlp_i8_tail.
+// (both halves hold the same values).  kI8: layer 2 as mlp_i8_tail, layer 1's outputs
+// turned into digits tile by tile.
 template <int KS1, int NH, bool kI8 = false>
 __device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int lane, float* head,
                                         const float* ttab) {
@@ -887,7 +894,9 @@ __device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int
   const int h = lane >> 5;
   const f32x4* w1 = reinterpret_cast<const f32x4*>(net + kF32W1) + lane;
   const f32x16* b1 = reinterpret_cast<const f32x16*>(net + kF32B1) + h;
-  f32x16 a1[4];
+  f32x16 a1[kI8 ? 1 : 4];
+  i32x4 xd[kI8 ? 4 : 1][4];
+  float chk = 0.0f;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const f32x4 w = w1[t * 64];
@@ -898,10 +907,26 @@ __device__ __forceinline__ void mlp_f32(const uint8_t* net, const float* xs, int
     for (int g = 0; g < 16; ++g) {
       c[g] = tanh_tab(c[g], ttab);
     }
-    a1[t] = c;
+    if constexpr (kI8) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const f32x4 v = {c[4 * e], c[4 * e + 1], c[4 * e + 2], c[4 * e + 3]};
+        chk += (v[0] + v[1]) + (v[2] + v[3]);  // |v| <= 1: NaN iff a NaN among them
+        uint32_t d[4];
+        i8x_digits4(v, 28, d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xd[t][i][e] = (int)d[i];
+      }
+    } else {
+      a1[t] = c;
+    }
   }
-  if constexpr (kI8) mlp_i8_tail<NH>(net, a1, lane, head, ttab);
-  else mlp_f32_tail<NH>(net + kF32W2, net + kF32B2, net + kF32H, net + kF32HB, a1, lane, head, ttab);
+  if constexpr (kI8) {
+    const bool bad = __builtin_isnan(chk + __shfl_xor(chk, 32, 64));
+    mlp_i8_tail<NH>(net, xd, bad, lane, head, ttab);
+  } else {
+    mlp_f32_tail<NH>(net + kF32W2, net + kF32B2, net + kF32H, net + kF32HB, a1, lane, head, ttab);
+  }
 }
 
 // this lane's layer-1 inputs from the env-owning lane (half 0) of its env
@@ -1984,7 +2009,7 @@ __device__ __forceinline__ void attn16_net_i8(const uint8_t* net, const I8Feat& 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float y = i8x_recombine(L[0][r], L[1][r], L[2][r], L[3][r], s1[16 * t + r] - qa) + bb[r];
-      a[r] = tanh_tab(bad ? __builtin_nanf("") : y, ttab);
+      a[r] = tanh_tab(y, ttab);  // (a bad env's garbage is replaced by NaN at the heads)
     }
     uint32_t d[4];
     i8x_digits4(a, 28, d);
@@ -2019,7 +2044,7 @@ __device__ __forceinline__ void attn16_net_i8(const uint8_t* net, const I8Feat& 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float y = i8x_recombine(Lc[0][r], Lc[1][r], Lc[2][r], Lc[3][r], s2[16 * t + r]) + bb[r];
-      const float v = tanh_tab(bad ? __builtin_nanf("") : y, ttab);
+      const float v = tanh_tab(y, ttab);
 #pragma unroll
       for (int j = 0; j < NH; ++j) acc[j] = fmaf(wh[j * 32 + 4 * t][r], v, acc[j]);
     }
@@ -2029,7 +2054,10 @@ __device__ __forceinline__ void attn16_net_i8(const uint8_t* net, const I8Feat& 
     }
   }
 #pragma unroll
-  for (int j = 0; j < NH; ++j) head[j] = group_sum4(acc[j]) + bh[j];
+  for (int j = 0; j < NH; ++j) {
+    const float r = group_sum4(acc[j]) + bh[j];
+    head[j] = bad ? __builtin_nanf("") : r;
+  }
 }
 
 template <int NH, bool kI8>

@@ -133,9 +133,9 @@ def test_i8x4_mlp_split_equals_one_wave_with_bootstrap(gl, pol, orc, n):
         res["terminal_obs"] = _np(b.terminal_obs[:m])[order]
         out.append(res)
         # the values and the bootstrap's V(terminal obs): the oracle's bits
-        obs = res["observations"].reshape(-1, 6)
-        _, v = orc.mlp_f32(sd, obs, precision="i8x4")
-        assert _eq(res["values"].reshape(-1), v)
+        rows = np.random.default_rng(n).choice(K * n, 3000, replace=False)
+        _, v = orc.mlp_f32(sd, res["observations"].reshape(-1, 6)[rows], precision="i8x4")
+        assert _eq(res["values"].reshape(-1)[rows], v)
         d = res["dones"]
         assert ((d & 2 != 0) & (d & 1 == 0)).sum() > 0  # truncations were bootstrapped
         env.close()
@@ -166,7 +166,7 @@ def test_i8x4_mlp_vs_sb3_torch_fp32(gl, pol):
 
 def test_i8x4_mlp_nan_obs_poisons_its_env_only(gl, pol, orc):
     env = gl.BatchedEnv("lorenz3", 64, seed=3)
-    sd = _random_policy(pol, 3, 1, seed=5, scale=0.2)
+    sd = _random_policy(pol, env.obs_dim, env.action_dim, seed=5, scale=0.2)
     col = pol.FusedRolloutCollector(env, sd, bootstrap=False, deterministic=True, precision="i8x4")
     col.reset()
     col.last_obs[9, 1] = float("nan")

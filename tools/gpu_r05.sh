@@ -88,6 +88,52 @@ mlp)  # i8x4 MlpPolicy: parity, then fp32 vs i8x4 at cfg5's 32,768 envs (split k
     LZ_POL_F32_WAVES=4 timeout -k 10 200 python bench.py $PB --envs 1048576 --K 64 --steps 256 --precision $p > $O/mlp1m_w4_${p}_$r.json 2>> $O/bench.err || exit 1
   done; done
   ;;
+ab2)  # two-pass MLP i8x4 tail + NaN at the attention heads (default) vs the r05a build
+  timeout -k 10 900 $PYT -m gpu --maxfail=5 tests/test_gpu_policy_mlp_i8x4.py tests/test_gpu_policy_i8x4.py \
+    > $O/tests.txt 2>&1 || exit 1
+  PB="--mode policy --system pmsm --vecnorm-update rollout --precision i8x4 $BQ"
+  timeout -k 10 900 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05a.so -- $PB --envs 32768 --K 2048 \
+    --steps 4096 > $O/mlp32k.json 2> $O/mlp32k.err || exit 1
+  timeout -k 10 900 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05a.so -- $PB --envs 1048576 --K 64 \
+    --steps 256 > $O/mlp1m.json 2> $O/mlp1m.err || exit 1
+  timeout -k 10 900 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05a.so -- --mode policy --system hr \
+    --envs 32768 --K 2048 --steps 4096 --policy attn --precision i8x4 $BQ > $O/attn.json 2> $O/attn.err || exit 1
+  ;;
+ab3)  # MLP i8x4 tail with hi / lo accumulated directly (two accumulators, shift between passes) vs r05a
+  timeout -k 10 900 $PYT -m gpu --maxfail=5 tests/test_gpu_policy_mlp_i8x4.py tests/test_gpu_policy_f32.py \
+    > $O/tests.txt 2>&1 || exit 1
+  PB="--mode policy --system pmsm --vecnorm-update rollout --precision i8x4 $BQ"
+  timeout -k 10 900 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05a.so -- $PB --envs 32768 --K 2048 \
+    --steps 4096 > $O/mlp32k.json 2> $O/mlp32k.err || exit 1
+  timeout -k 10 900 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05a.so -- $PB --envs 1048576 --K 64 \
+    --steps 256 > $O/mlp1m.json 2> $O/mlp1m.err || exit 1
+  timeout -k 10 900 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05a.so -- --mode policy --system hr \
+    --envs 32768 --K 2048 --steps 4096 --vecnorm-update rollout --precision i8x4 $BQ > $O/mlp_hr32k.json 2> $O/mlp_hr32k.err || exit 1
+  ;;
+table)  # the DESIGN §6.3 table at HEAD (every row one r05 file)
+  R="timeout -k 10 300 python bench.py $BQ"
+  $R --envs 65536 > $O/cfg3_step_65536.json 2>> $O/table.err || exit 1
+  $R --envs 131072 > $O/cfg3_step_131072.json 2>> $O/table.err || exit 1
+  $R --mode rollout --K 2048 --envs 32768 --steps 8192 > $O/cfg5_rollout_l3.json 2>> $O/table.err || exit 1
+  $R --mode rollout --system hr --K 2048 --envs 32768 --steps 4096 --warmup 2048 > $O/cfg5_rollout_hr.json 2>> $O/table.err || exit 1
+  $R --mode vecnorm --system pmsm --envs 262144 --steps 512 > $O/vecnorm_pmsm262k.json 2>> $O/table.err || exit 1
+  $R --mode policy --system pmsm --envs 262144 --K 16 --steps 512 > $O/mlp_f32_vnstep_pmsm262k.json 2>> $O/table.err || exit 1
+  $R --mode policy --system pmsm --envs 32768 --K 2048 --steps 4096 --precision bf16 > $O/mlp_bf16_pmsm32k.json 2>> $O/table.err || exit 1
+  $R --mode policy --system hr --envs 32768 --K 2048 --steps 4096 --policy attn --precision bf16 > $O/attn_bf16_hr32k.json 2>> $O/table.err || exit 1
+  $R --mode policy --system hr --envs 32768 --K 2048 --steps 4096 --policy attn_ln --precision bf16 > $O/attn_ln_bf16_hr32k.json 2>> $O/table.err || exit 1
+  timeout -k 10 300 python tools/frame_stack_bench.py > $O/frame_stack_hr1m.json 2>> $O/table.err || exit 1
+  timeout -k 10 300 python tools/resident_latency.py > $O/resident_latency.json 2>> $O/table.err || exit 1
+  ;;
+zpmc)  # counters of the rejected kZN noise pipelining (variant 1<<26) vs the default, PMSM 32,768 x 2048
+  for v in 0 67108864; do
+    B="python bench.py --system pmsm --mode rollout --K 2048 --envs 32768 --steps 4096 --warmup 2048 --add-noise 1 --variant $v $BQ"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/v${v}_prof -o run --output-format csv -- $B > $O/v${v}_prof.log 2>&1 || exit 1
+    timeout -k 10 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES \
+      -d $O/v${v}_pmc1 -o p1 --output-format csv -- $B > $O/v${v}_pmc1.log 2>&1 || exit 1
+    timeout -k 10 200 rocprofv3 --pmc SQ_INSTS_VALU_TRANS_F SQ_ACTIVE_INST_VMEM SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INST_LEVEL_VMEM GRBM_GUI_ACTIVE \
+      -d $O/v${v}_pmc2 -o p2 --output-format csv -- $B > $O/v${v}_pmc2.log 2>&1 || exit 1
+  done
+  ;;
 zn)  # software-pipelined noise draws in the PMSM / HR rollouts (variant 1<<26): parity, then A/B
   timeout -k 10 600 $PYT -m gpu --maxfail=3 "tests/test_gpu_parity.py::test_rollout_noise_producer_equals_steps" \
     > $O/zn_tests.txt 2>&1 || exit 1
