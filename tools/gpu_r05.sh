@@ -124,6 +124,17 @@ ab4)  # lz_policy.o built with MachineLICM sinking (fewer spills) vs the r05b bu
   $AB $P --system hr --envs 32768 --K 2048 --steps 4096 --policy attn_ln > $O/attn_ln_f32_hr.json 2>> $O/ab.err || exit 1
   $AB $P --system pmsm --envs 32768 --K 2048 --steps 4096 --precision bf16 > $O/mlp_bf16_32k.json 2>> $O/ab.err || exit 1
   ;;
+ab5)  # tanh_tab: clamp into a constant-1 segment (11 VALU) + 4-wide batched coefficient reads in the attention nets, vs r05c
+  timeout -k 10 1000 $PYT -m gpu --maxfail=5 tests/test_gpu_policy*.py > $O/tests.txt 2>&1 || exit 1
+  AB="timeout -k 10 600 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05c.so --"
+  P="--mode policy $BQ --envs 32768 --K 2048 --steps 4096"
+  $AB $P --system hr --policy attn > $O/attn_f32_hr.json 2>> $O/ab.err || exit 1
+  $AB $P --system hr --policy attn --precision i8x4 > $O/attn_i8_hr.json 2>> $O/ab.err || exit 1
+  $AB $P --system hr --policy attn_ln > $O/attn_ln_f32_hr.json 2>> $O/ab.err || exit 1
+  $AB $P --system hr --policy attn_ln --precision i8x4 > $O/attn_ln_i8_hr.json 2>> $O/ab.err || exit 1
+  $AB $P --system pmsm --vecnorm-update rollout > $O/mlp_f32_32k.json 2>> $O/ab.err || exit 1
+  $AB $P --system pmsm --vecnorm-update rollout --precision i8x4 > $O/mlp_i8_32k.json 2>> $O/ab.err || exit 1
+  ;;
 table)  # the DESIGN §6.3 table at HEAD (every row one r05 file)
   R="timeout -k 10 300 python bench.py $BQ"
   $R --envs 65536 > $O/cfg3_step_65536.json 2>> $O/table.err || exit 1
