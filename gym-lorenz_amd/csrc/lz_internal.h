@@ -189,8 +189,11 @@ constexpr int kF32HB = kF32H + 4 * 2 * 64 * 4;
 constexpr int kF32Sh2 = kF32HB + 64;
 constexpr int kF32Net = kF32Sh2 + 4 * 2 * 16 * 2;    // 73024 B
 constexpr int kF32LogStd = 2 * kF32Net;
-constexpr int kF32Tanh = kF32LogStd + 64;           // tanh table: 72 segments x 8 floats
-constexpr int kF32BlobBytes = kF32Tanh + 72 * 32;   // 148416 B (resident in LDS)
+// tanh_tab's table: 72 polynomial segments of width 1/8 over [0, 9) and a 73rd, the
+// constant 1 (|x| >= 9 clamps into it), 8 floats each
+constexpr int kTanhSegs = 73;
+constexpr int kF32Tanh = kF32LogStd + 64;
+constexpr int kF32BlobBytes = kF32Tanh + kTanhSegs * 32;  // 148448 B (resident in LDS)
 
 // The attention actor-critics at SB3's precision (float32 operands and accumulation;
 // lz_attn_policy_pack_f32 / lz_attn_ln_policy_pack_f32 -> k_rollout_policy_attn_f32).
@@ -238,11 +241,11 @@ constexpr int kAFNHB = kAFNH + 4 * 128 * 4;
 constexpr int kAFNet = 100 * 1024;                          // 101,392 B padded to whole 1-KiB DMA pieces
 static_assert(kAFNHB + 16 <= kAFNet, "attention net slot");
 constexpr int kAFPi = kAFExt, kAFVf = kAFExt + kAFNet;
-constexpr int kAFConst = 64 + 72 * 32;                      // log_std consts + tanh table
+constexpr int kAFConst = 64 + kTanhSegs * 32;               // log_std consts + tanh table
 constexpr int kAFLogStd = kAFExt + 2 * kAFNet;
 constexpr int kAFTanh = kAFLogStd + 64;
-constexpr int kAFBlobBytes = kAFLogStd + kAFConst;          // 261,568 B (device)
-constexpr int kAFLdsBytes = kAFExt + kAFConst + kAFNet;     // 159,168 B (LDS)
+constexpr int kAFBlobBytes = kAFLogStd + kAFConst;          // 261,600 B (device)
+constexpr int kAFLdsBytes = kAFExt + kAFConst + kAFNet;     // 159,200 B (LDS)
 // The opt-in "i8x4" nets (lz_attn_policy_pack_i8x4, LZ_POLICY_I8X4): the same blob, the
 // same extractor, the same offsets -- the two wide layers' float32 weights replaced by
 // their four int8 digits (4 B per weight either way, v_mfma_i32_16x16x64_i8 A operands)

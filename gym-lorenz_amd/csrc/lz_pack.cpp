@@ -653,6 +653,7 @@ static lz_status pack_mlp_f32(const lz_mlp_policy* p, int32_t hidden, void* host
   float* tt = reinterpret_cast<float*>(b + lz::kF32Tanh);
   for (int k = 0; k < 72; ++k)
     for (int j = 0; j < 8; ++j) tt[8 * k + j] = std::ldexp(kTanhTab[8 * k + j], -3 * j);
+  tt[8 * 72] = 1.0f;  // segment 72: the constant 1 (the rest stays zero)
   return LZ_OK;
 }
 
@@ -720,6 +721,7 @@ static lz_status pack_attn_f32_checked(const lz_attn_policy* p, const float* ln_
   float* tt = reinterpret_cast<float*>(b + lz::kAFTanh);
   for (int k = 0; k < 72; ++k)
     for (int j = 0; j < 8; ++j) tt[8 * k + j] = std::ldexp(kTanhTab[8 * k + j], -3 * j);
+  tt[8 * 72] = 1.0f;  // segment 72: the constant 1 (the rest stays zero)
   return LZ_OK;
 }
 

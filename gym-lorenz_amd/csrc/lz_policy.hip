@@ -701,13 +701,14 @@ __device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
 // |x| >= 9 (1 - tanh(9) < 2^-25).  The blob holds c_j 8^-j (exact scaling) so Horner
 // runs in u = fract(8|x|) = 8 t: every Horner step is the oracle's (t-form) value times
 // 8^-j exactly -- scaling by a power of two commutes with rounding -- so the result has
-// the oracle's bits with v_fract replacing a convert + fma.  ~13 instructions, two of
-// them LDS reads of the segment's coefficients (the table sits in the blob, tab = LDS).
+// the oracle's bits with v_fract replacing a convert + fma.  11 VALU instructions and two
+// LDS reads of the segment's coefficients (the table sits in the blob, tab = LDS).
 __device__ __forceinline__ float tanh_tab(float x, const float* tab) {
   const float ax = fabsf(x);
-  const float m = ax * 8.0f;                // exact
-  int k = (int)m;                           // NaN -> 0, inf -> INT_MAX
-  k = k < 71 ? k : 71;
+  // 8|x| exactly, clamped to 72 with NaN kept: |x| >= 9 (inf too) lands on segment 72,
+  // the constant 1 -- the oracle's "1 for |x| >= 9" without a compare and select
+  const float m = __builtin_elementwise_minimum(ax * 8.0f, 72.0f);
+  const int k = (int)m;                     // NaN -> 0
   const f32x4 lo = reinterpret_cast<const f32x4*>(tab)[2 * k];
   const f32x4 hi = reinterpret_cast<const f32x4*>(tab)[2 * k + 1];
   const float u = __builtin_amdgcn_fractf(m);  // m - floor(m), exact
@@ -715,9 +716,35 @@ __device__ __forceinline__ float tanh_tab(float x, const float* tab) {
   y = fmaf(y, u, lo[3]);
   y = fmaf(y, u, lo[2]);
   y = fmaf(y, u, lo[1]);
-  y = fmaf(y, u, lo[0]);
-  y = ax >= 9.0f ? 1.0f : y;  // NaN: the compare is false and u (so y) is already NaN
+  y = fmaf(y, u, lo[0]);      // NaN: u (so y) is NaN
   return __builtin_copysignf(y, x);
+}
+
+// tanh_tab of four values with all eight coefficient reads issued before the first
+// Horner step (one LDS round trip for the four instead of four in a row); the same bits
+template <class V4>
+__device__ __forceinline__ V4 tanh_tab4(V4 x, const float* tab) {
+  f32x4 lo[4], hi[4];
+  float u[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float m = __builtin_elementwise_minimum(fabsf(x[r]) * 8.0f, 72.0f);
+    const int k = (int)m;
+    lo[r] = reinterpret_cast<const f32x4*>(tab)[2 * k];
+    hi[r] = reinterpret_cast<const f32x4*>(tab)[2 * k + 1];
+    u[r] = __builtin_amdgcn_fractf(m);
+  }
+  V4 out;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float y = fmaf(hi[r][1], u[r], hi[r][0]);
+    y = fmaf(y, u[r], lo[r][3]);
+    y = fmaf(y, u[r], lo[r][2]);
+    y = fmaf(y, u[r], lo[r][1]);
+    y = fmaf(y, u[r], lo[r][0]);
+    out[r] = __builtin_copysignf(y, x[r]);
+  }
+  return out;
 }
 
 // Layer 2 (128 -> 128, tanh_tab) and the NH head rows of a float32 net, from layer 1's
@@ -1911,9 +1938,7 @@ __device__ __forceinline__ void attn16_net(const uint8_t* net, const f32x4* feat
 #pragma unroll
       for (int s = 0; s < 4; ++s) c = mfma16(w[f][s], feat[f][s], c);
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) c[r] = tanh_tab(c[r], ttab);
-    a1[t] = c;
+    a1[t] = tanh_tab4(c, ttab);
   }
   const f32x4* w2 = reinterpret_cast<const f32x4*>(net + kAFN2) + lane;
   const f32x4* b2 = reinterpret_cast<const f32x4*>(net + kAFNB2) + G;
@@ -1934,11 +1959,11 @@ __device__ __forceinline__ void attn16_net(const uint8_t* net, const f32x4* feat
 #pragma unroll
       for (int s = 0; s < 4; ++s) c = mfma16(w[q][s], a1[q][s], c);
     }
+    const f32x4 v = tanh_tab4(c, ttab);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float v = tanh_tab(c[r], ttab);
 #pragma unroll
-      for (int j = 0; j < NH; ++j) acc[j] = fmaf(wh[j * 32 + 4 * t][r], v, acc[j]);
+      for (int j = 0; j < NH; ++j) acc[j] = fmaf(wh[j * 32 + 4 * t][r], v[r], acc[j]);
     }
   }
 #pragma unroll
@@ -2005,12 +2030,11 @@ __device__ __forceinline__ void attn16_net_i8(const uint8_t* net, const I8Feat& 
     i32x4 L[4];
     i8x_tile<1>([&](int, int i) { return w1[(t * 4 + i) * 64]; }, xf, L);
     const f32x4 bb = b1[4 * t];
-    f32x4 a;
+    f32x4 y;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float y = i8x_recombine(L[0][r], L[1][r], L[2][r], L[3][r], s1[16 * t + r] - qa) + bb[r];
-      a[r] = tanh_tab(y, ttab);  // (a bad env's garbage is replaced by NaN at the heads)
-    }
+    for (int r = 0; r < 4; ++r)
+      y[r] = i8x_recombine(L[0][r], L[1][r], L[2][r], L[3][r], s1[16 * t + r] - qa) + bb[r];
+    const f32x4 a = tanh_tab4(y, ttab);  // (a bad env's garbage is replaced by NaN at the heads)
     uint32_t d[4];
     i8x_digits4(a, 28, d);
 #pragma unroll
@@ -2041,12 +2065,15 @@ __device__ __forceinline__ void attn16_net_i8(const uint8_t* net, const I8Feat& 
     if (!LZ_I8_PIPE) tile2(t, Lc);
     if (LZ_I8_PIPE && t + 1 < 8) tile2(t + 1, Ln);
     const f32x4 bb = b2[4 * t];
+    f32x4 y;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      y[r] = i8x_recombine(Lc[0][r], Lc[1][r], Lc[2][r], Lc[3][r], s2[16 * t + r]) + bb[r];
+    const f32x4 v = tanh_tab4(y, ttab);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float y = i8x_recombine(Lc[0][r], Lc[1][r], Lc[2][r], Lc[3][r], s2[16 * t + r]) + bb[r];
-      const float v = tanh_tab(y, ttab);
 #pragma unroll
-      for (int j = 0; j < NH; ++j) acc[j] = fmaf(wh[j * 32 + 4 * t][r], v, acc[j]);
+      for (int j = 0; j < NH; ++j) acc[j] = fmaf(wh[j * 32 + 4 * t][r], v[r], acc[j]);
     }
     if (LZ_I8_PIPE) {
 #pragma unroll
