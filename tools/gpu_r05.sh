@@ -135,6 +135,23 @@ ab5)  # tanh_tab: clamp into a constant-1 segment (11 VALU) + 4-wide batched coe
   $AB $P --system pmsm --vecnorm-update rollout > $O/mlp_f32_32k.json 2>> $O/ab.err || exit 1
   $AB $P --system pmsm --vecnorm-update rollout --precision i8x4 > $O/mlp_i8_32k.json 2>> $O/ab.err || exit 1
   ;;
+ab6)  # MLP i8x4 recombine as fma(t, packed float row scale, bias) vs r05d
+  timeout -k 10 900 $PYT -m gpu --maxfail=5 tests/test_gpu_policy_mlp_i8x4.py tests/test_gpu_policy_f32.py > $O/tests.txt 2>&1 || exit 1
+  AB="timeout -k 10 600 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05d.so --"
+  P="--mode policy $BQ --vecnorm-update rollout --precision i8x4"
+  $AB $P --system pmsm --envs 32768 --K 2048 --steps 4096 > $O/mlp_i8_32k.json 2>> $O/ab.err || exit 1
+  $AB $P --system pmsm --envs 1048576 --K 64 --steps 256 > $O/mlp_i8_1m.json 2>> $O/ab.err || exit 1
+  $AB $P --system hr --envs 32768 --K 2048 --steps 4096 > $O/mlp_i8_hr32k.json 2>> $O/ab.err || exit 1
+  ;;
+ab7)  # MLP i8x4 tail software-pipelined (tile t + 1's MFMA passes around tile t's VALU work) vs r05d
+  timeout -k 10 900 $PYT -m gpu --maxfail=5 tests/test_gpu_policy_mlp_i8x4.py > $O/tests.txt 2>&1 || exit 1
+  AB="timeout -k 10 600 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05d.so --"
+  P="--mode policy $BQ --vecnorm-update rollout --precision i8x4"
+  $AB $P --system pmsm --envs 32768 --K 2048 --steps 4096 > $O/mlp_i8_32k.json 2>> $O/ab.err || exit 1
+  $AB $P --system pmsm --envs 1048576 --K 64 --steps 256 > $O/mlp_i8_1m.json 2>> $O/ab.err || exit 1
+  $AB $P --system hr --envs 32768 --K 2048 --steps 4096 > $O/mlp_i8_hr32k.json 2>> $O/ab.err || exit 1
+  LZ_POL_F32_WAVES=4 $AB $P --system pmsm --envs 1048576 --K 64 --steps 256 > $O/mlp_i8_1m_w4.json 2>> $O/ab.err || exit 1
+  ;;
 table)  # the DESIGN §6.3 table at HEAD (every row one r05 file)
   R="timeout -k 10 300 python bench.py $BQ"
   $R --envs 65536 > $O/cfg3_step_65536.json 2>> $O/table.err || exit 1
