@@ -856,6 +856,8 @@ __device__ __forceinline__ void mlp_i8_tail(const uint8_t* net, const i32x4 (*xd
 #pragma unroll 1
   for (int t = 0; t < 4; ++t) {
     __builtin_amdgcn_sched_barrier(0);
+    // (software-pipelining tile t + 1's passes around tile t's VALU work measured 3-10 %
+    // slower, profiles/r05/mlp_i8/pipe_rejected/)
     const i32x16 z = {};
     const i32x4* wt = w2 + t * 4 * 4 * 64;
     // hi = L6 256 + L5 and lo = L4 256 + L3 accumulated directly: the first pass sums the

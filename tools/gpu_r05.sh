@@ -152,6 +152,22 @@ ab7)  # MLP i8x4 tail software-pipelined (tile t + 1's MFMA passes around tile t
   $AB $P --system hr --envs 32768 --K 2048 --steps 4096 > $O/mlp_i8_hr32k.json 2>> $O/ab.err || exit 1
   LZ_POL_F32_WAVES=4 $AB $P --system pmsm --envs 1048576 --K 64 --steps 256 > $O/mlp_i8_1m_w4.json 2>> $O/ab.err || exit 1
   ;;
+ab8)  # attention i8x4 layer 1 software-pipelined (tile t + 1's MFMAs before tile t's VALU) vs r05d
+  timeout -k 10 900 $PYT -m gpu --maxfail=5 tests/test_gpu_policy_i8x4.py tests/test_gpu_policy_mlp_i8x4.py > $O/tests.txt 2>&1 || exit 1
+  AB="timeout -k 10 600 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05d.so --"
+  P="--mode policy $BQ --envs 32768 --K 2048 --steps 4096 --precision i8x4"
+  $AB $P --system hr --policy attn > $O/attn_i8_hr.json 2>> $O/ab.err || exit 1
+  $AB $P --system hr --policy attn_ln > $O/attn_ln_i8_hr.json 2>> $O/ab.err || exit 1
+  $AB $P --system pmsm --vecnorm-update rollout > $O/mlp_i8_32k.json 2>> $O/ab.err || exit 1
+  ;;
+final)  # the closing run on the final tree: every GPU test, smoke, the bench lines and the headline's rocprof summary
+  timeout -k 10 1000 $PYT -x -m gpu tests > $O/gpu_tests.txt 2>&1 || exit 1
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" > $O/smoke.txt 2>&1 || exit 1
+  timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 1
+  timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $O/bench_steps20.json 2> $O/bench_steps20.err || exit 1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv \
+    -- python bench.py --no-cpu-baseline --no-drift > $O/bench_prof.json 2> $O/bench_prof.err || exit 1
+  ;;
 table)  # the DESIGN §6.3 table at HEAD (every row one r05 file)
   R="timeout -k 10 300 python bench.py $BQ"
   $R --envs 65536 > $O/cfg3_step_65536.json 2>> $O/table.err || exit 1
