@@ -168,6 +168,13 @@ final)  # the closing run on the final tree: every GPU test, smoke, the bench li
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv \
     -- python bench.py --no-cpu-baseline --no-drift > $O/bench_prof.json 2> $O/bench_prof.err || exit 1
   ;;
+ab9)  # attention i8x4 row shifts as per-value ds_read_i16 (no VALU unpack) vs r05d
+  timeout -k 10 900 $PYT -m gpu --maxfail=5 tests/test_gpu_policy_i8x4.py > $O/tests.txt 2>&1 || exit 1
+  AB="timeout -k 10 600 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05d.so --"
+  P="--mode policy $BQ --envs 32768 --K 2048 --steps 4096 --precision i8x4 --system hr"
+  $AB $P --policy attn > $O/attn_i8_hr.json 2>> $O/ab.err || exit 1
+  $AB $P --policy attn_ln > $O/attn_ln_i8_hr.json 2>> $O/ab.err || exit 1
+  ;;
 table)  # the DESIGN §6.3 table at HEAD (every row one r05 file)
   R="timeout -k 10 300 python bench.py $BQ"
   $R --envs 65536 > $O/cfg3_step_65536.json 2>> $O/table.err || exit 1
