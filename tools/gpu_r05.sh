@@ -175,6 +175,10 @@ ab9)  # attention i8x4 row shifts as per-value ds_read_i16 (no VALU unpack) vs r
   $AB $P --policy attn > $O/attn_i8_hr.json 2>> $O/ab.err || exit 1
   $AB $P --policy attn_ln > $O/attn_ln_i8_hr.json 2>> $O/ab.err || exit 1
   ;;
+pmc_mlp)  # counters of the MlpPolicy rollout, float32 vs i8x4 (PMSM 32,768 x 2048)
+  bash tools/policy_pmc.sh r05_mlp_i8x4 --system pmsm --envs 32768 --K 2048 --steps 4096 --vecnorm-update rollout --precision i8x4 $BQ || exit 1
+  bash tools/policy_pmc.sh r05_mlp_fp32 --system pmsm --envs 32768 --K 2048 --steps 4096 --vecnorm-update rollout --precision fp32 $BQ || exit 1
+  ;;
 table)  # the DESIGN §6.3 table at HEAD (every row one r05 file)
   R="timeout -k 10 300 python bench.py $BQ"
   $R --envs 65536 > $O/cfg3_step_65536.json 2>> $O/table.err || exit 1
