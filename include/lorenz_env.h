@@ -686,7 +686,8 @@ enum {
   LZ_CALL_STEP = 0,                        /* lz_step, noise drawn on the device (noise NULL) */
   LZ_CALL_ROLLOUT = 1,                     /* lz_rollout */
   LZ_CALL_ROLLOUT_POLICY = 2,              /* lz_rollout_policy (bf16 MlpPolicy) */
-  LZ_CALL_ROLLOUT_POLICY_F32 = 3,          /* lz_rollout_policy_f32 */
+  LZ_CALL_ROLLOUT_POLICY_F32 = 3,          /* lz_rollout_policy_f32 (LZ_POLICY_I8X4 runs the same
+                                              shape: the i8x4 instantiation of the kernel) */
   LZ_CALL_POLICY_STEP_F32 = 4,             /* lz_policy_step_f32 / lz_rollout_policy_f32_vn */
   LZ_CALL_ROLLOUT_POLICY_ATTN = 5,         /* lz_rollout_policy_attn */
   LZ_CALL_ROLLOUT_POLICY_ATTN_STACK = 6,   /* lz_rollout_policy_attn_stack */
