@@ -179,6 +179,17 @@ pmc_mlp)  # counters of the MlpPolicy rollout, float32 vs i8x4 (PMSM 32,768 x 20
   bash tools/policy_pmc.sh r05_mlp_i8x4 --system pmsm --envs 32768 --K 2048 --steps 4096 --vecnorm-update rollout --precision i8x4 $BQ || exit 1
   bash tools/policy_pmc.sh r05_mlp_fp32 --system pmsm --envs 32768 --K 2048 --steps 4096 --vecnorm-update rollout --precision fp32 $BQ || exit 1
   ;;
+dist)  # the driver's N > 1 launch path on this 1-GPU box: torchrun + RCCL at world size 1, and the
+       # refusal of more nccl ranks than GPUs (must exit non-zero, not share the card)
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+    --master-port 29517 bench.py --gpus 1 --steps 400 --warmup 40 > $O/torchrun_n1.json 2> $O/torchrun_n1.err || exit 1
+  if timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29518 bench.py --gpus 2 --steps 400 --warmup 40 > $O/torchrun_n2.json 2> $O/torchrun_n2.err; then
+    echo "UNEXPECTED: 2 nccl ranks on 1 GPU ran" > $O/refusal.txt; exit 1
+  else
+    echo "refused as intended (exit $?)" > $O/refusal.txt
+  fi
+  ;;
 table)  # the DESIGN §6.3 table at HEAD (every row one r05 file)
   R="timeout -k 10 300 python bench.py $BQ"
   $R --envs 65536 > $O/cfg3_step_65536.json 2>> $O/table.err || exit 1
