@@ -1702,9 +1702,10 @@ __device__ __forceinline__ float exp_att(float x) {
   p = fmaf(p, r, 0.5f);
   p = fmaf(p, r, 1.0f);
   p = fmaf(p, r, 1.0f);
-  float y = __builtin_ldexpf(p, (int)k);
-  y = x < -86.0f ? 0.0f : y;
-  return x != x ? x : y;
+  const float y = __builtin_ldexpf(p, (int)k);
+  // a NaN x is NaN here already (k, r and p are NaN; (int)NaN = 0): the oracle's explicit
+  // NaN return needs no select (any NaN is the oracle's NaN)
+  return x < -86.0f ? 0.0f : y;
 }
 
 __device__ __forceinline__ float relu_f(float v) { return v < 0.0f ? 0.0f : v; }  // NaN kept
@@ -1827,7 +1828,9 @@ __device__ __forceinline__ void attn16_extract(const uint8_t* ext, const float* 
     }
     float m = sc[0];
 #pragma unroll
-    for (int j = 1; j < kAttTokens; ++j) m = (m != m || m >= sc[j]) ? m : sc[j];
+    // NaN-propagating max (v_maximum_f32): the oracle's NaN-keeping select, except that
+    // +0 beats -0 -- which cannot change sc[j] - m or its exp
+    for (int j = 1; j < kAttTokens; ++j) m = __builtin_elementwise_maximum(m, sc[j]);
     float e[kAttTokens], sum = 0.0f;
 #pragma unroll
     for (int j = 0; j < kAttTokens; ++j) {

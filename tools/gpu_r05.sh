@@ -190,6 +190,16 @@ dist)  # the driver's N > 1 launch path on this 1-GPU box: torchrun + RCCL at wo
     echo "refused as intended (exit $?)" > $O/refusal.txt
   fi
   ;;
+ab10)  # attention softmax: NaN-propagating v_maximum for the max, no NaN select in exp_att, vs r05e
+  timeout -k 10 900 $PYT -m gpu --maxfail=5 tests/test_gpu_policy_attn_f32.py tests/test_gpu_policy_i8x4.py \
+    tests/test_gpu_policy_branches.py tests/test_gpu_policy_edges.py > $O/tests.txt 2>&1 || exit 1
+  AB="timeout -k 10 600 python tools/ab_libs.py 2 default ablib/libgym_lorenz_amd_r05e.so --"
+  P="--mode policy $BQ --envs 32768 --K 2048 --steps 4096 --system hr"
+  $AB $P --policy attn > $O/attn_f32_hr.json 2>> $O/ab.err || exit 1
+  $AB $P --policy attn --precision i8x4 > $O/attn_i8_hr.json 2>> $O/ab.err || exit 1
+  $AB $P --policy attn_ln > $O/attn_ln_f32_hr.json 2>> $O/ab.err || exit 1
+  $AB $P --policy attn_ln --precision i8x4 > $O/attn_ln_i8_hr.json 2>> $O/ab.err || exit 1
+  ;;
 table)  # the DESIGN §6.3 table at HEAD (every row one r05 file)
   R="timeout -k 10 300 python bench.py $BQ"
   $R --envs 65536 > $O/cfg3_step_65536.json 2>> $O/table.err || exit 1
