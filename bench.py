@@ -97,6 +97,11 @@ def parse(argv=None):
     p.add_argument("--integrator", choices=["euler", "rk4"], default="euler",
                    help="euler = the reference's (dynamic.py:70-75); rk4 = the opt-in RK4 mode "
                         "of lorenz3 / lorenz4 (lz_config.integrator)")
+    p.add_argument("--streams", type=int, default=0,
+                   help="step mode: split each rank's shard into S sub-handles of consecutive "
+                        "global env ids, each stepping on its own HIP stream with its own "
+                        "captured graphs, so the S dependent-launch chains overlap (1..4: "
+                        "GPU_MAX_HW_QUEUES is 4); 0 = auto (default_streams)")
     p.add_argument("--no-gather", action="store_true",
                    help="N > 1: skip the step + gather-to-rank-0 extra line")
     p.add_argument("--probe-ranks", action="store_true", help=argparse.SUPPRESS)
@@ -334,6 +339,9 @@ def bench_vecnorm(args, gl, nat, torch, env, device, world, total, n):
     h = env._h
     env.reset()
     nd = didx.data_ptr() + 4 * n
+    for r in range(R):  # lz_step_vecnorm takes lz_step's buffers: the same checked entry
+        env.step_args(acts[r], raw_o[r], raw_r[r], done[r], didx[:n], tobs, didx[n:])
+        env.step_args(acts[r], obs_n[r], rew_n[r], dones[r])
 
     def one(k):
         r = k % R
@@ -504,7 +512,10 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
     fl = attn_policy_flops(stack * O, A) if attn else policy_flops(O, A)
     achieved = fl * n * K / launch_s / 1e12
     peak = MFMA_F32_PEAK_TFLOPS if f32 else MFMA_BF16_PEAK_TFLOPS
-    num_cus = torch.cuda.get_device_properties(device).multi_processor_count
+    # the MlpPolicy fused rollout's kernel as its launcher chooses it (lz_get_launch_shape:
+    # size, LZ_POL_F32_WAVES and the variant bits included; i8x4 runs the same shape)
+    f32_shape = (nat.launch_shape(env._h, nat.CALL_ROLLOUT_POLICY_F32)
+                 if f32 and not attn and not per_step else None)
     mangled = {"pmsm": "7SysPMSME", "lorenz3": "5SysL3IfEE", "lorenz4": "5SysL4IfEE",
                "hr": "5SysHRIfEE"}[args.system]
     return {
@@ -518,9 +529,11 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": ("f32 MFMA extractor + exact int8 MFMA (4-digit fixed point) nets, f32 env" if i8 else
+        "dtype": ("f32 MFMA extractor + int8 MFMA nets (truncated 4-digit fixed point: digit levels >= 3 "
+                  "summed exactly in int32, two float32 roundings), f32 env" if i8 else
                   "f32 MFMA (f32 accumulate), f32 env" if f32 else "bf16 MFMA (fp32 accumulate), f32 env"),
-        "precision_note": ("opt-in i8x4: the nets' wide layers as exact fixed-point products, float32-"
+        "precision_note": ("opt-in i8x4: the nets' wide layers as truncated 4-digit fixed-point products "
+                           "(levels >= 3 summed exactly, recombined with two float32 roundings), float32-"
                            "level accuracy, bit-exact vs the C oracle (orc_attn_i8x4 / orc_mlp_i8x4); "
                            "frac = useful "
                            "FLOP against the f32 MFMA peak, like the fp32 line" if i8 else
@@ -532,14 +545,14 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
             "workload": ("%s with code/lorenz_filter/train.py's PPO actor-critic on "
                          "VecFrameStack(4) (attention + residual + LayerNorm extractor, pi/vf "
                          "[128,128] Tanh): %d-step fused rollout (lz_rollout_policy_attn_stack" +
-                         ("_f32 + LZ_POLICY_I8X4, exact int8 nets" if i8 else "_f32, float32 as SB3"
+                         ("_f32 + LZ_POLICY_I8X4, int8 fixed-point nets" if i8 else "_f32, float32 as SB3"
                           if f32 else ", bf16 MFMA") + ": "
                          "frame stack + extractor + nets + sample + clip + env step + bootstrap), "
                          "GAE (lz_gae); %d envs total, %d per GPU" if ln else
                          "%s with code/train.py's PPO actor-critic (AttentionFeaturesExtractor "
                          "fc1 + 4-head self-attention over 8 tokens + post_fc 64, then pi/vf "
                          "[128,128] Tanh) in the loop: %d-step fused rollout "
-                         "(lz_rollout_policy_attn" + ("_f32 + LZ_POLICY_I8X4, exact int8 nets" if i8 else
+                         "(lz_rollout_policy_attn" + ("_f32 + LZ_POLICY_I8X4, int8 fixed-point nets" if i8 else
                                                       "_f32, float32 as SB3" if f32 else ", bf16 MFMA")
                          + ": extractor + nets + DiagGaussian sample + clip "
                          "+ env step + truncation bootstrap), GAE (lz_gae); %d envs total, %d per "
@@ -552,7 +565,7 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
                             "truncation bootstraps valued with their step's statistics), GAE "
                             "(lz_gae); %d envs total, %d per GPU" if per_step else
                             "%d-step fused rollout (lz_rollout_policy" + (
-                                "_f32 + LZ_POLICY_I8X4, layer 2 as exact int8 products" if i8 else
+                                "_f32 + LZ_POLICY_I8X4, layer 2 as int8 fixed-point products" if i8 else
                                 "_f32, float32 as SB3" if f32 else ", bf16 MFMA")
                             + ": policy forward + DiagGaussian "
                             "sample + clip + env step + truncation bootstrap + VecNormalize obs with "
@@ -579,8 +592,9 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
                        if attn else
                        "_ZN2lz17k_policy_step_f32INS_%sLi8EEEvNS_5KArgsENS_5PArgsENS_9PStepArgsE"
                        if per_step else
-                       (("_ZN2lz16k_rollout_policyINS_%sLi8ELi32ELi" + "56"[i8] + "ELi1EEEvNS_5KArgsENS_5PArgsE")
-                        if n >= 8 * 32 * num_cus else
+                       (("_ZN2lz16k_rollout_policyINS_%sLi" + str(f32_shape["waves"]) + "ELi32ELi"
+                         + "56"[i8] + "ELi1EEEvNS_5KArgsENS_5PArgsE")
+                        if f32_shape["kernel"] == "policy" else
                         ("_ZN2lz26k_rollout_policy_f32_splitINS_%sLb" + "01"[i8] + "EEEvNS_5KArgsENS_5PArgsE"))
                        if f32 else "_ZN2lz16k_rollout_policyINS_%sLi8EEEvNS_5KArgsENS_5PArgsE")
                       % mangled,
@@ -601,6 +615,11 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
 def describe_launches(tm, rollout):
     """What one timed window of measure_steps actually launched: hipGraph replays and
     eager launches (the driver's --steps 20 is 0 replays of a 64-step graph + 20 eager)."""
+    S = tm.get("streams", 1)
+    if S > 1:
+        one = describe_launches(dict(tm, streams=1), rollout)
+        return one.replace("per timed window: ", "per timed window, on each of %d streams "
+                           "(one sub-handle of 1/%d of the shard each, concurrently): " % (S, S))
     per_win = tm["launches"] // tm["windows"]
     if rollout:
         return ("per timed window: %d eager %d-step lz_rollout launches (x%d windows)"
@@ -687,6 +706,26 @@ def rk4_line(args, gl, nat, torch, dist, device, n):
     return line
 
 
+def default_streams(system, mode, n):
+    """--streams 0 (auto): how many concurrent sub-handle chains a rank's per-step loop
+    uses for an n-env shard (see make_subs)."""
+    return 1
+
+
+def make_subs(args, gl, n, start, local, kw):
+    """--streams S > 1 (step mode): the rank's shard as S BatchedEnv sub-handles of
+    consecutive global ids (gym_lorenz.parallel.sub_shards), else None."""
+    from gym_lorenz.parallel import sub_shards
+
+    S = args.streams or default_streams(args.system, args.mode, n)
+    S = max(1, min(int(S), 4, n))
+    if S == 1:
+        return None
+    return [gl.BatchedEnv(args.system, c, dtype=args.dtype, seed=0, global_env_offset=o,
+                          autoreset=True, device=local, max_episode_steps=args.max_episode_steps,
+                          variant=args.variant, **kw) for o, c in sub_shards(n, start, S)]
+
+
 def scaling_line(args, gl, nat, torch, dist, device, world, rank):
     """N > 1: the headline step in the other scaling mode (the weak 1,048,576-per-GPU run
     next to the strong 1M-total headline, or the reverse with --scaling weak)."""
@@ -700,10 +739,13 @@ def scaling_line(args, gl, nat, torch, dist, device, world, rank):
         start, n = shard_bounds(total, rank, world)
     env = gl.BatchedEnv("lorenz3", n, dtype="float32", seed=0, global_env_offset=start,
                         autoreset=True, device=device.index)
-    tm = measure_steps(args, torch, dist, nat, env, device, world, rank, False)
+    subs = make_subs(args, gl, n, start, device.index, {})
+    tm = measure_steps(args, torch, dist, nat, env, device, world, rank, False, subs=subs)
     launch_s = tm["ev_ms"] / 1e3 / tm["launches"]
     achieved = env.info.bytes_per_env_step * n / launch_s / 1e9
-    env.close()
+    sub_n = subs[0].num_envs if subs else n
+    for e in [env] + (subs or []):
+        e.close()
     return {
         "metric": METRIC + " (%s scaling)" % mode,
         "value": total * tm["steps"] * tm["windows"] / tm["elapsed"], "unit": "env-steps/s",
@@ -715,7 +757,7 @@ def scaling_line(args, gl, nat, torch, dist, device, world, rank):
         "timing": tm["timing"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "avg_launch_us": launch_s * 1e6,
-                     "kernel": kernel_name("lorenz3", "step", n)},
+                     "kernel": kernel_name("lorenz3", "step", sub_n)},
     }
 
 
@@ -806,7 +848,52 @@ def gather_line(args, gl, nat, torch, dist, device, world, rank, total, n, start
     }
 
 
-def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min_window_s=0.2):
+class _Lane:
+    """One handle of a rank's shard with its own on-device ring, HIP stream and captured
+    hipGraphs (measure_steps drives 1 lane, or S with --streams S)."""
+
+    def __init__(self, args, torch, nat, env, device, rank, rollout, lane):
+        A, O = env.action_dim, env.obs_dim
+        arange = SYSTEM_INFO[args.system][2]
+        self.R = R = args.ring if not rollout else 1
+        self.T = T = args.K if rollout else 1
+        tdt = env.tdtype
+        g = torch.Generator(device=device).manual_seed(1000 + rank + 7919 * lane)
+        n = env.num_envs
+        self.buf = (
+            (torch.rand((R, T, n, A), generator=g, device=device) * 2 - 1) * arange,
+            torch.empty((R, T, n, O), device=device, dtype=tdt),
+            torch.empty((R, T, n), device=device, dtype=tdt),
+            torch.empty((R, T, n), dtype=torch.uint8, device=device))
+        acts, obs, rew, done = self.buf
+        env.reset()
+        self.env, self.h, self.rollout, self.counter = env, env._h, rollout, 0
+        # every ring slot through the checked caller-buffer entry once (dtype / device /
+        # contiguity / element count vs lz_info), then its pointer tuple is launched as is
+        if rollout:
+            self.slots = [env.rollout_args(T, acts[r], obs[r], rew[r], done[r]) for r in range(R)]
+        else:
+            self.slots = [env.step_args(acts[r, 0], obs[r, 0], rew[r, 0], done[r, 0],
+                                        env.done_idx, env.term_obs) for r in range(R)]
+        self.fn = nat.lib.lz_rollout if rollout else nat.lib.lz_step
+        self.nat = nat
+        self.stream = torch.cuda.Stream(device)
+        nat.check(nat.lib.lz_set_stream(self.h, ctypes.c_void_p(self.stream.cuda_stream)))
+        self.graph = self.graph_rem = None
+        self.flush = None
+
+    def one(self):
+        sl = self.slots[self.counter % self.R]
+        self.counter += 1
+        st = self.fn(self.h, *sl)
+        if st:
+            self.nat.check(st)
+        if self.flush is not None:
+            self.flush()
+
+
+def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min_window_s=0.2,
+                  subs=None):
     """Time EXACTLY K env steps (K = --steps; rollout mode: --steps rounded down to whole
     --K launches), each timed window bracketed by a barrier + torch.cuda.synchronize()
     on both sides.  When one window is shorter than `min_window_s` (e.g. the driver's
@@ -814,24 +901,16 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
     until their sum reaches it; value = windows x K x envs / summed window time (the
     MAX over ranks).  Step mode replays a hipGraph of L lz_step launches and launches
     the K mod L remainder eagerly; an odd remainder is followed by one untimed step so
-    the captured graph's ping-pong parity stays valid."""
-    A, O = env.action_dim, env.obs_dim
-    arange = SYSTEM_INFO[args.system][2]
-    R = args.ring if not rollout else 1
-    T = args.K if rollout else 1
-    tdt = env.tdtype
-    g = torch.Generator(device=device).manual_seed(1000 + rank)
-    acts = (torch.rand((R, T, env.num_envs, A), generator=g, device=device) * 2 - 1) * arange
-    obs = torch.empty((R, T, env.num_envs, O), device=device, dtype=tdt)
-    rew = torch.empty((R, T, env.num_envs), device=device, dtype=tdt)
-    done = torch.empty((R, T, env.num_envs), dtype=torch.uint8, device=device)
-    env.reset()
-    h = env._h
-    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    slots = [(P(acts[r]), P(obs[r]), P(rew[r]), P(done[r])) for r in range(R)]
-    didx, tobs = P(env.done_idx), P(env.term_obs)
-    lz_step, lz_rollout = nat.lib.lz_step, nat.lib.lz_rollout
-    counter = [0]
+    the captured graph's ping-pong parity stays valid.
+
+    subs (--streams S): the shard as S sub-handles of consecutive global_env_offset
+    (bit-identical to one handle: tests/test_gpu_streams.py), each with its own ring,
+    stream and graphs; every window runs all S chains of K steps concurrently, bracketed
+    by one device synchronize.  The HIP-event time is the span from the first stream's
+    start event to the last stream's end event."""
+    lanes = [_Lane(args, torch, nat, e, device, rank, rollout, j)
+             for j, e in enumerate(subs or [env])]
+    R, T = lanes[0].R, lanes[0].T
     flush = getattr(args, "ic_flush_mib", 0)
     if flush:  # A/B only: evict the Infinity Cache between steps (see --ic-flush-mib)
         fsrc = torch.ones((flush << 18,), device=device)
@@ -839,23 +918,9 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
         fsum = torch.empty((), device=device)
         if args.ic_flush_kind == "read":  # the same bytes read as the copy moves in total
             fsrc = torch.ones((flush << 19,), device=device)
+        lanes[0].flush = ((lambda: fdst.copy_(fsrc)) if args.ic_flush_kind == "copy"
+                          else (lambda: torch.sum(fsrc, dim=0, out=fsum)))
 
-    def one():
-        a, o, r_, d = slots[counter[0] % R]
-        counter[0] += 1
-        if rollout:
-            st = lz_rollout(h, T, a, o, r_, d, None, None, 0, None)
-        else:
-            st = lz_step(h, a, None, o, r_, d, didx, tobs, None)
-        if st:
-            nat.check(st)
-        if flush and args.ic_flush_kind == "copy":
-            fdst.copy_(fsrc)
-        elif flush:
-            torch.sum(fsrc, dim=0, out=fsum)
-
-    stream = torch.cuda.Stream(device)
-    graph = None
     L = max(2, args.graph_len - args.graph_len % 2)  # even: keeps the ping-pong parity
     if R > 1 and L % R and R % L:
         L = R
@@ -863,68 +928,83 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
     warm = args.warmup if not rollout else 2
     if rollout:
         L = 1
-    with torch.cuda.stream(stream):
-        nat.check(nat.lib.lz_set_stream(h, ctypes.c_void_p(stream.cuda_stream)))
-        for _ in range(max(warm, 2)):
-            one()
-        graph_rem, rem_n = None, 0
-        if args.launch == "graph" and not rollout:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=stream):
-                for _ in range(L):
-                    one()
-            # the window's K mod L remainder as a graph too (its even part: the captured
-            # ping-pong parity), so that a short window (the driver's --steps 20) is not
-            # paced by one Python launch per step
-            rem_n = (launches % L) - (launches % L) % 2
-            if rem_n:
-                graph_rem = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graph_rem, stream=stream):
-                    for _ in range(rem_n):
-                        one()
+    use_graph = args.launch == "graph" and not rollout
+    # the window's K mod L remainder as a graph too (its even part: the captured
+    # ping-pong parity), so that a short window (the driver's --steps 20) is not
+    # paced by one Python launch per step
+    rem_n = (launches % L) - (launches % L) % 2 if use_graph else 0
+    for ln in lanes:
+        with torch.cuda.stream(ln.stream):
+            for _ in range(max(warm, 2)):
+                ln.one()
+            if use_graph:
+                ln.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ln.graph, stream=ln.stream):
+                    for _ in range(L):
+                        ln.one()
+                if rem_n:
+                    ln.graph_rem = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(ln.graph_rem, stream=ln.stream):
+                        for _ in range(rem_n):
+                            ln.one()
+    torch.cuda.synchronize(device)
+
+    def run(nlaunch):  # exactly nlaunch launches on every lane, the lanes interleaved
+        if not use_graph:
+            for _ in range(nlaunch):
+                for ln in lanes:
+                    with torch.cuda.stream(ln.stream):
+                        ln.one()
+            return
+        for _ in range(nlaunch // L):
+            for ln in lanes:
+                with torch.cuda.stream(ln.stream):
+                    ln.graph.replay()
+        r = nlaunch % L
+        if rem_n and r >= rem_n:
+            for ln in lanes:
+                with torch.cuda.stream(ln.stream):
+                    ln.graph_rem.replay()
+            r -= rem_n
+        for _ in range(r):
+            for ln in lanes:
+                with torch.cuda.stream(ln.stream):
+                    ln.one()
+
+    def fix_parity(nlaunch):  # untimed: an odd eager remainder flipped the parity
+        if use_graph and (nlaunch % L) % 2:
+            for ln in lanes:
+                with torch.cuda.stream(ln.stream):
+                    ln.one()
+
+    if use_graph:
+        run(max(warm, L))  # warm the graph path too
+        fix_parity(max(warm, L))
+    torch.cuda.synchronize(device)
+
+    def window():
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize(device)
-
-        def run(nlaunch):  # exactly nlaunch launches
-            if graph is None:
-                for _ in range(nlaunch):
-                    one()
-                return
-            for _ in range(nlaunch // L):
-                graph.replay()
-            r = nlaunch % L
-            if graph_rem is not None and r >= rem_n:
-                graph_rem.replay()
-                r -= rem_n
-            for _ in range(r):
-                one()
-
-        def fix_parity(nlaunch):  # untimed: an odd eager remainder flipped the parity
-            if graph is not None and (nlaunch % L) % 2:
-                one()
-
-        if graph is not None:
-            run(max(warm, L))  # warm the graph path too
-            fix_parity(max(warm, L))
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in lanes]
+        t0 = time.perf_counter()
+        for ln, (e0, _) in zip(lanes, ev):
+            e0.record(ln.stream)
+        run(launches)
+        for ln, (_, e1) in zip(lanes, ev):
+            e1.record(ln.stream)
         torch.cuda.synchronize(device)
-
-        def window():
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize(device)
-            ev0 = torch.cuda.Event(enable_timing=True)
-            ev1 = torch.cuda.Event(enable_timing=True)
-            t0 = time.perf_counter()
-            ev0.record(stream)
-            run(launches)
-            ev1.record(stream)
-            torch.cuda.synchronize(device)
-            # stop before the closing barrier: a collective's latency is not part of the K
-            # steps (the path has none); the job's time is the MAX over ranks below
-            t1 = time.perf_counter()
-            if world > 1:
-                dist.barrier()
-            fix_parity(launches)
-            return t1 - t0, ev0.elapsed_time(ev1)
+        # stop before the closing barrier: a collective's latency is not part of the K
+        # steps (the path has none); the job's time is the MAX over ranks below
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        fix_parity(launches)
+        base = ev[0][0]
+        span = (max(base.elapsed_time(e1) for _, e1 in ev)
+                - min(0.0, min(base.elapsed_time(e0) for e0, _ in ev)))
+        return t1 - t0, span
 
         first = window()
         # windows until min_window_s are timed in total: batches sized from the windows
@@ -954,8 +1034,8 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
     wms = sorted(w[0] * 1e3 for w in wins)
     K = launches * T
     return {
-        "steps": K, "T": T, "ring": R, "graph_len": L, "graph": graph is not None,
-        "graph_rem": rem_n if graph_rem is not None else 0,
+        "steps": K, "T": T, "ring": R, "graph_len": L, "graph": use_graph,
+        "graph_rem": rem_n, "streams": len(lanes),
         "warmup": warm, "launches": launches * need, "windows": need,
         "elapsed": elapsed, "ev_ms": ev_ms,
         "timing": {
@@ -1101,7 +1181,11 @@ def main():
             print(json.dumps(out), flush=True)
         return
     rollout = args.mode == "rollout"
-    tm = measure_steps(args, torch, dist, nat, env, device, world, rank, rollout)
+    subs = make_subs(args, gl, n, start, local, kw) if not rollout else None
+    tm = measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, subs=subs)
+    sub_n = subs[0].num_envs if subs else n
+    for e in subs or []:
+        e.close()
     K, L, R, T = tm["steps"], tm["graph_len"], tm["ring"], tm["T"]
     elapsed, ev_ms, nl = tm["elapsed"], tm["ev_ms"], tm["launches"]
     warm = tm["warmup"]
@@ -1150,7 +1234,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": kernel_name(args.system, args.mode, n, f64=args.dtype == "float64",
+            "kernel": kernel_name(args.system, args.mode, sub_n, f64=args.dtype == "float64",
                                   no_done=args.max_episode_steps == 0,
                                   num_cus=torch.cuda.get_device_properties(device).multi_processor_count,
                                   variant=args.variant, integrator=kw.get("integrator", "euler"),
@@ -1161,7 +1245,12 @@ def main():
                     " x steps per launch) / HIP-event average launch time on the launch stream",
         },
     }
-    traffic = load_traffic(out["roofline"]["kernel"], n)
+    traffic = load_traffic(out["roofline"]["kernel"], n) if not subs else None
+    if subs:
+        out["config"]["streams"] = len(subs)
+        out["roofline"]["note"] += ("; --streams %d: the launch time is the span of one step of "
+                                    "all %d concurrent sub-handle chains (%d envs each)"
+                                    % (len(subs), len(subs), sub_n))
     if traffic is not None:
         out["roofline"]["traffic"] = traffic["bytes_per_launch"]
         out["roofline"]["traffic_source"] = traffic["source"]
@@ -1229,17 +1318,16 @@ def cold_state_probe(gl, nat, torch, device, n, reps=96, flush_mib=384):
     done = torch.empty((R, n), dtype=torch.uint8, device=device)
     big = torch.ones((flush_mib << 18,), device=device)
     out = torch.empty((), device=device)
-    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    slots = [(P(acts[r]), P(obs[r]), P(rew[r]), P(done[r])) for r in range(R)]
-    didx, tobs = P(env.done_idx), P(env.term_obs)
+    slots = [env.step_args(acts[r], obs[r], rew[r], done[r], env.done_idx, env.term_obs)
+             for r in range(R)]  # the checked caller-buffer entry (core.step_io_args)
     stream = torch.cuda.Stream(device)
     nat.check(nat.lib.lz_set_stream(env._h, ctypes.c_void_p(stream.cuda_stream)))
     k = [0]
 
     def step():
-        a, o, r_, d = slots[k[0] % R]
+        sl = slots[k[0] % R]
         k[0] += 1
-        nat.check(nat.lib.lz_step(env._h, a, None, o, r_, d, didx, tobs, None))
+        nat.check(nat.lib.lz_step(env._h, *sl))
 
     res = {}
     with torch.cuda.stream(stream):

@@ -266,6 +266,29 @@ constexpr int kAXSh2 = kAXSh1 + 128 * 2;                    // int16 [128]
 constexpr int kAXPostSh = kAXSh2 + 128 * 2;                 // int16 [64], pi slot only
 static_assert(kAXPostSh + 64 * 2 <= kAFNet, "i8x4 net slot");
 
+// Blob format tag: the float32 and i8x4 blobs of one policy family have the
+// same size and offsets, so only the launch's LZ_POLICY_I8X4 flag (and the entry point:
+// attention vs attention + LayerNorm) says how to read one.  Every packer of those blobs
+// writes a 16-B tag into spare bytes -- {kBlobMagic, format, ~format, kBlobMagic ^ format}
+// -- and every float32 / i8x4 policy kernel compares it with the format its launch
+// expects; on a mismatch the kernel's LDS copy of the blob is NaN (weights, Normal
+// constants, tanh table), so every action, value, log-prob, reward and observation the
+// launch writes is NaN instead of a silently wrong rollout.
+constexpr uint32_t kBlobMagic = 0x42505A4Cu;  // "LZPB"
+constexpr int kF32Tag = kF32HB + 48;          // net 0 (pi): the head bias uses 16 of its 64 B
+constexpr int kAXTag = kAXPostSh + 64 * 2;    // the pi slot's spare bytes (f32 and i8x4 alike)
+static_assert(kAXTag + 16 <= kAFNet, "blob tag in the attention net slot");
+constexpr int kAFTag = kAFPi + kAXTag;
+__host__ __device__ inline void blob_tag(uint32_t fmt, uint32_t t[4]) {
+  t[0] = kBlobMagic;
+  t[1] = fmt;
+  t[2] = ~fmt;
+  t[3] = kBlobMagic ^ fmt;
+}
+__host__ __device__ inline bool blob_tag_ok(const uint32_t t[4], uint32_t fmt) {
+  return t[0] == kBlobMagic && t[1] == fmt && t[2] == ~fmt && t[3] == (kBlobMagic ^ fmt);
+}
+
 struct PArgs {
   const uint8_t* blob;     // device copy of the packed policy
   const float* obs_in;     // [N, O] raw observation at rollout start

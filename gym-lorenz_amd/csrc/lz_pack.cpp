@@ -649,6 +649,7 @@ static lz_status pack_mlp_f32(const lz_mlp_policy* p, int32_t hidden, void* host
     pack_net_i8x4(b + lz::kF32Net, vw2);
   }
   pack_gauss(reinterpret_cast<float*>(b + lz::kF32LogStd), A, p->log_std);
+  lz::blob_tag(i8 ? LZ_BLOB_MLP_I8X4 : LZ_BLOB_MLP_F32, reinterpret_cast<uint32_t*>(b + lz::kF32Tag));
   // c_j 8^-j: the kernel's Horner runs in u = 8 t (tanh_tab)
   float* tt = reinterpret_cast<float*>(b + lz::kF32Tanh);
   for (int k = 0; k < 72; ++k)
@@ -718,6 +719,7 @@ static lz_status pack_attn_f32_checked(const lz_attn_policy* p, const float* ln_
   std::memset(b, 0, lz::kAFBlobBytes);
   pack_attn_f32(b, p, ln_w, ln_b);
   pack_gauss(reinterpret_cast<float*>(b + lz::kAFLogStd), p->act_dim, p->log_std);
+  lz::blob_tag(ln_w ? LZ_BLOB_ATTN_LN_F32 : LZ_BLOB_ATTN_F32, reinterpret_cast<uint32_t*>(b + lz::kAFTag));
   float* tt = reinterpret_cast<float*>(b + lz::kAFTanh);
   for (int k = 0; k < 72; ++k)
     for (int j = 0; j < 8; ++j) tt[8 * k + j] = std::ldexp(kTanhTab[8 * k + j], -3 * j);
@@ -741,7 +743,26 @@ static lz_status pack_attn_i8x4_checked(const lz_attn_policy* p, const float* ln
         return pfail(LZ_ERR_INVALID, "i8x4: the nets' and post_attention_fc's weights must be finite");
   }
   pack_attn_i8x4(static_cast<uint8_t*>(host_blob), p, ln_w, ln_b);
+  lz::blob_tag(ln_w ? LZ_BLOB_ATTN_LN_I8X4 : LZ_BLOB_ATTN_I8X4,
+               reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(host_blob) + lz::kAFTag));
   return LZ_OK;
+}
+
+int32_t lz_policy_blob_format(const void* host_blob, int64_t size) {
+  if (!host_blob) return LZ_BLOB_UNKNOWN;
+  const uint8_t* b = static_cast<const uint8_t*>(host_blob);
+  uint32_t t[4];
+  if (size >= lz::kAFBlobBytes) {  // attention families: the tag in the pi slot's spare bytes
+    std::memcpy(t, b + lz::kAFTag, 16);
+    for (uint32_t f : {LZ_BLOB_ATTN_F32, LZ_BLOB_ATTN_I8X4, LZ_BLOB_ATTN_LN_F32, LZ_BLOB_ATTN_LN_I8X4})
+      if (lz::blob_tag_ok(t, f)) return (int32_t)f;
+  }
+  if (size >= lz::kF32BlobBytes) {
+    std::memcpy(t, b + lz::kF32Tag, 16);
+    for (uint32_t f : {LZ_BLOB_MLP_F32, LZ_BLOB_MLP_I8X4})
+      if (lz::blob_tag_ok(t, f)) return (int32_t)f;
+  }
+  return LZ_BLOB_UNKNOWN;
 }
 
 lz_status lz_attn_policy_pack_i8x4(const lz_attn_policy* p, void* host_blob, int64_t cap) {

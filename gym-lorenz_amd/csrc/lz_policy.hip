@@ -978,6 +978,26 @@ constexpr int kMlpSerial = 0, kMlpPair = 1, kMlpPairPipe = 2, kAttn = 3, kAttnLn
               kMlpF32 = 5, kMlpI8 = 6;  // kMlpI8: kMlpF32 with layer 2 as mlp_i8_tail
 constexpr bool mlp_f32_kind(int k) { return k == kMlpF32 || k == kMlpI8; }
 
+// The blob's format tag (lz_internal.h kBlobMagic) against the format this launch expects.
+__device__ inline bool blob_is(const uint8_t* blob, int off, uint32_t fmt) {
+  const uint32_t* t = reinterpret_cast<const uint32_t*>(blob + off);
+  const uint32_t w[4] = {t[0], t[1], t[2], t[3]};
+  return blob_tag_ok(w, fmt);
+}
+
+// Copy n16 16-B pieces of the blob into LDS -- or, when its tag does not match the
+// launch (`bad`, workgroup-uniform), fill them with NaN: every weight, Normal constant
+// and tanh-table entry is NaN, so every output of the launch is NaN.
+__device__ inline void blob_to_lds(f4v* dst, const f4v* src, int n16, int tid, int stride, bool bad) {
+  if (bad) {
+    const float q = __builtin_nanf("");
+    const f4v nan4 = {q, q, q, q};
+    for (int v = tid; v < n16; v += stride) dst[v] = nan4;
+  } else {
+    for (int v = tid; v < n16; v += stride) dst[v] = src[v];
+  }
+}
+
 // V(x) alone (truncation bootstrap, last values): the value net, after the shared
 // attention extractor for kPair == kAttn
 template <int E, int O, int kPair>
@@ -1023,9 +1043,11 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy(KArgs a, PArgs p) {
   const int slot = E == 64 ? lane : (lane & 31);  // this lane's env within the tile
   const bool owner = E == 64 || h == 0;           // lanes that step an env
   {
-    const f4v* src = reinterpret_cast<const f4v*>(p.blob);
-    f4v* dst = reinterpret_cast<f4v*>(s_blob);
-    for (int v = tid; v < kBlob / 16; v += W * 64) dst[v] = src[v];
+    bool bad = false;
+    if constexpr (mlp_f32_kind(kPair))
+      bad = !blob_is(p.blob, kF32Tag, kPair == kMlpI8 ? LZ_BLOB_MLP_I8X4 : LZ_BLOB_MLP_F32);
+    blob_to_lds(reinterpret_cast<f4v*>(s_blob), reinterpret_cast<const f4v*>(p.blob), kBlob / 16,
+                tid, W * 64, bad);
   }
   if (tid < O) {  // VecNormalize: mean and sqrt(var + eps) per obs dim
     s_norm[tid] = p.norm ? p.norm[tid] : 0.0;
@@ -1316,11 +1338,8 @@ __global__ __launch_bounds__(512) void k_rollout_policy_f32_split(KArgs a, PArgs
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tw = wave & (T - 1);
   const bool owner = h == 0;
-  {
-    const f4v* src = reinterpret_cast<const f4v*>(p.blob);
-    f4v* dst = reinterpret_cast<f4v*>(s_blob);
-    for (int v = tid; v < kF32BlobBytes / 16; v += 2 * T * 64) dst[v] = src[v];
-  }
+  blob_to_lds(reinterpret_cast<f4v*>(s_blob), reinterpret_cast<const f4v*>(p.blob), kF32BlobBytes / 16,
+              tid, 2 * T * 64, !blob_is(p.blob, kF32Tag, kI8 ? LZ_BLOB_MLP_I8X4 : LZ_BLOB_MLP_F32));
   if (tid < O) {
     s_norm[tid] = p.norm ? p.norm[tid] : 0.0;
     s_norm[kPolMaxObs + tid] = p.norm ? sqrt(p.norm[O + tid] + p.eps) : 1.0;
@@ -1521,11 +1540,8 @@ __global__ __launch_bounds__(W * 64) void k_policy_step_f32(KArgs a, PArgs p, PS
   const int tid = (int)threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int slot = lane & 31;
-  {
-    const f4v* src = reinterpret_cast<const f4v*>(p.blob);
-    f4v* dst = reinterpret_cast<f4v*>(s_blob);
-    for (int v = tid; v < kF32BlobBytes / 16; v += W * 64) dst[v] = src[v];
-  }
+  blob_to_lds(reinterpret_cast<f4v*>(s_blob), reinterpret_cast<const f4v*>(p.blob), kF32BlobBytes / 16,
+              tid, W * 64, !blob_is(p.blob, kF32Tag, LZ_BLOB_MLP_F32));
   if (tid < O) {
     s_norm[tid] = p.norm[tid];
     s_norm[kPolMaxObs + tid] = sqrt(p.norm[O + tid] + p.eps);
@@ -2126,12 +2142,15 @@ __global__ __launch_bounds__(W * 64) void k_rollout_policy_attn_f32(KArgs a, PAr
   const int tid = (int)threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, G = lane >> 4, col = lane & 15;
   {
-    const f4v* src = reinterpret_cast<const f4v*>(p.blob);
-    f4v* dst = reinterpret_cast<f4v*>(s_lds);
-    for (int v = tid; v < kAFExt / 16; v += W * 64) dst[v] = src[v];
-    const f4v* sc = reinterpret_cast<const f4v*>(p.blob + kAFLogStd);
-    f4v* dc = reinterpret_cast<f4v*>(s_lds + kAFExt);
-    for (int v = tid; v < kAFConst / 16; v += W * 64) dc[v] = sc[v];
+    const bool bad = !blob_is(p.blob, kAFTag,
+                              kLn ? (kI8 ? LZ_BLOB_ATTN_LN_I8X4 : LZ_BLOB_ATTN_LN_F32)
+                                  : (kI8 ? LZ_BLOB_ATTN_I8X4 : LZ_BLOB_ATTN_F32));
+    // (a mismatch poisons the resident extractor and constants: the features, and with
+    // them both nets' outputs, are NaN whatever the DMA'd net slots hold)
+    blob_to_lds(reinterpret_cast<f4v*>(s_lds), reinterpret_cast<const f4v*>(p.blob), kAFExt / 16, tid,
+                W * 64, bad);
+    blob_to_lds(reinterpret_cast<f4v*>(s_lds + kAFExt), reinterpret_cast<const f4v*>(p.blob + kAFLogStd),
+                kAFConst / 16, tid, W * 64, bad);
     if constexpr (kI8) {
       if (tid < kAttFeat * 2 / 16)
         reinterpret_cast<f4v*>(s_psh)[tid] = reinterpret_cast<const f4v*>(p.blob + kAFPi + kAXPostSh)[tid];

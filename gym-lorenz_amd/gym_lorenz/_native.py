@@ -79,6 +79,9 @@ class LzInfo(ctypes.Structure):
 
 
 POLICY_DETERMINISTIC, POLICY_BOOTSTRAP, POLICY_I8X4 = 1, 2, 4
+# lz_policy_blob_format: the format tag every float32 / i8x4 packer writes (LZ_BLOB_*)
+(BLOB_UNKNOWN, BLOB_MLP_F32, BLOB_MLP_I8X4, BLOB_ATTN_F32, BLOB_ATTN_I8X4, BLOB_ATTN_LN_F32,
+ BLOB_ATTN_LN_I8X4) = range(7)
 POLICY_HIDDEN = 128
 
 
@@ -204,6 +207,7 @@ _SIGS = {
                                              ctypes.c_int64]),
     "lz_rollout_policy": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
     "lz_policy_f32_blob_bytes": (ctypes.c_int64, []),
+    "lz_policy_blob_format": (ctypes.c_int32, [VP, ctypes.c_int64]),
     "lz_policy_pack_f32": (ctypes.c_int, [ctypes.POINTER(LzMlpPolicy), ctypes.c_int32, VP,
                                           ctypes.c_int64]),
     "lz_rollout_policy_f32": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),

@@ -23,6 +23,83 @@ def _ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+def check_buffer(t, name, dtype, numel, device, required=True, at_least=False):
+    """One caller-owned buffer handed to the C-ABI as a raw pointer: the ABI has no sizes
+    (include/lorenz_env.h lz_step / lz_rollout), so a buffer of the wrong element count is
+    an out-of-bounds write on the device.  Refuses (LorenzEnvError LZ_ERR_INVALID) anything
+    but a contiguous tensor of exactly `numel` (at_least: at least `numel`, a capacity)
+    elements of `dtype` on `device`; returns its ctypes pointer (None for an absent
+    optional buffer)."""
+    if t is None:
+        if required:
+            raise nat.LorenzEnvError(nat.LZ_ERR_INVALID, "%s: required buffer is None" % name)
+        return None
+    if not isinstance(t, torch.Tensor):
+        raise nat.LorenzEnvError(nat.LZ_ERR_INVALID, "%s: expected a torch.Tensor, got %s"
+                                 % (name, type(t).__name__))
+    bad = []
+    if t.dtype != dtype:
+        bad.append("dtype %s (need %s)" % (t.dtype, dtype))
+    if t.device != device:
+        bad.append("device %s (need %s)" % (t.device, device))
+    if not t.is_contiguous():
+        bad.append("not contiguous")
+    if t.numel() < numel or (t.numel() != numel and not at_least):
+        bad.append("%d elements, shape %s (need %s%d)" % (t.numel(), tuple(t.shape),
+                                                          ">= " if at_least else "", numel))
+    if bad:
+        raise nat.LorenzEnvError(nat.LZ_ERR_INVALID, "%s: %s" % (name, "; ".join(bad)))
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def step_io_args(spec, actions, obs, rew, done, done_idx=None, term_obs=None, n_done=None,
+                 noise=None):
+    """Validated lz_step arguments after the handle (actions, noise, obs, rew, done,
+    done_idx, terminal_obs, n_done) for caller-owned buffers, checked against the
+    handle's lz_info: `spec` carries num_envs, obs_dim, action_dim, tdtype and device (a
+    BatchedEnv, or the CPU test double) and reads_actions.  actions float32 [N, A] (may
+    be None for LORENZ4 / SC, which read none: lz_api.cpp lz_step needs_act); noise
+    float64 [N, 3]; obs T [N, O]; rew T [N]; done uint8 [N]; the compact list int32 [>= N]
+    + T [>= N, O] (capacities; both or neither) + int32 [1]."""
+    n, o, a_dim, td, dev = spec.num_envs, spec.obs_dim, spec.action_dim, spec.tdtype, spec.device
+    need_a = getattr(spec, "reads_actions", True)
+    pa = check_buffer(actions, "actions", torch.float32, n * a_dim, dev, required=need_a)
+    pz = check_buffer(noise, "noise", torch.float64, n * 3, dev, required=False)
+    po = check_buffer(obs, "obs", td, n * o, dev)
+    pr = check_buffer(rew, "rew", td, n, dev)
+    pd = check_buffer(done, "done", torch.uint8, n, dev)
+    if (done_idx is None) != (term_obs is None):
+        raise nat.LorenzEnvError(nat.LZ_ERR_INVALID, "done_idx and term_obs: both or neither")
+    pi = check_buffer(done_idx, "done_idx", torch.int32, n, dev, required=False, at_least=True)
+    pt = check_buffer(term_obs, "term_obs", td, n * o, dev, required=False, at_least=True)
+    pn = check_buffer(n_done, "n_done", torch.int32, 1, dev, required=False)
+    return pa, pz, po, pr, pd, pi, pt, pn
+
+
+def rollout_io_args(spec, K, actions, obs, rew, done, done_idx=None, term_obs=None, cap=0,
+                    n_done=None):
+    """Validated lz_rollout arguments after the handle (K, actions, obs, rew, done,
+    done_idx, terminal_obs, cap, n_done): time-major actions float32 [K, N, A], obs
+    T [K, N, O], rew T [K, N], done uint8 [K, N]; the optional done list int64 [cap] +
+    T [cap, O] (both or neither, cap > 0) + int32 [1]."""
+    K, cap = int(K), int(cap)
+    if K < 1:
+        raise nat.LorenzEnvError(nat.LZ_ERR_INVALID, "K must be >= 1, got %d" % K)
+    n, o, a_dim, td, dev = spec.num_envs, spec.obs_dim, spec.action_dim, spec.tdtype, spec.device
+    need_a = getattr(spec, "reads_actions", True)
+    pa = check_buffer(actions, "actions", torch.float32, K * n * a_dim, dev, required=need_a)
+    po = check_buffer(obs, "obs", td, K * n * o, dev)
+    pr = check_buffer(rew, "rew", td, K * n, dev)
+    pd = check_buffer(done, "done", torch.uint8, K * n, dev)
+    if (done_idx is None) != (term_obs is None) or (done_idx is not None and cap < 1):
+        raise nat.LorenzEnvError(nat.LZ_ERR_INVALID, "done_idx / term_obs: both or neither, "
+                                 "with cap >= 1")
+    pi = check_buffer(done_idx, "done_idx", torch.int64, cap, dev, required=False)
+    pt = check_buffer(term_obs, "term_obs", td, cap * o, dev, required=False)
+    pn = check_buffer(n_done, "n_done", torch.int32, 1, dev, required=False)
+    return K, pa, po, pr, pd, pi, pt, (cap if pi is not None else 0), pn
+
+
 class BatchedEnv:
     """One handle = one shard of the env axis on one device and stream.
 
@@ -85,6 +162,8 @@ class BatchedEnv:
         self.config = got
         self.num_envs = int(num_envs)
         self.obs_dim, self.action_dim, self.init_dim = info.obs_dim, info.action_dim, info.init_dim
+        # LORENZ4 / SC read no actions (lz_api.cpp lz_step needs_act)
+        self.reads_actions = self.system not in (nat.LORENZ4, nat.SC)
         self.tdtype = _TDTYPE[cfg.dtype]
         self.global_env_offset = int(global_env_offset)
         n, o, dev = self.num_envs, self.obs_dim, self.device
@@ -137,7 +216,10 @@ class BatchedEnv:
         envs keep their previous values)."""
         mask = self._check_dev(mask, torch.uint8, (self.num_envs,), "mask")
         init = self._check_dev(init, self.tdtype, (self.num_envs, self.init_dim), "init")
-        out = self.obs if out is None else out
+        if out is None:
+            out = self.obs
+        else:  # a caller-owned obs buffer: the checked entry's rules (check_buffer)
+            check_buffer(out, "out", self.tdtype, self.num_envs * self.obs_dim, self.device)
         nat.check(nat.lib.lz_reset(self._h, _ptr(mask), _ptr(init), _ptr(out)))
         return out
 
@@ -150,22 +232,47 @@ class BatchedEnv:
         a = self._check_dev(actions, torch.float32, (self.num_envs, self.action_dim), "actions")
         nz = self._check_dev(noise, torch.float64, (self.num_envs, 3), "noise")
         obs, rew, done = (self.obs, self.rew, self.done) if out is None else out
-        if out is not None:
-            n = self.num_envs
-            if (obs.shape != (n, self.obs_dim) or obs.dtype != self.tdtype or rew.shape != (n,)
-                    or rew.dtype != self.tdtype or done.shape != (n,) or done.dtype != torch.uint8
-                    or not (obs.is_contiguous() and rew.is_contiguous() and done.is_contiguous())
-                    or {obs.device, rew.device, done.device} != {self.device}):
-                raise ValueError("step(out=...): wrong shape / dtype / device / layout")
         if compact_out is not None:
             didx, tobs, ndone = compact_out
         else:
             didx, tobs = self.done_idx, self.term_obs
             ndone = self.n_done_dev if (self.compact and want_n_done) else None
-        nat.check(nat.lib.lz_step(
-            self._h, _ptr(a), _ptr(nz), _ptr(obs), _ptr(rew), _ptr(done),
-            _ptr(didx), _ptr(tobs), _ptr(ndone)))
+        nat.check(nat.lib.lz_step(self._h, *step_io_args(self, a, obs, rew, done, didx, tobs,
+                                                         ndone, noise=nz)))
         self._last_actions = a  # keep alive until the stream consumed it
+        return obs, rew, done
+
+    def step_args(self, actions, obs, rew, done, done_idx=None, term_obs=None, n_done=None,
+                  noise=None):
+        """The checked entry for CALLER-OWNED buffers (rollout rings, graph-captured
+        loops): every buffer's dtype, device, contiguity and element count checked against
+        this handle's lz_info (core.step_io_args), then the pointer tuple that follows
+        the handle in lz_step.  Validate once, launch many times:
+        ``nat.lib.lz_step(env._h, *env.step_args(...))``.  No conversion: a wrong buffer
+        raises LorenzEnvError(LZ_ERR_INVALID) instead of reaching the kernel (an obs slot
+        of [N, 3] for LORENZ3's [N, 6] obs would be written 12 B per env past its end)."""
+        return step_io_args(self, actions, obs, rew, done, done_idx, term_obs, n_done, noise)
+
+    def step_into(self, actions, obs, rew, done, done_idx=None, term_obs=None, n_done=None,
+                  noise=None):
+        """lz_step into caller-owned device buffers, checked as step_args."""
+        nat.check(nat.lib.lz_step(self._h, *self.step_args(actions, obs, rew, done, done_idx,
+                                                           term_obs, n_done, noise)))
+        self._last_actions = actions
+        return obs, rew, done
+
+    def rollout_args(self, K, actions, obs, rew, done, done_idx=None, term_obs=None, cap=0,
+                     n_done=None):
+        """lz_rollout's arguments after the handle for caller-owned time-major buffers,
+        checked as step_args (core.rollout_io_args)."""
+        return rollout_io_args(self, K, actions, obs, rew, done, done_idx, term_obs, cap, n_done)
+
+    def rollout_into(self, K, actions, obs, rew, done, done_idx=None, term_obs=None, cap=0,
+                     n_done=None):
+        """lz_rollout into caller-owned device buffers, checked as rollout_args."""
+        nat.check(nat.lib.lz_rollout(self._h, *self.rollout_args(K, actions, obs, rew, done,
+                                                                 done_idx, term_obs, cap, n_done)))
+        self._last_actions = actions
         return obs, rew, done
 
     def step_vecnorm(self, actions, vn, out, compact_out):
@@ -209,8 +316,8 @@ class BatchedEnv:
             didx = torch.empty((capture_terminal,), dtype=torch.int64, device=dev)
             tobs = torch.empty((capture_terminal, o), dtype=self.tdtype, device=dev)
             ndone = torch.zeros((1,), dtype=torch.int32, device=dev)
-        nat.check(nat.lib.lz_rollout(self._h, K, _ptr(a), _ptr(obs), _ptr(rew), _ptr(done),
-                                     _ptr(didx), _ptr(tobs), int(capture_terminal), _ptr(ndone)))
+        nat.check(nat.lib.lz_rollout(self._h, *rollout_io_args(self, K, a, obs, rew, done, didx, tobs,
+                                                                capture_terminal, ndone)))
         self._last_actions = a
         if capture_terminal:
             return obs, rew, done, (didx, tobs, ndone)

@@ -48,6 +48,97 @@ def make_shard(system, global_num_envs, rank=None, world=None, device=None, **kw
                       global_env_offset=start, **kwargs)
 
 
+def sub_shards(num_envs, global_env_offset, streams):
+    """(global_env_offset, count) of each of `streams` contiguous sub-handles of one
+    shard (shard_bounds within the shard): consecutive global ids, so the sub-handles
+    step bit-identically to one handle of the whole shard (Philox keyed by global id)."""
+    out = []
+    for j in range(int(streams)):
+        o, c = shard_bounds(num_envs, j, streams)
+        out.append((global_env_offset + o, c))
+    return out
+
+
+class StreamSplitEnv:
+    """One shard as S sub-handles, each bound to its own HIP stream, so the S dependent
+    launch chains of a per-step loop overlap on the GPU (the per-step API pays one
+    kernel boundary per step; with S independent chains the boundaries of one chain
+    hide behind the kernels of the others).  Rows [lo_j, hi_j) of every caller buffer
+    belong to sub-handle j; step_into() forks the caller's current stream into the S
+    streams and joins them back, so it is stream-ordered like BatchedEnv.step_into and
+    graph-capturable.  Trajectories, done bits and the done SET are identical to one
+    handle of the whole shard (tests/test_gpu_streams.py); only the compact done list
+    is per sub-handle (done_list() merges it, ids mapped to shard rows)."""
+
+    def __init__(self, system, num_envs, streams, global_env_offset=0, device=None, **kwargs):
+        from .core import BatchedEnv
+
+        self.num_envs, self.global_env_offset = int(num_envs), int(global_env_offset)
+        self.subs, self.bounds = [], []
+        for off, cnt in sub_shards(num_envs, global_env_offset, streams):
+            if cnt == 0:
+                continue
+            self.subs.append(BatchedEnv(system, cnt, device=device, global_env_offset=off,
+                                        **kwargs))
+            lo = off - self.global_env_offset
+            self.bounds.append((lo, lo + cnt))
+        self.device = self.subs[0].device
+        self.streams = [torch.cuda.Stream(self.device) for _ in self.subs]
+        from . import _native as nat
+        import ctypes
+
+        for e, st in zip(self.subs, self.streams):
+            nat.check(nat.lib.lz_set_stream(e._h, ctypes.c_void_p(st.cuda_stream)))
+            e.stream = st
+        e0 = self.subs[0]
+        self.obs_dim, self.action_dim, self.tdtype = e0.obs_dim, e0.action_dim, e0.tdtype
+
+    def _fork(self, fn):
+        cur = torch.cuda.current_stream(self.device)
+        for st in self.streams:
+            st.wait_stream(cur)
+        for j, (e, st) in enumerate(zip(self.subs, self.streams)):
+            with torch.cuda.stream(st):
+                fn(j, e, *self.bounds[j])
+        for st in self.streams:
+            cur.wait_stream(st)
+
+    def reset(self, out):
+        """Device-drawn initial states of every env into out T [N, obs_dim]."""
+        self._fork(lambda j, e, lo, hi: e.reset(out=out[lo:hi]))
+        return out
+
+    def step_into(self, actions, obs, rew, done, compact=True):
+        """One step of every env into caller buffers ([N, A], [N, O], [N], [N]), each
+        sub-handle's slice checked by BatchedEnv.step_into; compact: each sub-handle's
+        done list into its own buffers (done_list())."""
+        def one(j, e, lo, hi):
+            c = (e.done_idx, e.term_obs, e.n_done_dev) if compact and e.compact else (None,) * 3
+            e.step_into(actions[lo:hi], obs[lo:hi], rew[lo:hi], done[lo:hi], *c)
+        self._fork(one)
+        return obs, rew, done
+
+    def done_list(self):
+        """(shard rows, terminal obs) of the envs done in the last step, sorted by row."""
+        torch.cuda.synchronize(self.device)
+        ids, tob = [], []
+        for e, (lo, _) in zip(self.subs, self.bounds):
+            i, t = e.done_list()
+            ids.append(i + lo)
+            tob.append(t)
+        return torch.cat(ids), torch.cat(tob)
+
+    def get_state(self, plane):
+        torch.cuda.synchronize(self.device)
+        parts = [e.get_state(plane) for e in self.subs]
+        torch.cuda.synchronize(self.device)
+        return torch.cat(parts)
+
+    def close(self):
+        for e in self.subs:
+            e.close()
+
+
 def gather_to_rank0(t, global_num_envs, group=None):
     """Concatenate every rank's [count_r, ...] shard on rank 0 (None elsewhere).
     Shards are padded to the largest count so that one gather moves equal-size

@@ -542,6 +542,15 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+def blob_format(attention, attention_ln, i8x4):
+    """The LZ_BLOB_* format a float32 / i8x4 launch reads (entry point + LZ_POLICY_I8X4)."""
+    if attention_ln:
+        return nat.BLOB_ATTN_LN_I8X4 if i8x4 else nat.BLOB_ATTN_LN_F32
+    if attention:
+        return nat.BLOB_ATTN_I8X4 if i8x4 else nat.BLOB_ATTN_F32
+    return nat.BLOB_MLP_I8X4 if i8x4 else nat.BLOB_MLP_F32
+
+
 class FusedRolloutCollector:
     """OnPolicyAlgorithm.collect_rollouts over a BatchedEnv, one launch per rollout.
 
@@ -640,6 +649,12 @@ class FusedRolloutCollector:
                     pack_policy_f32 if self.f32 else pack_policy)(state_dict, self.O, self.A)
         if self.vecnorm_update == "step" and (not self.f32 or self.attention or self.attention_ln):
             raise ValueError("vecnorm_update='step' runs the float32 MlpPolicy kernel")
+        if self.f32:  # the packer's format tag against the launch this collector will make
+            want = blob_format(self.attention, self.attention_ln, self.i8x4)
+            got = int(nat.lib.lz_policy_blob_format(blob.ctypes.data, blob.size))
+            if got != want:
+                raise nat.LorenzEnvError(nat.LZ_ERR_INVALID, "policy blob format %d, the launch "
+                                         "expects %d" % (got, want))
         self.blob = torch.from_numpy(blob).to(self.device)
 
     @property

@@ -314,6 +314,25 @@ lz_status lz_rollout(lz_handle* h, int32_t K, const void* actions, void* obs_out
 #define LZ_POLICY_I8X4 4u          /* the blob is an lz_*policy_pack_i8x4 blob (the float32
                                       attention / MlpPolicy rollouts; see there) */
 
+/* Formats of the float32 / i8x4 policy blobs.  The packers below write a 16-byte format
+ * tag into spare bytes of the blob; the float32 / i8x4 rollout kernels compare it with the
+ * format their launch implies (entry point + LZ_POLICY_I8X4) and, on a mismatch, run on
+ * an all-NaN copy of the blob: every output of the launch is NaN instead of a rollout on
+ * misread weights (a float32 blob's bits read as int8 digits, or the reverse). */
+enum {
+  LZ_BLOB_UNKNOWN = 0,
+  LZ_BLOB_MLP_F32 = 1,       /* lz_policy_pack_f32 */
+  LZ_BLOB_MLP_I8X4 = 2,      /* lz_policy_pack_i8x4 */
+  LZ_BLOB_ATTN_F32 = 3,      /* lz_attn_policy_pack_f32 */
+  LZ_BLOB_ATTN_I8X4 = 4,     /* lz_attn_policy_pack_i8x4 */
+  LZ_BLOB_ATTN_LN_F32 = 5,   /* lz_attn_ln_policy_pack_f32 */
+  LZ_BLOB_ATTN_LN_I8X4 = 6   /* lz_attn_ln_policy_pack_i8x4 */
+};
+/* The LZ_BLOB_* format of a packed host blob of `size` bytes (LZ_BLOB_UNKNOWN: not a
+ * tagged float32 / i8x4 blob, or too small).  Host-only; lets a C-ABI caller check a blob
+ * against the flags it is about to launch with. */
+int32_t lz_policy_blob_format(const void* host_blob, int64_t size);
+
 /* Float32 weights in torch nn.Linear layout ([out, in], row-major), host memory.
  * Names are the SB3 ActorCriticPolicy state_dict keys. */
 typedef struct lz_mlp_policy {
@@ -509,12 +528,14 @@ lz_status lz_rollout_policy_attn_f32(lz_handle* h, const lz_policy_rollout_args*
 /* Opt-in precision "i8x4" of the same actor-critics (same blob size, same rollout entry
  * points with LZ_POLICY_I8X4 in lz_policy_rollout_args.flags): the two wide layers of
  * each pi / vf net (64 -> 128, 128 -> 128: three quarters of the policy's multiplies) run
- * as EXACT fixed-point dot products on the int8 MFMA (v_mfma_i32_16x16x64_i8): every
+ * as truncated 4-digit fixed-point dot products on the int8 MFMA (v_mfma_i32_16x16x64_i8,
+ * digit levels >= 3 summed exactly in int32, recombined with two float32 roundings): every
  * float32 input and weight is the int32 V = rint(v 2^q), |V| <= 2^28 (q per weight row
  * from its largest |w|; per env from its largest feature; 28 for tanh outputs), split into
- * four balanced int8 digits; the 10 digit products of weight >= 2^-24 of the leading one
- * are summed exactly in int32 (no order, no rounding), then recombined and rounded to
- * float32 once (+ the bias).  Error vs the exact dot product: that of float32's own fmaf
+ * four balanced int8 digits; only the 10 digit products of levels i + j >= 3 (weight
+ * >= 2^-24 of the leading one) are summed -- exactly, in int32 (no order, no rounding);
+ * levels 0-2 are dropped -- then recombined as fmaf(float(hi), 2^16, float(lo)), i.e.
+ * rounded to float32 twice (lo, |lo| up to 2^31, is rounded before the fmaf), + the bias.  Error vs the exact dot product: that of float32's own fmaf
  * chain (tests/test_i8x4_host.py); bit-exact vs the C oracle (orc_attn_i8x4).  A NaN / inf
  * feature makes all of that env's outputs NaN.  The packers refuse non-finite net weights.
  * The extractor, softmax, heads and everything else are the float32 path's. */

@@ -10,6 +10,7 @@ import numpy as np
 import torch
 
 import oracle
+from gym_lorenz.core import rollout_io_args, step_io_args
 
 DONE_TERMINATED, DONE_TRUNCATED = 1, 2
 
@@ -29,6 +30,8 @@ class FakeBackend:
         self.alpha = alpha
         self.obs_dim = 6
         self.action_dim = 3 if system == "lorenz3" else 2
+        # the checked caller-buffer entry's view of the handle (BatchedEnv's lz_info fields)
+        self.tdtype, self.device, self.reads_actions = torch.float32, torch.device("cpu"), True
         self.tick = 0
         self.steps = np.zeros(n, np.int32)
         if system == "lorenz3":
@@ -84,6 +87,34 @@ class FakeBackend:
         self.rew.copy_(torch.from_numpy(r.astype(np.float32)))
         self.done.copy_(torch.from_numpy(flags))
         return self.obs, self.rew, self.done
+
+    def step_into(self, actions, obs, rew, done, done_idx=None, term_obs=None, n_done=None,
+                  noise=None):
+        """BatchedEnv.step_into's contract: the same buffer checks (core.step_io_args),
+        refused before any state changes; then the step's outputs land in the buffers."""
+        step_io_args(self, actions, obs, rew, done, done_idx, term_obs, n_done, noise)
+        o, r, d = self.step(actions)
+        obs.view(-1).copy_(o.reshape(-1))
+        rew.copy_(r)
+        done.copy_(d)
+        if done_idx is not None:
+            k = len(self._done_idx)
+            done_idx.view(-1)[:k] = torch.from_numpy(self._done_idx.astype(np.int32))
+            term_obs.view(-1)[: k * 6] = torch.from_numpy(self._term.reshape(-1))
+            if n_done is not None:
+                n_done.fill_(k)
+        return obs, rew, done
+
+    def rollout_into(self, K, actions, obs, rew, done, done_idx=None, term_obs=None, cap=0,
+                     n_done=None):
+        """BatchedEnv.rollout_into's contract (checks only the buffers here, then K steps)."""
+        rollout_io_args(self, K, actions, obs, rew, done, done_idx, term_obs, cap, n_done)
+        for k in range(int(K)):
+            o, r, d = self.step(actions[k])
+            obs[k].view(-1).copy_(o.reshape(-1))
+            rew[k].copy_(r)
+            done[k].copy_(d)
+        return obs, rew, done
 
     def done_list(self):
         return torch.from_numpy(self._done_idx), torch.from_numpy(self._term)

@@ -247,7 +247,7 @@ def test_packed_blob_dataflow_equals_oracle(orc, pol, ln):
     b32 = (pol.pack_attn_ln_policy_f32 if ln else pol.pack_attn_policy_f32)(sd, in_dim, 2)
     same = np.ones(blob.size, bool)
     same[POSTW: POSTB] = False
-    same[PI + POSTSH: PI + POSTSH + 128] = False
+    same[PI + POSTSH: PI + POSTSH + 128 + 16] = False  # shifts + the format tag (kAXTag)
     for base in (PI, VF):
         same[base + N1: base + NB1] = False
         same[base + SH1: base + SH2 + 256] = False

@@ -68,6 +68,7 @@ def test_packed_digits_where_the_kernel_reads_them(pol, orc, hidden):
                     assert sh[T, h, g] == 24 - orc.i8x_row_q(w[32 * T + _row(g, h)]) - 28
         same[base + W2: base + W2 + 4 * 16 * 64 * 16] = False
         same[base + SH2: base + NET] = False
+    same[SH2 - 16: SH2] = False  # the format tag (kF32Tag = kF32HB + 48, in net 0)
     # everything else is the float32 blob
     assert np.array_equal(blob[same], b32[same])
 

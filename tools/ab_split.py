@@ -35,8 +35,8 @@ def build(n, S):
     def enqueue(k):
         for s, (env, acts, obs, rew, done) in enumerate(parts):
             r = k % R
-            nat.check(nat.lib.lz_step(env._h, P(acts[r]), None, P(obs[r]), P(rew[r]), P(done[r]),
-                                      P(env.done_idx), P(env.term_obs), None))
+            nat.check(nat.lib.lz_step(env._h, *env.step_args(acts[r], obs[r], rew[r], done[r],
+                                                             env.done_idx, env.term_obs)))
 
     g = torch.cuda.CUDAGraph()
     with torch.cuda.stream(main):

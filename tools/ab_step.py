@@ -24,21 +24,19 @@ def make(variant, n, system="lorenz3", R=16):
     obs = torch.empty((R, n, env.obs_dim), device=dev)
     rew = torch.empty((R, n), device=dev)
     done = torch.empty((R, n), dtype=torch.uint8, device=dev)
-    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    slots = [(P(acts[r]), P(obs[r]), P(rew[r]), P(done[r])) for r in range(R)]
+    # the checked caller-buffer entry (BatchedEnv.step_args: sizes vs lz_info)
+    slots = [env.step_args(acts[r], obs[r], rew[r], done[r], env.done_idx, env.term_obs)
+             for r in range(R)]
     stream = torch.cuda.Stream()
     nat.check(nat.lib.lz_set_stream(env._h, ctypes.c_void_p(stream.cuda_stream)))
     g = torch.cuda.CUDAGraph()
     with torch.cuda.stream(stream):
         for k in range(4):
-            nat.check(nat.lib.lz_step(env._h, *slots[k % R][:1], None, *slots[k % R][1:],
-                                      P(env.done_idx), P(env.term_obs), None))
+            nat.check(nat.lib.lz_step(env._h, *slots[k % R]))
         torch.cuda.synchronize()
         with torch.cuda.graph(g, stream=stream):
             for k in range(32):
-                a, o, r_, d = slots[k % R]
-                nat.check(nat.lib.lz_step(env._h, a, None, o, r_, d, P(env.done_idx),
-                                          P(env.term_obs), None))
+                nat.check(nat.lib.lz_step(env._h, *slots[k % R]))
     keep = (env, acts, obs, rew, done)
     return g, stream, keep
 

@@ -43,7 +43,9 @@ def main():
     be.reset()
     stream = torch.cuda.Stream()
     nat.check(nat.lib.lz_set_stream(be._h, ctypes.c_void_p(stream.cuda_stream)))
-    sizes = (K * n * 3 * 4, K * n * be.obs_dim * 4, K * n * 4, K * n)
+    # raw (non-torch) buffers cannot go through BatchedEnv.rollout_args: size them from
+    # lz_info here (actions [K, N, A] f32, obs [K, N, O] f32, rew [K, N] f32, done [K, N] u8)
+    sizes = (K * n * be.action_dim * 4, K * n * be.obs_dim * 4, K * n * 4, K * n)
 
     def timed(ptrs):
         a, o, r, d = (ctypes.c_void_p(p.value if isinstance(p, ctypes.c_void_p) else p) for p in ptrs)
