@@ -1006,25 +1006,25 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
                 - min(0.0, min(base.elapsed_time(e0) for e0, _ in ev)))
         return t1 - t0, span
 
-        first = window()
-        # windows until min_window_s are timed in total: batches sized from the windows
-        # so far (the first window after warm-up runs slower than the rest), every rank
-        # running the same count (MAX over ranks)
-        wins, per = [], first[0]
-        while True:
-            left = min_window_s - sum(w[0] for w in wins)
-            need = max(1, min(math.ceil(left / max(per, 1e-9)), 5000 - len(wins)))
-            if world > 1:
-                t = torch.tensor([need if left > 0 else 0], device=device, dtype=torch.int64)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                need = int(t.item())
-            elif left <= 0:
-                need = 0
-            if need == 0 or len(wins) >= 5000:
-                break
-            wins += [window() for _ in range(need)]
-            per = sum(w[0] for w in wins) / len(wins)
-        need = len(wins)
+    first = window()
+    # windows until min_window_s are timed in total: batches sized from the windows
+    # so far (the first window after warm-up runs slower than the rest), every rank
+    # running the same count (MAX over ranks)
+    wins, per = [], first[0]
+    while True:
+        left = min_window_s - sum(w[0] for w in wins)
+        need = max(1, min(math.ceil(left / max(per, 1e-9)), 5000 - len(wins)))
+        if world > 1:
+            t = torch.tensor([need if left > 0 else 0], device=device, dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            need = int(t.item())
+        elif left <= 0:
+            need = 0
+        if need == 0 or len(wins) >= 5000:
+            break
+        wins += [window() for _ in range(need)]
+        per = sum(w[0] for w in wins) / len(wins)
+    need = len(wins)
     elapsed = sum(w[0] for w in wins)
     ev_ms = sum(w[1] for w in wins)
     if world > 1:
