@@ -283,6 +283,9 @@ def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=
             return "_ZN2lz12k_step_multiINS_%sLi%dELb0EEEvNS_5KArgsE" % (sysname, tiles)
         return "_ZN2lz6k_stepINS_%sLi0EEEvNS_5KArgsE" % sysname
     D = 7  # kDmaDist
+    if system == "pmsm" and variant & (1 << 27) and not variant & (1 << 28):
+        # the lane-pair rollout: k_rollout_pair<SysPMSM, float, D>
+        return "_ZN2lz14k_rollout_pairINS_7SysPMSMEfLi%dEEEvNS_5KArgsE" % D
     b = "Lb%dE" % int(no_done and system == "lorenz3")  # (SysL3RK4 never terminates either)
     # lz_kernels.hip launch_rollout_d: one-wave workgroups below 256 x CUs envs for
     # LORENZ3 f32 (3/4 of that for LORENZ4 f32, 131,072 for the others); two lanes per env for LORENZ3

@@ -104,7 +104,9 @@ __device__ __forceinline__ void make_noise(const Sys& sys, const KArgs& a, int64
 // k_rollout kZN) reads them from the caller's registers zpre[0..2] and draws the NEXT
 // step's normals (tick + 1) into the same registers here, in the basic block of sys.step,
 // so the scheduler interleaves that independent Philox + Box-Muller chain with the
-// integrator's.  The normals are keyed by (seed, env id, tick) only: bit-identical.
+// integrator's; 3 (the lane-pair rollout, k_rollout_pair) runs sys.step_pair with
+// lead = lane 0 of the pair and the slave lane's normals in zpre[0..2].  The normals are
+// keyed by (seed, env id, tick) only: bit-identical.
 template <class Sys, typename T, bool kRollout, bool kKeepTerm = false, bool kNoDone = false,
           bool kInject = !kRollout, int kZMode = 0>
 __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KArgs& a, int64_t i,
@@ -136,13 +138,19 @@ __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KAr
           float z[3] = {zpre[0], zpre[1], zpre[2]};
           normal3(a.seed, (uint64_t)(a.gid0 + i), tick + 1, const_cast<float*>(zpre));
           sys.noise_from_normals(z, nz);
+        } else if constexpr (kZMode == 3) {  // lane pair: the slave lane's normals, drawn by the
+          // pair's schedule (split_loop kPair) -- normal3(seed, gid, tick)'s values
+          float z[3] = {zpre[0], zpre[1], zpre[2]};
+          sys.noise_from_normals(z, nz);
         } else {
           make_noise<Sys, T, kInject>(sys, a, i, tick, nz);
         }
         use_nz = true;
       }
     }
-    bool term = sys.step(act, use_nz, nz, o, rew, a);
+    bool term;
+    if constexpr (kZMode == 3) term = sys.step_pair(!lead, act, use_nz, nz, o, rew, a);  // lane pair
+    else term = sys.step(act, use_nz, nz, o, rew, a);
     bool trunc = false;
     if (a.count_steps) {
       steps += 1;

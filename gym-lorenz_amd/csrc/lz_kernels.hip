@@ -997,7 +997,14 @@ __device__ __forceinline__ void store_half(T* p, const T* v) {
 // asm, so the compiler assumes the DMA writes it) -- the compiler then places the
 // lgkmcnt wait where the action is first used, and the state-only part of the step
 // (the RHS of the old state) overlaps the LDS latency.
-template <class Sys, typename T, int R, bool FULL, int D, bool kNoDone, int SV>
+// kPair (PMSM, k_rollout_pair): the lane pair SPLITS the step instead
+// of repeating it (SysPMSM::step_pair: lane q integrates system q, one division and two
+// square roots per lane, exchanged by DPP), and draws the slave's process noise two steps
+// at a time: at an even step k lane 1 draws normal3(tick + k) -- its own, for step k --
+// while lane 0 draws normal3(tick + k + 1) and hands it over (pair_swap) for step k + 1,
+// so each lane runs one Philox + Box-Muller per two steps.  The same values as
+// normal3(seed, gid, tick + k) at every step: bit-identical to k_rollout.
+template <class Sys, typename T, int R, bool FULL, int D, bool kNoDone, int SV, bool kPair = false>
 __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_reset,
                                            const KArgs& a, int64_t base, int tid, int nb,
                                            uint64_t tick, float* s_act) {
@@ -1036,6 +1043,7 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
     for (int d = 0; d < D; ++d) issue(dsrc + (int64_t)(d < a.K ? d : a.K - 1) * dstride, d);
     dsrc += (int64_t)(D < a.K ? D : a.K - 1) * dstride;
   }
+  float znext[3] = {0.0f, 0.0f, 0.0f};  // kPair: lane 0's normals for the next (odd) step
   auto run_step = [&](int k, auto ladder) __attribute__((always_inline)) {
     const int64_t off = (int64_t)k * a.n;
     float act[Sys::A];
@@ -1060,9 +1068,21 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
     T o[Sys::O];
     T rew = (T)0;
     bool did_reset;
-    const uint8_t dflag = step_body<Sys, T, true, false, kNoDone>(sys, steps, a, i, live, act,
-                                                                  tick + (uint64_t)k, k, o, rew,
-                                                                  did_reset, nullptr, lead);
+    float zcur[3] = {0.0f, 0.0f, 0.0f};
+    if constexpr (kPair) {
+      if (live && (a.flags & LZ_FLAG_ADD_NOISE)) {  // (both lanes of a pair: the same `live`)
+        if ((k & 1) == 0) {
+          normal3(a.seed, (uint64_t)(a.gid0 + i), tick + (uint64_t)k + (lead ? 1u : 0u), zcur);
+#pragma unroll
+          for (int j = 0; j < 3; ++j) znext[j] = pair_swap(zcur[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) zcur[j] = znext[j];
+        }
+      }
+    }
+    const uint8_t dflag = step_body<Sys, T, true, false, kNoDone, false, kPair ? 3 : 0>(
+        sys, steps, a, i, live, act, tick + (uint64_t)k, k, o, rew, did_reset, nullptr, lead, zcur);
     any_reset = any_reset || did_reset;
     if (!live) return;
     if (lead) gstore<(SV & 2) == 0>(static_cast<T*>(a.rew) + off + i, rew);
@@ -1093,8 +1113,8 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
 // the four waves' quarters before the line leaves, +7.8% at 32,768 envs, K = 2048,
 // profiles/r03/done_stores/), bit 1 the rewards, bit 2 the obs half rows (A/B only,
 // variant bits 18-20 = 1, 3, 4, 7 select SV = 0, 3, 5, 7)
-template <class Sys, typename T, int R, int D, bool kNoDone = false, int SV = 1>
-__global__ __launch_bounds__(64) void k_rollout_split(KArgs a) {
+template <class Sys, typename T, int R, int D, bool kNoDone = false, int SV = 1, bool kPair = false>
+__device__ __forceinline__ void rollout_split_body(KArgs a) {
   constexpr int E = 64 / R;  // envs per one-wave workgroup
   __shared__ __attribute__((aligned(16))) float s_act[dma_slots<D>() * (row_dma<Sys::A, 32>() ? kRowRegionF : 64 * Sys::A)];
   const int tid = (int)threadIdx.x;
@@ -1118,14 +1138,24 @@ __global__ __launch_bounds__(64) void k_rollout_split(KArgs a) {
     if (a.count_steps) steps = static_cast<const int32_t*>(a.pl[Sys::kStepPlane])[i];
   }
   if (nb == E && a.vec_ok)
-    split_loop<Sys, T, R, true, D, kNoDone, SV>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
+    split_loop<Sys, T, R, true, D, kNoDone, SV, kPair>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
   else
-    split_loop<Sys, T, R, false, D, kNoDone, SV>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
+    split_loop<Sys, T, R, false, D, kNoDone, SV, kPair>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
   if (live && lead) {
     sys.store(a, i);
     if (any_reset) sys.store_autoreset_extra(a, i);
     if (a.count_steps) static_cast<int32_t*>(a.pl[Sys::kStepPlane])[i] = steps;
   }
+}
+template <class Sys, typename T, int R, int D, bool kNoDone = false, int SV = 1>
+__global__ __launch_bounds__(64) void k_rollout_split(KArgs a) {
+  rollout_split_body<Sys, T, R, D, kNoDone, SV>(a);
+}
+// The lane-pair rollout (split_loop kPair; PMSM): the split-lane kernel's layout and I/O,
+// the step itself divided between the two lanes (SysPMSM::step_pair).
+template <class Sys, typename T, int D>
+__global__ __launch_bounds__(64) void k_rollout_pair(KArgs a) {
+  rollout_split_body<Sys, T, 2, D, false, 1, true>(a);
 }
 
 // ------------------------------------------------------------------ launchers
@@ -1138,6 +1168,18 @@ static inline int64_t grid_for(int64_t n) { return (n + kBlock - 1) / kBlock; }
 // 65,536 envs; slower at 16,384 (the wave's step chain, not the SIMD count, bounds it
 // there) and for PMSM at any N (its step is 3-4x the instructions: doubling them costs
 // more than the extra waves recover).
+// The lane-pair PMSM rollout (k_rollout_pair, SysPMSM::step_pair; variant bit 1<<27
+// forces it at any N, 1<<28 disables it).
+template <class Sys>
+static inline bool rollout_pair(const KArgs& a) {
+  if constexpr (!std::is_same<Sys, SysPMSM>::value) {
+    return false;
+  } else {
+    if (a.variant & (1 << 28)) return false;
+    return (a.variant & (1 << 27)) != 0;
+  }
+}
+
 template <class Sys>
 static inline bool rollout_split(const KArgs& a) {
   if constexpr (Sys::O % 2 != 0) return false;
@@ -1150,7 +1192,7 @@ static inline bool rollout_split(const KArgs& a) {
 // 256-lane k_rollout, 1 one-wave k_rollout, 2 the split-lane kernel; no_done = the
 // done-free instantiation.
 struct RolloutPlan {
-  int kind;
+  int kind;  // 0 256-lane, 1 one-wave, 2 split lanes, 3 lane pair (PMSM)
   bool no_done;
   bool np;  // one-wave groups with a noise-producer wave (k_rollout kNP)
 };
@@ -1163,6 +1205,7 @@ static RolloutPlan rollout_plan(const KArgs& a) {
                                                : 2 * 256 * (int64_t)kBlock;
   bool nd = false;
   if constexpr (never_terminates<Sys>::value && !Sys::kNoise) nd = no_done<Sys>(a) && !(a.variant & 2048);
+  if (rollout_pair<Sys>(a)) return {3, false, false};
   if ((a.n < one_wave_below || (a.variant & (1 << 24))) && !(a.variant & (1 << 23))) {
     if (rollout_split<Sys>(a)) return {2, nd, false};
     // variant bit 1<<25: with a noise-producer wave (k_rollout_np; A/B, measured slower:
@@ -1190,6 +1233,12 @@ static void launch_rollout_d(const KArgs& a, hipStream_t s) {
   // (rollout_plan: variant bit 1<<24 forces one-wave groups at any N, 1<<23 the 256-lane
   // kernel, 2048 keeps the done path -- A/B)
   const RolloutPlan plan = rollout_plan<Sys>(a);
+  if constexpr (std::is_same<Sys, SysPMSM>::value) {
+    if (plan.kind == 3) {
+      hipLaunchKernelGGL((k_rollout_pair<Sys, T, DS>), dim3((unsigned)((a.n + 31) / 32)), dim3(64), 0, s, a);
+      return;
+    }
+  }
   if (plan.kind != 0) {
     if (plan.kind == 2) {
       const dim3 g((unsigned)((a.n + 31) / 32));
@@ -1344,8 +1393,11 @@ static int env_shape_t(int which, const KArgs& a, int32_t* o) {
     return 0;
   }
   const RolloutPlan p = rollout_plan<Sys>(a);
-  o[0] = p.kind == 0 ? LZ_KERNEL_ROLLOUT : p.kind == 1 ? LZ_KERNEL_ROLLOUT_WAVE : LZ_KERNEL_ROLLOUT_SPLIT;
-  o[1] = p.kind == 2 ? 32 : 64;
+  o[0] = p.kind == 0   ? LZ_KERNEL_ROLLOUT
+         : p.kind == 1 ? LZ_KERNEL_ROLLOUT_WAVE
+         : p.kind == 2 ? LZ_KERNEL_ROLLOUT_SPLIT
+                       : LZ_KERNEL_ROLLOUT_PAIR;
+  o[1] = p.kind >= 2 ? 32 : 64;
   o[2] = p.kind == 0 ? kBlock / 64 : p.np ? 2 : 1;
   const int64_t per = p.kind == 0 ? kBlock : p.kind == 1 ? 64 : 32;
   o[3] = (int32_t)((a.n + per - 1) / per);

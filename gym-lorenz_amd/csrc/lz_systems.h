@@ -33,6 +33,13 @@ __device__ __forceinline__ T clip_nz(T x, T lo, T hi) {
     return clip(x, lo, hi);
 }
 
+// The partner lane's value in a lane pair (2e, 2e + 1): DPP quad_perm [1, 0, 3, 2], one
+// full-rate v_mov_b32_dpp -- the exchange of the lane-pair rollout (k_rollout_split with
+// kPair, SysPMSM::step_pair).
+__device__ __forceinline__ float pair_swap(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+
 template <typename T>
 __device__ __forceinline__ T ld(const void* p, int64_t i) {
   return static_cast<const T*>(p)[i];
@@ -484,6 +491,77 @@ struct SysPMSM {
     lam = clip(lam, 0.0f, 0.5f);                           // :138
     const float tiny = 1e-6f;                              // :158-160 (x + 1e-6)**alpha
     const float fp = (fpow(fabsf(e1) + tiny) + fpow(fabsf(e2) + tiny)) + fpow(fabsf(e3) + tiny);
+    const float ap = lam * (act[0] * act[0] + act[1] * act[1]);  // :165 raw action
+    float r = ((-es) - fp) - ap;                           // :167
+    bool te = false;
+    if (es > tterm) { r = -1000.0f; te = true; }           // :174-176
+    rew = r;
+    return te;
+  }
+  // step() split over a LANE PAIR (k_rollout_pair: lanes 2e, 2e + 1 both carry env
+  // e's full state; lane q = 1 is the "slave" lane).  Every value either lane ends with is
+  // the one step() computes -- the same operations on the same operands -- but the work
+  // that comes in independent halves runs once per pair instead of twice per lane:
+  //  * lane q integrates system q only (q = 0 the master s1 with actions 0 and no noise,
+  //    q = 1 the slave s2), then the pair swaps states and derivatives (pair_swap);
+  //    the master's RHS runs the noisy form with noise 0.0: (float)((double)t + 0.0) is
+  //    t + 0.0f for every float t (-0 -> +0 in both, NaN stays NaN);
+  //  * nz_slave: the slave's process noise (lane 1's value is used; the caller's pair
+  //    schedule draws the normals, see split_loop);
+  //  * the two bias-corrected moments are ONE division per lane (lane 0 mt / bcm, lane 1
+  //    vt / bcv) and, at alpha = 0.5, the four square roots TWO per lane (lane 0 sqrt(vh)
+  //    and fpow(e1), lane 1 fpow(e2) and fpow(e3)), exchanged.
+  __device__ bool step_pair(bool q, const float* act, bool use_nz, const double* nz_slave, float* o,
+                            float& rew, const KArgs& a) {
+    const BiasPre pre = bias_pre(a);
+    const float a1 = clip_nz(act[0], -1.0f, 1.0f) * fmax;  // :81-82
+    const float a2 = clip_nz(act[1], -1.0f, 1.0f) * fmax;
+    const float u1 = q ? a1 : 0.0f, u2 = q ? a2 : 0.0f;
+    double nz[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) nz[j] = q ? nz_slave[j] : 0.0;
+    float x[3], d[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = q ? s2[j] : s1[j];
+    rhs(x, u1, u2, use_nz, nz, d);                                 // :88-90
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = x[j] + d[j] * dt;           // :92-93
+    rhs(x, u1, u2, use_nz, nz, d);                                 // :95-97
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {                                  // :99-102
+      const float px = pair_swap(x[j]), pd = pair_swap(d[j]);
+      s1[j] = q ? px : x[j];
+      s2[j] = q ? x[j] : px;
+      const float d1 = q ? pd : d[j], d2 = q ? d[j] : pd;
+      o[j] = s1[j] - s2[j];
+      o[3 + j] = d1 - d2;
+    }
+    const float e1 = fabsf(o[0]), e2 = fabsf(o[1]), e3 = fabsf(o[2]);             // :105-107
+    const float es = (e1 + e2) + e3;                       // :108
+    const float grad = thr - es;                           // :118
+    adam += 1;                                             // :121
+    mt = b1 * mt + c1 * grad;                              // :124
+    vt = b2 * vt + c2 * (grad * grad);                     // :127
+    float bcm, bcv;
+    bias_pair(a, bcm, bcv, pre);
+    const float mv = (q ? vt : mt) / (q ? bcv : bcm);      // :130-131, one division per lane
+    const float mvp = pair_swap(mv);
+    const float mh = q ? mvp : mv, vh = q ? mv : mvp;
+    const float tiny = 1e-6f;                              // :158-160 (x + 1e-6)**alpha
+    float sv, fp;
+    if (alpha == 0.5f) {  // fpow = sqrtf: the four roots two per lane
+      const float ra = sqrtf(q ? fabsf(e2) + tiny : vh);
+      const float rb = sqrtf(q ? fabsf(e3) + tiny : fabsf(e1) + tiny);
+      const float pa = pair_swap(ra), pb = pair_swap(rb);
+      sv = q ? pa : ra;
+      const float f1 = q ? pb : rb, f2 = q ? ra : pa, f3 = q ? rb : pb;
+      fp = (f1 + f2) + f3;
+    } else {
+      sv = sqrtf(vh);
+      fp = (fpow(fabsf(e1) + tiny) + fpow(fabsf(e2) + tiny)) + fpow(fabsf(e3) + tiny);
+    }
+    lam = lam - (lr * mh) / (sv + eps);                    // :135
+    lam = clip(lam, 0.0f, 0.5f);                           // :138
     const float ap = lam * (act[0] * act[0] + act[1] * act[1]);  // :165 raw action
     float r = ((-es) - fp) - ap;                           // :167
     bool te = false;

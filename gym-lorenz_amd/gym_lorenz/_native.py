@@ -162,7 +162,7 @@ class LzLaunchShape(ctypes.Structure):
  CALL_ROLLOUT_POLICY_ATTN_STACK_F32, CALL_STEP_NOISE) = range(10)
 KERNELS = {1: "step", 2: "step_multi", 3: "rollout", 4: "rollout_wave", 5: "rollout_split",
            6: "policy", 7: "policy_pair", 8: "policy_pair_pipe", 9: "policy_split",
-           10: "policy_step", 11: "policy_attn", 12: "policy_attn_f32"}
+           10: "policy_step", 11: "policy_attn", 12: "policy_attn_f32", 13: "rollout_pair"}
 SHAPE_NO_DONE, SHAPE_GRID_STRIDE = 1, 2
 
 VP = ctypes.c_void_p

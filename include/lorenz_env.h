@@ -729,7 +729,9 @@ enum {
   LZ_KERNEL_POLICY_SPLIT = 9,     /* k_rollout_policy_f32_split: actor and critic waves */
   LZ_KERNEL_POLICY_STEP = 10,     /* k_policy_step_f32 */
   LZ_KERNEL_POLICY_ATTN = 11,     /* k_rollout_policy<..., kAttn / kAttnLn> (bf16) */
-  LZ_KERNEL_POLICY_ATTN_F32 = 12  /* k_rollout_policy_attn_f32 */
+  LZ_KERNEL_POLICY_ATTN_F32 = 12, /* k_rollout_policy_attn_f32 */
+  LZ_KERNEL_ROLLOUT_PAIR = 13     /* k_rollout_pair: PMSM, the step split over a lane
+                                     pair (SysPMSM::step_pair) */
 };
 #define LZ_SHAPE_NO_DONE 1u     /* the done-free instantiation (no done can occur) */
 #define LZ_SHAPE_GRID_STRIDE 2u /* fewer workgroups than env groups: workgroups loop */
