@@ -468,12 +468,15 @@ def test_rollout_noise_producer_equals_steps(gl, system, dtype, n, K):
     from gym_lorenz import _native as nat
 
     one_wave = n < 131072
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
     for variant in ((0, 1 << 25, 1 << 26) if one_wave else (0, 1 << 26)):
         a_be = gl.BatchedEnv(system, n, dtype=dtype, seed=9, max_episode_steps=37, add_noise=True, variant=variant)
         b_be = gl.BatchedEnv(system, n, dtype=dtype, seed=9, max_episode_steps=37, add_noise=True)
         sh = nat.launch_shape(a_be._h, nat.CALL_ROLLOUT)
-        assert sh["kernel"] == ("rollout_wave" if one_wave else "rollout"), sh
-        assert sh["waves"] == (2 if variant == 1 << 25 else 1 if one_wave else 4), sh
+        # (PMSM at <= 32 x 4 x CUs envs defaults to the lane-pair kernel, test_gpu_rollout_pair.py)
+        pair = system == "pmsm" and variant == 0 and (n + 31) // 32 <= 4 * cus
+        assert sh["kernel"] == ("rollout_pair" if pair else "rollout_wave" if one_wave else "rollout"), sh
+        assert sh["waves"] == (2 if variant == 1 << 25 else 1 if one_wave or pair else 4), sh
         a_be.reset()
         b_be.reset()
         A = torch.from_numpy(np.random.default_rng(5).uniform(-1.2, 1.2, (K, n, a_be.action_dim))

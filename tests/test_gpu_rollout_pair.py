@@ -37,14 +37,16 @@ def _np(t):
 @pytest.mark.parametrize("n,K,noise,alpha,arange", [
     (32768, 301, True, 0.5, 1.2), (65536, 200, True, 0.5, 1.2), (4097, 101, True, 0.5, 1.2),
     (4097, 64, False, 0.5, 1.2), (2050, 77, True, 0.7, 1.2), (140001, 40, True, 0.5, 1.2),
-    (4099, 60, True, 0.5, 40.0),  # huge actions: the slave runs away, es > tterm terminates
+    (4099, 60, True, 0.5, 0.0),  # term_threshold 25 (params[10]): es > 25 terminates often
 ])
 def test_pair_rollout_equals_steps(gl, n, K, noise, alpha, arange):
     from gym_lorenz import _native as nat
 
+    kw = {"params": {10: 25.0}} if arange == 0.0 else {}
+    arange = arange or 1.2
     a_be = gl.BatchedEnv("pmsm", n, seed=9, max_episode_steps=37, add_noise=noise, alpha=alpha,
-                         variant=PAIR)
-    b_be = gl.BatchedEnv("pmsm", n, seed=9, max_episode_steps=37, add_noise=noise, alpha=alpha)
+                         variant=PAIR, **kw)
+    b_be = gl.BatchedEnv("pmsm", n, seed=9, max_episode_steps=37, add_noise=noise, alpha=alpha, **kw)
     sh = nat.launch_shape(a_be._h, nat.CALL_ROLLOUT)
     assert sh["kernel"] == "rollout_pair" and sh["envs_per_wave"] == 32, sh
     assert sh["grid"] == (n + 31) // 32, sh
@@ -65,7 +67,7 @@ def test_pair_rollout_equals_steps(gl, n, K, noise, alpha, arange):
     wi = np.concatenate(want_idx)
     assert m == wi.size and m > 0
     assert np.array_equal(np.sort(_np(didx[:m])), wi)
-    if arange > 10:
+    if kw:
         assert want_term > 0  # the termination path ran
     for p in range(a_be.info.n_planes):
         assert bits_equal(_np(a_be.get_state(p)), _np(b_be.get_state(p))), p

@@ -52,6 +52,11 @@ def test_bench_kernel_names_exist():
         assert kernel_hash.kernel_code_sha256(k) is not None, k
         names.add(k)
     assert "_ZN2lz12k_step_multiINS_5SysHRIfEEfLi4ELb0EEEvNS_5KArgsE" in names
+    # PMSM rollouts: the lane-pair kernel up to 32 x 4 x CUs envs, the 256-lane one above
+    assert bench.kernel_name("pmsm", "rollout", 32768) == "_ZN2lz14k_rollout_pairINS_7SysPMSMEfLi7EEEvNS_5KArgsE"
+    assert "k_rolloutINS_7SysPMSMEfLi64E" in bench.kernel_name("pmsm", "rollout", 32800)
+    assert "k_rollout_pair" in bench.kernel_name("pmsm", "rollout", 262144, variant=1 << 27)
+    assert "k_rolloutINS_7SysPMSMEfLi64E" in bench.kernel_name("pmsm", "rollout", 4097, variant=1 << 28)
     # LORENZ4 f32 rollouts: one-wave groups below 3/4 x 256 x CUs envs, 256 lanes from there
     assert "k_rolloutINS_5SysL4IfEEfLi64E" in bench.kernel_name("lorenz4", "rollout", 40960)
     assert "k_rolloutINS_5SysL4IfEEfLi256E" in bench.kernel_name("lorenz4", "rollout", 49152)

@@ -22,7 +22,7 @@ for rep in 1 2 3; do
 done
 cd /tmp && export TMPDIR=/tmp
 for v in 0 134217728; do
-  timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof_v$v -o prof -- \
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof_v$v -o prof --output-format csv -- \
     python3 $GRAFT_REPO_ROOT/bench.py --system pmsm --mode rollout --envs 32768 --K 2048 --steps 8192 --variant $v \
     --no-cpu-baseline --no-drift --no-extras > $GRAFT_REPO_ROOT/$O/prof_v$v.json 2> $GRAFT_REPO_ROOT/$O/prof_v$v.err \
     || { echo PROF FAILED; tail -5 $GRAFT_REPO_ROOT/$O/prof_v$v.err; exit 1; }
