@@ -283,10 +283,10 @@ def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=
             return "_ZN2lz12k_step_multiINS_%sLi%dELb0EEEvNS_5KArgsE" % (sysname, tiles)
         return "_ZN2lz6k_stepINS_%sLi0EEEvNS_5KArgsE" % sysname
     D = 7  # kDmaDist
-    # lz_kernels.hip rollout_pair: PMSM while its 32-env waves are at most one per SIMD
+    # lz_kernels.hip rollout_pair: PMSM where its 32-env waves are 3 < waves / CU <= 4
     force_other = variant & (256 | 512 | (1 << 23) | (1 << 24) | (1 << 25) | (1 << 26))
     if system == "pmsm" and not variant & (1 << 28) and (
-            variant & (1 << 27) or (not force_other and -(-n // 32) <= 4 * num_cus)):
+            variant & (1 << 27) or (not force_other and 3 * num_cus < -(-n // 32) <= 4 * num_cus)):
         # the lane-pair rollout: k_rollout_pair<SysPMSM, float, D>
         return "_ZN2lz14k_rollout_pairINS_7SysPMSMEfLi%dEEEvNS_5KArgsE" % D
     b = "Lb%dE" % int(no_done and system == "lorenz3")  # (SysL3RK4 never terminates either)
@@ -470,6 +470,7 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
     per_step = f32 and not attn and args.vecnorm_update == "step"
     col = FusedRolloutCollector(env, net.state_dict(), gamma=0.99, gae_lambda=0.95, obs_rms=rms,
                                 clip_obs=10.0, training=True, bootstrap=True, frame_stack=stack,
+                                group=dist.group.WORLD if world > 1 else None,
                                 precision=args.precision,
                                 vecnorm_update=("step" if per_step else "rollout")
                                 if f32 and not attn else None)
@@ -524,16 +525,18 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
                  if f32 and not attn and not per_step else None)
     mangled = {"pmsm": "7SysPMSME", "lorenz3": "5SysL3IfEE", "lorenz4": "5SysL4IfEE",
                "hr": "5SysHRIfEE"}[args.system]
+    sf = scaling_fields(args, world, total, n, "no collective on step" + (
+        "" if attn else "; obs_rms moments all-reduced once per rollout"))
     return {
         "metric": METRIC,
         "value": total * steps / elapsed,
         "unit": "env-steps/s",
-        "n_gpus": world,
+        "n_gpus": sf["n_gpus"],
         "steps": steps,
         "warmup": warm * K,
         "ms_per_step": elapsed * 1e3 / steps,
         "higher_is_better": True,
-        "scaling": args.scaling,
+        "scaling": sf["scaling"],
         "vs_baseline": None,
         "dtype": ("f32 MFMA extractor + int8 MFMA nets (truncated 4-digit fixed point: digit levels >= 3 "
                   "summed exactly in int32, two float32 roundings), f32 env" if i8 else
@@ -578,12 +581,11 @@ def bench_policy(args, gl, nat, torch, env, device, world, rank, total, n):
                             "the rollout-start statistics), pooled obs_rms update, GAE (lz_gae); "
                             "%d envs total, %d per GPU"))
                         % (SYSTEM_INFO[args.system][0], K, total, n),
-            "system": args.system, "envs_total": total, "envs_per_gpu": n, "mode": "policy",
+            "system": args.system, "mode": "policy",
             "policy": args.policy, "precision": args.precision,
             "vecnorm_update": None if attn else ("step (SB3 order)" if per_step
                                                  else "rollout (pooled, opt-in)"),
-            "K": K, "parallelism": "env shard x%d (no collective on step; obs_rms moments "
-                                   "all-reduced once per rollout when N>1)" % world,
+            "K": K, **sf["config"],
         },
         "roofline": {
             "bound": "mfma", "achieved": achieved, "peak": peak,
@@ -1111,6 +1113,26 @@ def spawn_ranks(n, argv):
     return status
 
 
+def shard_plan(args, world, rank):
+    """(envs_total, first global env id, envs on this rank): --scaling strong splits the
+    --envs total over the ranks (gym_lorenz.parallel.shard_bounds: contiguous ids, the first
+    N mod W ranks one more), weak gives every rank --envs."""
+    from gym_lorenz.parallel import shard_bounds
+
+    if args.scaling == "strong":
+        start, n = shard_bounds(args.envs, rank, world)
+        return args.envs, start, n
+    return args.envs * world, rank * args.envs, args.envs
+
+
+def scaling_fields(args, world, total, n, collective):
+    """The line's scaling statement (every mode): n_gpus, scaling, and in config the job's
+    and one rank's env counts and what crosses ranks (`collective`)."""
+    return {"n_gpus": world, "scaling": args.scaling,
+            "config": {"envs_total": total, "envs_per_gpu": n,
+                       "parallelism": "env shard x%d (contiguous global ids; %s)" % (world, collective)}}
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -1151,15 +1173,8 @@ def main():
 
     import gym_lorenz as gl
     from gym_lorenz import _native as nat
-    from gym_lorenz.parallel import shard_bounds
 
-    if args.scaling == "strong":
-        total = args.envs
-        start, n = shard_bounds(total, rank, world)
-    else:
-        n = args.envs
-        total = n * world
-        start = rank * n
+    total, start, n = shard_plan(args, world, rank)
     kw = {"add_noise": True, "alpha": 0.5} if args.system == "pmsm" else {}
     if args.integrator == "rk4" and args.system in ("lorenz3", "lorenz4"):
         kw["integrator"] = "rk4"
@@ -1215,27 +1230,24 @@ def main():
     else:
         workload = ("%s%s step (lz_step, fp32), %d envs total, %d per GPU, actions/obs/reward/"
                     "done in a %d-slot on-device rollout ring" % (ref_env, integ, total, n, R))
+    sf = scaling_fields(args, world, total, n, "no collective on step")
     out = {
         "metric": METRIC,
         "value": total * K * tm["windows"] / elapsed,
         "unit": "env-steps/s",
-        "n_gpus": world,
+        "n_gpus": sf["n_gpus"],
         "steps": K,
         "warmup": warm,
         "ms_per_step": elapsed * 1e3 / (K * tm["windows"]),
         "higher_is_better": True,
-        "scaling": args.scaling,
+        "scaling": sf["scaling"],
         "vs_baseline": None,
         "dtype": "f64" if args.dtype == "float64" else "f32",
         "data": "synthetic: initial states from on-device Philox keyed by global env id "
                 "(reference distributions); actions ~ U(-%g,%g) f32 pre-generated on device"
                 % (arange, arange),
-        "config": {
-            "workload": workload, "system": args.system, "envs_total": total,
-            "envs_per_gpu": n, "mode": args.mode,
-            "parallelism": "env shard x%d (contiguous global ids, no collective on step)" % world,
-            "launch": launch_desc,
-        },
+        "config": dict({"workload": workload, "system": args.system, "mode": args.mode,
+                        "launch": launch_desc}, **sf["config"]),
         "timing": tm["timing"],
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -1168,11 +1168,12 @@ static inline int64_t grid_for(int64_t n) { return (n + kBlock - 1) / kBlock; }
 // 65,536 envs; slower at 16,384 (the wave's step chain, not the SIMD count, bounds it
 // there) and for PMSM at any N (its step is 3-4x the instructions: doubling them costs
 // more than the extra waves recover).
-// The lane-pair PMSM rollout (k_rollout_pair, SysPMSM::step_pair): by default while its
-// 32-env waves number at most one per SIMD (N <= 32 x 4 x CUs = 32,768 on 256 CUs), where
-// one env per lane leaves SIMDs idle and every wave's step chain is the launch's time:
-// PMSM 32,768 x 2048 2,087 -> 1,895 us; above, two 32-env waves per SIMD lose to one
-// 64-env wave (65,536: 1,958 vs 2,534 us; 131,072 3,009 vs 4,359; 262,144 5,982 vs 8,092;
+// The lane-pair PMSM rollout (k_rollout_pair, SysPMSM::step_pair): by default where its
+// 32-env waves number more than 3 and at most 4 per CU (24,576 < N <= 32,768 on 256
+// CUs: one wave per SIMD), measured: PMSM 32,768 x 2048 2,088 -> 1,890 us.  With fewer
+// envs the one-env-per-lane waves (at most 2 per CU) win (16,384: 1,934 vs 2,045 us), and
+// with more, two 32-env waves per SIMD lose to one 64-env wave (49,152: 1,956 vs 2,577;
+// 65,536: 1,958 vs 2,534; 131,072: 3,009 vs 4,359; 262,144: 5,982 vs 8,092;
 // profiles/r06/pair/).  Variant bit 1<<27 forces it at any N, 1<<28 disables it; the
 // other kernels' force bits (256 / 512 split choice, 1<<23 / 1<<24 group shape, 1<<25
 // producer wave, 1<<26 kZN) select theirs.
@@ -1184,8 +1185,8 @@ static inline bool rollout_pair(const KArgs& a) {
     if (a.variant & (1 << 28)) return false;
     if (a.variant & (1 << 27)) return true;
     if (a.variant & (256 | 512 | (1 << 23) | (1 << 24) | (1 << 25) | (1 << 26))) return false;
-    const int64_t cus = a.num_cus > 0 ? a.num_cus : 256;
-    return (a.n + 31) / 32 <= 4 * cus;
+    const int64_t cus = a.num_cus > 0 ? a.num_cus : 256, waves = (a.n + 31) / 32;
+    return waves > 3 * cus && waves <= 4 * cus;
   }
 }
 

@@ -138,3 +138,37 @@ def test_bench_line_contract_steps20():
     assert 0.3 < rf["frac"] < 1.0 and "traffic" in rf
     assert rf["achieved"] == pytest.approx(65 * (1 << 20) / (rf["avg_launch_us"] * 1e-6) / 1e9)
     assert "hipGraph replay of 20 lz_step launches" in d["config"]["launch"]
+
+
+@pytest.mark.parametrize("mode,extra", [("rollout", ["--K", "2048"]),
+                                        ("policy", ["--policy", "attn", "--K", "2048"]),
+                                        ("step", [])])
+def test_multi_rank_line_shape(mode, extra):
+    """the N > 1 lines of cfg5's modes state the scaling and the per-GPU
+    env count correctly.  Strong (default): --envs is the job's total, split over the
+    ranks in contiguous global ids (BASELINE configs[4]: 262,144 envs on 8 GPUs = 32,768
+    per GPU); weak: --envs per rank.  Every rank's shard together covers [0, total) once."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for world, envs in ((2, 65536), (8, 262144), (3, 100001)):
+        args = bench.parse(["--gpus", str(world), "--mode", mode, "--envs", str(envs)] + extra)
+        assert args.scaling == "strong"
+        plan = [bench.shard_plan(args, world, r) for r in range(world)]
+        assert all(p[0] == envs for p in plan)
+        assert [p[1] for p in plan] == [sum(q[2] for q in plan[:r]) for r in range(world)]
+        assert sum(p[2] for p in plan) == envs and max(p[2] for p in plan) - min(p[2] for p in plan) <= 1
+        total, _, n = plan[0]
+        sf = bench.scaling_fields(args, world, total, n, "no collective on step")
+        assert sf["n_gpus"] == world and sf["scaling"] == "strong"
+        assert sf["config"]["envs_total"] == envs and sf["config"]["envs_per_gpu"] == -(-envs // world)
+        assert ("x%d" % world) in sf["config"]["parallelism"]
+        wk = bench.parse(["--gpus", str(world), "--mode", mode, "--envs", "32768", "--scaling", "weak"] + extra)
+        wplan = [bench.shard_plan(wk, world, r) for r in range(world)]
+        assert all(p == (32768 * world, 32768 * r, 32768) for r, p in enumerate(wplan))
+        wsf = bench.scaling_fields(wk, world, *wplan[1][::2], "x")
+        assert wsf["scaling"] == "weak" and wsf["config"]["envs_per_gpu"] == 32768
+        assert wsf["config"]["envs_total"] == 32768 * world
+    if mode == "rollout":  # cfg5's per-GPU shard at 8 GPUs
+        a8 = bench.parse(["--gpus", "8", "--mode", "rollout", "--envs", "262144"])
+        assert bench.shard_plan(a8, 8, 7) == (262144, 7 * 32768, 32768)

@@ -52,7 +52,9 @@ def test_bench_kernel_names_exist():
         assert kernel_hash.kernel_code_sha256(k) is not None, k
         names.add(k)
     assert "_ZN2lz12k_step_multiINS_5SysHRIfEEfLi4ELb0EEEvNS_5KArgsE" in names
-    # PMSM rollouts: the lane-pair kernel up to 32 x 4 x CUs envs, the 256-lane one above
+    # PMSM rollouts: the lane-pair kernel at 3 < 32-env waves per CU <= 4, one-wave groups
+    # around it, the 256-lane kernel from 131,072
+    assert "k_rolloutINS_7SysPMSMEfLi64E" in bench.kernel_name("pmsm", "rollout", 16384)
     assert bench.kernel_name("pmsm", "rollout", 32768) == "_ZN2lz14k_rollout_pairINS_7SysPMSMEfLi7EEEvNS_5KArgsE"
     assert "k_rolloutINS_7SysPMSMEfLi64E" in bench.kernel_name("pmsm", "rollout", 32800)
     assert "k_rollout_pair" in bench.kernel_name("pmsm", "rollout", 262144, variant=1 << 27)
