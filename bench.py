@@ -283,10 +283,10 @@ def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=
             return "_ZN2lz12k_step_multiINS_%sLi%dELb0EEEvNS_5KArgsE" % (sysname, tiles)
         return "_ZN2lz6k_stepINS_%sLi0EEEvNS_5KArgsE" % sysname
     D = 7  # kDmaDist
-    # lz_kernels.hip rollout_pair: PMSM where its 32-env waves are 3 < waves / CU <= 4
+    # lz_kernels.hip rollout_pair: PMSM where its 32-env waves are 2 < waves / CU <= 4
     force_other = variant & (256 | 512 | (1 << 23) | (1 << 24) | (1 << 25) | (1 << 26))
     if system == "pmsm" and not variant & (1 << 28) and (
-            variant & (1 << 27) or (not force_other and 3 * num_cus < -(-n // 32) <= 4 * num_cus)):
+            variant & (1 << 27) or (not force_other and 2 * num_cus < -(-n // 32) <= 4 * num_cus)):
         # the lane-pair rollout: k_rollout_pair<SysPMSM, float, D>
         return "_ZN2lz14k_rollout_pairINS_7SysPMSMEfLi%dEEEvNS_5KArgsE" % D
     b = "Lb%dE" % int(no_done and system == "lorenz3")  # (SysL3RK4 never terminates either)

@@ -729,6 +729,7 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   if constexpr (kZN) {
     if (live && (a.flags & LZ_FLAG_ADD_NOISE)) normal3(a.seed, (uint64_t)(a.gid0 + i), tick, zn);
   }
+  float anext[Sys::A > 0 ? Sys::A : 1];  // !FULL: the next step's action row (prefetched)
   // kLadder: one of the first D steps (its wait count depends on k); later steps all
   // wait with the steady-state count -- peeled so the hot loop carries no ladder
   auto run_step = [&](int k, auto ladder) __attribute__((always_inline)) {
@@ -756,11 +757,23 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
         issue(dsrc, (k + D) % kDmaSlots);
         if (k + D + 1 < a.K) dsrc += dstride;
       } else {
-        stage_in<true, float, Sys::A, B>(s_act, gact + (off + base) * Sys::A, nb, tid, false);
+        // a ragged last group / unaligned actions: each lane loads its own row, ONE STEP
+        // AHEAD into registers (a load issued and waited for in the same step put a memory
+        // round trip into every step of the group's chain: PMSM 24,608 x 2048, one ragged
+        // group of 32 envs, 3,421 us against 2,094 at 24,576, profiles/r06/pair/); the
+        // barrier keeps the obs tile's reuse rule of the staged full path
         wg_barrier<false>();
         if (live) {
+          if (k == 0) {
 #pragma unroll
-          for (int j = 0; j < Sys::A; ++j) act[j] = s_act[tid * Sys::A + j];
+            for (int j = 0; j < Sys::A; ++j) anext[j] = gload<true>(gact + i * Sys::A + j);
+          }
+#pragma unroll
+          for (int j = 0; j < Sys::A; ++j) act[j] = anext[j];
+          if (k + 1 < a.K) {
+#pragma unroll
+            for (int j = 0; j < Sys::A; ++j) anext[j] = gload<true>(gact + (off + a.n + i) * Sys::A + j);
+          }
         }
       }
     }
@@ -1044,6 +1057,7 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
     dsrc += (int64_t)(D < a.K ? D : a.K - 1) * dstride;
   }
   float znext[3] = {0.0f, 0.0f, 0.0f};  // kPair: lane 0's normals for the next (odd) step
+  float anext[Sys::A > 0 ? Sys::A : 1];  // !FULL: the next step's action row (prefetched)
   auto run_step = [&](int k, auto ladder) __attribute__((always_inline)) {
     const int64_t off = (int64_t)k * a.n;
     float act[Sys::A];
@@ -1060,9 +1074,17 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
         }
         issue(dsrc, (k + D) % kDmaSlots);
         if (k + D + 1 < a.K) dsrc += dstride;
-      } else if (live) {
+      } else if (live) {  // ragged / unaligned: the lane's row, one step ahead (rollout_loop)
+        if (k == 0) {
 #pragma unroll
-        for (int j = 0; j < Sys::A; ++j) act[j] = gload<true>(gact + (off + i) * Sys::A + j);
+          for (int j = 0; j < Sys::A; ++j) anext[j] = gload<true>(gact + i * Sys::A + j);
+        }
+#pragma unroll
+        for (int j = 0; j < Sys::A; ++j) act[j] = anext[j];
+        if (k + 1 < a.K) {
+#pragma unroll
+          for (int j = 0; j < Sys::A; ++j) anext[j] = gload<true>(gact + (off + a.n + i) * Sys::A + j);
+        }
       }
     }
     T o[Sys::O];
@@ -1169,10 +1191,10 @@ static inline int64_t grid_for(int64_t n) { return (n + kBlock - 1) / kBlock; }
 // there) and for PMSM at any N (its step is 3-4x the instructions: doubling them costs
 // more than the extra waves recover).
 // The lane-pair PMSM rollout (k_rollout_pair, SysPMSM::step_pair): by default where its
-// 32-env waves number more than 3 and at most 4 per CU (24,576 < N <= 32,768 on 256
-// CUs: one wave per SIMD), measured: PMSM 32,768 x 2048 2,088 -> 1,890 us.  With fewer
-// envs the one-env-per-lane waves (at most 2 per CU) win (16,384: 1,934 vs 2,045 us), and
-// with more, two 32-env waves per SIMD lose to one 64-env wave (49,152: 1,956 vs 2,577;
+// 32-env waves number more than 2 and at most 4 per CU (16,384 < N <= 32,768 on 256 CUs),
+// measured: PMSM 32,768 x 2048 2,088 -> 1,890 us, 28,672 2,087 -> 1,950.  At 2 waves per
+// CU the one-env-per-lane waves (one per CU) win (16,384: 1,934 vs 2,045 us), and with
+// more, two 32-env waves per SIMD lose to one 64-env wave (49,152: 1,956 vs 2,577;
 // 65,536: 1,958 vs 2,534; 131,072: 3,009 vs 4,359; 262,144: 5,982 vs 8,092;
 // profiles/r06/pair/).  Variant bit 1<<27 forces it at any N, 1<<28 disables it; the
 // other kernels' force bits (256 / 512 split choice, 1<<23 / 1<<24 group shape, 1<<25
@@ -1186,7 +1208,7 @@ static inline bool rollout_pair(const KArgs& a) {
     if (a.variant & (1 << 27)) return true;
     if (a.variant & (256 | 512 | (1 << 23) | (1 << 24) | (1 << 25) | (1 << 26))) return false;
     const int64_t cus = a.num_cus > 0 ? a.num_cus : 256, waves = (a.n + 31) / 32;
-    return waves > 3 * cus && waves <= 4 * cus;
+    return waves > 2 * cus && waves <= 4 * cus;
   }
 }
 

@@ -473,9 +473,9 @@ def test_rollout_noise_producer_equals_steps(gl, system, dtype, n, K):
         a_be = gl.BatchedEnv(system, n, dtype=dtype, seed=9, max_episode_steps=37, add_noise=True, variant=variant)
         b_be = gl.BatchedEnv(system, n, dtype=dtype, seed=9, max_episode_steps=37, add_noise=True)
         sh = nat.launch_shape(a_be._h, nat.CALL_ROLLOUT)
-        # (PMSM at 3 < 32-env waves per CU <= 4 defaults to the lane-pair kernel,
+        # (PMSM at 2 < 32-env waves per CU <= 4 defaults to the lane-pair kernel,
         # test_gpu_rollout_pair.py)
-        pair = system == "pmsm" and variant == 0 and 3 * cus < (n + 31) // 32 <= 4 * cus
+        pair = system == "pmsm" and variant == 0 and 2 * cus < (n + 31) // 32 <= 4 * cus
         assert sh["kernel"] == ("rollout_pair" if pair else "rollout_wave" if one_wave else "rollout"), sh
         assert sh["waves"] == (2 if variant == 1 << 25 else 1 if one_wave or pair else 4), sh
         a_be.reset()

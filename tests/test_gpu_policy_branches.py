@@ -205,9 +205,9 @@ def test_bf16_mlp_shapes_bit_identical(gl, pol):
     ("lorenz4", 49152, 0, "rollout", False),         # LORENZ4 f32: 256-lane from 3/4 x 256 x CUs
     ("lorenz4", 40960, 0, "rollout_wave", False),
     ("pmsm", 100000, 0, "rollout_wave", False),      # PMSM / HR: one-wave below 131,072
-    ("pmsm", 32768, 0, "rollout_pair", False),       # PMSM: lane pairs at 3 < waves / CU <= 4
-    ("pmsm", 24577, 0, "rollout_pair", False),
-    ("pmsm", 24576, 0, "rollout_wave", False),
+    ("pmsm", 32768, 0, "rollout_pair", False),       # PMSM: lane pairs at 2 < waves / CU <= 4
+    ("pmsm", 16385, 0, "rollout_pair", False),
+    ("pmsm", 16384, 0, "rollout_wave", False),
     ("pmsm", 32769, 0, "rollout_wave", False),
     ("pmsm", 200000, 1 << 27, "rollout_pair", False),  # forced at any N
     ("pmsm", 4097, 1 << 28, "rollout_wave", False),    # disabled

@@ -52,7 +52,7 @@ def test_bench_kernel_names_exist():
         assert kernel_hash.kernel_code_sha256(k) is not None, k
         names.add(k)
     assert "_ZN2lz12k_step_multiINS_5SysHRIfEEfLi4ELb0EEEvNS_5KArgsE" in names
-    # PMSM rollouts: the lane-pair kernel at 3 < 32-env waves per CU <= 4, one-wave groups
+    # PMSM rollouts: the lane-pair kernel at 2 < 32-env waves per CU <= 4, one-wave groups
     # around it, the 256-lane kernel from 131,072
     assert "k_rolloutINS_7SysPMSMEfLi64E" in bench.kernel_name("pmsm", "rollout", 16384)
     assert bench.kernel_name("pmsm", "rollout", 32768) == "_ZN2lz14k_rollout_pairINS_7SysPMSMEfLi7EEEvNS_5KArgsE"
