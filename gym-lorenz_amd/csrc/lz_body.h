@@ -131,8 +131,15 @@ __device__ __forceinline__ uint8_t step_body(Sys& sys, int32_t& steps, const KAr
     if constexpr (Sys::kNoise) {
       if (a.flags & LZ_FLAG_ADD_NOISE) {
         if constexpr (kZMode == 1) {  // the normals drawn ahead by a producer wave (k_rollout kNP):
-          // zpre[0], zpre[64], zpre[128] -- the same normal3(seed, gid, tick) values
-          float z[3] = {zpre[0], zpre[64], zpre[128]};
+          // zpre[0], zpre[64], zpre[128] -- the same normal3(seed, gid, tick) values; zpre =
+          // nullptr: the producer timed out, the step runs on NaN normals
+          const float q = __builtin_nanf("");
+          float z[3] = {q, q, q};
+          if (zpre) {
+            z[0] = zpre[0];
+            z[1] = zpre[64];
+            z[2] = zpre[128];
+          }
           sys.noise_from_normals(z, nz);
         } else if constexpr (kZMode == 2) {  // this step's from registers; draw the next step's
           float z[3] = {zpre[0], zpre[1], zpre[2]};

@@ -790,15 +790,14 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
         ++spin;
       }
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      float* zs = const_cast<float*>(s_z) + (k % kZSlots) * 3 * B + tid;  // (LDS ring)
-      if (spin >= kZSpinCap) {  // the producer never delivered: poison this step's normals
-        // and every later step's (NaN obs / reward: a wrong result is visible, never silently
-        // stale); the producer leaves on its own cap and is not waited for again
-        zcap = kZSpinCap;
-        zs[0] = zs[B] = zs[2 * B] = __builtin_nanf("");
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      }
-      zp = zs;
+      const float* zs = s_z + (k % kZSlots) * 3 * B + tid;  // (LDS ring)
+      // the producer never delivered: this step's normals and every later step's are NaN
+      // (NaN obs / reward: a wrong result is visible, never silently stale), poisoned in
+      // the stepping wave's own registers (zp = nullptr: step_body kZMode 1) -- the ring
+      // slot is left alone, so a producer that is only slow cannot mix valid normals into
+      // a poisoned step; it leaves on its own cap and is not waited for again
+      if (spin >= kZSpinCap) zcap = kZSpinCap;
+      zp = spin >= kZSpinCap ? nullptr : zs;
     }
     if constexpr (kZN) zp = zn;
     const uint8_t dflag = step_body<Sys, T, true, false, kNoDone, false, kNP ? 1 : kZN ? 2 : 0>(
