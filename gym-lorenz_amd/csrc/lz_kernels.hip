@@ -655,8 +655,14 @@ __device__ __forceinline__ void ladder_wait(int k) {
 
 constexpr int kZSlots = 4;  // steps of normals a producer wave may draw ahead (k_rollout kNP)
 constexpr uint32_t kZSpinCap = 1u << 24;  // polls of one flag before a wave gives up (~1 s)
+// kRag (FULL one-wave groups only): the launch's ragged LAST group (nb < 64, N a multiple
+// of 4 -- vec_ok) runs the full path too: its DMA sources are clamped to the group's own
+// rows (nb * A floats, whole 16-B chunks since nb % 4 == 0), and the lanes past nb compute
+// on stale LDS but store nothing (their stores exec-masked: still issued, so the vmcnt
+// counts hold -- lane 0 is always live).  The staged path's per-step action load made that
+// one group the launch's straggler (LORENZ3 16,400 x 2048: 1,860 vs 465 us).
 template <class Sys, typename T, int B, bool FULL, int D, bool kNoDone, bool kDoneT, bool kNP = false,
-          bool kZN = false>
+          bool kZN = false, bool kRag = false>
 __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any_reset,
                                              const KArgs& a, int64_t base, int tid, int nb,
                                              uint64_t tick, float* s_act, T* s_obs,
@@ -665,7 +671,8 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   using CO = Chunk<Sys::O * (int)sizeof(T)>;
   using co_t = typename CO::t;
   const int64_t i = base + tid;
-  const bool live = FULL || tid < nb;
+  static_assert(!kRag || (FULL && B == 64), "kRag: full-path one-wave groups");
+  const bool live = (FULL && !kRag) || tid < nb;
   const float* gact = static_cast<const float*>(a.act);
   const int wave = tid >> 6;
   // One-wave workgroups (small N, latency-bound): no LDS obs staging and no barriers --
@@ -706,8 +713,10 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
   };
   // this lane's DMA source pointer for step kk, and the per-step advance
   const int64_t wave_row0 = (base + 64 * (int64_t)wave) * Sys::A;  // the wave's slice
-  const int64_t lane0 = kRow ? wave_row0 + 4 * (lane % (64 * Sys::A / 4))
-                             : kDirect ? (base + tid) * Sys::A : base * Sys::A + tid;
+  const int lane_src = kRag ? (kRow ? min(lane % (64 * Sys::A / 4), nb * Sys::A / 4 - 1) : min(tid, nb - 1))
+                            : (kRow ? lane % (64 * Sys::A / 4) : tid);
+  const int64_t lane0 = kRow ? wave_row0 + 4 * lane_src
+                             : kDirect ? (base + lane_src) * Sys::A : base * Sys::A + tid;
   const int64_t dstride = a.n * Sys::A;
   auto dma_src = [&](int kk) __attribute__((always_inline)) {
     return gact + ((int64_t)kk * dstride + lane0);
@@ -809,11 +818,13 @@ __device__ __forceinline__ void rollout_loop(Sys& sys, int32_t& steps, bool& any
     any_reset = any_reset || did_reset;
     T* gobs = static_cast<T*>(a.obs) + (off + base) * Sys::O;
     if constexpr (kDirect) {
-      gstore<true>(static_cast<T*>(a.rew) + off + i, rew);
-      gstore<!kDoneT>(a.done + off + i, dflag);
-      const co_t* src = reinterpret_cast<const co_t*>(o);
+      if (!kRag || live) {
+        gstore<true>(static_cast<T*>(a.rew) + off + i, rew);
+        gstore<!kDoneT>(a.done + off + i, dflag);
+        const co_t* src = reinterpret_cast<const co_t*>(o);
 #pragma unroll
-      for (int j = 0; j < CO::N; ++j) gstore<false>(reinterpret_cast<co_t*>(gobs) + tid * CO::N + j, src[j]);
+        for (int j = 0; j < CO::N; ++j) gstore<false>(reinterpret_cast<co_t*>(gobs) + tid * CO::N + j, src[j]);
+      }
       return;
     }
     // the obs tile of this step: systems with actions pass a workgroup barrier at the top
@@ -911,6 +922,9 @@ __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
   if (nb == B && a.vec_ok)
     rollout_loop<Sys, T, B, true, D, kNoDone, kDoneT, false, kZN>(sys, steps, any_reset, a, base, tid, nb, tick,
                                                                   s_act, s_obs);
+  else if (B == 64 && a.vec_ok)  // the ragged last one-wave group: the full path, kRag
+    rollout_loop<Sys, T, B, B == 64, D, kNoDone, kDoneT, false, kZN, B == 64>(sys, steps, any_reset, a, base, tid,
+                                                                              nb, tick, s_act, s_obs);
   else
     rollout_loop<Sys, T, B, false, D, kNoDone, kDoneT, false, kZN>(sys, steps, any_reset, a, base, tid, nb, tick,
                                                                    s_act, s_obs);
@@ -1016,7 +1030,8 @@ __device__ __forceinline__ void store_half(T* p, const T* v) {
 // while lane 0 draws normal3(tick + k + 1) and hands it over (pair_swap) for step k + 1,
 // so each lane runs one Philox + Box-Muller per two steps.  The same values as
 // normal3(seed, gid, tick + k) at every step: bit-identical to k_rollout.
-template <class Sys, typename T, int R, bool FULL, int D, bool kNoDone, int SV, bool kPair = false>
+template <class Sys, typename T, int R, bool FULL, int D, bool kNoDone, int SV, bool kPair = false,
+          bool kRag = false>  // kRag: the ragged last group on the full path (rollout_loop's)
 __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_reset,
                                            const KArgs& a, int64_t base, int tid, int nb,
                                            uint64_t tick, float* s_act) {
@@ -1026,7 +1041,7 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
   const int el = tid / R, q = tid % R;
   const bool lead = q == 0;
   const int64_t i = base + el;
-  const bool live = FULL || el < nb;
+  const bool live = (FULL && !kRag) || el < nb;
   const float* gact = static_cast<const float*>(a.act);
   // vector-memory ops every step issues after its DMA (lower bound): reward or done
   // (two exec-masked stores) + at least one obs store
@@ -1048,7 +1063,9 @@ __device__ __forceinline__ void split_loop(Sys& sys, int32_t& steps, bool& any_r
   const int64_t dstride = a.n * Sys::A;
   // kRow: lane tid loads chunk tid mod C of the wave's 32-env slice; else: lane tid
   // loads its own env's components
-  const float* dsrc = kRow ? gact + base * Sys::A + 4 * (tid % (32 * Sys::A / 4)) : gact + i * Sys::A;
+  const int64_t src_el = kRag ? min(el, nb - 1) : el;
+  const int src_chunk = kRag ? min(tid % (32 * Sys::A / 4), nb * Sys::A / 4 - 1) : tid % (32 * Sys::A / 4);
+  const float* dsrc = kRow ? gact + base * Sys::A + 4 * src_chunk : gact + (base + src_el) * Sys::A;
   if constexpr (FULL) __builtin_amdgcn_s_waitcnt(0x0F70);
   if constexpr (FULL && Sys::kUsesAction) {
 #pragma unroll
@@ -1160,6 +1177,8 @@ __device__ __forceinline__ void rollout_split_body(KArgs a) {
   }
   if (nb == E && a.vec_ok)
     split_loop<Sys, T, R, true, D, kNoDone, SV, kPair>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
+  else if (a.vec_ok)  // the ragged last group: the full path, kRag
+    split_loop<Sys, T, R, true, D, kNoDone, SV, kPair, true>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
   else
     split_loop<Sys, T, R, false, D, kNoDone, SV, kPair>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
   if (live && lead) {
