@@ -51,6 +51,13 @@ def parse(argv=None):
     p.add_argument("--launch", choices=["graph", "eager"], default="graph")
     p.add_argument("--graph-len", type=int, default=64, help="steps per captured hipGraph")
     p.add_argument("--ring", type=int, default=16, help="rollout-ring slots for actions/obs")
+    p.add_argument("--head-eager", type=int, default=0,
+                   help="step mode: launch each timed window's first E (even) steps eagerly, the "
+                        "rest from graphs (0 = off)")
+    p.add_argument("--head-graph", type=int, default=0,
+                   help="step mode: launch each timed window's first H (even) steps as a graph of "
+                        "their own, so the GPU starts on them while the host submits the rest "
+                        "(0 = off)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-drift", action="store_true")
     p.add_argument("--no-extras", action="store_true",
@@ -636,12 +643,16 @@ def describe_launches(tm, rollout):
         return ("per timed window: %d eager %d-step lz_rollout launches (x%d windows)"
                 % (per_win, tm["T"], tm["windows"]))
     if tm["graph"]:
-        L, G = tm["graph_len"], tm.get("graph_rem", 0)
-        rem = per_win % L
+        L, G, H = tm["graph_len"], tm.get("graph_rem", 0), tm.get("graph_head", 0)
+        E = tm.get("head_eager", 0)
+        head = ("1 hipGraph replay of %d lz_step launches (the head graph) + " % H) if H else \
+            ("%d eager lz_step launches (the head) + " % E) if E else ""
+        body = per_win - H - E
+        rem = body % L
         extra = ("1 hipGraph replay of %d lz_step launches + " % G) if G and rem >= G else ""
-        return ("per timed window: %d hipGraph replays of %d lz_step launches + %s%d eager "
+        return ("per timed window: %s%d hipGraph replays of %d lz_step launches + %s%d eager "
                 "lz_step launches (x%d windows)"
-                % (per_win // L, L, extra, rem - (G if extra else 0), tm["windows"]))
+                % (head, body // L, L, extra, rem - (G if extra else 0), tm["windows"]))
     return "per timed window: %d eager lz_step launches (x%d windows)" % (per_win, tm["windows"])
 
 
@@ -940,10 +951,17 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
     if rollout:
         L = 1
     use_graph = args.launch == "graph" and not rollout
-    # the window's K mod L remainder as a graph too (its even part: the captured
+    # --head-graph H: the window's first H launches as a short graph of their own (H even:
+    # the captured ping-pong parity)
+    H = getattr(args, "head_graph", 0)
+    H = H - H % 2 if use_graph and 0 < H <= launches else 0
+    E = getattr(args, "head_eager", 0)
+    E = E - E % 2 if use_graph and not H and 0 < E <= launches else 0
+    H = H or E  # (the remainder graph covers what follows the head either way)
+    # the window's (K - H) mod L remainder as a graph too (its even part: the captured
     # ping-pong parity), so that a short window (the driver's --steps 20) is not
     # paced by one Python launch per step
-    rem_n = (launches % L) - (launches % L) % 2 if use_graph else 0
+    rem_n = ((launches - H) % L) - ((launches - H) % L) % 2 if use_graph else 0
     for ln in lanes:
         with torch.cuda.stream(ln.stream):
             for _ in range(max(warm, 2)):
@@ -958,6 +976,11 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
                     with torch.cuda.graph(ln.graph_rem, stream=ln.stream):
                         for _ in range(rem_n):
                             ln.one()
+                if H and not E:
+                    ln.graph_head = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(ln.graph_head, stream=ln.stream):
+                        for _ in range(H):
+                            ln.one()
     torch.cuda.synchronize(device)
 
     def run(nlaunch):  # exactly nlaunch launches on every lane, the lanes interleaved
@@ -967,6 +990,17 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
                     with torch.cuda.stream(ln.stream):
                         ln.one()
             return
+        if E and nlaunch >= E:
+            for _ in range(E):
+                for ln in lanes:
+                    with torch.cuda.stream(ln.stream):
+                        ln.one()
+            nlaunch -= E
+        elif H and nlaunch >= H:
+            for ln in lanes:
+                with torch.cuda.stream(ln.stream):
+                    ln.graph_head.replay()
+            nlaunch -= H
         for _ in range(nlaunch // L):
             for ln in lanes:
                 with torch.cuda.stream(ln.stream):
@@ -983,7 +1017,7 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
                     ln.one()
 
     def fix_parity(nlaunch):  # untimed: an odd eager remainder flipped the parity
-        if use_graph and (nlaunch % L) % 2:
+        if use_graph and nlaunch % 2:  # (H, L and the remainder graph are all even)
             for ln in lanes:
                 with torch.cuda.stream(ln.stream):
                     ln.one()
@@ -1046,7 +1080,7 @@ def measure_steps(args, torch, dist, nat, env, device, world, rank, rollout, min
     K = launches * T
     return {
         "steps": K, "T": T, "ring": R, "graph_len": L, "graph": use_graph,
-        "graph_rem": rem_n, "streams": len(lanes),
+        "graph_rem": rem_n, "graph_head": 0 if E else H, "head_eager": E, "streams": len(lanes),
         "warmup": warm, "launches": launches * need, "windows": need,
         "elapsed": elapsed, "ev_ms": ev_ms,
         "timing": {
