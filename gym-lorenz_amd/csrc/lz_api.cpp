@@ -344,6 +344,26 @@ lz_status lz_destroy(lz_handle* h) {
   return LZ_OK;
 }
 
+lz_status lz_io_sizes_for(const lz_config* cfg, int32_t K, int64_t cap, lz_io_sizes* out) {
+  if (!cfg || !out) return fail(LZ_ERR_INVALID, "config/out is NULL");
+  if (cfg->system < LZ_SYS_LORENZ3 || cfg->system > LZ_SYS_SC) return fail(LZ_ERR_INVALID, "unknown system");
+  if (cfg->num_envs < 1 || K < 0 || cap < 0) return fail(LZ_ERR_INVALID, "num_envs >= 1, K >= 0, cap >= 0");
+  const SysDesc d = describe(cfg->system);
+  const int64_t n = cfg->num_envs, steps = K > 0 ? K : 1;
+  const int64_t t = (cfg->dtype == LZ_DTYPE_F64 && cfg->system != LZ_SYS_PMSM) ? 8 : 4;
+  const bool needs_act = cfg->system != LZ_SYS_LORENZ4 && cfg->system != LZ_SYS_SC;
+  std::memset(out, 0, sizeof *out);
+  out->actions = needs_act ? steps * n * d.action_dim * 4 : 0;
+  out->noise = K > 0 ? 0 : n * 3 * 8;
+  out->obs = steps * n * d.obs_dim * t;
+  out->rew = steps * n * t;
+  out->done = steps * n;
+  out->done_idx = K > 0 ? cap * 8 : n * 4;
+  out->terminal_obs = (K > 0 ? cap : n) * d.obs_dim * t;
+  out->n_done = 4;
+  return LZ_OK;
+}
+
 lz_status lz_get_info(const lz_handle* h, lz_info* info) {
   if (!h || !info) return fail(LZ_ERR_INVALID, "handle/info is NULL");
   std::memset(info, 0, sizeof *info);

@@ -47,6 +47,12 @@ class LorenzEnvError(RuntimeError):
         self.status = status
 
 
+class LzIoSizes(ctypes.Structure):
+    """lz_io_sizes: the bytes each caller buffer of lz_step / lz_rollout must cover."""
+    _fields_ = [(f, ctypes.c_int64) for f in ("actions", "noise", "obs", "rew", "done", "done_idx",
+                                              "terminal_obs", "n_done")]
+
+
 class LzConfig(ctypes.Structure):
     _fields_ = [
         ("system", ctypes.c_int32),
@@ -208,6 +214,8 @@ _SIGS = {
     "lz_rollout_policy": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),
     "lz_policy_f32_blob_bytes": (ctypes.c_int64, []),
     "lz_policy_blob_format": (ctypes.c_int32, [VP, ctypes.c_int64]),
+    "lz_io_sizes_for": (ctypes.c_int, [ctypes.POINTER(LzConfig), ctypes.c_int32, ctypes.c_int64,
+                                       ctypes.POINTER(LzIoSizes)]),
     "lz_policy_pack_f32": (ctypes.c_int, [ctypes.POINTER(LzMlpPolicy), ctypes.c_int32, VP,
                                           ctypes.c_int64]),
     "lz_rollout_policy_f32": (ctypes.c_int, [VP, ctypes.POINTER(LzPolicyRolloutArgs)]),

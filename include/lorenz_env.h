@@ -286,6 +286,23 @@ lz_status lz_resident_stop(lz_handle* h);
  * the device (synchronous). */
 lz_status lz_resident_read_state(lz_handle* h, int32_t plane, void* host_dst);
 
+/* The byte sizes the caller buffers of lz_step (K = 0) or lz_rollout (K >= 1, done list of
+ * `cap` entries) must each cover, for a config -- the raw pointers of those calls carry no
+ * sizes, and a buffer shorter than this is written past its end on the device (DESIGN
+ * §6.2.1: a LORENZ3 obs ring of [N, 3] for the [N, 6] observation).  Host-only, needs no
+ * GPU and no handle; gym_lorenz.core.check_buffer applies the same sizes. */
+typedef struct lz_io_sizes {
+  int64_t actions;      /* float32 [N, A] / [K, N, A]; 0: the system reads none (LORENZ4, SC) */
+  int64_t noise;        /* float64 [N, 3]: lz_step's optional injected noise (0 for K >= 1) */
+  int64_t obs;          /* T [N, O] / [K, N, O] */
+  int64_t rew;          /* T [N] / [K, N] */
+  int64_t done;         /* uint8 [N] / [K, N] */
+  int64_t done_idx;     /* int32 [N] (step) / int64 [cap] (rollout) */
+  int64_t terminal_obs; /* T [N, O] (step) / T [cap, O] (rollout) */
+  int64_t n_done;       /* int32 [1] */
+} lz_io_sizes;
+lz_status lz_io_sizes_for(const lz_config* cfg, int32_t K, int64_t cap, lz_io_sizes* out);
+
 /* K fused steps in ONE launch, state held in registers.  Time-major buffers:
  *   actions T [K, N, action_dim]; obs_out T [K, N, obs_dim]; rew_out T [K, N];
  *   done_out uint8 [K, N]; done_idx_out int64 [cap] (k * N + env) and

@@ -139,3 +139,58 @@ def test_actions_optional_only_where_the_system_reads_none():
     with pytest.raises(nat.LorenzEnvError):
         step_io_args(Spec, None, *out)
     assert check_buffer(None, "x", torch.float32, 1, torch.device("cpu"), required=False) is None
+
+
+@pytest.mark.parametrize("system", sorted({"lorenz3": 0, "lorenz4": 1, "pmsm": 2, "hr": 3,
+                                           "transient1": 4, "transient2": 5, "transient_pmsm": 6,
+                                           "singlecontrol": 7}))
+@pytest.mark.parametrize("dtype", ["float32", "float64"])
+def test_c_abi_io_sizes_agree_with_the_checker(system, dtype):
+    """lz_io_sizes_for (include/lorenz_env.h: the bytes every raw buffer of lz_step /
+    lz_rollout must cover, host-only) and the Python checker (core.step_io_args /
+    rollout_io_args) state the same contract, for every system and precision."""
+    import ctypes
+
+    from gym_lorenz.core import SYSTEMS
+
+    sysid = SYSTEMS[system]
+    cfg = nat.config_init(sysid)
+    f64 = dtype == "float64" and system != "pmsm"
+    cfg.dtype = nat.F64 if f64 else nat.F32
+    n, K, cap = 1000, 7, 33
+    cfg.num_envs = n
+    td = torch.float64 if f64 else torch.float32
+    es = 8 if f64 else 4
+    obs_dim = {"lorenz4": 8, "transient2": 8}.get(system, 6)
+    act_dim = {"lorenz3": 3, "lorenz4": 3, "transient2": 3}.get(system, 2)
+    reads = system not in ("lorenz4", "singlecontrol")
+
+    from types import SimpleNamespace
+
+    Spec = SimpleNamespace(num_envs=n, obs_dim=obs_dim, action_dim=act_dim, tdtype=td,
+                           device=torch.device("cpu"), reads_actions=reads)
+    for k in (0, K):
+        sz = nat.LzIoSizes()
+        nat.check(nat.lib.lz_io_sizes_for(ctypes.byref(cfg), k, cap if k else 0, ctypes.byref(sz)))
+        steps = max(k, 1)
+        assert sz.actions == (steps * n * act_dim * 4 if reads else 0)
+        assert sz.obs == steps * n * obs_dim * es and sz.rew == steps * n * es and sz.done == steps * n
+        assert sz.n_done == 4
+        bufs = [torch.empty(sz.actions // 4, dtype=torch.float32) if reads else None,
+                torch.empty(sz.obs // es, dtype=td), torch.empty(sz.rew // es, dtype=td),
+                torch.empty(sz.done, dtype=torch.uint8)]
+        if k == 0:
+            assert sz.noise == n * 24 and sz.done_idx == n * 4 and sz.terminal_obs == n * obs_dim * es
+            step_io_args(Spec, bufs[0], *bufs[1:], torch.empty(sz.done_idx // 4, dtype=torch.int32),
+                         torch.empty(sz.terminal_obs // es, dtype=td), torch.empty(1, dtype=torch.int32),
+                         noise=torch.empty(sz.noise // 8, dtype=torch.float64))
+            with pytest.raises(nat.LorenzEnvError):  # one element short of the C sizes: refused
+                step_io_args(Spec, bufs[0], torch.empty(sz.obs // es - 1, dtype=td), *bufs[2:])
+        else:
+            assert sz.noise == 0 and sz.done_idx == cap * 8 and sz.terminal_obs == cap * obs_dim * es
+            rollout_io_args(Spec, k, bufs[0], *bufs[1:], torch.empty(cap, dtype=torch.int64),
+                            torch.empty(sz.terminal_obs // es, dtype=td), cap)
+    bad = nat.LzIoSizes()
+    assert nat.lib.lz_io_sizes_for(None, 0, 0, ctypes.byref(bad)) == nat.LZ_ERR_INVALID
+    cfg.num_envs = 0
+    assert nat.lib.lz_io_sizes_for(ctypes.byref(cfg), 0, 0, ctypes.byref(bad)) == nat.LZ_ERR_INVALID
