@@ -661,6 +661,9 @@ __device__ __forceinline__ void ladder_wait(int k) {
 
 constexpr int kZSlots = 4;  // steps of normals a producer wave may draw ahead (k_rollout kNP)
 constexpr uint32_t kZSpinCap = 1u << 24;  // polls of one flag before a wave gives up (~1 s)
+#ifndef LZ_RAG
+#define LZ_RAG 1  // (A/B builds, tools/build_ab.sh: 0 = the ragged group takes the staged path)
+#endif
 // kRag (FULL one-wave groups only): the launch's ragged LAST group (nb < 64, N a multiple
 // of 4 -- vec_ok) runs the full path too: its DMA sources are clamped to the group's own
 // rows (nb * A floats, whole 16-B chunks since nb % 4 == 0), and the lanes past nb compute
@@ -928,7 +931,7 @@ __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
   if (nb == B && a.vec_ok)
     rollout_loop<Sys, T, B, true, D, kNoDone, kDoneT, false, kZN>(sys, steps, any_reset, a, base, tid, nb, tick,
                                                                   s_act, s_obs);
-  else if (B == 64 && a.vec_ok)  // the ragged last one-wave group: the full path, kRag
+  else if (LZ_RAG && B == 64 && a.vec_ok)  // the ragged last one-wave group: the full path, kRag
     rollout_loop<Sys, T, B, B == 64, D, kNoDone, kDoneT, false, kZN, B == 64>(sys, steps, any_reset, a, base, tid,
                                                                               nb, tick, s_act, s_obs);
   else
@@ -1183,7 +1186,7 @@ __device__ __forceinline__ void rollout_split_body(KArgs a) {
   }
   if (nb == E && a.vec_ok)
     split_loop<Sys, T, R, true, D, kNoDone, SV, kPair>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
-  else if (a.vec_ok)  // the ragged last group: the full path, kRag
+  else if (LZ_RAG && a.vec_ok)  // the ragged last group: the full path, kRag
     split_loop<Sys, T, R, true, D, kNoDone, SV, kPair, true>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
   else
     split_loop<Sys, T, R, false, D, kNoDone, SV, kPair>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
