@@ -661,9 +661,20 @@ __device__ __forceinline__ void ladder_wait(int k) {
 
 constexpr int kZSlots = 4;  // steps of normals a producer wave may draw ahead (k_rollout kNP)
 constexpr uint32_t kZSpinCap = 1u << 24;  // polls of one flag before a wave gives up (~1 s)
+// LZ_RAG: which systems' ragged last group takes the full path (kRag): 2 (default) the
+// noise-free systems (LORENZ3 / LORENZ4 / T1 / T2), 1 every system, 0 none (A/B builds,
+// tools/build_ab.sh).  Compiled into the noisy systems' rollout kernels (PMSM, HR, whose
+// loops are ~3x larger) the second copy of the loop slowed their WHOLE groups by 5-6 %
+// (PMSM lane pair 1,929 -> 2,038 us, HR 1,352 -> 1,419 at 32,768 x 2048; LORENZ3 unchanged,
+// profiles/r06/rag_ab/), so their ragged group keeps the staged path (its action row
+// prefetched one step ahead).
 #ifndef LZ_RAG
-#define LZ_RAG 1  // (A/B builds, tools/build_ab.sh: 0 = the ragged group takes the staged path)
+#define LZ_RAG 2
 #endif
+template <class Sys>
+constexpr bool rag_full() {
+  return LZ_RAG == 1 || (LZ_RAG == 2 && !Sys::kNoise);
+}
 // kRag (FULL one-wave groups only): the launch's ragged LAST group (nb < 64, N a multiple
 // of 4 -- vec_ok) runs the full path too: its DMA sources are clamped to the group's own
 // rows (nb * A floats, whole 16-B chunks since nb % 4 == 0), and the lanes past nb compute
@@ -931,7 +942,7 @@ __global__ __launch_bounds__(B) void k_rollout(KArgs a) {
   if (nb == B && a.vec_ok)
     rollout_loop<Sys, T, B, true, D, kNoDone, kDoneT, false, kZN>(sys, steps, any_reset, a, base, tid, nb, tick,
                                                                   s_act, s_obs);
-  else if (LZ_RAG && B == 64 && a.vec_ok)  // the ragged last one-wave group: the full path, kRag
+  else if (rag_full<Sys>() && B == 64 && a.vec_ok)  // the ragged last one-wave group: the full path, kRag
     rollout_loop<Sys, T, B, B == 64, D, kNoDone, kDoneT, false, kZN, B == 64>(sys, steps, any_reset, a, base, tid,
                                                                               nb, tick, s_act, s_obs);
   else
@@ -1186,7 +1197,7 @@ __device__ __forceinline__ void rollout_split_body(KArgs a) {
   }
   if (nb == E && a.vec_ok)
     split_loop<Sys, T, R, true, D, kNoDone, SV, kPair>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
-  else if (LZ_RAG && a.vec_ok)  // the ragged last group: the full path, kRag
+  else if (rag_full<Sys>() && a.vec_ok)  // the ragged last group: the full path, kRag
     split_loop<Sys, T, R, true, D, kNoDone, SV, kPair, true>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);
   else
     split_loop<Sys, T, R, false, D, kNoDone, SV, kPair>(sys, steps, any_reset, a, base, tid, nb, tick, s_act);

@@ -1,10 +1,11 @@
 """A rollout's ragged LAST group on the full DMA path (r06; lz_kernels.hip rollout_loop /
 split_loop kRag): N a multiple of 4 (the launch's vec_ok) but not of the group's env count.
 The group's DMA sources are clamped to its own rows and the lanes past its envs store
-nothing.  Bar: K fused steps == K lz_step calls bit for bit (obs, reward, done, the
-compact done list, every final state plane) for each kernel family whose last group is
-partial: one-wave (LORENZ3, PMSM, HR), split lanes (LORENZ3), lane pairs (PMSM), with
-TimeLimit truncations inside the launch.  (N not a multiple of 4 keeps the staged path:
+nothing (the noise-free systems, LZ_RAG = 2; PMSM / HR keep the staged path with a
+one-step register prefetch).  Bar: K fused steps == K lz_step calls bit for bit (obs,
+reward, done, the compact done list, every final state plane) for each kernel family
+whose last group is partial: one-wave (LORENZ3, PMSM, HR), split lanes (LORENZ3), lane
+pairs (PMSM), with TimeLimit truncations inside the launch.  (N not a multiple of 4 keeps the staged path:
 test_gpu_parity.py's 4,097 / 70,001 cases.)"""
 import numpy as np
 import pytest
