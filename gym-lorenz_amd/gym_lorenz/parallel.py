@@ -11,10 +11,13 @@ The only collectives are optional and outside the step kernel:
 Launch: python -m torch.distributed.run --nproc-per-node N ... (RANK / WORLD_SIZE /
 LOCAL_RANK from the environment).
 """
+import ctypes
 import os
 
 import torch
 import torch.distributed as dist
+
+from . import _native as nat
 
 
 def shard_bounds(global_num_envs, rank, world):
@@ -84,9 +87,6 @@ class StreamSplitEnv:
             self.bounds.append((lo, lo + cnt))
         self.device = self.subs[0].device
         self.streams = [torch.cuda.Stream(self.device) for _ in self.subs]
-        from . import _native as nat
-        import ctypes
-
         for e, st in zip(self.subs, self.streams):
             nat.check(nat.lib.lz_set_stream(e._h, ctypes.c_void_p(st.cuda_stream)))
             e.stream = st

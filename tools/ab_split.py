@@ -12,7 +12,6 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import gym_lorenz as gl  # noqa: E402
 from gym_lorenz import _native as nat  # noqa: E402
 
-P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 L, R = 32, 16
 
 
