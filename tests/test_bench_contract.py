@@ -172,3 +172,27 @@ def test_multi_rank_line_shape(mode, extra):
     if mode == "rollout":  # cfg5's per-GPU shard at 8 GPUs
         a8 = bench.parse(["--gpus", "8", "--mode", "rollout", "--envs", "262144"])
         assert bench.shard_plan(a8, 8, 7) == (262144, 7 * 32768, 32768)
+
+
+def test_launch_description_and_sub_shards():
+    """describe_launches states what a window ran (the driver's --steps 20: one 20-launch
+    remainder graph; --streams S: per stream); sub_shards tiles a rank's shard with
+    consecutive global ids (StreamSplitEnv, bench.py --streams)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from gym_lorenz.parallel import sub_shards
+
+    tm = {"launches": 20 * 3, "windows": 3, "graph": True, "graph_len": 64, "graph_rem": 20,
+          "graph_head": 0, "head_eager": 0, "streams": 1}
+    d = bench.describe_launches(tm, False)
+    assert "1 hipGraph replay of 20 lz_step launches" in d and "0 eager" in d and "x3 windows" in d
+    tm2 = dict(tm, launches=4000, windows=1, graph_rem=32)
+    d2 = bench.describe_launches(tm2, False)
+    assert "62 hipGraph replays of 64" in d2 and "1 hipGraph replay of 32" in d2
+    d3 = bench.describe_launches(dict(tm, streams=4), False)
+    assert d3.startswith("per timed window, on each of 4 streams")
+    for n, off, S in ((131072, 0, 4), (70001, 3 * 70001, 4), (5, 10, 3)):
+        subs = sub_shards(n, off, S)
+        assert len(subs) == S and subs[0][0] == off
+        assert all(a[0] + a[1] == b[0] for a, b in zip(subs, subs[1:]))
+        assert sum(c for _, c in subs) == n
