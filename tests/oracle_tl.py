@@ -14,10 +14,15 @@ import numpy as np
 
 
 class OracleTL:
-    def __init__(self, orc, system, dtype, n, seed, L, steps0=None, rk4=False):
+    def __init__(self, orc, system, dtype, n, seed, L, steps0=None, rk4=False, gids=None):
+        """gids: the global env ids of the n rows (a sample of a larger batch; default
+        0 .. n - 1): the Philox draws are keyed by the global id, so any subset runs alone."""
         self.orc, self.sys, self.dt, self.seed, self.L = orc, system, dtype, seed, L
         self.rk4 = rk4
-        self.st = np.ascontiguousarray(orc.reset_draw(system, dtype, n, 0, seed, 0).copy())
+        self.gids = None if gids is None else np.ascontiguousarray(gids, dtype=np.int64)
+        st = (orc.reset_draw(system, dtype, n, 0, seed, 0) if gids is None
+              else orc.reset_draw_idx(system, dtype, self.gids, seed, 0))
+        self.st = np.ascontiguousarray(st.copy())
         self.steps = (np.zeros(n, np.int64) if steps0 is None else steps0.astype(np.int64).copy())
         self.tick = 0
 
@@ -36,7 +41,8 @@ class OracleTL:
         idx = np.nonzero(d)[0]
         term = o[idx].copy()
         if idx.size:
-            fresh = orc.reset_draw_idx(self.sys, self.dt, idx, self.seed, self.tick)
+            gi = idx if self.gids is None else self.gids[idx]
+            fresh = orc.reset_draw_idx(self.sys, self.dt, gi, self.seed, self.tick)
             self.st[idx] = fresh
             o[idx] = orc.l3_reset_obs(fresh) if self.sys == "l3" else orc.l4_reset_obs(fresh)
             self.steps[idx] = 0
