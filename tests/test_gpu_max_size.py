@@ -33,7 +33,8 @@ def gl():
 
     assert torch.cuda.is_available(), "GPU tests need an MI355X"
     free, _ = torch.cuda.mem_get_info()
-    assert free > 160 * 2**30, f"the max-size cases need ~160 GB of HBM free ({free / 2**30:.0f} GiB)"
+    if free < 160 * 2**30:  # an MI355X has 288 GB; a smaller or shared card cannot hold these
+        pytest.skip(f"the max-size cases need ~160 GiB of HBM free ({free / 2**30:.0f} GiB)")
     return gym_lorenz
 
 
