@@ -307,7 +307,10 @@ def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=
                       else 256 * num_cus * 3 // 4 if system == "lorenz4" and not f64 and not rk4
                       else 2 * 256 * 256)
     if n < one_wave_below:
-        if system == "lorenz3" and not f64 and not rk4 and n >= 32768:
+        # rollout_split: variant 256 / 512 force one / two lanes per env (every system's
+        # obs width is even), else LORENZ3 f32 (Euler) from 32,768
+        if not variant & 256 and (variant & 512 or (system == "lorenz3" and not f64 and not rk4
+                                                   and n >= 32768)):
             return "_ZN2lz15k_rollout_splitINS_%sLi2ELi%dE%sLi1EEEvNS_5KArgsE" % (sysname, D, b)
         if (system == "pmsm" if noise is None else noise) and system in ("pmsm", "hr") \
                 and variant & (1 << 25):  # opt-in noise-producer wave
