@@ -62,6 +62,12 @@ def test_bench_kernel_names_exist():
     # LORENZ4 f32 rollouts: one-wave groups below 3/4 x 256 x CUs envs, 256 lanes from there
     assert "k_rolloutINS_5SysL4IfEEfLi64E" in bench.kernel_name("lorenz4", "rollout", 40960)
     assert "k_rolloutINS_5SysL4IfEEfLi256E" in bench.kernel_name("lorenz4", "rollout", 49152)
+    # the split-lane force bits: 512 two lanes per env for any system, 256 one lane
+    for system, n, v, want in (("hr", 32768, 512, "k_rollout_splitINS_5SysHR"),
+                               ("pmsm", 4097, 512, "k_rollout_splitINS_7SysPMSM"),
+                               ("lorenz3", 32768, 256, "k_rolloutINS_5SysL3IfEEfLi64E")):
+        k = bench.kernel_name(system, "rollout", n, variant=v)
+        assert want in k and kernel_hash.kernel_code_sha256(k) is not None, (system, v, k)
     assert bench.step_tiles("pmsm", 262144) == 1 and bench.step_tiles("hr", 1 << 20) == 4
     assert bench.step_tiles("hr", 1 << 21) == 1 and bench.step_tiles("lorenz3", 1 << 20) == 4
     assert bench.step_tiles("lorenz3", 131072) == 1 and bench.step_tiles("lorenz3", 1 << 21) == 1
