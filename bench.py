@@ -263,12 +263,9 @@ def step_tiles(system, n, f64=False, num_cus=256, variant=0, integrator="euler")
     forced = (variant >> 14) & 3
     if forced:
         return {1: 1, 2: 2, 3: 4}[forced]
-    # step_tiles_balanced: exactly 4 (LORENZ3 / PMSM: or 3) workgroups of 1,024 envs per CU;
-    # LORENZ3: 2 tiles at exactly 2 workgroups of 512 envs per CU
+    # step_tiles_balanced: exactly 4 (LORENZ3 / PMSM: or 3) workgroups of 1,024 envs per CU
     groups = -(-n // 1024)
-    if groups == 4 * num_cus or (system != "hr" and groups == 3 * num_cus):
-        return 4
-    return 2 if system == "lorenz3" and -(-n // 512) == 2 * num_cus else 1
+    return 4 if groups == 4 * num_cus or (system != "hr" and groups == 3 * num_cus) else 1
 
 
 def kernel_name(system, mode, n, f64=False, no_done=False, num_cus=256, variant=0,

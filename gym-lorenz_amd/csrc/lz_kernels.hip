@@ -531,14 +531,15 @@ struct multi_step_ok<SysL3<float>> {
 // 11.26, 917,504 9.54 -> 11.69; PMSM 786,432 19.46 -> 18.16, 851,968 21.20 -> 21.49,
 // 917,504 22.83 -> 22.61; HR 786,432 14.89 -> 15.38, 851,968 15.75 -> 16.90, 917,504
 // 16.73 -> 17.39 (HR 1M: +3.5-4.8%, above).
-// Round 6: LORENZ3 also takes TWO tiles where that grid is exactly 2 workgroups of 512 envs
-// per CU (262,144 envs on 256 CUs: the per-GPU shard of the 4-GPU strong headline): 3.96 ->
-// 3.74 us per step, two repeats each; its neighbours 229,376 / 294,912 and PMSM / HR at
-// 262,144 lose with two tiles (profiles/r06/tiles/).
-inline int step_tiles_balanced(int64_t n, int num_cus, bool three, bool two = false) {
+// Round 6: TWO tiles for LORENZ3 where that grid is exactly 2 workgroups of 512 envs per CU
+// (262,144 envs on 256 CUs, the 4-GPU strong shard) measured 3.74 vs 3.96 us per step on
+// the first boxes (profiles/r06/tiles/), then proved bimodal: per HANDLE (buffer placement,
+// profiles/r06/tile_probe/), 3.76 - 3.90 or 4.22 - 4.25 us, about half of 22 handles slow,
+// while one tile holds 3.94 - 4.03.  A 4-GPU line is the max over its ranks, so the default
+// stays one tile; variant 32768 still forces two.
+inline int step_tiles_balanced(int64_t n, int num_cus, bool three) {
   const int64_t groups = (n + 4 * kBlock - 1) / (4 * kBlock);
-  if (groups == 4 * (int64_t)num_cus || (three && groups == 3 * (int64_t)num_cus)) return 4;
-  return two && (n + 2 * kBlock - 1) / (2 * kBlock) == 2 * (int64_t)num_cus ? 2 : 1;
+  return groups == 4 * (int64_t)num_cus || (three && groups == 3 * (int64_t)num_cus) ? 4 : 1;
 }
 template <class Sys>
 inline int step_tiles(const KArgs& a) {
@@ -548,8 +549,7 @@ inline int step_tiles(const KArgs& a) {
     case 2: return 2;
     case 3: return 4;
     default:
-      return step_tiles_balanced(a.n, a.num_cus > 0 ? a.num_cus : 256, !std::is_same<Sys, SysHR<float>>::value,
-                                 std::is_same<Sys, SysL3<float>>::value);
+      return step_tiles_balanced(a.n, a.num_cus > 0 ? a.num_cus : 256, !std::is_same<Sys, SysHR<float>>::value);
   }
 }
 

@@ -41,10 +41,10 @@ def _np(t):
     return t.detach().cpu().numpy()
 
 
-def _balanced(n, cus, three, two=False):
+def _balanced(n, cus, three):
     """lz_kernels.hip step_tiles_balanced (mirrored in test_kernel_hash.py): multi-tile?"""
     groups = (n + 1023) // 1024
-    return groups == 4 * cus or (three and groups == 3 * cus) or (two and (n + 511) // 512 == 2 * cus)
+    return groups == 4 * cus or (three and groups == 3 * cus)
 
 
 def _bits(t):
@@ -59,19 +59,25 @@ def _same(a, b):
 CASES = [("pmsm", 1 << 20, {"add_noise": True}), ("hr", 1 << 20, {"add_noise": True}),
          ("pmsm", 786432, {"add_noise": True}), ("lorenz3", 786432, {}),
          ("lorenz3", 1 << 20, {}), ("hr", 786432, {"add_noise": True}),
-         ("lorenz3", 262144, {})]  # r06: two tiles at 2 workgroups of 512 envs per CU
+         ("lorenz3", 262144, {}),  # r06: one tile by default (the two-tile mode is bimodal) ...
+         ("lorenz3", 262144, {"variant": 32768})]  # ... and two tiles, forced
 
 
-@pytest.mark.parametrize("system,n,kw", CASES, ids=["%s-%d" % (c[0], c[1]) for c in CASES])
+@pytest.mark.parametrize("system,n,kw", CASES,
+                         ids=["%s-%d%s" % (c[0], c[1], "-v%d" % c[2]["variant"] if "variant" in c[2] else "")
+                              for c in CASES])
 def test_default_step_launch_vs_forced_k_step(gl, cus, system, n, kw):
     from gym_lorenz import _native as nat
 
-    be = gl.BatchedEnv(system, n, dtype="float32", seed=31, max_episode_steps=9, **kw)
+    kw = dict(kw)
+    forced = kw.pop("variant", 0)
+    be = gl.BatchedEnv(system, n, dtype="float32", seed=31, max_episode_steps=9, variant=forced, **kw)
     tw = gl.BatchedEnv(system, n, dtype="float32", seed=31, max_episode_steps=9,
                        variant=FORCE_K_STEP, **kw)
-    want = "step_multi" if _balanced(n, cus, system != "hr", system == "lorenz3") else "step"
+    want = "step_multi" if forced or _balanced(n, cus, system != "hr") else "step"
     if cus == 256:  # MI355X: the sizes above are exactly the ones that select each branch
-        assert want == ("step" if (system, n) == ("hr", 786432) else "step_multi")
+        assert want == ("step" if (system, n, forced) in (("hr", 786432, 0), ("lorenz3", 262144, 0))
+                        else "step_multi")
     assert nat.launch_shape(be._h, nat.CALL_STEP)["kernel"] == want
     assert nat.launch_shape(be._h, nat.CALL_STEP_NOISE)["kernel"] == "step"
     assert nat.launch_shape(tw._h, nat.CALL_STEP)["kernel"] == "step"

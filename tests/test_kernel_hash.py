@@ -71,8 +71,9 @@ def test_bench_kernel_names_exist():
     assert bench.step_tiles("pmsm", 262144) == 1 and bench.step_tiles("hr", 1 << 20) == 4
     assert bench.step_tiles("hr", 1 << 21) == 1 and bench.step_tiles("lorenz3", 1 << 20) == 4
     assert bench.step_tiles("lorenz3", 131072) == 1 and bench.step_tiles("lorenz3", 1 << 21) == 1
-    assert bench.step_tiles("lorenz3", 262144) == 2 and bench.step_tiles("lorenz3", 229376) == 1
-    assert "k_step_multiINS_5SysL3IfEEfLi2E" in bench.kernel_name("lorenz3", "step", 262144)
+    assert bench.step_tiles("lorenz3", 262144) == 1 and bench.step_tiles("lorenz3", 229376) == 1
+    assert "k_step_multiINS_5SysL3IfEEfLi2E" in bench.kernel_name("lorenz3", "step", 262144, variant=32768)
+    assert "k_stepINS_5SysL3" in bench.kernel_name("lorenz3", "step", 262144)
     assert bench.step_tiles("lorenz3", 1 << 20, f64=True) == 1
     assert bench.step_tiles("lorenz3", 786432) == 4 and bench.step_tiles("lorenz3", 851968) == 1
     assert bench.step_tiles("pmsm", 786432) == 4 and bench.step_tiles("pmsm", 917504) == 1
