@@ -4,7 +4,7 @@
 # torchrun launch at world size 1, and cfg5 / cfg4 lines.
 set -o pipefail
 cd "$(dirname "$0")/.."
-O=gpurun_out/r06_final2
+O=${O:-gpurun_out/r06_final2}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests \
