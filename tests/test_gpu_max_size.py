@@ -156,3 +156,79 @@ def test_pmsm_step_max_size_vs_oracle(gl):
     be.close()
     del be
     _free()
+
+
+def _sample_n(n, seed):
+    rng = np.random.default_rng(seed)
+    parts = [np.arange(0, 1024), np.arange(n - 1024, n), rng.integers(0, n, 2048)]
+    parts += [np.arange(max(0, c - 256), min(n, c + 256)) for c in (1 << 28, 1 << 29, (1 << 31) // 8)]
+    return np.unique(np.concatenate(parts)).astype(np.int64)
+
+
+def test_l4_step_max_size_vs_oracle(gl):
+    """LORENZ4 (eight float32 planes, obs 8: element indices pass 2^32 at env 536,870,912)
+    at 536,870,913 envs, TimeLimit(3) with staggered counters, 4 steps: the sample vs the
+    oracle bit for bit, and the done bytes of every env vs the schedule (its own
+    termination, reward < -1e6, cannot fire in 4 steps from the reference's initial
+    states: asserted through the oracle's sample)."""
+    import oracle as orc
+    from gym_lorenz import _native as nat
+
+    n, seed = 536_870_913, 37
+    gids = _sample_n(n, 3)
+    gd = torch.from_numpy(gids).cuda()
+    be = gl.BatchedEnv("lorenz4", n, dtype="float32", seed=seed, max_episode_steps=L)
+    be.reset()
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    steps = torch.randint(0, L, (n,), dtype=torch.int32, device="cuda", generator=g)
+    be.set_state(nat.L4_STEP, steps)
+    ref = OracleTL(orc, "l4", np.float32, gids.size, seed, L, steps[gd].cpu().numpy(), gids=gids)
+    for k in range(4):
+        a = torch.rand((n, 3), dtype=torch.float32, device="cuda", generator=g).mul_(2.0).sub_(1.0)
+        o, r, d = be.step(a)
+        oo, rr, dd, idx, term = ref.step(a[gd].cpu().numpy())
+        assert bits_equal(o[gd].cpu().numpy(), oo), k
+        assert bits_equal(r[gd].cpu().numpy(), rr), k
+        assert np.array_equal(d[gd].cpu().numpy(), dd), k
+        assert not (dd & 1).any(), k
+        steps += 1
+        due = steps >= L
+        steps[due] = 0
+        assert torch.equal(d, due.to(torch.uint8) << 1), k
+        del a, due
+    for p in range(8):
+        assert bits_equal(be.get_state(p, gd).cpu().numpy(), ref.st[:, p]), p
+    be.close()
+    del be, steps
+    _free()
+
+
+def test_hr_step_max_size_vs_oracle(gl):
+    """Hindmarsh-Rose (RK4 in registers, obs 6) at 400,000,003 envs (odd N; obs element
+    indices past 2^31), noise off, 3 steps: the sample's obs, reward, termination bits and
+    master / slave planes vs the oracle's DEV restatement, bit for bit."""
+    import oracle as orc
+    from gym_lorenz import _native as nat
+
+    n, seed = 400_000_003, 41
+    gids = _sample_n(n, 4)
+    gd = torch.from_numpy(gids).cuda()
+    be = gl.BatchedEnv("hr", n, dtype="float32", seed=seed, autoreset=False, add_noise=False)
+    be.reset()
+    init = orc.reset_draw_idx("hr", np.float32, gids, seed, 0)
+    st = np.ascontiguousarray(init[:, :6])
+    fa = np.zeros((gids.size, 2), np.float32)
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    with np.errstate(all="ignore"):
+        for k in range(3):
+            a = torch.rand((n, 2), dtype=torch.float32, device="cuda", generator=g).mul_(2.4).sub_(1.2)
+            o, r, d = be.step(a)
+            oo, rr, tt = orc.hr_step(st, fa, a[gd].cpu().numpy(), None, False, False, orc.DEV)
+            assert bits_equal(o[gd].cpu().numpy(), oo) and bits_equal(r[gd].cpu().numpy(), rr), k
+            assert np.array_equal((d[gd].cpu().numpy() & 1).astype(bool), tt), k
+            del a
+    got = np.stack([be.get_state(nat.HR_M + j, gd).cpu().numpy() for j in range(6)], 1)
+    assert bits_equal(got, st)
+    be.close()
+    del be
+    _free()
